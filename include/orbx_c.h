@@ -1,0 +1,229 @@
+/*
+ * orbx_c.h — C ABI of the MI355X-native ORB front-end (liborbx.so).
+ *
+ * This is the drop-in boundary for ORB-SLAM2's ORBextractor / ORBmatcher hot
+ * path (reference: falfab/orb_slam_cuda). Plain C types only; device memory
+ * is addressed by plain pointers and HIP streams by `void*`.
+ *
+ * Entry points and the reference interface each one replaces:
+ *   orbx_create            ORBextractor::ORBextractor(nfeatures, scaleFactor,
+ *                          nlevels, iniThFAST, minThFAST, width, height)
+ *                          include/ORBextractor.h:82-83, src/ORBextractor.cc:496-560
+ *   orbx_destroy           ORBextractor::~ORBextractor  src/ORBextractor.cc:800
+ *   orbx_extract           ORBextractor::operator()(image, mask, keypoints,
+ *                          descriptors)  include/ORBextractor.h:90-92,
+ *                          src/ORBextractor.cc:1538-1815 (CPU branch 1701-1809)
+ *   orbx_extract_batch     same, B frames per call, device-resident in/out
+ *                          (frame batching for MI355X; no reference equivalent)
+ *   orbx_get_scales        GetScaleFactors / GetInverseScaleFactors /
+ *                          GetScaleSigmaSquares / GetInverseScaleSigmaSquares
+ *                          include/ORBextractor.h:94-114
+ *   orbx_get_levels_info   GetLevels + per-level sizes / mnFeaturesPerLevel
+ *   orbx_get_level         public mvImagePyramid[level]  include/ORBextractor.h:116
+ *                          (read by Frame::ComputeStereoMatches src/Frame.cc:472,562,579)
+ *   orbm_descriptor_distance  ORBmatcher::DescriptorDistance
+ *                          include/ORBmatcher.h:44, src/ORBmatcher.cc:1647-1663
+ *   orbm_search_for_initialization  ORBmatcher::SearchForInitialization
+ *                          include/ORBmatcher.h:69, src/ORBmatcher.cc:405-520
+ *                          (+ Frame::AssignFeaturesToGrid/GetFeaturesInArea
+ *                          src/Frame.cc:229-244,326-391)
+ *   orbm_search_by_bow     ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...)
+ *                          include/ORBmatcher.h:65, src/ORBmatcher.cc:159-288;
+ *                          kf_vs_kf=1: SearchByBoW(KeyFrame*, KeyFrame*, ...)
+ *                          include/ORBmatcher.h:66, src/ORBmatcher.cc:522-655
+ *   orbm_hamming_top2      the best/second Hamming inner loop shared by every
+ *                          matcher (dense, device-resident, batched)
+ *
+ * Error behaviour: every call returns ORBX_OK or a negative code; the
+ * message of the last failure on the calling thread is orbx_last_error().
+ * The C++ shim (include/orb_slam2/ORBextractor.h) turns codes into
+ * std::runtime_error, as the reference's NVXIO_SAFE_CALL does
+ * (nvxio/include/OVX/UtilityOVX.hpp:129-137).
+ *
+ * Threading: handles are independent and may be used concurrently from
+ * different threads (the reference runs two extractors at once for stereo,
+ * src/Frame.cc:77-80). One handle is not reentrant.
+ */
+#ifndef ORBX_C_H
+#define ORBX_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBX_OK 0
+#define ORBX_EINVAL (-1)    /* bad argument / unsupported configuration   */
+#define ORBX_EDEVICE (-2)   /* HIP runtime error or no gfx950 device       */
+#define ORBX_ECAPACITY (-3) /* caller buffer or internal capacity too small */
+#define ORBX_ENOMEM (-4)    /* device allocation failed                    */
+
+/* Binary-identical to cv::KeyPoint: pt.x, pt.y, size, angle, response
+ * (float), octave, class_id (int) = 28 bytes. class_id is always -1. */
+typedef struct orbx_kp {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} orbx_kp;
+
+/* Parity-mode switches. */
+#define ORBX_SCALE_U 0        /* level geometry from scaleFactor^l (default)   */
+#define ORBX_SCALE_F 1        /* fork: VX ORB pyramid sizes override scales    */
+#define ORBX_PATTERN_FORK 0   /* bit_pattern_31_[96] = VX_FAILURE-2 = -3 (default) */
+#define ORBX_PATTERN_UPSTREAM 1 /* upstream ORB-SLAM2 table (-2)              */
+
+typedef struct orbx_config {
+  int nfeatures;      /* ORBextractor.nFeatures                  */
+  float scale_factor; /* ORBextractor.scaleFactor                */
+  int nlevels;        /* ORBextractor.nLevels (1..16)            */
+  int ini_th_fast;    /* ORBextractor.iniThFAST                  */
+  int min_th_fast;    /* ORBextractor.minThFAST                  */
+  int width, height;  /* frame size (Camera.width / Camera.height) */
+  int device;         /* HIP device ordinal                       */
+  int max_batch;      /* frames per orbx_extract_batch call (>=1) */
+  int scale_mode;     /* ORBX_SCALE_*                             */
+  int pattern_mode;   /* ORBX_PATTERN_*                           */
+  int reserved[5];    /* must be zero                             */
+} orbx_config;
+
+typedef struct orbx_extractor* orbx_handle;
+
+const char* orbx_last_error(void);
+const char* orbx_version(void);
+
+int orbx_create(const orbx_config* cfg, orbx_handle* out);
+int orbx_destroy(orbx_handle h);
+
+/* Maximum keypoints one frame can produce (sizes per-frame output slots). */
+int orbx_frame_capacity(orbx_handle h);
+
+/* ORBextractor::operator(): host image in, host keypoints/descriptors out.
+ * Synchronous. Empty image (w==0||h==0) -> *n = 0, ORBX_OK (reference
+ * returns with outputs untouched, src/ORBextractor.cc:1542-1543). */
+int orbx_extract(orbx_handle h, const uint8_t* img, int w, int h_, size_t stride,
+                 orbx_kp* kps, int cap, uint8_t* desc, int* n);
+
+/* Batched, device-resident, asynchronous on `stream` (hipStream_t or NULL).
+ * d_frames: batch frames of (height x width) u8, row stride `row_stride`,
+ * frame i at d_frames + i*frame_pitch. Outputs: frame i's keypoints at
+ * d_kps + i*cap, descriptors at d_desc + i*cap*32, count in d_counts[i],
+ * where cap = orbx_frame_capacity(h). Level-major order as the reference. */
+int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch,
+                       size_t frame_pitch, size_t row_stride, orbx_kp* d_kps,
+                       uint8_t* d_desc, int* d_counts, void* stream);
+
+int orbx_get_scales(orbx_handle h, float* scale, float* inv_scale,
+                    float* sigma2, float* inv_sigma2);
+int orbx_get_levels_info(orbx_handle h, int* nlevels, int* level_w,
+                         int* level_h, int* nfeatures_per_level);
+/* Copy pyramid level `level` of frame `frame` of the last extraction to host
+ * (mvImagePyramid). `blurred`=1 returns the 7x7 Gaussian-blurred level used
+ * for the descriptors instead (stage probe). */
+int orbx_get_level(orbx_handle h, int frame, int level, int blurred,
+                   uint8_t* out, size_t out_stride);
+/* Stage probe: FAST + per-cell NMS candidates of (frame, level) of the last
+ * extraction, in reference order, as keypoints (x,y relative to the border
+ * box, response = FAST score). */
+int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out,
+                             int cap, int* n);
+/* Per-stage device time (ms) of the last extraction, stage names as the
+ * reference's GetTime labels (src/ORBextractor.cc:1131,1331,1737,1753,1841).
+ * Filled only when the handle was created with timing enabled
+ * (ORBX_TIMING=1 in the environment). */
+int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap,
+                         int* n);
+
+/* ------------------------------------------------------------- matcher */
+typedef struct orbx_matcher* orbm_handle;
+
+/* Workspace for batched matching of up to max_pairs frame pairs with up to
+ * max_kps keypoints per frame. */
+int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out);
+int orbm_destroy(orbm_handle m);
+
+/* Hamming distance of two 32-byte descriptors (host, exact). */
+int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Dense best/second search, device-resident, batched over `pairs`:
+ * for pair p, A = d_A + p*a_pitch (nA[p] rows of 32 B), B likewise.
+ * Outputs per query row (stride a_cap): best index (-1 if none), best
+ * distance and second-best distance (256 when absent), with SearchByBoW's
+ * sequential semantics (strict '<', first index wins ties). */
+int orbm_hamming_top2(orbm_handle m, const uint8_t* d_A, size_t a_pitch,
+                      const int* d_nA, int a_cap, const uint8_t* d_B,
+                      size_t b_pitch, const int* d_nB, int pairs,
+                      int* d_best_idx, int* d_best, int* d_second, void* stream);
+
+/* Frame-side inputs of SearchForInitialization: mvKeysUn (orbx_kp) and
+ * descriptors, plus the image bounds Frame uses for its 64x48 grid
+ * (mnMinX, mnMaxX, mnMinY, mnMaxY). */
+typedef struct orbm_grid_bounds {
+  float min_x, max_x, min_y, max_y;
+} orbm_grid_bounds;
+
+/* ORBmatcher::SearchForInitialization on host buffers (synchronous).
+ * prev_xy: 2*n1 floats, vbPrevMatched, updated in place. matches12: n1. */
+int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1,
+                                   const uint8_t* desc1, int n1,
+                                   const orbx_kp* kp2, const uint8_t* desc2,
+                                   int n2, orbm_grid_bounds bounds,
+                                   float* prev_xy, int window, float nnratio,
+                                   int check_ori, int* matches12,
+                                   int* nmatches);
+
+/* Batched device-resident variant: pair p matches frame F1 = (d_kp1 +
+ * p*kp_pitch, d_desc1 + p*kp_pitch*32, d_n1[p]) against F2 likewise.
+ * d_prev_xy: pairs x kp_pitch x 2 floats (in/out); d_matches12: pairs x
+ * kp_pitch; d_nmatches: pairs. */
+int orbm_search_for_initialization_batch(
+    orbm_handle m, const orbx_kp* d_kp1, const uint8_t* d_desc1,
+    const int* d_n1, const orbx_kp* d_kp2, const uint8_t* d_desc2,
+    const int* d_n2, int kp_pitch, int pairs, orbm_grid_bounds bounds,
+    float* d_prev_xy, int window, float nnratio, int check_ori,
+    int* d_matches12, int* d_nmatches, void* stream);
+
+/* DBoW2::FeatureVector as CSR: nodes[k] ascending NodeIds; the feature
+ * indices of node k are idx[off[k] .. off[k+1]). Each feature index appears
+ * in at most one node (DBoW2 guarantees it; checked). */
+typedef struct orbm_feature_vector {
+  const uint32_t* nodes;
+  const int* off;
+  const int* idx;
+  int n_nodes;
+} orbm_feature_vector;
+
+/* ORBmatcher::SearchByBoW on host buffers (synchronous).
+ * A = KeyFrame (descriptors, mvKeysUn angles, MapPoint-valid mask = pMP &&
+ * !pMP->isBad()). kf_vs_kf = 0: B = Frame (mp_validB ignored), out[nB] =
+ * matched KF feature index per frame feature or -1 (vpMapPointMatches).
+ * kf_vs_kf = 1: B = KeyFrame 2, out[nA] = idx2 or -1 (vpMatches12). */
+int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
+                       const uint8_t* mp_validA, int nA,
+                       orbm_feature_vector fvA, const uint8_t* descB,
+                       const float* angleB, const uint8_t* mp_validB, int nB,
+                       orbm_feature_vector fvB, float nnratio, int check_ori,
+                       int kf_vs_kf, int* out, int* nmatches);
+
+/* --------------------------------------------- device plumbing for hosts
+ * Thin wrappers so a host without its own HIP binding (ctypes, cgo, JNI)
+ * can stage buffers for the batched entry points. */
+int orbx_device_count(int* n);
+int orbx_set_device(int device);
+int orbx_malloc(void** p, size_t bytes);
+int orbx_free(void* p);
+int orbx_memcpy_htod(void* dst, const void* src, size_t bytes);
+int orbx_memcpy_dtoh(void* dst, const void* src, size_t bytes);
+int orbx_memset(void* dst, int value, size_t bytes);
+int orbx_stream_create(void** stream);
+int orbx_stream_destroy(void* stream);
+int orbx_stream_synchronize(void* stream);
+int orbx_event_create(void** ev);
+int orbx_event_destroy(void* ev);
+int orbx_event_record(void* ev, void* stream);
+int orbx_event_elapsed_ms(void* start, void* stop, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBX_C_H */

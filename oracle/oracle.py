@@ -1,0 +1,165 @@
+"""ctypes wrapper of the CPU ORACLE (oracle/liborb_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package. The oracle is the
+checker: a CPU restatement of the reference path (see orb_oracle.h for the
+per-function reference citations and the "parity unpinned" status).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborb_oracle.so")
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KP_DTYPE.itemsize == 28
+
+
+class OrcConfig(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int), ("width", C.c_int),
+                ("height", C.c_int), ("scale_mode", C.c_int), ("pattern_mode", C.c_int)]
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.orc_fast_atan2.restype = C.c_float
+        _lib.orc_fast_atan2.argtypes = [C.c_float, C.c_float]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def config(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, width=1241,
+           height=376, scale_mode=0, pattern_mode=0) -> OrcConfig:
+    return OrcConfig(nfeatures, scale_factor, nlevels, ini_th, min_th, width, height,
+                     scale_mode, pattern_mode)
+
+
+def level_info(cfg: OrcConfig) -> dict:
+    L = cfg.nlevels
+    w = np.zeros(L, np.int32); h = np.zeros(L, np.int32)
+    s = np.zeros(L, np.float32); inv = np.zeros(L, np.float32)
+    s2 = np.zeros(L, np.float32); is2 = np.zeros(L, np.float32)
+    nf = np.zeros(L, np.int32); umax = np.zeros(16, np.int32)
+    lib().orc_level_info(C.byref(cfg), _p(w), _p(h), _p(s), _p(inv), _p(s2), _p(is2), _p(nf), _p(umax))
+    return dict(w=w, h=h, scale=s, inv_scale=inv, sigma2=s2, inv_sigma2=is2, nfeat=nf, umax=umax)
+
+
+def extract(cfg: OrcConfig, img: np.ndarray):
+    img = np.ascontiguousarray(img, np.uint8)
+    cap = max(16 * cfg.nfeatures, 4096)
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int(0)
+    rc = lib().orc_extract(C.byref(cfg), _p(img), img.shape[1], img.shape[0],
+                           C.c_size_t(img.strides[0]), _p(kps), cap, _p(desc), C.byref(n))
+    assert rc == 0, rc
+    return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def pyramid_level(cfg: OrcConfig, img: np.ndarray, level: int) -> np.ndarray:
+    info = level_info(cfg)
+    out = np.zeros((info["h"][level], info["w"][level]), np.uint8)
+    img = np.ascontiguousarray(img, np.uint8)
+    lib().orc_pyramid_level(C.byref(cfg), _p(img), img.shape[1], img.shape[0],
+                            C.c_size_t(img.strides[0]), level, _p(out))
+    return out
+
+
+def blur_level(cfg: OrcConfig, img: np.ndarray, level: int) -> np.ndarray:
+    info = level_info(cfg)
+    out = np.zeros((info["h"][level], info["w"][level]), np.uint8)
+    img = np.ascontiguousarray(img, np.uint8)
+    lib().orc_blur_level(C.byref(cfg), _p(img), img.shape[1], img.shape[0],
+                         C.c_size_t(img.strides[0]), level, _p(out))
+    return out
+
+
+def fast_level(cfg: OrcConfig, img: np.ndarray, level: int) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    cap = 1 << 20
+    kps = np.zeros(cap, KP_DTYPE)
+    n = C.c_int(0)
+    rc = lib().orc_fast_level(C.byref(cfg), _p(img), img.shape[1], img.shape[0],
+                              C.c_size_t(img.strides[0]), level, _p(kps), cap, C.byref(n))
+    assert rc == 0
+    return kps[:n.value].copy()
+
+
+def distribute(keys: np.ndarray, minX: int, maxX: int, minY: int, maxY: int, N: int) -> np.ndarray:
+    keys = np.ascontiguousarray(keys, KP_DTYPE)
+    cap = max(len(keys), N) + 8
+    out = np.zeros(cap, KP_DTYPE)
+    n = C.c_int(0)
+    rc = lib().orc_distribute(_p(keys), len(keys), minX, maxX, minY, maxY, N, _p(out), cap, C.byref(n))
+    assert rc == 0
+    return out[:n.value].copy()
+
+
+def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.ascontiguousarray(a, np.uint8); b = np.ascontiguousarray(b, np.uint8)
+    return lib().orc_descriptor_distance(_p(a), _p(b))
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return lib().orc_fast_atan2(y, x)
+
+
+def hamming_top2(A: np.ndarray, B: np.ndarray):
+    A = np.ascontiguousarray(A, np.uint8); B = np.ascontiguousarray(B, np.uint8)
+    nA = len(A)
+    bi = np.zeros(nA, np.int32); bd = np.zeros(nA, np.int32); sd = np.zeros(nA, np.int32)
+    lib().orc_hamming_top2(_p(A), nA, _p(B), len(B), _p(bi), _p(bd), _p(sd))
+    return bi, bd, sd
+
+
+def search_for_initialization(kp1, desc1, kp2, desc2, bounds, prev_xy, window=100,
+                              nnratio=0.9, check_ori=True):
+    """Returns (matches12, nmatches, updated prev_xy). bounds = (minX, maxX, minY, maxY)."""
+    kp1 = np.ascontiguousarray(kp1, KP_DTYPE); kp2 = np.ascontiguousarray(kp2, KP_DTYPE)
+    desc1 = np.ascontiguousarray(desc1, np.uint8); desc2 = np.ascontiguousarray(desc2, np.uint8)
+    prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.zeros(len(kp1), np.int32)
+    nm = C.c_int(0)
+    lib().orc_search_for_initialization(
+        _p(kp1), _p(desc1), len(kp1), _p(kp2), _p(desc2), len(kp2),
+        C.c_float(bounds[0]), C.c_float(bounds[1]), C.c_float(bounds[2]), C.c_float(bounds[3]),
+        _p(prev), window, C.c_float(nnratio), int(check_ori), _p(m12), C.byref(nm))
+    return m12, nm.value, prev
+
+
+def search_by_bow(descA, angleA, mpA, fvA, descB, angleB, mpB, fvB, nnratio, check_ori,
+                  kf_vs_kf):
+    """fvX = (nodes u32, off i32, idx i32). Returns (out, nmatches)."""
+    descA = np.ascontiguousarray(descA, np.uint8); descB = np.ascontiguousarray(descB, np.uint8)
+    angleA = np.ascontiguousarray(angleA, np.float32); angleB = np.ascontiguousarray(angleB, np.float32)
+    mpA = np.ascontiguousarray(mpA, np.uint8); mpB = np.ascontiguousarray(mpB, np.uint8)
+    fa = [np.ascontiguousarray(x) for x in fvA]; fb = [np.ascontiguousarray(x) for x in fvB]
+    nA, nB = len(descA), len(descB)
+    out = np.zeros(nA if kf_vs_kf else nB, np.int32)
+    nm = C.c_int(0)
+    lib().orc_search_by_bow(_p(descA), _p(angleA), _p(mpA), nA, _p(fa[0]), _p(fa[1]), _p(fa[2]),
+                            len(fa[0]), _p(descB), _p(angleB), _p(mpB), nB, _p(fb[0]), _p(fb[1]),
+                            _p(fb[2]), len(fb[0]), C.c_float(nnratio), int(check_ori),
+                            int(kf_vs_kf), _p(out), C.byref(nm))
+    return out, nm.value

@@ -1,0 +1,1074 @@
+/*
+ * orb_oracle.cpp — CPU ORACLE for the ORB hot path. TEST INFRASTRUCTURE ONLY.
+ *
+ * A line-faithful CPU restatement of the reference's CPU branch
+ * (built with DONT_USE_OPENVX, /root/reference/src/ORBextractor.cc:1701-1873)
+ * and of ORBmatcher's SearchForInitialization / SearchByBoW, with the OpenCV
+ * primitives those call restated from OpenCV 3.x scalar semantics because
+ * OpenCV is not vendored in the reference.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py (cpu_baseline) load this.
+ * PARITY UNPINNED at the OpenCV boundary (no reference test or fixture pins
+ * resize/FAST/GaussianBlur/fastAtan2); see DESIGN.md "Oracle".
+ *
+ * Build: oracle/Makefile (g++ -O2 -ffp-contract=off, no fast-math).
+ */
+#include "orb_oracle.h"
+#include "orb_pattern_tbl.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <list>
+#include <vector>
+
+namespace {
+
+typedef orc_kp KeyPoint;
+
+// ---------------------------------------------------------------- OpenCV bits
+// cvRound: round half to even (x86 cvtss2si under default MXCSR).
+inline int cv_round(float v) { return (int)lrintf(v); }
+inline int cv_round(double v) { return (int)lrint(v); }
+// cvFloor / cvCeil as in OpenCV core/fast_math.hpp.
+inline int cv_floor(float v) { int i = (int)v; return i - (i > v); }
+inline int cv_floor(double v) { int i = (int)v; return i - (i > v); }
+inline int cv_ceil(double v) { int i = (int)v; return i + (i < v); }
+inline short sat_short(int v) { return (short)std::min(std::max(v, (int)SHRT_MIN), (int)SHRT_MAX); }
+inline uint8_t sat_u8(int v) { return (uint8_t)std::min(std::max(v, 0), 255); }
+
+struct Mat8 {
+  int w = 0, h = 0;
+  std::vector<uint8_t> px;
+  void alloc(int W, int H) { w = W; h = H; px.assign((size_t)W * H, 0); }
+  uint8_t* row(int y) { return px.data() + (size_t)y * w; }
+  const uint8_t* row(int y) const { return px.data() + (size_t)y * w; }
+  uint8_t at(int y, int x) const { return px[(size_t)y * w + x]; }
+};
+
+// cv::fastAtan2, OpenCV 3.x core/src/mathfuncs_core.cpp (polynomial version).
+const float atan2_p1 = 0.9997878412794807f * (float)(180 / M_PI);
+const float atan2_p3 = -0.3258083974640975f * (float)(180 / M_PI);
+const float atan2_p5 = 0.1555786518463281f * (float)(180 / M_PI);
+const float atan2_p7 = -0.04432655554792128f * (float)(180 / M_PI);
+float fast_atan2(float y, float x) {
+  float ax = std::fabs(x), ay = std::fabs(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + (float)DBL_EPSILON);
+    c2 = c * c;
+    a = (((atan2_p7 * c2 + atan2_p5) * c2 + atan2_p3) * c2 + atan2_p1) * c;
+  } else {
+    c = ax / (ay + (float)DBL_EPSILON);
+    c2 = c * c;
+    a = 90.f - (((atan2_p7 * c2 + atan2_p5) * c2 + atan2_p3) * c2 + atan2_p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+// cv::resize(src, dst, Size(dw,dh), 0, 0, INTER_LINEAR) on CV_8UC1, OpenCV
+// 3.x imgproc/src/resize.cpp scalar path: 11-bit fixed-point coefficients,
+// HResizeLinear<uchar,int,short,2048> + VResizeLinear with FixedPtCast<22>.
+// Includes the INTER_LINEAR -> INTER_AREA switch for an exact 2x downscale.
+void resize_linear_u8(const Mat8& src, Mat8& dst, int dw, int dh) {
+  dst.alloc(dw, dh);
+  const double inv_scale_x = (double)dw / src.w, inv_scale_y = (double)dh / src.h;
+  const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+  const int iscale_x = (int)lrint(scale_x), iscale_y = (int)lrint(scale_y);
+  const bool is_area_fast = std::fabs(scale_x - iscale_x) < DBL_EPSILON &&
+                            std::fabs(scale_y - iscale_y) < DBL_EPSILON;
+  if (is_area_fast && iscale_x == 2 && iscale_y == 2) {
+    // resizeAreaFast_ 2x2: (a+b+c+d+2)>>2
+    for (int y = 0; y < dh; ++y) {
+      const uint8_t* S = src.row(2 * y);
+      const uint8_t* nS = src.row(std::min(2 * y + 1, src.h - 1));
+      uint8_t* D = dst.row(y);
+      for (int x = 0; x < dw; ++x) {
+        int i = 2 * x;
+        D[x] = (uint8_t)((S[i] + S[i + 1] + nS[i] + nS[i + 1] + 2) >> 2);
+      }
+    }
+    return;
+  }
+  const int ONE = 2048;  // INTER_RESIZE_COEF_SCALE
+  std::vector<int> xofs(dw);
+  std::vector<short> ialpha(2 * dw);
+  int xmax = dw;
+  for (int dx = 0; dx < dw; ++dx) {
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = cv_floor(fx);
+    fx -= sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx + 1 >= src.w) {
+      xmax = std::min(xmax, dx);
+      if (sx >= src.w - 1) { fx = 0; sx = src.w - 1; }
+    }
+    xofs[dx] = sx;
+    ialpha[2 * dx] = sat_short(cv_round((1.f - fx) * ONE));
+    ialpha[2 * dx + 1] = sat_short(cv_round(fx * ONE));
+  }
+  std::vector<int> rows0(dw), rows1(dw);
+  auto hresize = [&](const uint8_t* S, int* D) {
+    int dx = 0;
+    for (; dx < xmax; ++dx) {
+      int sx = xofs[dx];
+      D[dx] = S[sx] * ialpha[2 * dx] + S[sx + 1] * ialpha[2 * dx + 1];
+    }
+    for (; dx < dw; ++dx) D[dx] = S[xofs[dx]] * ONE;
+  };
+  auto clip = [](int x, int a, int b) { return x >= a ? (x < b ? x : b - 1) : a; };
+  for (int dy = 0; dy < dh; ++dy) {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = cv_floor(fy);
+    fy -= sy;
+    const int b0 = sat_short(cv_round((1.f - fy) * ONE));
+    const int b1 = sat_short(cv_round(fy * ONE));
+    hresize(src.row(clip(sy, 0, src.h)), rows0.data());
+    hresize(src.row(clip(sy + 1, 0, src.h)), rows1.data());
+    uint8_t* D = dst.row(dy);
+    for (int x = 0; x < dw; ++x)
+      D[x] = sat_u8((rows0[x] * b0 + rows1[x] * b1 + (1 << 21)) >> 22);
+  }
+}
+
+// BORDER_REFLECT_101 index (cv::borderInterpolate).
+inline int reflect101(int p, int len) {
+  if (len == 1) return 0;
+  while (p < 0 || p >= len) {
+    if (p < 0) p = -p;
+    if (p >= len) p = 2 * len - 2 - p;
+  }
+  return p;
+}
+
+// Gaussian kernel of getGaussianKernel(7, 2, CV_32F) converted to CV_32S with
+// scale 256 (createSeparableLinearFilter 8U smooth-symmetric branch).
+void gauss7_int(int k[7]) {
+  const int n = 7;
+  const double sigma = 2.0, scale2X = -0.5 / (sigma * sigma);
+  float cf[7];
+  double sum = 0;
+  for (int i = 0; i < n; ++i) {
+    double x = i - (n - 1) * 0.5;
+    cf[i] = (float)std::exp(scale2X * x * x);
+    sum += cf[i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < n; ++i) cf[i] = (float)(cf[i] * sum);
+  for (int i = 0; i < n; ++i) k[i] = cv_round(cf[i] * 256.f);
+}
+
+// GaussianBlur(src, dst, Size(7,7), 2, 2, BORDER_REFLECT_101) on CV_8UC1:
+// integer row pass, column pass sat_u8((acc + 2^15) >> 16).
+void gaussian_blur7(const Mat8& src, Mat8& dst) {
+  int k[7];
+  gauss7_int(k);
+  const int W = src.w, H = src.h;
+  std::vector<int> tmp((size_t)W * H);
+  for (int y = 0; y < H; ++y) {
+    const uint8_t* S = src.row(y);
+    for (int x = 0; x < W; ++x) {
+      int acc = 0;
+      for (int i = 0; i < 7; ++i) acc += k[i] * S[reflect101(x + i - 3, W)];
+      tmp[(size_t)y * W + x] = acc;
+    }
+  }
+  dst.alloc(W, H);
+  for (int y = 0; y < H; ++y) {
+    uint8_t* D = dst.row(y);
+    for (int x = 0; x < W; ++x) {
+      int acc = 0;
+      for (int i = 0; i < 7; ++i) acc += k[i] * tmp[(size_t)reflect101(y + i - 3, H) * W + x];
+      D[x] = sat_u8((acc + (1 << 15)) >> 16);
+    }
+  }
+}
+
+// ------------------------------------------------------------------- FAST
+// cv::FAST(img, kps, threshold, nonmax=true, TYPE_9_16): OpenCV 3.x
+// features2d/src/fast.cpp FAST_t<16> + cornerScore<16>, scalar path.
+const int kRingX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+const int kRingY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+int corner_score16(const uint8_t* ptr, const int pixel[25], int threshold) {
+  const int K = 8, N = K * 3 + 1;
+  int k, v = ptr[0];
+  short d[N];
+  for (k = 0; k < N; k++) d[k] = (short)(v - ptr[pixel[k]]);
+  int a0 = threshold;
+  for (k = 0; k < 16; k += 2) {
+    int a = std::min((int)d[k + 1], (int)d[k + 2]);
+    a = std::min(a, (int)d[k + 3]);
+    if (a <= a0) continue;
+    a = std::min(a, (int)d[k + 4]);
+    a = std::min(a, (int)d[k + 5]);
+    a = std::min(a, (int)d[k + 6]);
+    a = std::min(a, (int)d[k + 7]);
+    a = std::min(a, (int)d[k + 8]);
+    a0 = std::max(a0, std::min(a, (int)d[k]));
+    a0 = std::max(a0, std::min(a, (int)d[k + 9]));
+  }
+  int b0 = -a0;
+  for (k = 0; k < 16; k += 2) {
+    int b = std::max((int)d[k + 1], (int)d[k + 2]);
+    b = std::max(b, (int)d[k + 3]);
+    b = std::max(b, (int)d[k + 4]);
+    b = std::max(b, (int)d[k + 5]);
+    if (b >= b0) continue;
+    b = std::max(b, (int)d[k + 6]);
+    b = std::max(b, (int)d[k + 7]);
+    b = std::max(b, (int)d[k + 8]);
+    b0 = std::min(b0, std::max(b, (int)d[k]));
+    b0 = std::min(b0, std::max(b, (int)d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+// FAST on the ROI [x0, x0+cols) x [y0, y0+rows) of `img`; keypoints are
+// reported in ROI coordinates, row-major (the order FAST_t pushes them).
+void fast_roi(const Mat8& img, int x0, int y0, int cols, int rows, int threshold,
+              std::vector<KeyPoint>& out) {
+  out.clear();
+  if (rows < 7 || cols < 7) return;  // no candidate rows/cols in [3, n-3)
+  const int K = 8, N = 16 + K + 1;
+  threshold = std::min(std::max(threshold, 0), 255);
+  const int step = img.w;
+  int pixel[25];
+  for (int k = 0; k < 16; ++k) pixel[k] = kRingX[k] + kRingY[k] * step;
+  for (int k = 16; k < 25; ++k) pixel[k] = pixel[k - 16];
+  uint8_t threshold_tab[512];
+  for (int i = -255; i <= 255; i++)
+    threshold_tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
+  std::vector<uint8_t> buf(3 * (size_t)cols, 0);
+  std::vector<int> cpbuf(3 * ((size_t)cols + 1), 0);
+  uint8_t* bufp[3] = {buf.data(), buf.data() + cols, buf.data() + 2 * cols};
+  int* cpb[3] = {cpbuf.data() + 1, cpbuf.data() + 1 + (cols + 1), cpbuf.data() + 1 + 2 * (cols + 1)};
+  for (int i = 3; i < rows - 2; i++) {
+    const uint8_t* ptr = img.row(y0 + i) + x0 + 3;
+    uint8_t* curr = bufp[(i - 3) % 3];
+    int* cornerpos = cpb[(i - 3) % 3];
+    std::memset(curr, 0, cols);
+    int ncorners = 0;
+    if (i < rows - 3) {
+      for (int j = 3; j < cols - 3; j++, ptr++) {
+        int v = ptr[0];
+        const uint8_t* tab = &threshold_tab[0] - v + 255;
+        int d = tab[ptr[pixel[0]]] | tab[ptr[pixel[8]]];
+        if (d == 0) continue;
+        d &= tab[ptr[pixel[2]]] | tab[ptr[pixel[10]]];
+        d &= tab[ptr[pixel[4]]] | tab[ptr[pixel[12]]];
+        d &= tab[ptr[pixel[6]]] | tab[ptr[pixel[14]]];
+        if (d == 0) continue;
+        d &= tab[ptr[pixel[1]]] | tab[ptr[pixel[9]]];
+        d &= tab[ptr[pixel[3]]] | tab[ptr[pixel[11]]];
+        d &= tab[ptr[pixel[5]]] | tab[ptr[pixel[13]]];
+        d &= tab[ptr[pixel[7]]] | tab[ptr[pixel[15]]];
+        if (d & 1) {
+          int vt = v - threshold, count = 0;
+          for (int k = 0; k < N; k++) {
+            int x = ptr[pixel[k]];
+            if (x < vt) {
+              if (++count > K) {
+                cornerpos[ncorners++] = j;
+                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                break;
+              }
+            } else {
+              count = 0;
+            }
+          }
+        }
+        if (d & 2) {
+          int vt = v + threshold, count = 0;
+          for (int k = 0; k < N; k++) {
+            int x = ptr[pixel[k]];
+            if (x > vt) {
+              if (++count > K) {
+                cornerpos[ncorners++] = j;
+                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                break;
+              }
+            } else {
+              count = 0;
+            }
+          }
+        }
+      }
+    }
+    cornerpos[-1] = ncorners;
+    if (i == 3) continue;
+    const uint8_t* prev = bufp[(i - 4 + 3) % 3];
+    const uint8_t* pprev = bufp[(i - 5 + 3) % 3];
+    cornerpos = cpb[(i - 4 + 3) % 3];
+    ncorners = cornerpos[-1];
+    for (int k = 0; k < ncorners; k++) {
+      int j = cornerpos[k];
+      int score = prev[j];
+      if (score > prev[j + 1] && score > prev[j - 1] && score > pprev[j - 1] &&
+          score > pprev[j] && score > pprev[j + 1] && score > curr[j - 1] &&
+          score > curr[j] && score > curr[j + 1]) {
+        KeyPoint kp;
+        kp.x = (float)j;
+        kp.y = (float)(i - 1);
+        kp.size = 7.f;
+        kp.angle = -1.f;
+        kp.response = (float)score;
+        kp.octave = 0;
+        kp.class_id = -1;
+        out.push_back(kp);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------- extractor state
+const int PATCH_SIZE = 31;
+const int HALF_PATCH_SIZE = 15;
+const int EDGE_THRESHOLD = 19;
+
+struct Extractor {
+  orc_config cfg;
+  std::vector<float> mvScaleFactor, mvInvScaleFactor, mvLevelSigma2, mvInvLevelSigma2;
+  std::vector<int> mnFeaturesPerLevel, umax;
+  signed char tests[256][4];
+  std::vector<Mat8> pyr;
+
+  // ORBextractor::ORBextractor (src/ORBextractor.cc:496-560) incl. the fork's
+  // buildGraph scale override (:640-680) when scale_mode == 1.
+  explicit Extractor(const orc_config& c) : cfg(c) {
+    const int nlevels = cfg.nlevels;
+    const float scaleFactor = cfg.scale_factor;
+    mvScaleFactor.resize(nlevels);
+    mvLevelSigma2.resize(nlevels);
+    mvScaleFactor[0] = 1.0f;
+    mvLevelSigma2[0] = 1.0f;
+    for (int i = 1; i < nlevels; i++) {
+      mvScaleFactor[i] = mvScaleFactor[i - 1] * scaleFactor;
+      mvLevelSigma2[i] = mvScaleFactor[i] * mvScaleFactor[i];
+    }
+    mvInvScaleFactor.resize(nlevels);
+    mvInvLevelSigma2.resize(nlevels);
+    for (int i = 0; i < nlevels; i++) {
+      mvInvScaleFactor[i] = 1.0f / mvScaleFactor[i];
+      mvInvLevelSigma2[i] = 1.0f / mvLevelSigma2[i];
+    }
+    mnFeaturesPerLevel.resize(nlevels);
+    float factor = 1.0f / scaleFactor;
+    float nDesiredFeaturesPerScale =
+        cfg.nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)nlevels));
+    int sumFeatures = 0;
+    for (int level = 0; level < nlevels - 1; level++) {
+      mnFeaturesPerLevel[level] = cv_round(nDesiredFeaturesPerScale);
+      sumFeatures += mnFeaturesPerLevel[level];
+      nDesiredFeaturesPerScale *= factor;
+    }
+    mnFeaturesPerLevel[nlevels - 1] = std::max(cfg.nfeatures - sumFeatures, 0);
+
+    std::memcpy(tests, kOracleBriefTests, sizeof(tests));
+    if (cfg.pattern_mode == 1) tests[kOracleForkIndex / 4][kOracleForkIndex % 4] = kOracleUpstreamValue;
+
+    umax.resize(HALF_PATCH_SIZE + 1);
+    int v, v0, vmax = cv_floor(HALF_PATCH_SIZE * sqrt(2.f) / 2 + 1);
+    int vmin = cv_ceil(HALF_PATCH_SIZE * sqrt(2.f) / 2);
+    const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+    for (v = 0; v <= vmax; ++v) umax[v] = cv_round(sqrt(hp2 - v * v));
+    for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+      while (umax[v0] == umax[v0 + 1]) ++v0;
+      umax[v] = v0;
+      ++v0;
+    }
+    if (cfg.scale_mode == 1) {
+      // VX_SCALE_PYRAMID_ORB level widths, OpenVX ceil(w * 0.8408964^l).
+      // VisionWorks' own rounding is unverifiable offline.
+      for (int level = 0; level < nlevels; ++level) {
+        unsigned v_width = (unsigned)std::ceil(cfg.width * std::pow(0.8408964, level));
+        mvScaleFactor[level] = ((float)cfg.width) / v_width;
+        mvInvScaleFactor[level] = ((float)v_width) / cfg.width;
+      }
+    }
+  }
+
+  void level_size(int level, int cols, int rows, int* w, int* h) const {
+    float scale = mvInvScaleFactor[level];
+    *w = cv_round((float)cols * scale);
+    *h = cv_round((float)rows * scale);
+  }
+
+  // ComputePyramid (src/ORBextractor.cc:1837-1863): chained INTER_LINEAR.
+  // The 19-px REFLECT_101 border is never read by extraction.
+  void compute_pyramid(const Mat8& image) {
+    pyr.assign(cfg.nlevels, Mat8());
+    for (int level = 0; level < cfg.nlevels; ++level) {
+      int w, h;
+      level_size(level, image.w, image.h, &w, &h);
+      if (level != 0)
+        resize_linear_u8(pyr[level - 1], pyr[level], w, h);
+      else
+        pyr[0] = image;
+    }
+  }
+
+  // FAST stage of ComputeKeyPointsOctTree (src/ORBextractor.cc:1128-1299).
+  void fast_level(int level, std::vector<KeyPoint>& vToDistributeKeys, int* bx) const {
+    const float W = 30;
+    const Mat8& im = pyr[level];
+    const int minBorderX = EDGE_THRESHOLD - 3;
+    const int minBorderY = minBorderX;
+    const int maxBorderX = im.w - EDGE_THRESHOLD + 3;
+    const int maxBorderY = im.h - EDGE_THRESHOLD + 3;
+    bx[0] = minBorderX; bx[1] = maxBorderX; bx[2] = minBorderY; bx[3] = maxBorderY;
+    vToDistributeKeys.clear();
+    vToDistributeKeys.reserve(cfg.nfeatures * 10);
+    const float width = (maxBorderX - minBorderX);
+    const float height = (maxBorderY - minBorderY);
+    const int nCols = width / W;
+    const int nRows = height / W;
+    const int wCell = ceil(width / nCols);
+    const int hCell = ceil(height / nRows);
+    std::vector<KeyPoint> vKeysCell;
+    for (int i = 0; i < nRows; i++) {
+      const float iniY = minBorderY + i * hCell;
+      float maxY = iniY + hCell + 6;
+      if (iniY >= maxBorderY - 3) continue;
+      if (maxY > maxBorderY) maxY = maxBorderY;
+      for (int j = 0; j < nCols; j++) {
+        const float iniX = minBorderX + j * wCell;
+        float maxX = iniX + wCell + 6;
+        if (iniX >= maxBorderX - 6) continue;
+        if (maxX > maxBorderX) maxX = maxBorderX;
+        const int r0 = (int)iniY, r1 = (int)maxY, c0 = (int)iniX, c1 = (int)maxX;
+        fast_roi(im, c0, r0, c1 - c0, r1 - r0, cfg.ini_th_fast, vKeysCell);
+        if (vKeysCell.empty())
+          fast_roi(im, c0, r0, c1 - c0, r1 - r0, cfg.min_th_fast, vKeysCell);
+        for (auto& kp : vKeysCell) {
+          kp.x += j * wCell;
+          kp.y += i * hCell;
+          vToDistributeKeys.push_back(kp);
+        }
+      }
+    }
+  }
+
+  void extract(const Mat8& image, std::vector<KeyPoint>& out, std::vector<uint8_t>& desc);
+};
+
+// --------------------------------------------------------------- quadtree
+// ExtractorNode / DivideNode / DistributeOctTree (src/ORBextractor.cc:831-1120).
+// The reference sorts pair<int, ExtractorNode*> (:1041), i.e. breaks size ties
+// by heap address; the restatement breaks them by node creation sequence
+// (`seq`), the documented stand-in shared with the HIP kernel.
+struct ExtractorNode {
+  std::vector<KeyPoint> vKeys;
+  int ULx = 0, ULy = 0, URx = 0, URy = 0, BLx = 0, BLy = 0, BRx = 0, BRy = 0;
+  std::list<ExtractorNode>::iterator lit;
+  bool bNoMore = false;
+  long seq = 0;
+  void DivideNode(ExtractorNode& n1, ExtractorNode& n2, ExtractorNode& n3, ExtractorNode& n4) {
+    const int halfX = ceil(static_cast<float>(URx - ULx) / 2);
+    const int halfY = ceil(static_cast<float>(BRy - ULy) / 2);
+    n1.ULx = ULx; n1.ULy = ULy;
+    n1.URx = ULx + halfX; n1.URy = ULy;
+    n1.BLx = ULx; n1.BLy = ULy + halfY;
+    n1.BRx = ULx + halfX; n1.BRy = ULy + halfY;
+    n1.vKeys.reserve(vKeys.size());
+    n2.ULx = n1.URx; n2.ULy = n1.URy;
+    n2.URx = URx; n2.URy = URy;
+    n2.BLx = n1.BRx; n2.BLy = n1.BRy;
+    n2.BRx = URx; n2.BRy = ULy + halfY;
+    n2.vKeys.reserve(vKeys.size());
+    n3.ULx = n1.BLx; n3.ULy = n1.BLy;
+    n3.URx = n1.BRx; n3.URy = n1.BRy;
+    n3.BLx = BLx; n3.BLy = BLy;
+    n3.BRx = n1.BRx; n3.BRy = BLy;
+    n3.vKeys.reserve(vKeys.size());
+    n4.ULx = n3.URx; n4.ULy = n3.URy;
+    n4.URx = n2.BRx; n4.URy = n2.BRy;
+    n4.BLx = n3.BRx; n4.BLy = n3.BRy;
+    n4.BRx = BRx; n4.BRy = BRy;
+    n4.vKeys.reserve(vKeys.size());
+    for (size_t i = 0; i < vKeys.size(); i++) {
+      const KeyPoint& kp = vKeys[i];
+      if (kp.x < n1.URx) {
+        if (kp.y < n1.BRy) n1.vKeys.push_back(kp);
+        else n3.vKeys.push_back(kp);
+      } else if (kp.y < n1.BRy) {
+        n2.vKeys.push_back(kp);
+      } else {
+        n4.vKeys.push_back(kp);
+      }
+    }
+    if (n1.vKeys.size() == 1) n1.bNoMore = true;
+    if (n2.vKeys.size() == 1) n2.bNoMore = true;
+    if (n3.vKeys.size() == 1) n3.bNoMore = true;
+    if (n4.vKeys.size() == 1) n4.bNoMore = true;
+  }
+};
+
+struct SizeSeqNode {
+  int size;
+  long seq;
+  ExtractorNode* node;
+  bool operator<(const SizeSeqNode& o) const {
+    return size != o.size ? size < o.size : seq < o.seq;
+  }
+};
+
+std::vector<KeyPoint> distribute_oct_tree(const std::vector<KeyPoint>& vToDistributeKeys,
+                                          int minX, int maxX, int minY, int maxY, int N) {
+  const int nIni = round(static_cast<float>(maxX - minX) / (maxY - minY));
+  const float hX = static_cast<float>(maxX - minX) / nIni;
+  long seq = 0;
+  std::list<ExtractorNode> lNodes;
+  std::vector<ExtractorNode*> vpIniNodes(nIni);
+  for (int i = 0; i < nIni; i++) {
+    ExtractorNode ni;
+    ni.ULx = (int)(hX * static_cast<float>(i)); ni.ULy = 0;
+    ni.URx = (int)(hX * static_cast<float>(i + 1)); ni.URy = 0;
+    ni.BLx = ni.ULx; ni.BLy = maxY - minY;
+    ni.BRx = ni.URx; ni.BRy = maxY - minY;
+    ni.vKeys.reserve(vToDistributeKeys.size());
+    ni.seq = seq++;
+    lNodes.push_back(ni);
+    vpIniNodes[i] = &lNodes.back();
+  }
+  for (size_t i = 0; i < vToDistributeKeys.size(); i++) {
+    const KeyPoint& kp = vToDistributeKeys[i];
+    vpIniNodes[(size_t)(kp.x / hX)]->vKeys.push_back(kp);
+  }
+  auto lit = lNodes.begin();
+  while (lit != lNodes.end()) {
+    if (lit->vKeys.size() == 1) {
+      lit->bNoMore = true;
+      lit++;
+    } else if (lit->vKeys.empty()) {
+      lit = lNodes.erase(lit);
+    } else {
+      lit++;
+    }
+  }
+  bool bFinish = false;
+  std::vector<SizeSeqNode> vSizeAndPointerToNode;
+  vSizeAndPointerToNode.reserve(lNodes.size() * 4);
+  auto push_child = [&](ExtractorNode& n, std::vector<SizeSeqNode>& v, int* nToExpand) {
+    if (n.vKeys.size() > 0) {
+      n.seq = seq++;
+      lNodes.push_front(n);
+      if (n.vKeys.size() > 1) {
+        if (nToExpand) (*nToExpand)++;
+        v.push_back({(int)n.vKeys.size(), lNodes.front().seq, &lNodes.front()});
+        lNodes.front().lit = lNodes.begin();
+      }
+    }
+  };
+  while (!bFinish) {
+    int prevSize = lNodes.size();
+    lit = lNodes.begin();
+    int nToExpand = 0;
+    vSizeAndPointerToNode.clear();
+    while (lit != lNodes.end()) {
+      if ((int)lNodes.size() >= N) {
+        bFinish = true;
+        break;
+      }
+      if (lit->bNoMore) {
+        lit++;
+        continue;
+      } else {
+        ExtractorNode n1, n2, n3, n4;
+        lit->DivideNode(n1, n2, n3, n4);
+        push_child(n1, vSizeAndPointerToNode, &nToExpand);
+        push_child(n2, vSizeAndPointerToNode, &nToExpand);
+        push_child(n3, vSizeAndPointerToNode, &nToExpand);
+        push_child(n4, vSizeAndPointerToNode, &nToExpand);
+        lit = lNodes.erase(lit);
+        continue;
+      }
+    }
+    if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) {
+      bFinish = true;
+    } else if (((int)lNodes.size() + nToExpand * 3) > N) {
+      while (!bFinish) {
+        prevSize = lNodes.size();
+        std::vector<SizeSeqNode> vPrevSizeAndPointerToNode = vSizeAndPointerToNode;
+        vSizeAndPointerToNode.clear();
+        std::sort(vPrevSizeAndPointerToNode.begin(), vPrevSizeAndPointerToNode.end());
+        for (int j = vPrevSizeAndPointerToNode.size() - 1; j >= 0; j--) {
+          ExtractorNode n1, n2, n3, n4;
+          vPrevSizeAndPointerToNode[j].node->DivideNode(n1, n2, n3, n4);
+          push_child(n1, vSizeAndPointerToNode, nullptr);
+          push_child(n2, vSizeAndPointerToNode, nullptr);
+          push_child(n3, vSizeAndPointerToNode, nullptr);
+          push_child(n4, vSizeAndPointerToNode, nullptr);
+          lNodes.erase(vPrevSizeAndPointerToNode[j].node->lit);
+          if ((int)lNodes.size() >= N) break;
+        }
+        if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) bFinish = true;
+      }
+    }
+  }
+  std::vector<KeyPoint> vResultKeys;
+  vResultKeys.reserve(lNodes.size());
+  for (auto it = lNodes.begin(); it != lNodes.end(); it++) {
+    std::vector<KeyPoint>& vNodeKeys = it->vKeys;
+    KeyPoint* pKP = &vNodeKeys[0];
+    float maxResponse = pKP->response;
+    for (size_t k = 1; k < vNodeKeys.size(); k++) {
+      if (vNodeKeys[k].response > maxResponse) {
+        pKP = &vNodeKeys[k];
+        maxResponse = vNodeKeys[k].response;
+      }
+    }
+    vResultKeys.push_back(*pKP);
+  }
+  return vResultKeys;
+}
+
+// IC_Angle (src/ORBextractor.cc:164-191) on the unblurred level.
+float ic_angle(const Mat8& image, float ptx, float pty, const std::vector<int>& u_max) {
+  int m_01 = 0, m_10 = 0;
+  const uint8_t* center = image.px.data() + (size_t)cv_round(pty) * image.w + cv_round(ptx);
+  for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u) m_10 += u * center[u];
+  const int step = image.w;
+  for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+    int v_sum = 0;
+    int d = u_max[v];
+    for (int u = -d; u <= d; ++u) {
+      int val_plus = center[u + v * step], val_minus = center[u - v * step];
+      v_sum += (val_plus - val_minus);
+      m_10 += u * (val_plus + val_minus);
+    }
+    m_01 += v * v_sum;
+  }
+  return fast_atan2((float)m_01, (float)m_10);
+}
+
+// computeOrbDescriptor (src/ORBextractor.cc:195-233) on the blurred level.
+const float factorPI = (float)(M_PI / 180.f);
+void orb_descriptor(const KeyPoint& kpt, const Mat8& img, const signed char tests[256][4],
+                    uint8_t* desc) {
+  float angle = (float)kpt.angle * factorPI;
+  float a = (float)cosf(angle), b = (float)sinf(angle);
+  const uint8_t* center = img.px.data() + (size_t)cv_round(kpt.y) * img.w + cv_round(kpt.x);
+  const int step = img.w;
+  auto get = [&](int x, int y) {
+    return center[cv_round(x * b + y * a) * step + cv_round(x * a - y * b)];
+  };
+  for (int i = 0; i < 32; ++i) {
+    int val = 0;
+    for (int k = 0; k < 8; ++k) {
+      const signed char* t = tests[i * 8 + k];
+      int t0 = get(t[0], t[1]), t1 = get(t[2], t[3]);
+      val |= (t0 < t1) << k;
+    }
+    desc[i] = (uint8_t)val;
+  }
+}
+
+// operator() CPU branch (src/ORBextractor.cc:1701-1809) + ComputeKeyPointsOctTree.
+void Extractor::extract(const Mat8& image, std::vector<KeyPoint>& out, std::vector<uint8_t>& desc) {
+  out.clear();
+  desc.clear();
+  if (image.w == 0 || image.h == 0) return;
+  compute_pyramid(image);
+  std::vector<std::vector<KeyPoint>> allKeypoints(cfg.nlevels);
+  std::vector<KeyPoint> cand;
+  for (int level = 0; level < cfg.nlevels; ++level) {
+    int bx[4];
+    fast_level(level, cand, bx);
+    std::vector<KeyPoint>& keypoints = allKeypoints[level];
+    keypoints = distribute_oct_tree(cand, bx[0], bx[1], bx[2], bx[3], mnFeaturesPerLevel[level]);
+    const int scaledPatchSize = PATCH_SIZE * mvScaleFactor[level];
+    for (auto& kp : keypoints) {
+      kp.x += bx[0];
+      kp.y += bx[2];
+      kp.octave = level;
+      kp.size = scaledPatchSize;
+    }
+  }
+  for (int level = 0; level < cfg.nlevels; ++level)
+    for (auto& kp : allKeypoints[level]) kp.angle = ic_angle(pyr[level], kp.x, kp.y, umax);
+  for (int level = 0; level < cfg.nlevels; ++level) {
+    std::vector<KeyPoint>& keypoints = allKeypoints[level];
+    if (keypoints.empty()) continue;
+    Mat8 working;
+    gaussian_blur7(pyr[level], working);
+    size_t off = desc.size();
+    desc.resize(off + 32 * keypoints.size());
+    for (size_t i = 0; i < keypoints.size(); ++i)
+      orb_descriptor(keypoints[i], working, tests, desc.data() + off + 32 * i);
+    if (level != 0) {
+      float scale = mvScaleFactor[level];
+      for (auto& kp : keypoints) { kp.x *= scale; kp.y *= scale; }
+    }
+    out.insert(out.end(), keypoints.begin(), keypoints.end());
+  }
+}
+
+Mat8 wrap_image(const uint8_t* img, int w, int h, size_t stride) {
+  Mat8 m;
+  m.alloc(w, h);
+  for (int y = 0; y < h; ++y) std::memcpy(m.row(y), img + (size_t)y * stride, w);
+  return m;
+}
+
+// ------------------------------------------------------------------ matcher
+const int TH_LOW = 50;
+const int HISTO_LENGTH = 30;
+
+int descriptor_distance(const uint8_t* a, const uint8_t* b) {
+  const int32_t* pa = (const int32_t*)a;
+  const int32_t* pb = (const int32_t*)b;
+  int dist = 0;
+  for (int i = 0; i < 8; i++, pa++, pb++) {
+    unsigned int v = *pa ^ *pb;
+    v = v - ((v >> 1) & 0x55555555);
+    v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+    dist += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
+  }
+  return dist;
+}
+
+// ComputeThreeMaxima (src/ORBmatcher.cc:1601-1642).
+void compute_three_maxima(const std::vector<int>* histo, const int L, int& ind1, int& ind2, int& ind3) {
+  int max1 = 0, max2 = 0, max3 = 0;
+  for (int i = 0; i < L; i++) {
+    const int s = histo[i].size();
+    if (s > max1) {
+      max3 = max2; max2 = max1; max1 = s;
+      ind3 = ind2; ind2 = ind1; ind1 = i;
+    } else if (s > max2) {
+      max3 = max2; max2 = s;
+      ind3 = ind2; ind2 = i;
+    } else if (s > max3) {
+      max3 = s;
+      ind3 = i;
+    }
+  }
+  if (max2 < 0.1f * (float)max1) {
+    ind2 = -1;
+    ind3 = -1;
+  } else if (max3 < 0.1f * (float)max1) {
+    ind3 = -1;
+  }
+}
+
+const int FRAME_GRID_ROWS = 48;
+const int FRAME_GRID_COLS = 64;
+
+// The Frame fields SearchForInitialization touches (src/Frame.cc:229-391).
+struct GridFrame {
+  const KeyPoint* keys;
+  const uint8_t* desc;
+  int N;
+  float mnMinX, mnMaxX, mnMinY, mnMaxY, invW, invH;
+  std::vector<size_t> mGrid[FRAME_GRID_COLS][FRAME_GRID_ROWS];
+  GridFrame(const KeyPoint* k, const uint8_t* d, int n, float minX, float maxX, float minY, float maxY)
+      : keys(k), desc(d), N(n), mnMinX(minX), mnMaxX(maxX), mnMinY(minY), mnMaxY(maxY) {
+    invW = static_cast<float>(FRAME_GRID_COLS) / static_cast<float>(mnMaxX - mnMinX);
+    invH = static_cast<float>(FRAME_GRID_ROWS) / static_cast<float>(mnMaxY - mnMinY);
+    for (int i = 0; i < N; i++) {
+      int px, py;
+      if (pos_in_grid(keys[i], px, py)) mGrid[px][py].push_back(i);
+    }
+  }
+  bool pos_in_grid(const KeyPoint& kp, int& posX, int& posY) const {
+    posX = round((kp.x - mnMinX) * invW);
+    posY = round((kp.y - mnMinY) * invH);
+    if (posX < 0 || posX >= FRAME_GRID_COLS || posY < 0 || posY >= FRAME_GRID_ROWS) return false;
+    return true;
+  }
+  std::vector<size_t> features_in_area(const float& x, const float& y, const float& r,
+                                       const int minLevel, const int maxLevel) const {
+    std::vector<size_t> vIndices;
+    const int nMinCellX = std::max(0, (int)floor((x - mnMinX - r) * invW));
+    if (nMinCellX >= FRAME_GRID_COLS) return vIndices;
+    const int nMaxCellX = std::min((int)FRAME_GRID_COLS - 1, (int)ceil((x - mnMinX + r) * invW));
+    if (nMaxCellX < 0) return vIndices;
+    const int nMinCellY = std::max(0, (int)floor((y - mnMinY - r) * invH));
+    if (nMinCellY >= FRAME_GRID_ROWS) return vIndices;
+    const int nMaxCellY = std::min((int)FRAME_GRID_ROWS - 1, (int)ceil((y - mnMinY + r) * invH));
+    if (nMaxCellY < 0) return vIndices;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+      for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+        const std::vector<size_t>& vCell = mGrid[ix][iy];
+        for (size_t j = 0; j < vCell.size(); j++) {
+          const KeyPoint& kpUn = keys[vCell[j]];
+          if (bCheckLevels) {
+            if (kpUn.octave < minLevel) continue;
+            if (maxLevel >= 0)
+              if (kpUn.octave > maxLevel) continue;
+          }
+          const float distx = kpUn.x - x;
+          const float disty = kpUn.y - y;
+          if (fabs(distx) < r && fabs(disty) < r) vIndices.push_back(vCell[j]);
+        }
+      }
+    }
+    return vIndices;
+  }
+};
+
+}  // namespace
+
+// ===================================================================== C ABI
+extern "C" {
+
+int orc_level_info(const orc_config* cfg, int* level_w, int* level_h, float* scale,
+                   float* inv_scale, float* sigma2, float* inv_sigma2, int* nfeat, int* umax16) {
+  Extractor ex(*cfg);
+  for (int l = 0; l < cfg->nlevels; ++l) {
+    int w, h;
+    ex.level_size(l, cfg->width, cfg->height, &w, &h);
+    if (level_w) level_w[l] = w;
+    if (level_h) level_h[l] = h;
+    if (scale) scale[l] = ex.mvScaleFactor[l];
+    if (inv_scale) inv_scale[l] = ex.mvInvScaleFactor[l];
+    if (sigma2) sigma2[l] = ex.mvLevelSigma2[l];
+    if (inv_sigma2) inv_sigma2[l] = ex.mvInvLevelSigma2[l];
+    if (nfeat) nfeat[l] = ex.mnFeaturesPerLevel[l];
+  }
+  if (umax16)
+    for (int v = 0; v <= HALF_PATCH_SIZE; ++v) umax16[v] = ex.umax[v];
+  return 0;
+}
+
+int orc_extract(const orc_config* cfg, const uint8_t* img, int w, int h, size_t stride,
+                orc_kp* kps, int cap, uint8_t* desc, int* n) {
+  Extractor ex(*cfg);
+  Mat8 im = wrap_image(img, w, h, stride);
+  std::vector<KeyPoint> out;
+  std::vector<uint8_t> d;
+  ex.extract(im, out, d);
+  *n = (int)out.size();
+  if ((int)out.size() > cap) return -1;
+  std::memcpy(kps, out.data(), out.size() * sizeof(KeyPoint));
+  std::memcpy(desc, d.data(), d.size());
+  return 0;
+}
+
+int orc_pyramid_level(const orc_config* cfg, const uint8_t* img, int w, int h, size_t stride,
+                      int level, uint8_t* out) {
+  Extractor ex(*cfg);
+  ex.compute_pyramid(wrap_image(img, w, h, stride));
+  std::memcpy(out, ex.pyr[level].px.data(), ex.pyr[level].px.size());
+  return 0;
+}
+
+int orc_blur_level(const orc_config* cfg, const uint8_t* img, int w, int h, size_t stride,
+                   int level, uint8_t* out) {
+  Extractor ex(*cfg);
+  ex.compute_pyramid(wrap_image(img, w, h, stride));
+  Mat8 b;
+  gaussian_blur7(ex.pyr[level], b);
+  std::memcpy(out, b.px.data(), b.px.size());
+  return 0;
+}
+
+int orc_fast_level(const orc_config* cfg, const uint8_t* img, int w, int h, size_t stride,
+                   int level, orc_kp* kps, int cap, int* n) {
+  Extractor ex(*cfg);
+  ex.compute_pyramid(wrap_image(img, w, h, stride));
+  std::vector<KeyPoint> cand;
+  int bx[4];
+  ex.fast_level(level, cand, bx);
+  *n = (int)cand.size();
+  if (*n > cap) return -1;
+  std::memcpy(kps, cand.data(), cand.size() * sizeof(KeyPoint));
+  return 0;
+}
+
+int orc_distribute(const orc_kp* keys, int nkeys, int minX, int maxX, int minY, int maxY, int N,
+                   orc_kp* out, int cap, int* n) {
+  std::vector<KeyPoint> in(keys, keys + nkeys);
+  std::vector<KeyPoint> r = distribute_oct_tree(in, minX, maxX, minY, maxY, N);
+  *n = (int)r.size();
+  if (*n > cap) return -1;
+  std::memcpy(out, r.data(), r.size() * sizeof(KeyPoint));
+  return 0;
+}
+
+int orc_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
+
+float orc_fast_atan2(float y, float x) { return fast_atan2(y, x); }
+
+void orc_hamming_top2(const uint8_t* A, int nA, const uint8_t* B, int nB, int* best_idx,
+                      int* best_dist, int* second_dist) {
+  for (int i = 0; i < nA; ++i) {
+    int bestDist1 = 256, bestIdx = -1, bestDist2 = 256;
+    for (int j = 0; j < nB; ++j) {
+      const int dist = descriptor_distance(A + 32 * (size_t)i, B + 32 * (size_t)j);
+      if (dist < bestDist1) {
+        bestDist2 = bestDist1;
+        bestDist1 = dist;
+        bestIdx = j;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    best_idx[i] = bestIdx;
+    best_dist[i] = bestDist1;
+    second_dist[i] = bestDist2;
+  }
+}
+
+int orc_search_for_initialization(const orc_kp* kp1, const uint8_t* desc1, int n1,
+                                  const orc_kp* kp2, const uint8_t* desc2, int n2, float min_x,
+                                  float max_x, float min_y, float max_y, float* prev_xy,
+                                  int windowSize, float mfNNratio, int mbCheckOrientation,
+                                  int* vnMatches12, int* out_nmatches) {
+  GridFrame F2(kp2, desc2, n2, min_x, max_x, min_y, max_y);
+  int nmatches = 0;
+  for (int i = 0; i < n1; ++i) vnMatches12[i] = -1;
+  std::vector<int> rotHist[HISTO_LENGTH];
+  const float factor = 1.0f / HISTO_LENGTH;
+  std::vector<int> vMatchedDistance(n2, INT_MAX);
+  std::vector<int> vnMatches21(n2, -1);
+  for (int i1 = 0; i1 < n1; i1++) {
+    const KeyPoint& kp1i = kp1[i1];
+    int level1 = kp1i.octave;
+    if (level1 > 0) continue;
+    const float r = (float)windowSize;
+    std::vector<size_t> vIndices2 =
+        F2.features_in_area(prev_xy[2 * i1], prev_xy[2 * i1 + 1], r, level1, level1);
+    if (vIndices2.empty()) continue;
+    const uint8_t* d1 = desc1 + 32 * (size_t)i1;
+    int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+    for (size_t i2 : vIndices2) {
+      int dist = descriptor_distance(d1, desc2 + 32 * i2);
+      if (vMatchedDistance[i2] <= dist) continue;
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestIdx2 = i2;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= TH_LOW) {
+      if (bestDist < (float)bestDist2 * mfNNratio) {
+        if (vnMatches21[bestIdx2] >= 0) {
+          vnMatches12[vnMatches21[bestIdx2]] = -1;
+          nmatches--;
+        }
+        vnMatches12[i1] = bestIdx2;
+        vnMatches21[bestIdx2] = i1;
+        vMatchedDistance[bestIdx2] = bestDist;
+        nmatches++;
+        if (mbCheckOrientation) {
+          float rot = kp1[i1].angle - kp2[bestIdx2].angle;
+          if (rot < 0.0) rot += 360.0f;
+          int bin = round(rot * factor);
+          if (bin == HISTO_LENGTH) bin = 0;
+          rotHist[bin].push_back(i1);
+        }
+      }
+    }
+  }
+  if (mbCheckOrientation) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    compute_three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+      if (i == ind1 || i == ind2 || i == ind3) continue;
+      for (size_t j = 0; j < rotHist[i].size(); j++) {
+        int idx1 = rotHist[i][j];
+        if (vnMatches12[idx1] >= 0) {
+          vnMatches12[idx1] = -1;
+          nmatches--;
+        }
+      }
+    }
+  }
+  for (int i1 = 0; i1 < n1; i1++)
+    if (vnMatches12[i1] >= 0) {
+      prev_xy[2 * i1] = kp2[vnMatches12[i1]].x;
+      prev_xy[2 * i1 + 1] = kp2[vnMatches12[i1]].y;
+    }
+  *out_nmatches = nmatches;
+  return 0;
+}
+
+int orc_search_by_bow(const uint8_t* descA, const float* angleA, const uint8_t* mpA, int nA,
+                      const uint32_t* fvA_nodes, const int* fvA_off, const int* fvA_idx, int fvA_n,
+                      const uint8_t* descB, const float* angleB, const uint8_t* mpB, int nB,
+                      const uint32_t* fvB_nodes, const int* fvB_off, const int* fvB_idx, int fvB_n,
+                      float mfNNratio, int mbCheckOrientation, int kf_vs_kf, int* out,
+                      int* out_nmatches) {
+  const int nout = kf_vs_kf ? nA : nB;
+  for (int i = 0; i < nout; ++i) out[i] = -1;
+  std::vector<char> vbMatched2(nB, 0);
+  std::vector<int> rotHist[HISTO_LENGTH];
+  const float factor = 1.0f / HISTO_LENGTH;
+  int nmatches = 0;
+  int ia = 0, ib = 0;
+  while (ia < fvA_n && ib < fvB_n) {
+    if (fvA_nodes[ia] == fvB_nodes[ib]) {
+      for (int p = fvA_off[ia]; p < fvA_off[ia + 1]; ++p) {
+        const int idx1 = fvA_idx[p];
+        if (!mpA[idx1]) continue;  // !pMP || pMP->isBad()
+        const uint8_t* d1 = descA + 32 * (size_t)idx1;
+        int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+        for (int q = fvB_off[ib]; q < fvB_off[ib + 1]; ++q) {
+          const int idx2 = fvB_idx[q];
+          if (kf_vs_kf) {
+            if (vbMatched2[idx2] || !mpB[idx2]) continue;
+          } else {
+            if (out[idx2] >= 0) continue;  // vpMapPointMatches[realIdxF] already set
+          }
+          const int dist = descriptor_distance(d1, descB + 32 * (size_t)idx2);
+          if (dist < bestDist1) {
+            bestDist2 = bestDist1;
+            bestDist1 = dist;
+            bestIdx2 = idx2;
+          } else if (dist < bestDist2) {
+            bestDist2 = dist;
+          }
+        }
+        const bool pass_th = kf_vs_kf ? (bestDist1 < TH_LOW) : (bestDist1 <= TH_LOW);
+        if (pass_th) {
+          if (static_cast<float>(bestDist1) < mfNNratio * static_cast<float>(bestDist2)) {
+            if (kf_vs_kf) {
+              out[idx1] = bestIdx2;
+              vbMatched2[bestIdx2] = 1;
+            } else {
+              out[bestIdx2] = idx1;
+            }
+            if (mbCheckOrientation) {
+              float rot = angleA[idx1] - angleB[bestIdx2];
+              if (rot < 0.0) rot += 360.0f;
+              int bin = round(rot * factor);
+              if (bin == HISTO_LENGTH) bin = 0;
+              rotHist[bin].push_back(kf_vs_kf ? idx1 : bestIdx2);
+            }
+            nmatches++;
+          }
+        }
+      }
+      ia++;
+      ib++;
+    } else if (fvA_nodes[ia] < fvB_nodes[ib]) {
+      ia = std::lower_bound(fvA_nodes + ia, fvA_nodes + fvA_n, fvB_nodes[ib]) - fvA_nodes;
+    } else {
+      ib = std::lower_bound(fvB_nodes + ib, fvB_nodes + fvB_n, fvA_nodes[ia]) - fvB_nodes;
+    }
+  }
+  if (mbCheckOrientation) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    compute_three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+      if (i == ind1 || i == ind2 || i == ind3) continue;
+      for (size_t j = 0; j < rotHist[i].size(); j++) {
+        out[rotHist[i][j]] = -1;
+        nmatches--;
+      }
+    }
+  }
+  *out_nmatches = nmatches;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+/*
+ * orb_oracle.h — C ABI of the CPU ORACLE (test infrastructure only).
+ *
+ * This library is a CPU restatement of the reference's ORB hot path
+ * (falfab/orb_slam_cuda, CPU branch of ORBextractor::operator() and the
+ * ORBmatcher searches). It exists ONLY to check the HIP product and to time
+ * a CPU baseline: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it. The product library never links it.
+ *
+ * Parity status: the reference cannot be compiled here (it needs OpenCV,
+ * VisionWorks and CUDA), and it ships no tests or golden
+ * vectors for this path. The OpenCV primitives are restated from OpenCV 3.x
+ * scalar semantics. => PARITY UNPINNED at the OpenCV
+ * boundary; pinned only by the known-answer checks in tests/test_oracle.py
+ * (umax, features-per-level, Hamming vs numpy on Examples/Monocular/map.yml).
+ */
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Binary-identical to cv::KeyPoint (pt.x, pt.y, size, angle, response,
+ * octave, class_id) = 28 bytes. */
+typedef struct orc_kp {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} orc_kp;
+
+typedef struct orc_config {
+  int nfeatures;       /* ORBextractor.nFeatures                          */
+  float scale_factor;  /* ORBextractor.scaleFactor                        */
+  int nlevels;         /* ORBextractor.nLevels                            */
+  int ini_th_fast;     /* ORBextractor.iniThFAST                          */
+  int min_th_fast;     /* ORBextractor.minThFAST                          */
+  int width, height;   /* Camera.width/height (fork ctor args)            */
+  int scale_mode;      /* 0 = U (1.2^l geometry), 1 = F (VX ORB pyramid)  */
+  int pattern_mode;    /* 0 = fork table (entry 96 = -3), 1 = upstream    */
+} orc_config;
+
+/* Per-level geometry the extractor derives in its constructor. */
+int orc_level_info(const orc_config* cfg, int* level_w, int* level_h,
+                   float* scale, float* inv_scale, float* sigma2,
+                   float* inv_sigma2, int* nfeat_per_level, int* umax16);
+
+/* Full ORBextractor::operator(): returns n keypoints (level-major order) and
+ * n x 32 descriptor bytes. Returns 0, or -1 if cap is too small. */
+int orc_extract(const orc_config* cfg, const uint8_t* img, int w, int h,
+                size_t stride, orc_kp* kps, int cap, uint8_t* desc, int* n);
+
+/* Stage probes (for stage-level parity tests). `out` receives level `level`
+ * of the pyramid (w_l x h_l, packed) or its 7x7 Gaussian blur. */
+int orc_pyramid_level(const orc_config* cfg, const uint8_t* img, int w, int h,
+                      size_t stride, int level, uint8_t* out);
+int orc_blur_level(const orc_config* cfg, const uint8_t* img, int w, int h,
+                   size_t stride, int level, uint8_t* out);
+/* FAST + per-cell NMS output of one level, in reference push order
+ * (x,y relative to the border box, response = FAST score). */
+int orc_fast_level(const orc_config* cfg, const uint8_t* img, int w, int h,
+                   size_t stride, int level, orc_kp* kps, int cap, int* n);
+/* Quadtree distribution of arbitrary keys (DistributeOctTree). */
+int orc_distribute(const orc_kp* keys, int nkeys, int minX, int maxX,
+                   int minY, int maxY, int N, orc_kp* out, int cap, int* n);
+
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1647-1663). */
+int orc_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Dense best/second Hamming search (SearchByBoW inner loop semantics:
+ * strict '<', first index wins ties, distances start at 256). */
+void orc_hamming_top2(const uint8_t* A, int nA, const uint8_t* B, int nB,
+                      int* best_idx, int* best_dist, int* second_dist);
+
+/* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:405-520) over the
+ * Frame grid (src/Frame.cc:229-244, 326-391). kp arrays are mvKeysUn.
+ * prev_xy (2*n1 floats) is updated in place like vbPrevMatched. */
+int orc_search_for_initialization(
+    const orc_kp* kp1, const uint8_t* desc1, int n1,
+    const orc_kp* kp2, const uint8_t* desc2, int n2,
+    float min_x, float max_x, float min_y, float max_y,
+    float* prev_xy, int window, float nnratio, int check_ori,
+    int* matches12, int* nmatches);
+
+/* ORBmatcher::SearchByBoW. FeatureVectors are CSR: fv_nodes[k] (ascending
+ * NodeId), fv_off[k]..fv_off[k+1] index fv_idx. mp_valid = "MapPoint exists
+ * and !isBad()". kf_vs_kf=0 -> (KeyFrame*, Frame&) variant (:159-288):
+ * out[nB] = KF index matched to each frame feature or -1. kf_vs_kf=1 ->
+ * (KeyFrame*, KeyFrame*) variant (:522-655): out[nA] = idx2 or -1. */
+int orc_search_by_bow(
+    const uint8_t* descA, const float* angleA, const uint8_t* mp_validA,
+    int nA, const uint32_t* fvA_nodes, const int* fvA_off, const int* fvA_idx,
+    int fvA_n,
+    const uint8_t* descB, const float* angleB, const uint8_t* mp_validB,
+    int nB, const uint32_t* fvB_nodes, const int* fvB_off, const int* fvB_idx,
+    int fvB_n,
+    float nnratio, int check_ori, int kf_vs_kf, int* out, int* nmatches);
+
+/* Elementary OpenCV restatements, exported for unit tests. */
+float orc_fast_atan2(float y, float x);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,193 @@
+"""Loader for the HIP product library liborbx.so (built in-tree by build()).
+
+There is no CPU fallback: if the library or a gfx950 device is missing,
+every entry point raises. The ctypes signatures mirror include/orbx_c.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborbx.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "orbx_c.h")
+
+ORBX_OK, ORBX_EINVAL, ORBX_EDEVICE, ORBX_ECAPACITY, ORBX_ENOMEM = 0, -1, -2, -3, -4
+
+# cv::KeyPoint layout (include/orbx_c.h orbx_kp)
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KP_DTYPE.itemsize == 28
+
+
+class OrbxConfig(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int), ("width", C.c_int),
+                ("height", C.c_int), ("device", C.c_int), ("max_batch", C.c_int),
+                ("scale_mode", C.c_int), ("pattern_mode", C.c_int), ("reserved", C.c_int * 5)]
+
+
+class GridBounds(C.Structure):
+    _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float)]
+
+
+class FeatureVectorC(C.Structure):
+    _fields_ = [("nodes", C.c_void_p), ("off", C.c_void_p), ("idx", C.c_void_p), ("n_nodes", C.c_int)]
+
+
+class OrbxError(RuntimeError):
+    """Raised for any non-zero status (the reference throws std::runtime_error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"orbx error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OrbxError(ORBX_EDEVICE, f"{LIB_PATH} not built; run __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        L.orbx_last_error.restype = C.c_char_p
+        L.orbm_last_error.restype = C.c_char_p
+        L.orbx_version.restype = C.c_char_p
+        L.orbx_create.argtypes = [C.POINTER(OrbxConfig), C.POINTER(C.c_void_p)]
+        for name in ("orbx_destroy", "orbx_frame_capacity"):
+            getattr(L, name).argtypes = [C.c_void_p]
+        L.orbx_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p,
+                                   C.c_int, C.c_void_p, C.POINTER(C.c_int)]
+        L.orbx_extract_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_size_t, C.c_size_t,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orbx_get_scales.argtypes = [C.c_void_p] + [C.c_void_p] * 4
+        L.orbx_get_levels_info.argtypes = [C.c_void_p] + [C.c_void_p] * 4
+        L.orbx_get_level.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t]
+        L.orbx_get_fast_candidates.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                               C.POINTER(C.c_int)]
+        L.orbx_get_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+        L.orbm_create.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+        L.orbm_destroy.argtypes = [C.c_void_p]
+        L.orbm_descriptor_distance.argtypes = [C.c_void_p, C.c_void_p]
+        L.orbm_hamming_top2.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int,
+                                        C.c_void_p, C.c_size_t, C.c_void_p, C.c_int, C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orbm_search_for_initialization.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, GridBounds,
+            C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.POINTER(C.c_int)]
+        L.orbm_search_for_initialization_batch.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+            C.c_int, GridBounds, C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p,
+            C.c_void_p]
+        L.orbm_search_by_bow.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, FeatureVectorC, C.c_void_p,
+            C.c_void_p, C.c_void_p, C.c_int, FeatureVectorC, C.c_float, C.c_int, C.c_int, C.c_void_p,
+            C.POINTER(C.c_int)]
+        L.orbx_device_count.argtypes = [C.POINTER(C.c_int)]
+        L.orbx_set_device.argtypes = [C.c_int]
+        L.orbx_malloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        L.orbx_free.argtypes = [C.c_void_p]
+        L.orbx_memcpy_htod.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.orbx_memcpy_dtoh.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.orbx_memset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+        L.orbx_stream_create.argtypes = [C.POINTER(C.c_void_p)]
+        L.orbx_stream_destroy.argtypes = [C.c_void_p]
+        L.orbx_stream_synchronize.argtypes = [C.c_void_p]
+        L.orbx_event_create.argtypes = [C.POINTER(C.c_void_p)]
+        L.orbx_event_destroy.argtypes = [C.c_void_p]
+        L.orbx_event_record.argtypes = [C.c_void_p, C.c_void_p]
+        L.orbx_event_elapsed_ms.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]
+        _lib = L
+    return _lib
+
+
+def check(rc: int, matcher: bool = False) -> None:
+    if rc != ORBX_OK:
+        L = lib()
+        msg = (L.orbm_last_error() if matcher else L.orbx_last_error()) or b""
+        raise OrbxError(rc, msg.decode(errors="replace"))
+
+
+def header_functions(path: str = HEADER) -> list[str]:
+    """Names of every function declared in include/orbx_c.h."""
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b((?:orbx|orbm)_[a-z0-9_]+)\s*\(", src)))
+
+
+def ptr(a) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data) if a is not None else C.c_void_p(0)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().orbx_device_count(C.byref(n)))
+    return n.value
+
+
+class DeviceArray:
+    """Owning device allocation (hipMalloc through the C ABI)."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self.p = C.c_void_p(0)
+        check(lib().orbx_malloc(C.byref(self.p), max(self.nbytes, 1)))
+
+    @property
+    def ptr(self) -> int:
+        return self.p.value
+
+    def upload(self, a: np.ndarray, offset: int = 0) -> None:
+        a = np.ascontiguousarray(a)
+        assert offset + a.nbytes <= self.nbytes
+        check(lib().orbx_memcpy_htod(C.c_void_p(self.ptr + offset), ptr(a), a.nbytes))
+
+    def download(self, shape, dtype, offset: int = 0) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        assert offset + out.nbytes <= self.nbytes
+        check(lib().orbx_memcpy_dtoh(ptr(out), C.c_void_p(self.ptr + offset), out.nbytes))
+        return out
+
+    def zero(self) -> None:
+        check(lib().orbx_memset(self.p, 0, self.nbytes))
+
+    def __del__(self):
+        if getattr(self, "p", None) and self.p.value and _lib is not None:
+            _lib.orbx_free(self.p)
+            self.p = C.c_void_p(0)
+
+
+class Stream:
+    def __init__(self):
+        self.s = C.c_void_p(0)
+        check(lib().orbx_stream_create(C.byref(self.s)))
+
+    def synchronize(self) -> None:
+        check(lib().orbx_stream_synchronize(self.s))
+
+    def __del__(self):
+        if getattr(self, "s", None) and self.s.value and _lib is not None:
+            _lib.orbx_stream_destroy(self.s)
+
+
+class Event:
+    def __init__(self):
+        self.e = C.c_void_p(0)
+        check(lib().orbx_event_create(C.byref(self.e)))
+
+    def record(self, stream: Stream) -> None:
+        check(lib().orbx_event_record(self.e, stream.s))
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = C.c_float(0)
+        check(lib().orbx_event_elapsed_ms(self.e, end.e, C.byref(ms)))
+        return ms.value
+
+    def __del__(self):
+        if getattr(self, "e", None) and self.e.value and _lib is not None:
+            _lib.orbx_event_destroy(self.e)

@@ -1,0 +1,578 @@
+// orbx_host.hip — host plan + C ABI of the extractor (include/orbx_c.h).
+//
+// The constructor arithmetic of ORBextractor (src/ORBextractor.cc:496-560)
+// and the per-level geometry of ComputePyramid / ComputeKeyPointsOctTree /
+// DistributeOctTree are evaluated once per (config, frame size) on the host
+// in the same float arithmetic as the reference, and shipped to the kernels
+// as tables: resize coefficients, the FAST cell list with its slot ranges,
+// quadtree roots. Everything per frame runs on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cstdarg>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "orbx_internal.h"
+
+namespace orbx {
+size_t quadtree_lds_bytes(const ExtractParams& P);
+extern const void* quadtree_kernel_ptr();
+}  // namespace orbx
+
+using namespace orbx;
+
+static thread_local std::string g_err;
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIP_OK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return fail(ORBX_EDEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+// ------------------------------------------------------------ plan
+namespace {
+
+inline int cv_round(float v) { return (int)lrintf(v); }
+inline int cv_floor(float v) { int i = (int)v; return i - (i > v); }
+inline short sat_short(int v) { return (short)std::min(std::max(v, (int)SHRT_MIN), (int)SHRT_MAX); }
+
+struct DeviceBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  ~DeviceBuf() { if (p) (void)hipFree(p); }
+  int alloc(size_t bytes) {
+    if (p) { (void)hipFree(p); p = nullptr; }
+    n = bytes;
+    if (!bytes) return ORBX_OK;
+    if (hipMalloc(&p, bytes) != hipSuccess) return fail(ORBX_ENOMEM, "hipMalloc(%zu) failed", bytes);
+    return ORBX_OK;
+  }
+  template <class T> T* as() const { return (T*)p; }
+};
+
+struct Plan {
+  int W = 0, H = 0, B = 0;
+  ExtractParams P{};
+  std::vector<CellGeom> cells;
+  std::vector<int2> rtab;
+  DeviceBuf pyr, blur, rtab_d, cells_d, umax_d, slots, cell_counts, qkeys, qcounts, qscratch, qnscratch, err;
+};
+
+}  // namespace
+
+struct orbx_extractor {
+  orbx_config cfg{};
+  std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+  std::vector<int> nfeat;
+  int umax[16];
+  Plan plan;
+  hipStream_t stream = nullptr;
+  // staging for the synchronous API
+  DeviceBuf d_in, d_kps, d_desc, d_counts;
+  int last_batch = 0;
+  const uint8_t* last_frames = nullptr;
+  size_t last_fpitch = 0, last_rstride = 0;
+  bool timing = false;
+  hipEvent_t ev[6] = {};
+  std::mutex mu;
+};
+
+// ORBextractor::ORBextractor scalar tables (src/ORBextractor.cc:500-532) and
+// umax (:540-555); the fork's scale override (:674-680) in mode F.
+static void compute_scales(orbx_extractor* h) {
+  const orbx_config& c = h->cfg;
+  const int L = c.nlevels;
+  h->scale.assign(L, 1.f);
+  h->sigma2.assign(L, 1.f);
+  for (int i = 1; i < L; i++) {
+    h->scale[i] = h->scale[i - 1] * c.scale_factor;
+    h->sigma2[i] = h->scale[i] * h->scale[i];
+  }
+  h->inv_scale.resize(L);
+  h->inv_sigma2.resize(L);
+  for (int i = 0; i < L; i++) {
+    h->inv_scale[i] = 1.0f / h->scale[i];
+    h->inv_sigma2[i] = 1.0f / h->sigma2[i];
+  }
+  h->nfeat.assign(L, 0);
+  const float factor = 1.0f / c.scale_factor;
+  float nDesired = c.nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)L));
+  int sum = 0;
+  for (int l = 0; l < L - 1; l++) {
+    h->nfeat[l] = cv_round(nDesired);
+    sum += h->nfeat[l];
+    nDesired *= factor;
+  }
+  h->nfeat[L - 1] = std::max(c.nfeatures - sum, 0);
+  const int HP = kHalfPatch;
+  int v, v0;
+  const int vmax = cv_floor(HP * sqrtf(2.f) / 2 + 1);
+  const int vmin = (int)std::ceil(HP * sqrtf(2.f) / 2);
+  const double hp2 = HP * HP;
+  for (v = 0; v <= vmax; ++v) h->umax[v] = (int)lrint(sqrt(hp2 - v * v));
+  for (v = HP, v0 = 0; v >= vmin; --v) {
+    while (h->umax[v0] == h->umax[v0 + 1]) ++v0;
+    h->umax[v] = v0;
+    ++v0;
+  }
+  if (c.scale_mode == ORBX_SCALE_F) {
+    for (int l = 0; l < L; ++l) {
+      const unsigned vw = (unsigned)std::ceil(c.width * std::pow(0.8408964, l));
+      h->scale[l] = ((float)c.width) / vw;
+      h->inv_scale[l] = ((float)vw) / c.width;
+    }
+  }
+}
+
+// getGaussianKernel(7, 2, CV_32F) -> CV_32S x256 (the 8U smooth branch of
+// createSeparableLinearFilter): [18, 34, 49, 55, 49, 34, 18].
+static void gaussian7(int k[7]) {
+  float cf[7];
+  double sum = 0;
+  for (int i = 0; i < 7; ++i) {
+    const double x = i - 3.0;
+    cf[i] = (float)std::exp(-0.5 / (2.0 * 2.0) * x * x);
+    sum += cf[i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < 7; ++i) cf[i] = (float)(cf[i] * sum);
+  for (int i = 0; i < 7; ++i) k[i] = cv_round(cf[i] * 256.f);
+}
+
+// OpenCV 3.x INTER_LINEAR coefficient tables from (sw,sh) to (dw,dh):
+// x entries {sx, a0 | a1<<16}, y entries {sy0 | sy1<<16, b0 | b1<<16}.
+static void resize_tables(int sw, int sh, int dw, int dh, std::vector<int2>& xt, std::vector<int2>& yt,
+                          int* xmax_out, int* area2x) {
+  const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+  const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+  const int isx = (int)lrint(scale_x), isy = (int)lrint(scale_y);
+  const bool fast = std::fabs(scale_x - isx) < DBL_EPSILON && std::fabs(scale_y - isy) < DBL_EPSILON;
+  *area2x = (fast && isx == 2 && isy == 2) ? 1 : 0;
+  xt.resize(dw);
+  yt.resize(dh);
+  int xmax = dw;
+  for (int dx = 0; dx < dw; ++dx) {
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = cv_floor(fx);
+    fx -= sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx + 1 >= sw) {
+      xmax = std::min(xmax, dx);
+      if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+    }
+    const int a0 = sat_short(cv_round((1.f - fx) * 2048)), a1 = sat_short(cv_round(fx * 2048));
+    xt[dx] = make_int2(sx, (a0 & 0xFFFF) | (a1 << 16));
+  }
+  *xmax_out = xmax;
+  auto clip = [](int x, int a, int b) { return x >= a ? (x < b ? x : b - 1) : a; };
+  for (int dy = 0; dy < dh; ++dy) {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = cv_floor(fy);
+    fy -= sy;
+    const int b0 = sat_short(cv_round((1.f - fy) * 2048)), b1 = sat_short(cv_round(fy * 2048));
+    yt[dy] = make_int2(clip(sy, 0, sh) | (clip(sy + 1, 0, sh) << 16), (b0 & 0xFFFF) | (b1 << 16));
+  }
+}
+
+static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
+  Plan& pl = h->plan;
+  const orbx_config& c = h->cfg;
+  const int L = c.nlevels;
+  ExtractParams P{};
+  P.L = L;
+  P.B = B;
+  const int ini = std::min(std::max(c.ini_th_fast, 0), 255), mn = std::min(std::max(c.min_th_fast, 0), 255);
+  P.t_ini = ini;
+  P.t_min = mn;
+  P.t_low = std::min(ini, mn);
+  P.pattern_upstream = c.pattern_mode == ORBX_PATTERN_UPSTREAM;
+  gaussian7(P.gauss);
+  pl.cells.clear();
+  pl.rtab.clear();
+  long long lvl_off = 0;  // level planes [l][B][h][pitch], same offsets in pyramid and blur
+  int slot = 0, kbase = 0, maxnodes = 0, maxcells = 0;
+  for (int l = 0; l < L; ++l) {
+    LevelGeom& g = P.lv[l];
+    const float inv = h->inv_scale[l];
+    g.w = cv_round((float)W * inv);
+    g.h = cv_round((float)Hh * inv);
+    if (g.w > kMaxLevelDim || g.h > kMaxLevelDim)
+      return fail(ORBX_EINVAL, "level %d is %dx%d; at most %d px per side", l, g.w, g.h, kMaxLevelDim);
+    g.pitch = (g.w + 63) & ~63;
+    g.plane = (long long)g.h * g.pitch;
+    // FAST grid (src/ORBextractor.cc:1133-1147)
+    g.minBX = kEdgeThreshold - 3;
+    g.minBY = g.minBX;
+    g.maxBX = g.w - kEdgeThreshold + 3;
+    g.maxBY = g.h - kEdgeThreshold + 3;
+    const float width = (float)(g.maxBX - g.minBX), height = (float)(g.maxBY - g.minBY);
+    g.nCols = (int)(width / kGridW);
+    g.nRows = (int)(height / kGridW);
+    if (g.nCols < 1 || g.nRows < 1)
+      return fail(ORBX_EINVAL,
+                  "level %d (%dx%d) is smaller than one %d-px FAST cell inside the %d-px border; "
+                  "the reference divides by zero here (src/ORBextractor.cc:1144-1147)",
+                  l, g.w, g.h, kGridW, kEdgeThreshold);
+    g.wCell = (int)std::ceil(width / g.nCols);
+    g.hCell = (int)std::ceil(height / g.nRows);
+    if (g.wCell + 6 > kMaxRoi - 1 || g.hCell + 6 > kMaxRoi - 1)
+      return fail(ORBX_EINVAL, "level %d cell %dx%d exceeds the ROI tile", l, g.wCell, g.hCell);
+    g.cell0 = (int)pl.cells.size();
+    g.slot0 = slot;
+    for (int i = 0; i < g.nRows; i++) {
+      const float iniY = g.minBY + i * g.hCell;
+      float maxY = iniY + g.hCell + 6;
+      const bool skipRow = iniY >= g.maxBY - 3;
+      if (maxY > g.maxBY) maxY = g.maxBY;
+      for (int j = 0; j < g.nCols; j++) {
+        const float iniX = g.minBX + j * g.wCell;
+        float maxX = iniX + g.wCell + 6;
+        const bool skip = skipRow || iniX >= g.maxBX - 6;
+        if (maxX > g.maxBX) maxX = g.maxBX;
+        CellGeom cg{};
+        cg.level = (int16_t)l;
+        cg.c0 = (int16_t)(int)iniX;
+        cg.r0 = (int16_t)(int)iniY;
+        cg.c1 = (int16_t)(int)maxX;
+        cg.r1 = (int16_t)(int)maxY;
+        const int bw = cg.c1 - cg.c0 - 6, bh = cg.r1 - cg.r0 - 6;
+        cg.cap = (skip || bw <= 0 || bh <= 0) ? 0 : (int16_t)(((bw + 1) / 2) * ((bh + 1) / 2));
+        cg.slot_off = slot;
+        slot += cg.cap;
+        pl.cells.push_back(cg);
+      }
+    }
+    g.ncells = (int)pl.cells.size() - g.cell0;
+    g.nslots = slot - g.slot0;
+    maxcells = std::max(maxcells, g.ncells);
+    // DistributeOctTree (src/ORBextractor.cc:894-898)
+    g.N = h->nfeat[l];
+    g.boxW = g.maxBX - g.minBX;
+    g.boxH = g.maxBY - g.minBY;
+    g.nIni = (int)roundf(static_cast<float>(g.boxW) / g.boxH);
+    if (g.nIni < 1) return fail(ORBX_EINVAL, "level %d: nIni = 0 (image taller than 1.5x its width)", l);
+    g.hX = static_cast<float>(g.boxW) / g.nIni;
+    g.kcap = std::max(g.N + 3, g.nIni);
+    g.kbase = kbase;
+    kbase += g.kcap;
+    maxnodes = std::max(maxnodes, g.kcap + 4);
+    g.scale = h->scale[l];
+    g.size = (float)(int)(kPatchSize * h->scale[l]);
+    g.off = lvl_off;
+    lvl_off += (long long)B * g.plane;
+    if (l >= 1) {
+      std::vector<int2> xt, yt;
+      resize_tables(P.lv[l - 1].w, P.lv[l - 1].h, g.w, g.h, xt, yt, &g.xmax, &g.area2x);
+      g.xtab = (int)pl.rtab.size();
+      pl.rtab.insert(pl.rtab.end(), xt.begin(), xt.end());
+      g.ytab = (int)pl.rtab.size();
+      pl.rtab.insert(pl.rtab.end(), yt.begin(), yt.end());
+    }
+  }
+  if (maxnodes > 65000) return fail(ORBX_EINVAL, "nfeatures too large for the quadtree node table");
+  P.slots_per_frame = slot;
+  P.ncells_total = (int)pl.cells.size();
+  P.kp_per_frame = kbase;
+  P.maxnodes = maxnodes;
+  int sn = 1;
+  while (sn < maxnodes) sn <<= 1;
+  P.sortn = sn;
+  P.max_cells_level = maxcells;
+  P.kcap_lds = 0;
+  {
+    // keep the LDS footprint near 64 KiB so two quadtree blocks fit one CU
+    const size_t base = quadtree_lds_bytes(P);
+    const size_t budget = 64 * 1024;
+    P.kcap_lds = base < budget ? (int)((budget - base) / 6) & ~15 : 0;
+  }
+  pl.P = P;
+  pl.W = W;
+  pl.H = Hh;
+  pl.B = B;
+  // device buffers (the pyramid's level-0 planes stay unused: level 0 is the caller's frames)
+  int rc;
+  if ((rc = pl.pyr.alloc((size_t)lvl_off))) return rc;
+  if ((rc = pl.blur.alloc((size_t)lvl_off))) return rc;
+  if ((rc = pl.rtab_d.alloc(std::max<size_t>(pl.rtab.size(), 1) * sizeof(int2)))) return rc;
+  if ((rc = pl.cells_d.alloc(pl.cells.size() * sizeof(CellGeom)))) return rc;
+  if ((rc = pl.umax_d.alloc(16 * sizeof(int)))) return rc;
+  if ((rc = pl.slots.alloc((size_t)B * slot * 4 + 4))) return rc;
+  if ((rc = pl.cell_counts.alloc((size_t)B * P.ncells_total * 4))) return rc;
+  if ((rc = pl.qkeys.alloc((size_t)B * P.kp_per_frame * 4))) return rc;
+  if ((rc = pl.qcounts.alloc((size_t)B * L * 4))) return rc;
+  if ((rc = pl.qscratch.alloc((size_t)B * slot * 4 + 4))) return rc;
+  if ((rc = pl.qnscratch.alloc((size_t)B * slot * 2 + 4))) return rc;
+  if ((rc = pl.err.alloc(16))) return rc;
+  HIP_OK(hipMemcpy(pl.rtab_d.p, pl.rtab.data(), pl.rtab.size() * sizeof(int2), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(pl.cells_d.p, pl.cells.data(), pl.cells.size() * sizeof(CellGeom), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(pl.umax_d.p, h->umax, 16 * sizeof(int), hipMemcpyHostToDevice));
+  HIP_OK(hipMemset(pl.err.p, 0, 16));
+  HIP_OK(hipFuncSetAttribute(quadtree_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)quadtree_lds_bytes(P)));
+  return ORBX_OK;
+}
+
+static ExtractBuffers buffers_of(const Plan& pl) {
+  ExtractBuffers X;
+  X.pyr = pl.pyr.as<uint8_t>();
+  X.blur = pl.blur.as<uint8_t>();
+  X.rtab = pl.rtab_d.as<int2>();
+  X.cells = pl.cells_d.as<CellGeom>();
+  X.umax = pl.umax_d.as<int>();
+  X.slots = pl.slots.as<uint32_t>();
+  X.cell_counts = pl.cell_counts.as<int>();
+  X.qkeys = pl.qkeys.as<uint32_t>();
+  X.qcounts = pl.qcounts.as<int>();
+  X.qscratch = pl.qscratch.as<uint32_t>();
+  X.qnode_scratch = pl.qnscratch.as<uint16_t>();
+  X.qscratch_per_fl = 0;
+  X.err = pl.err.as<int>();
+  return X;
+}
+
+// ------------------------------------------------------------ C ABI
+extern "C" {
+
+const char* orbx_last_error(void) { return g_err.c_str(); }
+const char* orbx_version(void) { return "orbx 0.1 (gfx950)"; }
+
+int orbx_create(const orbx_config* cfg, orbx_handle* out) {
+  if (!cfg || !out) return fail(ORBX_EINVAL, "null argument");
+  *out = nullptr;
+  const orbx_config& c = *cfg;
+  if (c.nlevels < 1 || c.nlevels > kMaxLevels) return fail(ORBX_EINVAL, "nlevels must be 1..%d", kMaxLevels);
+  if (c.nfeatures < 0) return fail(ORBX_EINVAL, "nfeatures < 0");
+  if (!(c.scale_factor > 1.0f)) return fail(ORBX_EINVAL, "scaleFactor must be > 1");
+  if (c.width <= 0 || c.height <= 0) return fail(ORBX_EINVAL, "width/height must be > 0 (Camera.width/height)");
+  if (c.max_batch < 1) return fail(ORBX_EINVAL, "max_batch must be >= 1");
+  if (c.scale_mode != ORBX_SCALE_U && c.scale_mode != ORBX_SCALE_F) return fail(ORBX_EINVAL, "bad scale_mode");
+  if (c.pattern_mode != ORBX_PATTERN_FORK && c.pattern_mode != ORBX_PATTERN_UPSTREAM)
+    return fail(ORBX_EINVAL, "bad pattern_mode");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(ORBX_EDEVICE, "no HIP device");
+  if (c.device < 0 || c.device >= ndev) return fail(ORBX_EINVAL, "device %d out of range", c.device);
+  HIP_OK(hipSetDevice(c.device));
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, c.device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(ORBX_EDEVICE, "device %d is %s; liborbx is built for gfx950 only", c.device, prop.gcnArchName);
+  orbx_extractor* h = new orbx_extractor();
+  h->cfg = c;
+  compute_scales(h);
+  int rc = build_plan(h, c.width, c.height, c.max_batch);
+  if (rc) { delete h; return rc; }
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return fail(ORBX_EDEVICE, "hipStreamCreate failed");
+  }
+  const char* t = getenv("ORBX_TIMING");
+  h->timing = t && t[0] == '1';
+  if (h->timing)
+    for (auto& e : h->ev) (void)hipEventCreate(&e);
+  *out = h;
+  return ORBX_OK;
+}
+
+int orbx_destroy(orbx_handle h) {
+  if (!h) return ORBX_OK;
+  (void)hipSetDevice(h->cfg.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return ORBX_OK;
+}
+
+int orbx_frame_capacity(orbx_handle h) { return h ? h->plan.P.kp_per_frame : 0; }
+
+int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch, size_t frame_pitch, size_t row_stride,
+                       orbx_kp* d_kps, uint8_t* d_desc, int* d_counts, void* stream) {
+  if (!h || !d_frames || !d_kps || !d_desc || !d_counts) return fail(ORBX_EINVAL, "null argument");
+  if (batch < 1 || batch > h->plan.B) return fail(ORBX_EINVAL, "batch %d not in 1..max_batch(%d)", batch, h->plan.B);
+  if (row_stride < (size_t)h->plan.W) return fail(ORBX_EINVAL, "row_stride < width");
+  HIP_OK(hipSetDevice(h->cfg.device));
+  const int rc = launch_extract(h->plan.P, buffers_of(h->plan), d_frames, batch, frame_pitch, row_stride, d_kps,
+                                d_desc, d_counts, stream ? stream : (void*)h->stream,
+                                h->timing ? (void**)h->ev : nullptr);
+  h->last_batch = batch;
+  h->last_frames = d_frames;
+  h->last_fpitch = frame_pitch;
+  h->last_rstride = row_stride;
+  if (rc) return fail(rc, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return ORBX_OK;
+}
+
+int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride, orbx_kp* kps, int cap,
+                 uint8_t* desc, int* n) {
+  if (!h || !n) return fail(ORBX_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  *n = 0;
+  if (w == 0 || hh == 0) return ORBX_OK;  // src/ORBextractor.cc:1542-1543
+  if (!img || w < 0 || hh < 0 || stride < (size_t)w) return fail(ORBX_EINVAL, "bad image");
+  HIP_OK(hipSetDevice(h->cfg.device));
+  if (w != h->plan.W || hh != h->plan.H) {
+    // the reference accepts any image size per call: re-plan for it
+    (void)hipStreamSynchronize(h->stream);
+    const int rc = build_plan(h, w, hh, h->plan.B);
+    if (rc) return rc;
+    h->d_in.alloc(0);
+  }
+  const int cap_frame = h->plan.P.kp_per_frame;
+  const size_t pitch = ((size_t)w + 63) & ~(size_t)63;
+  int rc;
+  if (h->d_in.n < pitch * hh && (rc = h->d_in.alloc(pitch * hh))) return rc;
+  if (h->d_kps.n < (size_t)cap_frame * sizeof(orbx_kp) && (rc = h->d_kps.alloc((size_t)cap_frame * sizeof(orbx_kp))))
+    return rc;
+  if (h->d_desc.n < (size_t)cap_frame * 32 && (rc = h->d_desc.alloc((size_t)cap_frame * 32))) return rc;
+  if (h->d_counts.n < 4 && (rc = h->d_counts.alloc(4))) return rc;
+  HIP_OK(hipMemcpy2DAsync(h->d_in.p, pitch, img, stride, w, hh, hipMemcpyHostToDevice, h->stream));
+  rc = orbx_extract_batch(h, h->d_in.as<uint8_t>(), 1, pitch * hh, pitch, h->d_kps.as<orbx_kp>(),
+                          h->d_desc.as<uint8_t>(), h->d_counts.as<int>(), h->stream);
+  if (rc) return rc;
+  int cnt = 0, err = 0;
+  HIP_OK(hipMemcpyAsync(&cnt, h->d_counts.p, 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipMemcpyAsync(&err, h->plan.err.p, 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  if (err) return fail(ORBX_ECAPACITY, "device error word 0x%x", err);
+  *n = cnt;
+  if (cnt > cap) return fail(ORBX_ECAPACITY, "%d keypoints do not fit cap %d", cnt, cap);
+  if (kps) HIP_OK(hipMemcpy(kps, h->d_kps.p, (size_t)cnt * sizeof(orbx_kp), hipMemcpyDeviceToHost));
+  if (desc) HIP_OK(hipMemcpy(desc, h->d_desc.p, (size_t)cnt * 32, hipMemcpyDeviceToHost));
+  return ORBX_OK;
+}
+
+int orbx_get_scales(orbx_handle h, float* s, float* is, float* s2, float* is2) {
+  if (!h) return fail(ORBX_EINVAL, "null handle");
+  const int L = h->cfg.nlevels;
+  for (int l = 0; l < L; ++l) {
+    if (s) s[l] = h->scale[l];
+    if (is) is[l] = h->inv_scale[l];
+    if (s2) s2[l] = h->sigma2[l];
+    if (is2) is2[l] = h->inv_sigma2[l];
+  }
+  return ORBX_OK;
+}
+
+int orbx_get_levels_info(orbx_handle h, int* nlevels, int* lw, int* lh, int* nf) {
+  if (!h) return fail(ORBX_EINVAL, "null handle");
+  const ExtractParams& P = h->plan.P;
+  if (nlevels) *nlevels = P.L;
+  for (int l = 0; l < P.L; ++l) {
+    if (lw) lw[l] = P.lv[l].w;
+    if (lh) lh[l] = P.lv[l].h;
+    if (nf) nf[l] = h->nfeat[l];
+  }
+  return ORBX_OK;
+}
+
+int orbx_get_level(orbx_handle h, int frame, int level, int blurred, uint8_t* out, size_t out_stride) {
+  if (!h || !out) return fail(ORBX_EINVAL, "null argument");
+  const Plan& pl = h->plan;
+  if (level < 0 || level >= pl.P.L || frame < 0 || frame >= h->last_batch)
+    return fail(ORBX_EINVAL, "no such frame/level");
+  HIP_OK(hipSetDevice(h->cfg.device));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  const LevelGeom& g = pl.P.lv[level];
+  const ExtractBuffers X = buffers_of(pl);
+  const uint8_t* src;
+  size_t spitch;
+  if (blurred) {
+    src = X.blur + g.off + (long long)frame * g.plane;
+    spitch = g.pitch;
+  } else if (level == 0) {
+    src = h->last_frames + (long long)frame * h->last_fpitch;
+    spitch = h->last_rstride;
+  } else {
+    src = X.pyr + g.off + (long long)frame * g.plane;
+    spitch = g.pitch;
+  }
+  HIP_OK(hipMemcpy2D(out, out_stride, src, spitch, g.w, g.h, hipMemcpyDeviceToHost));
+  return ORBX_OK;
+}
+
+int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out, int cap, int* n) {
+  if (!h || !n) return fail(ORBX_EINVAL, "null argument");
+  const Plan& pl = h->plan;
+  if (level < 0 || level >= pl.P.L || frame < 0 || frame >= h->last_batch)
+    return fail(ORBX_EINVAL, "no such frame/level");
+  HIP_OK(hipSetDevice(h->cfg.device));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  const LevelGeom& g = pl.P.lv[level];
+  std::vector<int> cnt(g.ncells);
+  std::vector<uint32_t> slots(std::max(g.nslots, 1));
+  HIP_OK(hipMemcpy(cnt.data(), pl.cell_counts.as<int>() + (size_t)frame * pl.P.ncells_total + g.cell0,
+                   g.ncells * 4, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(slots.data(), pl.slots.as<uint32_t>() + (size_t)frame * pl.P.slots_per_frame + g.slot0,
+                   (size_t)g.nslots * 4, hipMemcpyDeviceToHost));
+  int k = 0;
+  for (int c = 0; c < g.ncells; ++c) {
+    const CellGeom& cg = pl.cells[g.cell0 + c];
+    for (int i = 0; i < cnt[c]; ++i, ++k) {
+      if (k >= cap || !out) continue;
+      const uint32_t key = slots[cg.slot_off - g.slot0 + i];
+      orbx_kp kp{(float)key_x(key), (float)key_y(key), 7.f, -1.f, (float)key_score(key), 0, -1};
+      out[k] = kp;
+    }
+  }
+  *n = k;
+  return k > cap ? fail(ORBX_ECAPACITY, "cap too small") : ORBX_OK;
+}
+
+int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap, int* n) {
+  static const char* kNames[5] = {"Pyramid/Resize", "Gaussian Blur", "FAST+Grid", "Make quadtree",
+                                  "Compute angle+ORB descriptor+scale"};
+  if (!h || !n) return fail(ORBX_EINVAL, "null argument");
+  *n = 0;
+  if (!h->timing) return ORBX_OK;
+  HIP_OK(hipEventSynchronize(h->ev[5]));
+  for (int i = 0; i < 5 && i < cap; ++i) {
+    float t = 0;
+    HIP_OK(hipEventElapsedTime(&t, h->ev[i], h->ev[i + 1]));
+    if (ms) ms[i] = t;
+    if (names) names[i] = kNames[i];
+    *n = i + 1;
+  }
+  return ORBX_OK;
+}
+
+// ---------------------------------------------------------- plumbing
+int orbx_device_count(int* n) {
+  if (!n) return fail(ORBX_EINVAL, "null");
+  HIP_OK(hipGetDeviceCount(n));
+  return ORBX_OK;
+}
+int orbx_set_device(int d) { HIP_OK(hipSetDevice(d)); return ORBX_OK; }
+int orbx_malloc(void** p, size_t b) { HIP_OK(hipMalloc(p, b)); return ORBX_OK; }
+int orbx_free(void* p) { HIP_OK(hipFree(p)); return ORBX_OK; }
+int orbx_memcpy_htod(void* d, const void* s, size_t b) { HIP_OK(hipMemcpy(d, s, b, hipMemcpyHostToDevice)); return ORBX_OK; }
+int orbx_memcpy_dtoh(void* d, const void* s, size_t b) { HIP_OK(hipMemcpy(d, s, b, hipMemcpyDeviceToHost)); return ORBX_OK; }
+int orbx_memset(void* d, int v, size_t b) { HIP_OK(hipMemset(d, v, b)); return ORBX_OK; }
+int orbx_stream_create(void** s) { HIP_OK(hipStreamCreateWithFlags((hipStream_t*)s, hipStreamNonBlocking)); return ORBX_OK; }
+int orbx_stream_destroy(void* s) { HIP_OK(hipStreamDestroy((hipStream_t)s)); return ORBX_OK; }
+int orbx_stream_synchronize(void* s) { HIP_OK(hipStreamSynchronize((hipStream_t)s)); return ORBX_OK; }
+int orbx_event_create(void** e) { HIP_OK(hipEventCreate((hipEvent_t*)e)); return ORBX_OK; }
+int orbx_event_destroy(void* e) { HIP_OK(hipEventDestroy((hipEvent_t)e)); return ORBX_OK; }
+int orbx_event_record(void* e, void* s) { HIP_OK(hipEventRecord((hipEvent_t)e, (hipStream_t)s)); return ORBX_OK; }
+int orbx_event_elapsed_ms(void* a, void* b, float* ms) {
+  HIP_OK(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
+  return ORBX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+// orbx_internal.h — device/host shared layout of the MI355X ORB front-end.
+//
+// Memory layout in HBM (one extractor handle, B = max_batch frames):
+//   level 0          : the caller's frames (read in place, never copied)
+//   pyramid levels>=1: level-major planes  [l][B][h_l][pitch_l]   u8
+//   blurred levels   : level-major planes  [l][B][h_l][pitch_l]   u8
+//   FAST key slots   : [B][slots_per_frame]  u32 packed (x|y<<12|score<<24),
+//                      one fixed slot range per grid cell (cap = NMS bound)
+//   cell counts      : [B][ncells_total]     i32
+//   quadtree keys    : [B][kp_per_frame]     u32 packed, level-major slots
+//   quadtree counts  : [B][L]                i32
+//   outputs          : caller's [B][cap] orbx_kp + [B][cap][32] u8 + [B] i32
+#pragma once
+#include <stdint.h>
+
+#include "../../include/orbx_c.h"
+
+namespace orbx {
+
+constexpr int kMaxLevels = 16;
+constexpr int kEdgeThreshold = 19;      // EDGE_THRESHOLD  src/ORBextractor.cc:97
+constexpr int kPatchSize = 31;          // PATCH_SIZE      src/ORBextractor.cc:95
+constexpr int kHalfPatch = 15;          // HALF_PATCH_SIZE src/ORBextractor.cc:96
+constexpr int kGridW = 30;              // W               src/ORBextractor.cc:1126
+constexpr int kMaxRoi = 66;             // largest FAST cell ROI side (+6 halo)
+constexpr int kMaxLevelDim = 4096;      // packed key coordinates are 12 bits
+constexpr int kQtThreads = 256;
+
+struct LevelGeom {
+  int w, h, pitch, pad0;
+  long long plane;   // bytes of one frame's plane (h * pitch)
+  long long off;     // byte offset of this level's planes in the pyramid / blur buffers
+  // INTER_LINEAR resize from level l-1 (l >= 1): offsets into the resize table
+  int xtab, ytab, xmax, area2x;
+  // FAST grid (ComputeKeyPointsOctTree src/ORBextractor.cc:1133-1147)
+  int minBX, minBY, maxBX, maxBY;
+  int nCols, nRows, wCell, hCell;
+  int cell0, ncells;     // range in the cell table
+  int slot0, nslots;     // key-slot range of this level inside a frame's slots
+  // DistributeOctTree (src/ORBextractor.cc:889-898)
+  int N, nIni, boxW, boxH;
+  float hX;
+  int kcap, kbase;       // quadtree output slots of this level inside a frame
+  float scale;           // mvScaleFactor[l]
+  float size;            // (float)(int)(PATCH_SIZE * mvScaleFactor[l])
+  int pad1;
+};
+
+struct CellGeom {
+  int16_t c0, r0, c1, r1;  // ROI [c0,c1) x [r0,r1) in level coordinates
+  int slot_off;            // first key slot (frame-relative)
+  int16_t cap, level;      // slot capacity (0 = cell skipped by the reference)
+};
+
+struct ExtractParams {
+  int L, B;
+  int t_low, t_ini, t_min;
+  int slots_per_frame, ncells_total;
+  int kp_per_frame;            // == output capacity per frame
+  int maxnodes, sortn;         // quadtree node-table size, bitonic size (pow2)
+  int max_cells_level;         // largest ncells of any level
+  int kcap_lds;                // quadtree keys kept in LDS up to this count
+  int pattern_upstream;
+  int gauss[7];                // 7-tap Gaussian fixed-point kernel (sum 257)
+  LevelGeom lv[kMaxLevels];
+};
+
+// Pointers to level data for one launch. Level 0 is the caller's frames.
+struct LevelPtrs {
+  const uint8_t* base[kMaxLevels];
+  long long fstride[kMaxLevels];  // bytes between frames
+  int pitch[kMaxLevels];          // bytes between rows
+};
+
+__host__ __device__ inline uint32_t pack_key(int x, int y, int score) {
+  return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)score << 24);
+}
+__host__ __device__ inline int key_x(uint32_t k) { return (int)(k & 0xFFFu); }
+__host__ __device__ inline int key_y(uint32_t k) { return (int)((k >> 12) & 0xFFFu); }
+__host__ __device__ inline int key_score(uint32_t k) { return (int)(k >> 24); }
+
+// ------------------------------------------------------------ launchers
+// (implemented in orbx_extract.hip; all asynchronous on `stream`)
+struct ExtractBuffers {
+  uint8_t* pyr;        // levels >= 1
+  uint8_t* blur;       // all levels
+  const int2* rtab;    // resize tables
+  const CellGeom* cells;
+  const int* umax;     // 16 ints
+  uint32_t* slots;
+  int* cell_counts;
+  uint32_t* qkeys;
+  int* qcounts;
+  uint32_t* qscratch;  // global fallback for quadtree keys (K > kcap_lds)
+  uint16_t* qnode_scratch;
+  long long qscratch_per_fl;  // entries per (frame, level)
+  int* err;            // device error word
+};
+
+int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames,
+                   int batch, size_t frame_pitch, size_t row_stride, orbx_kp* d_kps,
+                   uint8_t* d_desc, int* d_counts, void* stream, void** stage_events);
+
+// orbx_match.hip
+struct MatchBuffers {
+  uint32_t* cand;       // candidate (i2 | dist << 24) per pair
+  long long cand_cap;   // entries per pair
+  int* cand_off;        // per pair x kp_cap
+  int* err;
+};
+int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap,
+                        const uint8_t* B, size_t b_pitch, const int* nB, int pairs, int* best_idx,
+                        int* best, int* second, void* stream);
+int launch_search_init(const MatchBuffers& M, const orbx_kp* kp1, const uint8_t* desc1,
+                       const int* n1, const orbx_kp* kp2, const uint8_t* desc2, const int* n2,
+                       int kp_pitch, int pairs, orbm_grid_bounds b, float* prev_xy, int window,
+                       float nnratio, int check_ori, int* matches12, int* nmatches, void* stream);
+int launch_search_bow(const uint8_t* descA, const float* angleA, const uint8_t* mpA, int nA,
+                      const uint32_t* nodesA, const int* offA, const int* idxA, int nnA,
+                      const uint8_t* descB, const float* angleB, const uint8_t* mpB, int nB,
+                      const uint32_t* nodesB, const int* offB, const int* idxB, int nnB,
+                      float nnratio, int check_ori, int kf_vs_kf, int* out, int* nmatches,
+                      int* scratch, void* stream);
+
+}  // namespace orbx

@@ -1,0 +1,856 @@
+// orbx_match.hip — Hamming matchers of ORBmatcher for gfx950.
+//
+//   hamming_top2_kernel   dense best/second search (the inner loop shared by
+//                         every ORBmatcher search), lane-per-query, candidate
+//                         rows broadcast from LDS, 4 x v_bcnt per pair
+//   search_init_kernel    SearchForInitialization   src/ORBmatcher.cc:405-520
+//                         + Frame::AssignFeaturesToGrid / GetFeaturesInArea
+//                         src/Frame.cc:229-244, 326-391
+//   search_bow_kernel     SearchByBoW (KF-F :159-288, KF-KF :522-655)
+//
+// The reference resolves matches greedily in a fixed order (a later query can
+// steal a frame feature from an earlier one, SearchForInitialization
+// :444-445,463-470; matched features drop out of SearchByBoW :205-210). The
+// kernels keep that order exactly: candidate lists and all 256-bit distances
+// are computed in parallel, the order-dependent resolution runs as one
+// wavefront walking the queries in reference order with the per-query
+// best/second reduction done across lanes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "orbx_internal.h"
+
+namespace orbx {
+
+constexpr int kGridCols = 64;  // FRAME_GRID_COLS include/Frame.h:38
+constexpr int kGridRows = 48;  // FRAME_GRID_ROWS include/Frame.h:37
+constexpr int kHistoLength = 30;
+constexpr int kThLow = 50;
+
+__device__ __forceinline__ int hamming256(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// ------------------------------------------------------------ dense top-2
+constexpr int kTopChunk = 256;
+__global__ __launch_bounds__(256) void hamming_top2_kernel(const uint8_t* __restrict__ A, long long a_pitch,
+                                                           const int* __restrict__ nA, int a_cap,
+                                                           const uint8_t* __restrict__ B, long long b_pitch,
+                                                           const int* __restrict__ nB, int* __restrict__ best_idx,
+                                                           int* __restrict__ best, int* __restrict__ second) {
+  __shared__ uint4 sB[kTopChunk][2];
+  const int p = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int na = nA[p], nb = nB[p];
+  if (blockIdx.x * 256 >= na) return;
+  const uint4* Ap = (const uint4*)(A + p * a_pitch);
+  const uint4* Bp = (const uint4*)(B + p * b_pitch);
+  uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+  if (i < na) {
+    a0 = Ap[2 * i];
+    a1 = Ap[2 * i + 1];
+  }
+  int b1d = 256, b2d = 256, bi = -1;
+  for (int j0 = 0; j0 < nb; j0 += kTopChunk) {
+    const int n = min(kTopChunk, nb - j0);
+    __syncthreads();
+    if (threadIdx.x < n) {
+      sB[threadIdx.x][0] = Bp[2 * (j0 + threadIdx.x)];
+      sB[threadIdx.x][1] = Bp[2 * (j0 + threadIdx.x) + 1];
+    }
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+      const int d = hamming256(a0, a1, sB[j][0], sB[j][1]);
+      if (d < b1d) {
+        b2d = b1d;
+        b1d = d;
+        bi = j0 + j;
+      } else if (d < b2d) {
+        b2d = d;
+      }
+    }
+  }
+  if (i < na) {
+    const long long o = (long long)p * a_cap + i;
+    best_idx[o] = bi;
+    best[o] = b1d;
+    second[o] = b2d;
+  }
+}
+
+// ------------------------------------------------------------ wave helpers
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// best / second of the multiset of valid distances, first position wins ties
+// (the sequential "if(d<best){second=best;best=d;idx=i} else if(d<second)"
+// loop computes exactly this). Returns wave-uniform values.
+struct Top2 {
+  int best, pos, second;
+};
+__device__ __forceinline__ Top2 wave_top2(bool valid, int dist, int pos) {
+  const int BIG = INT_MAX;
+  const int d = valid ? dist : BIG;
+  const int b = wave_min(d);
+  const uint64_t eq = __ballot(valid && d == b);
+  Top2 r;
+  r.best = b;
+  if (eq == 0) {
+    r.pos = -1;
+    r.second = BIG;
+    return r;
+  }
+  const int first_lane = __ffsll((long long)eq) - 1;
+  r.pos = __shfl(pos, first_lane, 64);
+  if (__popcll(eq) >= 2) {
+    r.second = b;
+  } else {
+    const int lane = threadIdx.x & 63;
+    r.second = wave_min(lane == first_lane ? BIG : d);
+  }
+  return r;
+}
+
+// ------------------------------------------------------------ SearchForInitialization
+struct InitParams {
+  float minX, maxX, minY, maxY, invW, invH;
+  float r;  // windowSize
+  float nnratio;
+  int check_ori;
+  int kp_pitch;
+  int sortn;       // pow2 >= kp_pitch
+  long long cand_cap;
+};
+
+// Frame::PosInGrid (src/Frame.cc:381-391)
+__device__ __forceinline__ bool pos_in_grid(float x, float y, const InitParams& P, int* gx, int* gy) {
+  const int px = (int)roundf(__fmul_rn(__fsub_rn(x, P.minX), P.invW));
+  const int py = (int)roundf(__fmul_rn(__fsub_rn(y, P.minY), P.invH));
+  *gx = px;
+  *gy = py;
+  return !(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows);
+}
+
+__device__ int block_scan_excl256(int* a, int n, int* s_tmp) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int per = (n + 255) / 256;
+  const int b = min(tid * per, n), e = min(b + per, n);
+  int sum = 0;
+  for (int i = b; i < e; ++i) sum += a[i];
+  int x = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_tmp[w] = x;
+  __syncthreads();
+  int wpre = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = s_tmp[i];
+    if (i < w) wpre += v;
+    total += v;
+  }
+  int run = wpre + x - sum;
+  for (int i = b; i < e; ++i) {
+    const int v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+__global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const orbx_kp* __restrict__ kp1_all,
+                                                          const uint8_t* __restrict__ desc1_all,
+                                                          const int* __restrict__ n1_all,
+                                                          const orbx_kp* __restrict__ kp2_all,
+                                                          const uint8_t* __restrict__ desc2_all,
+                                                          const int* __restrict__ n2_all, float* __restrict__ prev_all,
+                                                          uint32_t* __restrict__ cand_all, int* __restrict__ coff_all,
+                                                          int* __restrict__ matches_all, int* __restrict__ nmatches,
+                                                          int* err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n1 = n1_all[pr], n2 = n2_all[pr];
+  const orbx_kp* kp1 = kp1_all + (long long)pr * P.kp_pitch;
+  const orbx_kp* kp2 = kp2_all + (long long)pr * P.kp_pitch;
+  const uint8_t* desc1 = desc1_all + (long long)pr * P.kp_pitch * 32;
+  const uint8_t* desc2 = desc2_all + (long long)pr * P.kp_pitch * 32;
+  float* prev = prev_all + (long long)pr * P.kp_pitch * 2;
+  int* m12 = matches_all + (long long)pr * P.kp_pitch;
+  int* coff = coff_all + (long long)pr * (P.kp_pitch + 1);
+  uint32_t* cand = cand_all + (long long)pr * P.cand_cap;
+
+  unsigned char* sp = smem;
+  auto take = [&](size_t bytes) { unsigned char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
+  uint32_t* s_sort = (uint32_t*)take(4ull * P.sortn);
+  int* s_cell = (int*)take(4ull * (kGridCols * kGridRows + 1));  // first sorted entry of each cell
+  int* s_md = (int*)take(4ull * P.kp_pitch);                      // vMatchedDistance
+  int* s_m21 = (int*)take(4ull * P.kp_pitch);                     // vnMatches21
+  int* s_bin = (int*)take(4ull * P.kp_pitch);                     // rotation bin per i1 or -1
+  int* s_tmp = (int*)take(64);
+  int* s_var = (int*)take(64);
+  int* s_hist = (int*)take(4 * 32);
+
+  // ---- grid of F2 restricted to octave 0 (the only level SearchForInitialization asks for)
+  for (int i = tid; i < P.sortn; i += 256) {
+    uint32_t key = 0xFFFFFFFFu;
+    if (i < n2) {
+      const orbx_kp k = kp2[i];
+      int gx, gy;
+      if (k.octave == 0 && pos_in_grid(k.x, k.y, P, &gx, &gy)) key = ((uint32_t)(gx * kGridRows + gy) << 16) | (uint32_t)i;
+    }
+    s_sort[i] = key;
+  }
+  for (int i = tid; i < n2; i += 256) {
+    s_md[i] = INT_MAX;
+    s_m21[i] = -1;
+  }
+  for (int i = tid; i < n1; i += 256) {
+    s_bin[i] = -1;
+    m12[i] = -1;
+  }
+  if (tid < 32) s_hist[tid] = 0;
+  __syncthreads();
+  for (int kk = 2; kk <= P.sortn; kk <<= 1) {
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P.sortn; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint32_t a = s_sort[i], b = s_sort[ixj];
+          const bool up = (i & kk) == 0;
+          if (up ? (a > b) : (a < b)) {
+            s_sort[i] = b;
+            s_sort[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // s_cell[c] = first sorted position with cell >= c (lower bound)
+  for (int c = tid; c <= kGridCols * kGridRows; c += 256) {
+    int lo = 0, hi = P.sortn;
+    const uint32_t key = (uint32_t)c << 16;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_sort[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    s_cell[c] = lo;
+  }
+  __syncthreads();
+
+  // ---- candidate windows (Frame::GetFeaturesInArea, minLevel = maxLevel = 0)
+  auto window = [&](int i1, int* cx0, int* cx1, int* cy0, int* cy1) -> bool {
+    const float x = prev[2 * i1], y = prev[2 * i1 + 1], r = P.r;
+    const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, P.minX), r), P.invW)));
+    if (nMinCellX >= kGridCols) return false;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, P.minX), r), P.invW)));
+    if (nMaxCellX < 0) return false;
+    const int nMinCellY = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, P.minY), r), P.invH)));
+    if (nMinCellY >= kGridRows) return false;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, P.minY), r), P.invH)));
+    if (nMaxCellY < 0) return false;
+    *cx0 = nMinCellX;
+    *cx1 = nMaxCellX;
+    *cy0 = nMinCellY;
+    *cy1 = nMaxCellY;
+    return true;
+  };
+  // enumerate candidate k (0-based, reference order) of query i1 -> sorted position
+  // pass 1: counts
+  for (int i1 = wv; i1 < n1; i1 += 4) {
+    int cnt = 0;
+    int cx0, cx1, cy0, cy1;
+    if (kp1[i1].octave == 0 && window(i1, &cx0, &cx1, &cy0, &cy1)) {
+      const float x = prev[2 * i1], y = prev[2 * i1 + 1];
+      for (int ix = cx0; ix <= cx1; ++ix) {
+        const int s0 = s_cell[ix * kGridRows + cy0], s1 = s_cell[ix * kGridRows + cy1 + 1];
+        for (int s = s0 + lane; s < s1; s += 64) {
+          const orbx_kp k = kp2[s_sort[s] & 0xFFFF];
+          cnt += (fabsf(__fsub_rn(k.x, x)) < P.r && fabsf(__fsub_rn(k.y, y)) < P.r) ? 1 : 0;
+        }
+      }
+    }
+    cnt = wave_sum_i(cnt);
+    if (lane == 0) coff[i1] = cnt;
+  }
+  __syncthreads();
+  if (tid == 0) coff[n1] = 0;
+  __syncthreads();
+  const int total = block_scan_excl256(coff, n1 + 1, s_tmp);
+  if (total > P.cand_cap) {
+    if (tid == 0) atomicOr(err, 8);
+    return;
+  }
+  // pass 2: fill (candidate order preserved by ballot compaction) + distances
+  for (int i1 = wv; i1 < n1; i1 += 4) {
+    int cx0, cx1, cy0, cy1;
+    if (!(kp1[i1].octave == 0 && window(i1, &cx0, &cx1, &cy0, &cy1))) continue;
+    const float x = prev[2 * i1], y = prev[2 * i1 + 1];
+    const uint4* d1 = (const uint4*)(desc1 + (long long)i1 * 32);
+    const uint4 a0 = d1[0], a1 = d1[1];
+    int base = coff[i1];
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int ix = cx0; ix <= cx1; ++ix) {
+      const int s0 = s_cell[ix * kGridRows + cy0], s1 = s_cell[ix * kGridRows + cy1 + 1];
+      for (int sb = s0; sb < s1; sb += 64) {
+        const int s = sb + lane;
+        bool ok = false;
+        int i2 = 0;
+        if (s < s1) {
+          i2 = (int)(s_sort[s] & 0xFFFF);
+          const orbx_kp k = kp2[i2];
+          ok = fabsf(__fsub_rn(k.x, x)) < P.r && fabsf(__fsub_rn(k.y, y)) < P.r;
+        }
+        const uint64_t m = __ballot(ok);
+        if (ok) {
+          const uint4* d2 = (const uint4*)(desc2 + (long long)i2 * 32);
+          const int d = hamming256(a0, a1, d2[0], d2[1]);
+          cand[base + __popcll(m & lt)] = (uint32_t)i2 | ((uint32_t)d << 23);
+        }
+        base += __popcll(m);
+      }
+    }
+  }
+  __syncthreads();
+  // pass 3: greedy resolution in i1 order (one wavefront)
+  if (wv == 0) {
+    volatile int* md = s_md;
+    volatile int* m21 = s_m21;
+    int nm = 0;
+    const float factor = 1.0f / kHistoLength;
+    for (int i1 = 0; i1 < n1; ++i1) {
+      const int c0 = coff[i1], c1 = coff[i1 + 1];
+      if (c0 == c1) continue;
+      Top2 acc{INT_MAX, -1, INT_MAX};
+      for (int cb = c0; cb < c1; cb += 64) {
+        const int c = cb + lane;
+        bool valid = false;
+        int dist = 0, i2 = -1;
+        if (c < c1) {
+          const uint32_t e = cand[c];
+          i2 = (int)(e & 0x7FFFFF);
+          dist = (int)(e >> 23);
+          valid = !(md[i2] <= dist);
+        }
+        const Top2 t = wave_top2(valid, dist, i2);
+        // merge chunk (later) into acc (earlier)
+        const int nb = min(acc.best, t.best);
+        const int npos = (acc.best <= t.best) ? acc.pos : t.pos;
+        const int nsec = min(min(max(acc.best, t.best), acc.second), t.second);
+        acc.best = nb;
+        acc.pos = npos;
+        acc.second = nsec;
+      }
+      const int bestDist = acc.best, bestDist2 = acc.second, bestIdx2 = acc.pos;
+      if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)bestDist2, P.nnratio)) {
+        if (lane == 0) {
+          const int old = m21[bestIdx2];
+          if (old >= 0) {
+            m12[old] = -1;
+            nm--;
+          }
+          m12[i1] = bestIdx2;
+          m21[bestIdx2] = i1;
+          md[bestIdx2] = bestDist;
+          nm++;
+          if (P.check_ori) {
+            float rot = __fsub_rn(kp1[i1].angle, kp2[bestIdx2].angle);
+            if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+            int bin = (int)roundf(__fmul_rn(rot, factor));
+            if (bin == kHistoLength) bin = 0;
+            s_bin[i1] = bin;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (lane == 0) s_var[0] = nm;
+  }
+  __syncthreads();
+  // rotation consistency (ComputeThreeMaxima src/ORBmatcher.cc:1601-1642)
+  if (P.check_ori) {
+    for (int i = tid; i < n1; i += 256)
+      if (s_bin[i] >= 0) atomicAdd(&s_hist[s_bin[i]], 1);
+    __syncthreads();
+    if (tid == 0) {
+      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+      for (int i = 0; i < kHistoLength; i++) {
+        const int s = s_hist[i];
+        if (s > max1) {
+          max3 = max2; max2 = max1; max1 = s;
+          ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+          max3 = max2; max2 = s;
+          ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+          max3 = s;
+          ind3 = i;
+        }
+      }
+      if (max2 < __fmul_rn(0.1f, (float)max1)) {
+        ind2 = -1;
+        ind3 = -1;
+      } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
+        ind3 = -1;
+      }
+      s_var[1] = ind1;
+      s_var[2] = ind2;
+      s_var[3] = ind3;
+      s_var[4] = 0;
+    }
+    __syncthreads();
+    const int ind1 = s_var[1], ind2 = s_var[2], ind3 = s_var[3];
+    for (int i = tid; i < n1; i += 256) {
+      const int b = s_bin[i];
+      if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
+      if (m12[i] >= 0) {
+        m12[i] = -1;
+        atomicSub(&s_var[0], 1);
+      }
+    }
+    __syncthreads();
+  }
+  // vbPrevMatched update
+  for (int i = tid; i < n1; i += 256) {
+    const int j = m12[i];
+    if (j >= 0) {
+      prev[2 * i] = kp2[j].x;
+      prev[2 * i + 1] = kp2[j].y;
+    }
+  }
+  if (tid == 0) nmatches[pr] = s_var[0];
+}
+
+// ------------------------------------------------------------ SearchByBoW
+// One block; shared vocabulary nodes are independent (DBoW2 puts every
+// feature in exactly one node), so each wave takes whole nodes and runs the
+// reference's greedy per-node loop with the best/second reduction across
+// lanes. scratch: [nnA] shared-node partner index.
+__global__ __launch_bounds__(256) void search_bow_kernel(
+    const uint8_t* __restrict__ descA, const float* __restrict__ angleA, const uint8_t* __restrict__ mpA, int nA,
+    const uint32_t* __restrict__ nodesA, const int* __restrict__ offA, const int* __restrict__ idxA, int nnA,
+    const uint8_t* __restrict__ descB, const float* __restrict__ angleB, const uint8_t* __restrict__ mpB, int nB,
+    const uint32_t* __restrict__ nodesB, const int* __restrict__ offB, const int* __restrict__ idxB, int nnB,
+    float nnratio, int check_ori, int kf_vs_kf, int* __restrict__ out, int* __restrict__ nmatches,
+    int* __restrict__ binOf /* nA or nB entries */) {
+  __shared__ int s_hist[32];
+  __shared__ int s_var[8];
+  __shared__ uint32_t s_taken_[2048];  // one bit per B feature: matched (vbMatched2 / vpMapPointMatches set)
+  volatile uint32_t* s_taken = s_taken_;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nout = kf_vs_kf ? nA : nB;
+  for (int i = tid; i < 2048; i += 256) s_taken_[i] = 0;
+  for (int i = tid; i < nout; i += 256) {
+    out[i] = -1;
+    binOf[i] = -1;
+  }
+  if (tid < 32) s_hist[tid] = 0;
+  if (tid == 0) s_var[0] = 0;
+  __syncthreads();
+  const float factor = 1.0f / kHistoLength;
+  for (int ka = wv; ka < nnA; ka += 4) {
+    // lower_bound of nodesA[ka] in nodesB
+    const uint32_t id = nodesA[ka];
+    int lo = 0, hi = nnB;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (nodesB[mid] < id) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo >= nnB || nodesB[lo] != id) continue;
+    const int kb = lo;
+    const int b0 = offB[kb], b1 = offB[kb + 1];
+    for (int pa = offA[ka]; pa < offA[ka + 1]; ++pa) {
+      const int idx1 = idxA[pa];
+      if (!mpA[idx1]) continue;
+      const uint4* d1 = (const uint4*)(descA + (long long)idx1 * 32);
+      const uint4 a0 = d1[0], a1 = d1[1];
+      Top2 acc{256, -1, 256};
+      for (int cb = b0; cb < b1; cb += 64) {
+        const int q = cb + lane;
+        bool valid = false;
+        int dist = 0, idx2 = -1;
+        if (q < b1) {
+          idx2 = idxB[q];
+          const bool taken = (s_taken[idx2 >> 5] >> (idx2 & 31)) & 1u;
+          valid = !taken && (!kf_vs_kf || mpB[idx2] != 0);
+          if (valid) {
+            const uint4* d2 = (const uint4*)(descB + (long long)idx2 * 32);
+            dist = hamming256(a0, a1, d2[0], d2[1]);
+          }
+        }
+        const Top2 t = wave_top2(valid, dist, idx2);
+        const int nb = min(acc.best, t.best);
+        const int npos = (acc.best <= t.best) ? acc.pos : t.pos;
+        const int nsec = min(min(max(acc.best, t.best), acc.second), t.second);
+        acc.best = nb;
+        acc.pos = npos;
+        acc.second = nsec;
+      }
+      const bool pass = kf_vs_kf ? (acc.best < kThLow) : (acc.best <= kThLow);
+      if (pass && (float)acc.best < __fmul_rn(nnratio, (float)acc.second)) {
+        if (lane == 0) {
+          const int bestIdx2 = acc.pos;
+          int histIdx;
+          if (kf_vs_kf) {
+            out[idx1] = bestIdx2;
+            histIdx = idx1;
+          } else {
+            out[bestIdx2] = idx1;
+            histIdx = bestIdx2;
+          }
+          atomicOr((unsigned*)&s_taken[bestIdx2 >> 5], 1u << (bestIdx2 & 31));
+          atomicAdd(&s_var[0], 1);
+          if (check_ori) {
+            float rot = __fsub_rn(angleA[idx1], angleB[bestIdx2]);
+            if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+            int bin = (int)roundf(__fmul_rn(rot, factor));
+            if (bin == kHistoLength) bin = 0;
+            binOf[histIdx] = bin;
+            atomicAdd(&s_hist[bin], 1);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+  __syncthreads();
+  if (check_ori) {
+    if (tid == 0) {
+      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+      for (int i = 0; i < kHistoLength; i++) {
+        const int s = s_hist[i];
+        if (s > max1) {
+          max3 = max2; max2 = max1; max1 = s;
+          ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+          max3 = max2; max2 = s;
+          ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+          max3 = s;
+          ind3 = i;
+        }
+      }
+      if (max2 < __fmul_rn(0.1f, (float)max1)) {
+        ind2 = -1;
+        ind3 = -1;
+      } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
+        ind3 = -1;
+      }
+      s_var[1] = ind1;
+      s_var[2] = ind2;
+      s_var[3] = ind3;
+    }
+    __syncthreads();
+    const int ind1 = s_var[1], ind2 = s_var[2], ind3 = s_var[3];
+    for (int i = tid; i < nout; i += 256) {
+      const int b = binOf[i];
+      if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
+      out[i] = -1;
+      atomicSub(&s_var[0], 1);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *nmatches = s_var[0];
+}
+
+// ------------------------------------------------------------ launchers
+int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap, const uint8_t* B,
+                        size_t b_pitch, const int* nB, int pairs, int* best_idx, int* best, int* second,
+                        void* stream) {
+  dim3 grid((a_cap + 255) / 256, pairs);
+  hipLaunchKernelGGL(hamming_top2_kernel, grid, dim3(256), 0, (hipStream_t)stream, A, (long long)a_pitch, nA, a_cap,
+                     B, (long long)b_pitch, nB, best_idx, best, second);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+static size_t init_lds_bytes(const InitParams& P) {
+  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  return r16(4ull * P.sortn) + r16(4ull * (kGridCols * kGridRows + 1)) + 3 * r16(4ull * P.kp_pitch) + 2 * r16(64) +
+         r16(128);
+}
+
+}  // namespace orbx
+
+// ============================================================ C ABI (matcher)
+using namespace orbx;
+
+namespace {
+thread_local std::string g_merr;
+int mfail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_merr = buf;
+  return code;
+}
+}  // namespace
+
+extern "C" const char* orbm_last_error(void) { return g_merr.c_str(); }
+
+#define MHIP(expr)                                                                             \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess) return mfail(ORBX_EDEVICE, "%s: %s", #expr, hipGetErrorString(e_));  \
+  } while (0)
+
+struct orbx_matcher {
+  int device = 0, max_pairs = 0, max_kps = 0;
+  int sortn = 1;
+  long long cand_cap = 0;
+  uint32_t* cand = nullptr;
+  int* coff = nullptr;
+  int* err = nullptr;
+  hipStream_t stream = nullptr;
+  // staging for the synchronous entry points
+  void* stage = nullptr;
+  size_t stage_bytes = 0;
+};
+
+static int stage_reserve(orbx_matcher* m, size_t bytes) {
+  if (m->stage_bytes >= bytes) return ORBX_OK;
+  if (m->stage) (void)hipFree(m->stage);
+  m->stage = nullptr;
+  m->stage_bytes = 0;
+  MHIP(hipMalloc(&m->stage, bytes));
+  m->stage_bytes = bytes;
+  return ORBX_OK;
+}
+
+extern "C" {
+
+int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out) {
+  if (!out || max_pairs < 1 || max_kps < 1) return mfail(ORBX_EINVAL, "bad argument");
+  if (max_kps > 65535) return mfail(ORBX_EINVAL, "max_kps must be <= 65535");
+  MHIP(hipSetDevice(device));
+  orbx_matcher* m = new orbx_matcher();
+  m->device = device;
+  m->max_pairs = max_pairs;
+  m->max_kps = max_kps;
+  while (m->sortn < max_kps) m->sortn <<= 1;
+  // candidate budget per pair: every level-0 pair of a 200 x 200 window is far
+  // below this; overflow is reported (ORBX_ECAPACITY), never truncated.
+  m->cand_cap = std::min<long long>((long long)max_kps * max_kps, 4ll << 20);
+  if (hipMalloc(&m->cand, (size_t)max_pairs * m->cand_cap * 4) != hipSuccess ||
+      hipMalloc(&m->coff, (size_t)max_pairs * (max_kps + 1) * 4) != hipSuccess ||
+      hipMalloc(&m->err, 16) != hipSuccess ||
+      hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
+    orbm_destroy(m);
+    return mfail(ORBX_ENOMEM, "matcher workspace allocation failed");
+  }
+  (void)hipMemset(m->err, 0, 16);
+  const int lds = (int)init_lds_bytes(InitParams{0, 0, 0, 0, 0, 0, 0, 0, 0, max_kps, m->sortn, 0});
+  if (lds > 160 * 1024) {
+    orbm_destroy(m);
+    return mfail(ORBX_EINVAL, "max_kps too large for the LDS grid");
+  }
+  (void)hipFuncSetAttribute((const void*)search_init_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  *out = m;
+  return ORBX_OK;
+}
+
+int orbm_destroy(orbm_handle m) {
+  if (!m) return ORBX_OK;
+  (void)hipSetDevice(m->device);
+  if (m->stream) (void)hipStreamSynchronize(m->stream);
+  if (m->cand) (void)hipFree(m->cand);
+  if (m->coff) (void)hipFree(m->coff);
+  if (m->err) (void)hipFree(m->err);
+  if (m->stage) (void)hipFree(m->stage);
+  if (m->stream) (void)hipStreamDestroy(m->stream);
+  delete m;
+  return ORBX_OK;
+}
+
+int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+  int d = 0;
+  for (int i = 0; i < 32; ++i) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+  return d;
+}
+
+int orbm_hamming_top2(orbm_handle m, const uint8_t* d_A, size_t a_pitch, const int* d_nA, int a_cap,
+                      const uint8_t* d_B, size_t b_pitch, const int* d_nB, int pairs, int* d_best_idx, int* d_best,
+                      int* d_second, void* stream) {
+  if (!m || !d_A || !d_B || !d_nA || !d_nB || pairs < 1) return mfail(ORBX_EINVAL, "bad argument");
+  if ((a_pitch | b_pitch) & 15) return mfail(ORBX_EINVAL, "pitches must be multiples of 16 bytes");
+  MHIP(hipSetDevice(m->device));
+  const int rc = launch_hamming_top2(d_A, a_pitch, d_nA, a_cap, d_B, b_pitch, d_nB, pairs, d_best_idx, d_best,
+                                     d_second, stream ? stream : m->stream);
+  return rc ? mfail(rc, "launch failed") : ORBX_OK;
+}
+
+int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, const uint8_t* d_desc1,
+                                         const int* d_n1, const orbx_kp* d_kp2, const uint8_t* d_desc2,
+                                         const int* d_n2, int kp_pitch, int pairs, orbm_grid_bounds b,
+                                         float* d_prev_xy, int window, float nnratio, int check_ori,
+                                         int* d_matches12, int* d_nmatches, void* stream) {
+  if (!m || pairs < 1 || pairs > m->max_pairs || kp_pitch < 1 || kp_pitch > m->max_kps)
+    return mfail(ORBX_EINVAL, "pairs/kp_pitch exceed the matcher workspace");
+  MHIP(hipSetDevice(m->device));
+  InitParams P;
+  P.minX = b.min_x;
+  P.maxX = b.max_x;
+  P.minY = b.min_y;
+  P.maxY = b.max_y;
+  P.invW = static_cast<float>(kGridCols) / static_cast<float>(b.max_x - b.min_x);
+  P.invH = static_cast<float>(kGridRows) / static_cast<float>(b.max_y - b.min_y);
+  P.r = (float)window;
+  P.nnratio = nnratio;
+  P.check_ori = check_ori;
+  P.kp_pitch = kp_pitch;
+  P.sortn = 1;
+  while (P.sortn < kp_pitch) P.sortn <<= 1;
+  P.cand_cap = m->cand_cap;
+  hipLaunchKernelGGL(search_init_kernel, dim3(pairs), dim3(256), init_lds_bytes(P),
+                     (hipStream_t)(stream ? stream : m->stream), P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2,
+                     d_prev_xy, m->cand, m->coff, d_matches12, d_nmatches, m->err);
+  MHIP(hipGetLastError());
+  return ORBX_OK;
+}
+
+int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1, const uint8_t* desc1, int n1,
+                                   const orbx_kp* kp2, const uint8_t* desc2, int n2, orbm_grid_bounds bounds,
+                                   float* prev_xy, int window, float nnratio, int check_ori, int* matches12,
+                                   int* nmatches) {
+  if (!m || !nmatches || n1 < 0 || n2 < 0) return mfail(ORBX_EINVAL, "bad argument");
+  if (n1 > m->max_kps || n2 > m->max_kps) return mfail(ORBX_ECAPACITY, "more keypoints than max_kps");
+  MHIP(hipSetDevice(m->device));
+  const int pitch = std::max(std::max(n1, n2), 1);
+  const size_t kpb = (size_t)pitch * sizeof(orbx_kp), db = (size_t)pitch * 32;
+  const size_t bytes = 2 * kpb + 2 * db + (size_t)pitch * 8 + (size_t)pitch * 4 + 64;
+  int rc;
+  if ((rc = stage_reserve(m, bytes))) return rc;
+  uint8_t* s = (uint8_t*)m->stage;
+  orbx_kp* dk1 = (orbx_kp*)s;
+  orbx_kp* dk2 = (orbx_kp*)(s + kpb);
+  uint8_t* dd1 = s + 2 * kpb;
+  uint8_t* dd2 = dd1 + db;
+  float* dprev = (float*)(dd2 + db);
+  int* dm = (int*)(dprev + 2 * pitch);
+  int* dn = dm + pitch;  // n1, n2, nmatches
+  hipStream_t st = m->stream;
+  const int hn[2] = {n1, n2};
+  if (n1) {
+    MHIP(hipMemcpyAsync(dk1, kp1, (size_t)n1 * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(dd1, desc1, (size_t)n1 * 32, hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(dprev, prev_xy, (size_t)n1 * 8, hipMemcpyHostToDevice, st));
+  }
+  if (n2) {
+    MHIP(hipMemcpyAsync(dk2, kp2, (size_t)n2 * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(dd2, desc2, (size_t)n2 * 32, hipMemcpyHostToDevice, st));
+  }
+  MHIP(hipMemcpyAsync(dn, hn, 8, hipMemcpyHostToDevice, st));
+  rc = orbm_search_for_initialization_batch(m, dk1, dd1, dn, dk2, dd2, dn + 1, pitch, 1, bounds, dprev, window,
+                                            nnratio, check_ori, dm, dn + 2, st);
+  if (rc) return rc;
+  int err = 0, nm = 0;
+  MHIP(hipMemcpyAsync(&err, m->err, 4, hipMemcpyDeviceToHost, st));
+  MHIP(hipMemcpyAsync(&nm, dn + 2, 4, hipMemcpyDeviceToHost, st));
+  if (n1) {
+    MHIP(hipMemcpyAsync(matches12, dm, (size_t)n1 * 4, hipMemcpyDeviceToHost, st));
+    MHIP(hipMemcpyAsync(prev_xy, dprev, (size_t)n1 * 8, hipMemcpyDeviceToHost, st));
+  }
+  MHIP(hipStreamSynchronize(st));
+  if (err) {
+    (void)hipMemset(m->err, 0, 16);
+    return mfail(ORBX_ECAPACITY, "candidate workspace overflow (err 0x%x)", err);
+  }
+  *nmatches = nm;
+  return ORBX_OK;
+}
+
+int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA, const uint8_t* mpA, int nA,
+                       orbm_feature_vector fvA, const uint8_t* descB, const float* angleB, const uint8_t* mpB,
+                       int nB, orbm_feature_vector fvB, float nnratio, int check_ori, int kf_vs_kf, int* out,
+                       int* nmatches) {
+  if (!m || !nmatches || nA < 0 || nB < 0) return mfail(ORBX_EINVAL, "bad argument");
+  // DBoW2 precondition: each feature sits in at most one node; node ids ascending
+  auto check_fv = [&](const orbm_feature_vector& fv, int n) -> bool {
+    std::vector<char> seen(std::max(n, 1), 0);
+    for (int k = 0; k < fv.n_nodes; ++k) {
+      if (k && fv.nodes[k] <= fv.nodes[k - 1]) return false;
+      for (int p = fv.off[k]; p < fv.off[k + 1]; ++p) {
+        const int i = fv.idx[p];
+        if (i < 0 || i >= n || seen[i]) return false;
+        seen[i] = 1;
+      }
+    }
+    return true;
+  };
+  if (nB > 65536) return mfail(ORBX_EINVAL, "nB must be <= 65536");
+  if (!check_fv(fvA, nA) || !check_fv(fvB, nB))
+    return mfail(ORBX_EINVAL, "FeatureVector must have ascending node ids and disjoint in-range indices");
+  MHIP(hipSetDevice(m->device));
+  const int nout = kf_vs_kf ? nA : nB;
+  const int ia = fvA.n_nodes ? fvA.off[fvA.n_nodes] : 0, ib = fvB.n_nodes ? fvB.off[fvB.n_nodes] : 0;
+  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  const size_t sz[] = {r16((size_t)nA * 32), r16((size_t)nA * 4), r16((size_t)nA), r16((size_t)fvA.n_nodes * 4),
+                       r16((size_t)(fvA.n_nodes + 1) * 4), r16((size_t)ia * 4), r16((size_t)nB * 32),
+                       r16((size_t)nB * 4), r16((size_t)nB), r16((size_t)fvB.n_nodes * 4),
+                       r16((size_t)(fvB.n_nodes + 1) * 4), r16((size_t)ib * 4), r16((size_t)nout * 4),
+                       r16((size_t)nout * 4), 16};
+  size_t tot = 0;
+  for (size_t v : sz) tot += v;
+  int rc;
+  if ((rc = stage_reserve(m, tot))) return rc;
+  uint8_t* p = (uint8_t*)m->stage;
+  void* d[15];
+  for (int i = 0; i < 15; ++i) {
+    d[i] = p;
+    p += sz[i];
+  }
+  hipStream_t st = m->stream;
+  auto up = [&](void* dst, const void* src, size_t n) -> int {
+    if (n && src) MHIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));
+    return ORBX_OK;
+  };
+  std::vector<uint8_t> mpBdef;
+  if (!mpB) mpBdef.assign(std::max(nB, 1), 1), mpB = mpBdef.data();
+  if ((rc = up(d[0], descA, (size_t)nA * 32)) || (rc = up(d[1], angleA, (size_t)nA * 4)) ||
+      (rc = up(d[2], mpA, (size_t)nA)) || (rc = up(d[3], fvA.nodes, (size_t)fvA.n_nodes * 4)) ||
+      (rc = up(d[4], fvA.off, (size_t)(fvA.n_nodes + 1) * 4)) || (rc = up(d[5], fvA.idx, (size_t)ia * 4)) ||
+      (rc = up(d[6], descB, (size_t)nB * 32)) || (rc = up(d[7], angleB, (size_t)nB * 4)) ||
+      (rc = up(d[8], mpB, (size_t)nB)) || (rc = up(d[9], fvB.nodes, (size_t)fvB.n_nodes * 4)) ||
+      (rc = up(d[10], fvB.off, (size_t)(fvB.n_nodes + 1) * 4)) || (rc = up(d[11], fvB.idx, (size_t)ib * 4)))
+    return rc;
+  hipLaunchKernelGGL(search_bow_kernel, dim3(1), dim3(256), 0, st, (const uint8_t*)d[0], (const float*)d[1],
+                     (const uint8_t*)d[2], nA, (const uint32_t*)d[3], (const int*)d[4], (const int*)d[5],
+                     fvA.n_nodes, (const uint8_t*)d[6], (const float*)d[7], (const uint8_t*)d[8], nB,
+                     (const uint32_t*)d[9], (const int*)d[10], (const int*)d[11], fvB.n_nodes, nnratio, check_ori,
+                     kf_vs_kf, (int*)d[12], (int*)d[14], (int*)d[13]);
+  MHIP(hipGetLastError());
+  int nm = 0;
+  MHIP(hipMemcpyAsync(&nm, d[14], 4, hipMemcpyDeviceToHost, st));
+  if (nout) MHIP(hipMemcpyAsync(out, d[12], (size_t)nout * 4, hipMemcpyDeviceToHost, st));
+  MHIP(hipStreamSynchronize(st));
+  *nmatches = nm;
+  return ORBX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,151 @@
+"""ORBextractor — host-side mirror of ORB_SLAM2::ORBextractor over liborbx.
+
+Same constructor arguments, call signature, getters and error behaviour as
+the reference (include/ORBextractor.h:75-197, src/ORBextractor.cc:496-1815):
+
+    ext = ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
+                       width, height)
+    keypoints, descriptors = ext(image)          # operator()(image, mask, kps, desc)
+    ext.GetScaleFactors(); ext.mvImagePyramid    # getters / public pyramid
+
+Keypoints come back as a numpy structured array with the cv::KeyPoint field
+layout (KP_DTYPE), descriptors as an (N, 32) uint8 array, in the reference
+order (level-major, quadtree order inside a level). All computation runs in
+the HIP kernels of liborbx.so; nothing here computes features.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import KP_DTYPE, OrbxConfig, check, lib, ptr
+
+SCALE_MODES = {"U": 0, "F": 1}
+PATTERNS = {"fork": 0, "upstream": 1}
+
+
+class ORBextractor:
+    HARRIS_SCORE, FAST_SCORE = 0, 1  # include/ORBextractor.h:80 (unused by the reference)
+
+    def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int,
+                 minThFAST: int, width: int, height: int, *, device: int = 0, max_batch: int = 1,
+                 scale_mode: str = "U", pattern: str = "fork"):
+        cfg = OrbxConfig()
+        cfg.nfeatures, cfg.scale_factor, cfg.nlevels = int(nfeatures), float(scaleFactor), int(nlevels)
+        cfg.ini_th_fast, cfg.min_th_fast = int(iniThFAST), int(minThFAST)
+        cfg.width, cfg.height = int(width), int(height)
+        cfg.device, cfg.max_batch = int(device), int(max_batch)
+        cfg.scale_mode, cfg.pattern_mode = SCALE_MODES[scale_mode], PATTERNS[pattern]
+        self.cfg = cfg
+        self._h = C.c_void_p(0)
+        check(lib().orbx_create(C.byref(cfg), C.byref(self._h)))
+        self.nfeatures, self.scaleFactor, self.nlevels = cfg.nfeatures, cfg.scale_factor, cfg.nlevels
+        self.iniThFAST, self.minThFAST = cfg.ini_th_fast, cfg.min_th_fast
+
+    # ------------------------------------------------------------- lifetime
+    def close(self) -> None:
+        if self._h and self._h.value:
+            lib().orbx_destroy(self._h)
+            self._h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    @property
+    def frame_capacity(self) -> int:
+        return lib().orbx_frame_capacity(self._h)
+
+    # ------------------------------------------------------------- operator()
+    def __call__(self, image: np.ndarray, mask=None):
+        """ORBextractor::operator()(image, mask, keypoints, descriptors); mask is ignored
+        like the reference (include/ORBextractor.h:89)."""
+        img = np.asarray(image)
+        if img.size == 0:
+            return np.zeros(0, KP_DTYPE), np.zeros((0, 32), np.uint8)
+        if img.dtype != np.uint8 or img.ndim != 2:
+            raise _lib.OrbxError(_lib.ORBX_EINVAL, "image must be CV_8UC1 (2-D uint8)")  # :1546 assert
+        if img.strides[1] != 1:
+            img = np.ascontiguousarray(img)
+        cap = self.frame_capacity
+        kps = np.empty(cap, KP_DTYPE)
+        desc = np.empty((cap, 32), np.uint8)
+        n = C.c_int(0)
+        check(lib().orbx_extract(self._h, ptr(img), img.shape[1], img.shape[0], img.strides[0],
+                                 ptr(kps), cap, ptr(desc), C.byref(n)))
+        cap = self.frame_capacity  # a new image size re-plans the handle
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def extract_batch_device(self, d_frames: int, batch: int, frame_pitch: int, row_stride: int,
+                             d_kps: int, d_desc: int, d_counts: int, stream=None) -> None:
+        """Asynchronous batched extraction on device pointers (orbx_extract_batch)."""
+        s = stream.s if stream is not None else C.c_void_p(0)
+        check(lib().orbx_extract_batch(self._h, C.c_void_p(d_frames), batch, frame_pitch, row_stride,
+                                       C.c_void_p(d_kps), C.c_void_p(d_desc), C.c_void_p(d_counts), s))
+
+    # ------------------------------------------------------------- getters
+    def GetLevels(self) -> int:
+        return self.nlevels
+
+    def GetScaleFactor(self) -> float:
+        return self.scaleFactor
+
+    def _scales(self):
+        L = self.nlevels
+        a = [np.zeros(L, np.float32) for _ in range(4)]
+        check(lib().orbx_get_scales(self._h, *(ptr(x) for x in a)))
+        return a
+
+    def GetScaleFactors(self) -> list[float]:
+        return self._scales()[0].tolist()
+
+    def GetInverseScaleFactors(self) -> list[float]:
+        return self._scales()[1].tolist()
+
+    def GetScaleSigmaSquares(self) -> list[float]:
+        return self._scales()[2].tolist()
+
+    def GetInverseScaleSigmaSquares(self) -> list[float]:
+        return self._scales()[3].tolist()
+
+    def levels_info(self) -> dict:
+        L = self.nlevels
+        n = C.c_int(0)
+        w, h, nf = (np.zeros(L, np.int32) for _ in range(3))
+        check(lib().orbx_get_levels_info(self._h, C.byref(n), ptr(w), ptr(h), ptr(nf)))
+        return {"w": w, "h": h, "nfeatures": nf}
+
+    def level_image(self, level: int, frame: int = 0, blurred: bool = False) -> np.ndarray:
+        info = self.levels_info()
+        out = np.empty((info["h"][level], info["w"][level]), np.uint8)
+        check(lib().orbx_get_level(self._h, frame, level, int(blurred), ptr(out), out.strides[0]))
+        return out
+
+    @property
+    def mvImagePyramid(self) -> list[np.ndarray]:
+        """Pyramid of the last extraction (public member, include/ORBextractor.h:116)."""
+        return [self.level_image(l) for l in range(self.nlevels)]
+
+    def fast_candidates(self, level: int, frame: int = 0) -> np.ndarray:
+        """Stage probe: per-cell FAST+NMS output of the last extraction (pre-quadtree)."""
+        cap = 1 << 20
+        out = np.empty(cap, KP_DTYPE)
+        n = C.c_int(0)
+        check(lib().orbx_get_fast_candidates(self._h, frame, level, ptr(out), cap, C.byref(n)))
+        return out[:n.value].copy()
+
+    def stage_times(self) -> dict[str, float]:
+        """Device ms per stage of the last extraction (needs ORBX_TIMING=1)."""
+        ms = np.zeros(8, np.float32)
+        names = (C.c_char_p * 8)()
+        n = C.c_int(0)
+        check(lib().orbx_get_stage_times(self._h, ptr(ms), names, 8, C.byref(n)))
+        return {names[i].decode(): float(ms[i]) for i in range(n.value)}

@@ -1,0 +1,119 @@
+"""Seeded synthetic grayscale frames shaped like KITTI / EuRoC input.
+
+KITTI and EuRoC images are not available offline, so the
+benchmark and the parity tests run on synthetic scenes: a smooth gradient,
+axis-aligned rectangles, ellipses and small textured blobs with uniform
+intensities, plus uniform pixel noise. This gives a corner density in the
+range of a real urban frame (thousands of FAST-7 corners at level 0).
+
+A *sequence* is a random walk of a window over one larger canvas (integer
+shifts in [-8, 8] per frame) with fresh noise per frame, so consecutive
+frames share structure and the matchers find real correspondences.
+
+All randomness comes from numpy's PCG64 (`np.random.default_rng(seed)`),
+which is reproducible across platforms.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+KITTI_WH = (1241, 376)
+EUROC_WH = (752, 480)
+
+
+def _paint_canvas(rng: np.random.Generator, W: int, H: int) -> np.ndarray:
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    base = rng.uniform(60, 190)
+    gx, gy = rng.uniform(-0.08, 0.08, size=2)
+    img = base + gx * (xx - W / 2) + gy * (yy - H / 2)
+    area = W * H
+    n_rect = max(8, int(90 * area / (1241 * 376)))
+    n_ell = max(4, int(45 * area / (1241 * 376)))
+    n_blob = max(4, int(60 * area / (1241 * 376)))
+    for _ in range(n_rect):
+        w = int(rng.integers(6, max(8, W // 6)))
+        h = int(rng.integers(6, max(8, H // 4)))
+        x0 = int(rng.integers(-w // 2, W))
+        y0 = int(rng.integers(-h // 2, H))
+        img[max(0, y0):max(0, y0 + h), max(0, x0):max(0, x0 + w)] = rng.uniform(0, 255)
+    for _ in range(n_ell):
+        cx, cy = rng.uniform(0, W), rng.uniform(0, H)
+        a, b = rng.uniform(4, W / 10), rng.uniform(4, H / 6)
+        th = rng.uniform(0, np.pi)
+        x0, x1 = int(max(0, cx - a - b)), int(min(W, cx + a + b + 1))
+        y0, y1 = int(max(0, cy - a - b)), int(min(H, cy + a + b + 1))
+        if x1 <= x0 or y1 <= y0:
+            continue
+        sx = xx[y0:y1, x0:x1] - cx
+        sy = yy[y0:y1, x0:x1] - cy
+        u = sx * np.cos(th) + sy * np.sin(th)
+        v = -sx * np.sin(th) + sy * np.cos(th)
+        m = (u / a) ** 2 + (v / b) ** 2 <= 1.0
+        img[y0:y1, x0:x1][m] = rng.uniform(0, 255)
+    for _ in range(n_blob):
+        # small checker / speckle patches: dense, strong corners (windows, foliage)
+        bw, bh = int(rng.integers(10, 40)), int(rng.integers(10, 30))
+        x0, y0 = int(rng.integers(0, max(1, W - bw))), int(rng.integers(0, max(1, H - bh)))
+        cell = int(rng.integers(3, 8))
+        lo, hi = sorted(rng.uniform(0, 255, size=2))
+        pat = ((xx[y0:y0 + bh, x0:x0 + bw] // cell + yy[y0:y0 + bh, x0:x0 + bw] // cell) % 2)
+        img[y0:y0 + bh, x0:x0 + bw] = np.where(pat > 0, hi, lo)
+    return img
+
+
+def synth_frame(seed: int, W: int = KITTI_WH[0], H: int = KITTI_WH[1]) -> np.ndarray:
+    """One synthetic u8 frame (H x W, C-contiguous)."""
+    rng = np.random.default_rng(seed)
+    img = _paint_canvas(rng, W, H)
+    img = img + rng.integers(-6, 7, size=img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+class SynthSequence:
+    """A camera-like stream: a window random-walking over one canvas."""
+
+    MARGIN = 96
+
+    def __init__(self, seed: int, W: int = KITTI_WH[0], H: int = KITTI_WH[1]):
+        self.W, self.H = W, H
+        self.rng = np.random.default_rng(seed)
+        M = self.MARGIN
+        self.canvas = _paint_canvas(self.rng, W + 2 * M, H + 2 * M)
+        self.ox, self.oy = M, M
+
+    def shift(self) -> tuple[int, int]:
+        dx, dy = (int(v) for v in self.rng.integers(-8, 9, size=2))
+        M = self.MARGIN
+        nx, ny = self.ox + dx, self.oy + dy
+        # reflect the walk at the canvas edge
+        if not 0 <= nx <= 2 * M:
+            dx = -dx
+        if not 0 <= ny <= 2 * M:
+            dy = -dy
+        self.ox += dx
+        self.oy += dy
+        return dx, dy
+
+    def frame(self) -> np.ndarray:
+        win = self.canvas[self.oy:self.oy + self.H, self.ox:self.ox + self.W]
+        noisy = win + self.rng.integers(-6, 7, size=win.shape)
+        return np.clip(np.rint(noisy), 0, 255).astype(np.uint8)
+
+    def frames(self, n: int) -> np.ndarray:
+        out = np.empty((n, self.H, self.W), np.uint8)
+        for i in range(n):
+            if i:
+                self.shift()
+            out[i] = self.frame()
+        return out
+
+
+def stereo_pair(seed: int, W: int = KITTI_WH[0], H: int = KITTI_WH[1]) -> tuple[np.ndarray, np.ndarray]:
+    """Left/right pair: right = left content shifted left by a disparity in [5, 40]."""
+    rng = np.random.default_rng(seed)
+    canvas = _paint_canvas(rng, W + 48, H)
+    disp = int(rng.integers(5, 41))
+    left = canvas[:, 48:48 + W]
+    right = canvas[:, 48 - disp:48 - disp + W]
+    n = lambda a: np.clip(np.rint(a + rng.integers(-6, 7, size=a.shape)), 0, 255).astype(np.uint8)
+    return n(left), n(right)
