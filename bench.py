@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""bench.py — ORB extract + match throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], "C3"): KITTI-shaped 1241x376 mono u8
+frames, nFeatures=2000, 8 levels, scale 1.2, iniThFAST 20 / minThFAST 7.
+One step = one batch of B frames resident in HBM:
+  * ORBextractor::operator() on all B frames (orbx_extract_batch), and
+  * for every frame t, matching against frame t-1: the dense brute-force
+    2000 x 2000 Hamming best/second search (orbm_hamming_top2) and the exact
+    ORBmatcher::SearchForInitialization (window 100, ratio 0.9, rotation
+    check) used by monocular initialisation.
+Frame t-1 of the first frame of a batch is the last frame of the previous
+batch (carried on device), so every step does B extractions + B matches.
+
+Multi-GPU: one process per GPU, frames sharded by rank (each rank streams its
+own synthetic sequence), no data-path collective ("weak" scaling). The
+barrier and the max-over-ranks of the timed region go through
+torch.distributed with the gloo backend (control plane only).
+
+Prints ONE JSON line (rank 0). Per-kernel durations are measured live with
+HIP events recorded on the launch stream around every stage of every step.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/s ORB extract+match, 1241×376 mono nFeatures=2000; achieved HBM GB/s"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_top2", "search_init"]
+KERNELS = {"pyramid": "pyr_resize_kernel (x7)", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
+           "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
+           "hamming_top2": "hamming_top2_kernel", "search_init": "search_init_kernel"}
+
+CONFIGS = {
+    "kitti": dict(W=1241, H=376, nfeatures=2000,
+                  workload="C3: KITTI-shaped 1241x376 mono u8, nFeatures=2000, 8 levels x1.2, "
+                           "extract + match vs t-1 (dense 2000x2000 Hamming top-2 + SearchForInitialization)"),
+    "euroc": dict(W=752, H=480, nfeatures=1000,
+                  workload="C5: EuRoC-shaped 752x480 mono u8, nFeatures=1000, 8 levels x1.2, "
+                           "extract + match vs t-1 (dense Hamming top-2 + SearchForInitialization)"),
+}
+
+
+def level_sizes(W, H, L=8, s=1.2):
+    sc = [1.0]
+    for _ in range(1, L):
+        sc.append(np.float32(sc[-1]) * np.float32(s))
+    out = []
+    for f in sc:
+        inv = np.float32(1.0) / np.float32(f)
+        out.append((int(np.rint(np.float32(W) * inv)), int(np.rint(np.float32(H) * inv))))
+    return out
+
+
+def algorithmic_bytes(W, H, nkp):
+    """Per-frame algorithmic HBM bytes of each stage (DESIGN.md "Roofline")."""
+    P = [w * h for w, h in level_sizes(W, H)]
+    return {
+        "pyramid": sum(P[l - 1] + P[l] for l in range(1, 8)),         # read l-1, write l
+        "blur": 2 * sum(P),                                            # read + write every level
+        "fast_grid": sum(P),                                           # read every level once
+        "pyr_fast_pass": P[0] + sum(P[:7]) + sum(P[1:]) + sum(P),      # BASELINE.md B_pf
+        "orient_brief": nkp * (2 * 31 * 31 + 60),                      # patch gathers + outputs
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
+    ap.add_argument("--cpu-sample", type=int, default=24, help="frames in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--no-match", action="store_true", help="extract only (C2)")
+    args = ap.parse_args()
+
+    from orb_slam_cuda_amd import sharding
+    rank, world, local = sharding.rank_info()
+    # control plane only (gloo); initialised before liborbx loads so one HIP runtime is in the process
+    dist = sharding.init_control_plane()
+
+    import orb_slam_cuda_amd as pkg
+    from orb_slam_cuda_amd import _lib
+    from orb_slam_cuda_amd.synth import SynthSequence
+
+    L = _lib.lib()
+    cfg = CONFIGS[args.config]
+    W, H, NF, B = cfg["W"], cfg["H"], cfg["nfeatures"], args.batch
+    pitch = (W + 63) & ~63
+
+    seq = SynthSequence(sharding.sequence_seed(rank), W, H)
+    frames = seq.frames(B)
+    host = np.zeros((B, H, pitch), np.uint8)
+    host[:, :, :W] = frames
+    d_frames = _lib.DeviceArray(host.nbytes)
+    check = _lib.check
+    check(L.orbx_set_device(local))
+    d_frames.upload(host)
+
+    ext = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=B)
+    cap = ext.frame_capacity
+    KP, DS = 28, 32
+    d_kps = _lib.DeviceArray((B + 1) * cap * KP)
+    d_desc = _lib.DeviceArray((B + 1) * cap * DS)
+    d_counts = _lib.DeviceArray((B + 1) * 4)
+    d_counts.zero()
+    matcher = pkg.ORBmatcher(0.9, True, device=local, max_pairs=B, max_kps=cap)
+    d_bi, d_bd, d_sd = (_lib.DeviceArray(B * cap * 4) for _ in range(3))
+    d_m12 = _lib.DeviceArray(B * cap * 4)
+    d_nm = _lib.DeviceArray(B * 4)
+    stream = _lib.Stream()
+    bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
+    vp = lambda a: C.c_void_p(a)
+
+    def step(evs=None):
+        if evs is not None:
+            arr = (C.c_void_p * 6)(*[e.e.value for e in evs[:6]])
+            check(L.orbx_set_stage_events(ext.handle, arr))
+        check(L.orbx_extract_batch(ext.handle, vp(d_frames.ptr), B, H * pitch, pitch,
+                                   vp(d_kps.ptr + cap * KP), vp(d_desc.ptr + cap * DS), vp(d_counts.ptr + 4),
+                                   stream.s))
+        if not args.no_match:
+            # query = frame t (slots 1..B), candidates = frame t-1 (slots 0..B-1)
+            check(L.orbm_hamming_top2(matcher.handle, vp(d_desc.ptr + cap * DS), cap * DS, vp(d_counts.ptr + 4),
+                                      cap, vp(d_desc.ptr), cap * DS, vp(d_counts.ptr), B, vp(d_bi.ptr),
+                                      vp(d_bd.ptr), vp(d_sd.ptr), stream.s), matcher=True)
+            if evs is not None:
+                evs[6].record(stream)
+            check(L.orbm_search_for_initialization_batch(
+                matcher.handle, vp(d_kps.ptr), vp(d_desc.ptr), vp(d_counts.ptr), vp(d_kps.ptr + cap * KP),
+                vp(d_desc.ptr + cap * DS), vp(d_counts.ptr + 4), cap, B, bounds, None, 100, C.c_float(0.9), 1,
+                vp(d_m12.ptr), vp(d_nm.ptr), stream.s), matcher=True)
+            if evs is not None:
+                evs[7].record(stream)
+        # carry frame B-1 into slot 0 as the next batch's frame t-1
+        check(L.orbx_memcpy_dtod_async(vp(d_kps.ptr), vp(d_kps.ptr + B * cap * KP), cap * KP, stream.s))
+        check(L.orbx_memcpy_dtod_async(vp(d_desc.ptr), vp(d_desc.ptr + B * cap * DS), cap * DS, stream.s))
+        check(L.orbx_memcpy_dtod_async(vp(d_counts.ptr), vp(d_counts.ptr + B * 4), 4, stream.s))
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    counts = d_counts.download(B + 1, np.int32)[1:]
+    nkp_mean = float(counts.mean())
+
+    evsets = [[_lib.Event() for _ in range(8)] for _ in range(args.steps)]
+    t_start, t_end = _lib.Event(), _lib.Event()
+    if dist is not None:
+        dist.barrier()
+    stream.synchronize()
+    t0 = time.perf_counter()
+    t_start.record(stream)
+    for k in range(args.steps):
+        step(evsets[k])
+    t_end.record(stream)
+    stream.synchronize()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    wall = sharding.max_over_ranks(t1 - t0, dist)
+    ev_ms = t_start.elapsed_ms(t_end)
+
+    # per-stage average durations over the timed steps (ms per launch-group, B frames)
+    st = {s: 0.0 for s in STAGES}
+    for evs in evsets:
+        for i, s in enumerate(STAGES[:5]):
+            st[s] += evs[i].elapsed_ms(evs[i + 1])
+        if not args.no_match:
+            st["hamming_top2"] += evs[5].elapsed_ms(evs[6])
+            st["search_init"] += evs[6].elapsed_ms(evs[7])
+    st = {s: v / args.steps for s, v in st.items()}
+
+    nm = d_nm.download(B, np.int32)
+    frames_total = B * args.steps * world
+    value = frames_total / wall
+    ab = algorithmic_bytes(W, H, nkp_mean)
+    extract_ms = sum(st[s] for s in STAGES[:5])
+    dominant = max(STAGES, key=lambda s: st[s])
+    # roofline of the pyramid+FAST pass and of the dominant kernel
+    pf_ms = st["pyramid"] + st["fast_grid"]
+    pf_gbs = ab["pyr_fast_pass"] * B / (pf_ms * 1e-3) / 1e9
+    roof = None
+    hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
+                  "orient_brief": ab["orient_brief"]}
+    rk = dominant if dominant in hbm_stages else max(hbm_stages, key=lambda s: st[s])
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get(KERNELS[rk].split(" ")[0], {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    ach = hbm_stages[rk] * B / (st[rk] * 1e-3) / 1e9
+    roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_launch": int(hbm_stages[rk] * B),
+            "avg_launch_ms": round(st[rk], 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(frames, cfg, args.cpu_sample, args.no_match)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded shapes + noise sequence, orb_slam_cuda_amd/synth.py)",
+            "config": {"workload": cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only",
+                       "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
+                       "frames_per_step_per_gpu": B, "parallelism": f"frame-sharded x{world}, no collectives"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "pyr_fast_pass_hbm_gbs": round(pf_gbs, 1),
+            "dominant_kernel": KERNELS[dominant],
+            "stage_ms_per_step": {s: round(v, 4) for s, v in st.items()},
+            "extract_only_frames_per_s": round(B / (extract_ms * 1e-3), 1),
+            "event_ms_per_step": round(ev_ms / args.steps, 4),
+            "keypoints_per_frame": round(nkp_mean, 1),
+            "init_matches_per_pair": round(float(nm[1:].mean()), 1),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(frames, cfg, n, no_match):
+    """The CPU oracle (restatement of the reference CPU path) on a bounded sample, 1 thread."""
+    from oracle import oracle as O
+    W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
+    oc = O.config(nfeatures=NF, width=W, height=H)
+    n = min(n, len(frames))
+    t0 = time.perf_counter()
+    prev = None
+    for i in range(n):
+        kp, desc = O.extract(oc, frames[i])
+        if prev is not None and not no_match:
+            pk, pd = prev
+            O.hamming_top2(desc, pd)
+            O.search_for_initialization(pk, pd, kp, desc, (0, W, 0, H), np.stack([pk["x"], pk["y"]], 1),
+                                        100, 0.9, True)
+        prev = (kp, desc)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} consecutive frames of the same synthetic sequence, oracle extract"
+                      + ("" if no_match else " + dense top-2 + SearchForInitialization vs t-1")
+                      + f", single thread, {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -104,7 +104,8 @@ int orbx_frame_capacity(orbx_handle h);
 int orbx_extract(orbx_handle h, const uint8_t* img, int w, int h_, size_t stride,
                  orbx_kp* kps, int cap, uint8_t* desc, int* n);
 
-/* Batched, device-resident, asynchronous on `stream` (hipStream_t or NULL).
+/* Batched, device-resident, asynchronous on `stream` (hipStream_t; NULL =
+ * the default stream).
  * d_frames: batch frames of (height x width) u8, row stride `row_stride`,
  * frame i at d_frames + i*frame_pitch. Outputs: frame i's keypoints at
  * d_kps + i*cap, descriptors at d_desc + i*cap*32, count in d_counts[i],
@@ -133,9 +134,18 @@ int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out,
  * (ORBX_TIMING=1 in the environment). */
 int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap,
                          int* n);
+/* Record caller-owned HIP events (ORBX_STAGE_EVENTS of them, hipEvent_t as
+ * void*) between the stages of the NEXT orbx_extract_batch call on its
+ * stream: ev[0] before the pyramid, ev[1] after it, then after blur, FAST,
+ * quadtree and angle/descriptor. Lets a caller time every kernel of every
+ * call without a host synchronisation. One-shot. */
+#define ORBX_STAGE_EVENTS 6
+int orbx_set_stage_events(orbx_handle h, void** events);
 
 /* ------------------------------------------------------------- matcher */
 typedef struct orbx_matcher* orbm_handle;
+
+const char* orbm_last_error(void);
 
 /* Workspace for batched matching of up to max_pairs frame pairs with up to
  * max_kps keypoints per frame. */
@@ -174,8 +184,10 @@ int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1,
 
 /* Batched device-resident variant: pair p matches frame F1 = (d_kp1 +
  * p*kp_pitch, d_desc1 + p*kp_pitch*32, d_n1[p]) against F2 likewise.
- * d_prev_xy: pairs x kp_pitch x 2 floats (in/out); d_matches12: pairs x
- * kp_pitch; d_nmatches: pairs. */
+ * d_prev_xy: pairs x kp_pitch x 2 floats (in/out), or NULL to centre the
+ * windows on F1's own keypoints (the initial mvbPrevMatched of
+ * Tracking::MonocularInitialization, src/Tracking.cc:645-647; nothing is
+ * written back then); d_matches12: pairs x kp_pitch; d_nmatches: pairs. */
 int orbm_search_for_initialization_batch(
     orbm_handle m, const orbx_kp* d_kp1, const uint8_t* d_desc1,
     const int* d_n1, const orbx_kp* d_kp2, const uint8_t* d_desc2,
@@ -215,6 +227,7 @@ int orbx_free(void* p);
 int orbx_memcpy_htod(void* dst, const void* src, size_t bytes);
 int orbx_memcpy_dtoh(void* dst, const void* src, size_t bytes);
 int orbx_memset(void* dst, int value, size_t bytes);
+int orbx_memcpy_dtod_async(void* dst, const void* src, size_t bytes, void* stream);
 int orbx_stream_create(void** stream);
 int orbx_stream_destroy(void* stream);
 int orbx_stream_synchronize(void* stream);

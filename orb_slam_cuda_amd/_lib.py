@@ -71,6 +71,7 @@ def lib() -> C.CDLL:
         L.orbx_get_fast_candidates.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
                                                C.POINTER(C.c_int)]
         L.orbx_get_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+        L.orbx_set_stage_events.argtypes = [C.c_void_p, C.c_void_p]
         L.orbm_create.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
         L.orbm_destroy.argtypes = [C.c_void_p]
         L.orbm_descriptor_distance.argtypes = [C.c_void_p, C.c_void_p]
@@ -95,6 +96,7 @@ def lib() -> C.CDLL:
         L.orbx_memcpy_htod.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.orbx_memcpy_dtoh.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.orbx_memset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+        L.orbx_memcpy_dtod_async.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.orbx_stream_create.argtypes = [C.POINTER(C.c_void_p)]
         L.orbx_stream_destroy.argtypes = [C.c_void_p]
         L.orbx_stream_synchronize.argtypes = [C.c_void_p]

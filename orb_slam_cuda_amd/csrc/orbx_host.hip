@@ -90,6 +90,8 @@ struct orbx_extractor {
   size_t last_fpitch = 0, last_rstride = 0;
   bool timing = false;
   hipEvent_t ev[6] = {};
+  void* user_ev[ORBX_STAGE_EVENTS] = {};
+  bool has_user_ev = false;
   std::mutex mu;
 };
 
@@ -408,9 +410,10 @@ int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch, size_t
   if (batch < 1 || batch > h->plan.B) return fail(ORBX_EINVAL, "batch %d not in 1..max_batch(%d)", batch, h->plan.B);
   if (row_stride < (size_t)h->plan.W) return fail(ORBX_EINVAL, "row_stride < width");
   HIP_OK(hipSetDevice(h->cfg.device));
+  void** ev = h->has_user_ev ? h->user_ev : (h->timing ? (void**)h->ev : nullptr);
+  h->has_user_ev = false;
   const int rc = launch_extract(h->plan.P, buffers_of(h->plan), d_frames, batch, frame_pitch, row_stride, d_kps,
-                                d_desc, d_counts, stream ? stream : (void*)h->stream,
-                                h->timing ? (void**)h->ev : nullptr);
+                                d_desc, d_counts, stream, ev);
   h->last_batch = batch;
   h->last_frames = d_frames;
   h->last_fpitch = frame_pitch;
@@ -552,6 +555,13 @@ int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap, 
   return ORBX_OK;
 }
 
+int orbx_set_stage_events(orbx_handle h, void** events) {
+  if (!h || !events) return fail(ORBX_EINVAL, "null argument");
+  for (int i = 0; i < ORBX_STAGE_EVENTS; ++i) h->user_ev[i] = events[i];
+  h->has_user_ev = true;
+  return ORBX_OK;
+}
+
 // ---------------------------------------------------------- plumbing
 int orbx_device_count(int* n) {
   if (!n) return fail(ORBX_EINVAL, "null");
@@ -564,6 +574,10 @@ int orbx_free(void* p) { HIP_OK(hipFree(p)); return ORBX_OK; }
 int orbx_memcpy_htod(void* d, const void* s, size_t b) { HIP_OK(hipMemcpy(d, s, b, hipMemcpyHostToDevice)); return ORBX_OK; }
 int orbx_memcpy_dtoh(void* d, const void* s, size_t b) { HIP_OK(hipMemcpy(d, s, b, hipMemcpyDeviceToHost)); return ORBX_OK; }
 int orbx_memset(void* d, int v, size_t b) { HIP_OK(hipMemset(d, v, b)); return ORBX_OK; }
+int orbx_memcpy_dtod_async(void* d, const void* s, size_t b, void* st) {
+  HIP_OK(hipMemcpyAsync(d, s, b, hipMemcpyDeviceToDevice, (hipStream_t)st));
+  return ORBX_OK;
+}
 int orbx_stream_create(void** s) { HIP_OK(hipStreamCreateWithFlags((hipStream_t*)s, hipStreamNonBlocking)); return ORBX_OK; }
 int orbx_stream_destroy(void* s) { HIP_OK(hipStreamDestroy((hipStream_t)s)); return ORBX_OK; }
 int orbx_stream_synchronize(void* s) { HIP_OK(hipStreamSynchronize((hipStream_t)s)); return ORBX_OK; }

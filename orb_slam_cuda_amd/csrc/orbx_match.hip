@@ -195,7 +195,11 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
   const orbx_kp* kp2 = kp2_all + (long long)pr * P.kp_pitch;
   const uint8_t* desc1 = desc1_all + (long long)pr * P.kp_pitch * 32;
   const uint8_t* desc2 = desc2_all + (long long)pr * P.kp_pitch * 32;
-  float* prev = prev_all + (long long)pr * P.kp_pitch * 2;
+  // prev_all == nullptr: windows centred on F1's own keypoints, the initial
+  // mvbPrevMatched of Tracking::MonocularInitialization (src/Tracking.cc:645-647)
+  float* prev = prev_all ? prev_all + (long long)pr * P.kp_pitch * 2 : nullptr;
+  auto px = [&](int i) { return prev ? prev[2 * i] : kp1[i].x; };
+  auto py = [&](int i) { return prev ? prev[2 * i + 1] : kp1[i].y; };
   int* m12 = matches_all + (long long)pr * P.kp_pitch;
   int* coff = coff_all + (long long)pr * (P.kp_pitch + 1);
   uint32_t* cand = cand_all + (long long)pr * P.cand_cap;
@@ -262,7 +266,7 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
 
   // ---- candidate windows (Frame::GetFeaturesInArea, minLevel = maxLevel = 0)
   auto window = [&](int i1, int* cx0, int* cx1, int* cy0, int* cy1) -> bool {
-    const float x = prev[2 * i1], y = prev[2 * i1 + 1], r = P.r;
+    const float x = px(i1), y = py(i1), r = P.r;
     const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, P.minX), r), P.invW)));
     if (nMinCellX >= kGridCols) return false;
     const int nMaxCellX = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, P.minX), r), P.invW)));
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
     int cnt = 0;
     int cx0, cx1, cy0, cy1;
     if (kp1[i1].octave == 0 && window(i1, &cx0, &cx1, &cy0, &cy1)) {
-      const float x = prev[2 * i1], y = prev[2 * i1 + 1];
+      const float x = px(i1), y = py(i1);
       for (int ix = cx0; ix <= cx1; ++ix) {
         const int s0 = s_cell[ix * kGridRows + cy0], s1 = s_cell[ix * kGridRows + cy1 + 1];
         for (int s = s0 + lane; s < s1; s += 64) {
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
   for (int i1 = wv; i1 < n1; i1 += 4) {
     int cx0, cx1, cy0, cy1;
     if (!(kp1[i1].octave == 0 && window(i1, &cx0, &cx1, &cy0, &cy1))) continue;
-    const float x = prev[2 * i1], y = prev[2 * i1 + 1];
+    const float x = px(i1), y = py(i1);
     const uint4* d1 = (const uint4*)(desc1 + (long long)i1 * 32);
     const uint4 a0 = d1[0], a1 = d1[1];
     int base = coff[i1];
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
     __syncthreads();
   }
   // vbPrevMatched update
-  for (int i = tid; i < n1; i += 256) {
+  for (int i = tid; i < n1 && prev; i += 256) {
     const int j = m12[i];
     if (j >= 0) {
       prev[2 * i] = kp2[j].x;
@@ -701,7 +705,7 @@ int orbm_hamming_top2(orbm_handle m, const uint8_t* d_A, size_t a_pitch, const i
   if ((a_pitch | b_pitch) & 15) return mfail(ORBX_EINVAL, "pitches must be multiples of 16 bytes");
   MHIP(hipSetDevice(m->device));
   const int rc = launch_hamming_top2(d_A, a_pitch, d_nA, a_cap, d_B, b_pitch, d_nB, pairs, d_best_idx, d_best,
-                                     d_second, stream ? stream : m->stream);
+                                     d_second, stream);
   return rc ? mfail(rc, "launch failed") : ORBX_OK;
 }
 
@@ -728,7 +732,7 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
   while (P.sortn < kp_pitch) P.sortn <<= 1;
   P.cand_cap = m->cand_cap;
   hipLaunchKernelGGL(search_init_kernel, dim3(pairs), dim3(256), init_lds_bytes(P),
-                     (hipStream_t)(stream ? stream : m->stream), P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2,
+                     (hipStream_t)stream, P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2,
                      d_prev_xy, m->cand, m->coff, d_matches12, d_nmatches, m->err);
   MHIP(hipGetLastError());
   return ORBX_OK;

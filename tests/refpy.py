@@ -1,0 +1,347 @@
+"""Second, independent restatement of the reference path in numpy / pure Python.
+
+Used only by tests/test_oracle.py to cross-check the C++ oracle on small
+inputs (it is far too slow for full frames). Each function follows the same
+reference lines as the oracle, written from the reference text again rather
+than from the oracle's code, so a slip in either shows up as a mismatch.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+f32 = np.float32
+
+
+def cv_round(v) -> int:
+    return int(np.rint(v))  # round half to even, like cvRound
+
+
+# -------------------------------------------------------------- resize
+def resize_linear_u8(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    """cv::resize INTER_LINEAR on u8 (OpenCV 3.x scalar fixed point)."""
+    sh, sw = src.shape
+    sx_scale, sy_scale = 1.0 / (dw / sw), 1.0 / (dh / sh)
+    xofs = np.zeros(dw, np.int64)
+    a = np.zeros((dw, 2), np.int64)
+    xmax = dw
+    for dx in range(dw):
+        fx = f32((dx + 0.5) * sx_scale - 0.5)
+        sx = int(math.floor(fx))
+        fx = f32(fx - f32(sx))
+        if sx < 0:
+            fx, sx = f32(0), 0
+        if sx + 1 >= sw:
+            xmax = min(xmax, dx)
+            if sx >= sw - 1:
+                fx, sx = f32(0), sw - 1
+        xofs[dx] = sx
+        a[dx] = (cv_round(f32(f32(1) - fx) * f32(2048)), cv_round(fx * f32(2048)))
+    out = np.zeros((dh, dw), np.uint8)
+    S = src.astype(np.int64)
+    cols = np.arange(dw)
+    inside = cols < xmax
+    nxt = np.minimum(xofs + 1, sw - 1)
+    for dy in range(dh):
+        fy = f32((dy + 0.5) * sy_scale - 0.5)
+        sy = int(math.floor(fy))
+        fy = f32(fy - f32(sy))
+        b0, b1 = cv_round(f32(f32(1) - fy) * f32(2048)), cv_round(fy * f32(2048))
+        rows = []
+        for r in (min(max(sy, 0), sh - 1), min(max(sy + 1, 0), sh - 1)):
+            R = S[r]
+            rows.append(np.where(inside, R[xofs] * a[:, 0] + R[nxt] * a[:, 1], R[xofs] * 2048))
+        out[dy] = np.clip((rows[0] * b0 + rows[1] * b1 + (1 << 21)) >> 22, 0, 255)
+    return out
+
+
+# -------------------------------------------------------------- blur
+GAUSS7 = np.array([18, 34, 49, 55, 49, 34, 18], np.int64)
+
+
+def gaussian_blur7(img: np.ndarray) -> np.ndarray:
+    """GaussianBlur 7x7 sigma 2 BORDER_REFLECT_101, 8U fixed point."""
+    p = np.pad(img.astype(np.int64), 3, mode="reflect")  # numpy 'reflect' == REFLECT_101
+    H, W = img.shape
+    row = sum(GAUSS7[i] * p[:, i:i + W] for i in range(7))
+    col = sum(GAUSS7[i] * row[i:i + H, :] for i in range(7))
+    return np.clip((col + (1 << 15)) >> 16, 0, 255).astype(np.uint8)
+
+
+# -------------------------------------------------------------- FAST
+RING = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3),
+        (0, -3), (-1, -3), (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+
+
+def fast_score(img, x, y, t):
+    """FAST-9 score of OpenCV (largest threshold still detecting, minus 1) or 0."""
+    v = int(img[y, x])
+    d = [v - int(img[y + dy, x + dx]) for dx, dy in RING]
+    best = -1
+    for s in range(16):
+        arc = [d[(s + k) % 16] for k in range(9)]
+        best = max(best, min(arc), -max(arc))
+    # detected at t <=> some arc has all |d| > t in one direction
+    return best - 1 if best - 1 >= t else 0
+
+
+def fast_roi(img, x0, y0, cols, rows, t):
+    """cv::FAST(ROI, t, nonmax=true): keypoints (x, y, score) in ROI coordinates."""
+    sc = np.zeros((rows, cols), np.int64)
+    for i in range(3, rows - 3):
+        for j in range(3, cols - 3):
+            sc[i, j] = fast_score(img, x0 + j, y0 + i, t)
+    out = []
+    for i in range(3, rows - 3):
+        for j in range(3, cols - 3):
+            s = sc[i, j]
+            if s and all(s > sc[i + a, j + b] for a in (-1, 0, 1) for b in (-1, 0, 1) if a or b):
+                out.append((j, i, s))
+    return out
+
+
+def fast_level(img, ini=20, mn=7, W=30.0):
+    """FAST + per-cell grid of ComputeKeyPointsOctTree for one level."""
+    minB = 16
+    maxBX, maxBY = img.shape[1] - 16, img.shape[0] - 16
+    width, height = f32(maxBX - minB), f32(maxBY - minB)
+    nCols, nRows = int(width / f32(W)), int(height / f32(W))
+    wCell, hCell = int(math.ceil(f32(width / f32(nCols)))), int(math.ceil(f32(height / f32(nRows))))
+    keys = []
+    for i in range(nRows):
+        iniY = minB + i * hCell
+        maxY = min(iniY + hCell + 6, maxBY)
+        if iniY >= maxBY - 3:
+            continue
+        for j in range(nCols):
+            iniX = minB + j * wCell
+            maxX = min(iniX + wCell + 6, maxBX)
+            if iniX >= maxBX - 6:
+                continue
+            k = fast_roi(img, iniX, iniY, maxX - iniX, maxY - iniY, ini)
+            if not k:
+                k = fast_roi(img, iniX, iniY, maxX - iniX, maxY - iniY, mn)
+            keys += [(x + j * wCell, y + i * hCell, s) for x, y, s in k]
+    return keys, (minB, maxBX, minB, maxBY)
+
+
+# -------------------------------------------------------------- quadtree
+class _Node:
+    __slots__ = ("x0", "y0", "x1", "y1", "keys", "seq")
+
+    def __init__(self, x0, y0, x1, y1, keys, seq):
+        self.x0, self.y0, self.x1, self.y1, self.keys, self.seq = x0, y0, x1, y1, keys, seq
+
+
+def _divide(n):
+    hx = int(math.ceil(f32(n.x1 - n.x0) / f32(2)))
+    hy = int(math.ceil(f32(n.y1 - n.y0) / f32(2)))
+    mx, my = n.x0 + hx, n.y0 + hy
+    boxes = [(n.x0, n.y0, mx, my), (mx, n.y0, n.x1, my), (n.x0, my, mx, n.y1), (mx, my, n.x1, n.y1)]
+    parts = [[], [], [], []]
+    for k in n.keys:
+        parts[(0 if k[0] < mx else 1) + (0 if k[1] < my else 2)].append(k)
+    return boxes, parts
+
+
+def distribute(keys, minX, maxX, minY, maxY, N):
+    """DistributeOctTree with a Python list as the std::list (front = index 0)."""
+    nIni = int(round(float(f32(maxX - minX) / f32(maxY - minY))))
+    hX = f32(f32(maxX - minX) / f32(nIni))
+    seq = [0]
+
+    def nxt():
+        seq[0] += 1
+        return seq[0]
+
+    roots = [_Node(int(hX * f32(i)), 0, int(hX * f32(i + 1)), maxY - minY, [], nxt()) for i in range(nIni)]
+    for k in keys:
+        roots[int(f32(k[0]) / hX)].keys.append(k)
+    lst = [n for n in roots if n.keys]
+    expand = []
+    phase2 = False
+    while True:
+        prev = len(lst)
+        if not phase2:
+            expand = []
+            new_front, kept = [], []
+            for pos, n in enumerate(lst):
+                # list size right now: pushed children + surviving old nodes (incl. n)
+                if len(new_front) + len(kept) + (len(lst) - pos) >= N:
+                    kept += lst[pos:]
+                    break
+                if len(n.keys) == 1:
+                    kept.append(n)
+                    continue
+                boxes, parts = _divide(n)
+                for b, p in zip(boxes, parts):
+                    if p:
+                        c = _Node(*b, p, nxt())
+                        new_front.insert(0, c)
+                        if len(p) > 1:
+                            expand.append(c)
+            lst = new_front + kept
+            if len(lst) >= N or len(lst) == prev:
+                break
+            if len(lst) + 3 * len(expand) > N:
+                phase2 = True
+        else:
+            order = sorted(expand, key=lambda n: (len(n.keys), n.seq), reverse=True)
+            expand = []
+            for n in order:
+                boxes, parts = _divide(n)
+                for b, p in zip(boxes, parts):
+                    if p:
+                        c = _Node(*b, p, nxt())
+                        lst.insert(0, c)
+                        if len(p) > 1:
+                            expand.append(c)
+                lst.remove(n)
+                if len(lst) >= N:
+                    break
+            if len(lst) >= N or len(lst) == prev:
+                break
+    out = []
+    for n in lst:
+        best = n.keys[0]
+        for k in n.keys[1:]:
+            if k[2] > best[2]:
+                best = k
+        out.append(best)
+    return out
+
+
+# -------------------------------------------------------------- matchers
+def hamming(a, b) -> int:
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+def three_maxima(hist):
+    m = [0, 0, 0]
+    ind = [-1, -1, -1]
+    for i, s in enumerate(hist):
+        if s > m[0]:
+            m = [s, m[0], m[1]]
+            ind = [i, ind[0], ind[1]]
+        elif s > m[1]:
+            m = [m[0], s, m[1]]
+            ind = [ind[0], i, ind[1]]
+        elif s > m[2]:
+            m[2] = s
+            ind[2] = i
+    if m[1] < f32(0.1) * f32(m[0]):
+        ind[1] = ind[2] = -1
+    elif m[2] < f32(0.1) * f32(m[0]):
+        ind[2] = -1
+    return ind
+
+
+def rot_bin(a1, a2):
+    rot = f32(f32(a1) - f32(a2))
+    if rot < 0:
+        rot = f32(rot + f32(360))
+    v = float(f32(rot * f32(f32(1) / f32(30))))
+    b = int(math.floor(v + 0.5))  # round(): half away from zero (v >= 0)
+    return 0 if b == 30 else b
+
+
+def search_for_initialization(kp1, d1, kp2, d2, bounds, prev, r, ratio, check_ori):
+    minX, maxX, minY, maxY = (f32(b) for b in bounds)
+    invW, invH = f32(f32(64) / f32(maxX - minX)), f32(f32(48) / f32(maxY - minY))
+    grid = [[[] for _ in range(48)] for _ in range(64)]
+    for i, k in enumerate(kp2):
+        gx = int(math.floor(float(f32(f32(k["x"]) - minX) * invW) + 0.5))
+        gy = int(math.floor(float(f32(f32(k["y"]) - minY) * invH) + 0.5))
+        if 0 <= gx < 64 and 0 <= gy < 48:
+            grid[gx][gy].append(i)
+    r = f32(r)
+    m12 = [-1] * len(kp1)
+    m21 = [-1] * len(kp2)
+    md = [2 ** 31 - 1] * len(kp2)
+    hist = [[] for _ in range(30)]
+    nm = 0
+    for i1, k1 in enumerate(kp1):
+        if k1["octave"] > 0:
+            continue
+        x, y = f32(prev[i1][0]), f32(prev[i1][1])
+        cx0 = max(0, int(math.floor(f32(f32(x - minX) - r) * invW)))
+        cx1 = min(63, int(math.ceil(f32(f32(x - minX) + r) * invW)))
+        cy0 = max(0, int(math.floor(f32(f32(y - minY) - r) * invH)))
+        cy1 = min(47, int(math.ceil(f32(f32(y - minY) + r) * invH)))
+        if cx0 >= 64 or cx1 < 0 or cy0 >= 48 or cy1 < 0:
+            continue
+        cand = [j for ix in range(cx0, cx1 + 1) for iy in range(cy0, cy1 + 1) for j in grid[ix][iy]
+                if kp2[j]["octave"] == 0 and abs(f32(kp2[j]["x"]) - x) < r and abs(f32(kp2[j]["y"]) - y) < r]
+        best, second, bi = 2 ** 31 - 1, 2 ** 31 - 1, -1
+        for j in cand:
+            d = hamming(d1[i1], d2[j])
+            if md[j] <= d:
+                continue
+            if d < best:
+                second, best, bi = best, d, j
+            elif d < second:
+                second = d
+        if best <= 50 and f32(best) < f32(f32(second) * f32(ratio)):
+            if m21[bi] >= 0:
+                m12[m21[bi]] = -1
+                nm -= 1
+            m12[i1], m21[bi], md[bi] = bi, i1, best
+            nm += 1
+            if check_ori:
+                hist[rot_bin(kp1[i1]["angle"], kp2[bi]["angle"])].append(i1)
+    if check_ori:
+        ind = three_maxima([len(h) for h in hist])
+        for b in range(30):
+            if b in ind:
+                continue
+            for i1 in hist[b]:
+                if m12[i1] >= 0:
+                    m12[i1] = -1
+                    nm -= 1
+    return np.array(m12, np.int32), nm
+
+
+def search_by_bow(dA, angA, mpA, fvA, dB, angB, mpB, fvB, ratio, check_ori, kf_vs_kf):
+    nodesA, offA, idxA = fvA
+    nodesB, offB, idxB = fvB
+    out = [-1] * (len(dA) if kf_vs_kf else len(dB))
+    taken = [False] * len(dB)
+    hist = [[] for _ in range(30)]
+    nm = 0
+    posB = {int(n): k for k, n in enumerate(nodesB)}
+    for ka, n in enumerate(nodesA):
+        kb = posB.get(int(n))
+        if kb is None:
+            continue
+        for i1 in idxA[offA[ka]:offA[ka + 1]]:
+            if not mpA[i1]:
+                continue
+            best, second, bi = 256, 256, -1
+            for i2 in idxB[offB[kb]:offB[kb + 1]]:
+                if taken[i2] or (kf_vs_kf and not mpB[i2]):
+                    continue
+                d = hamming(dA[i1], dB[i2])
+                if d < best:
+                    second, best, bi = best, d, i2
+                elif d < second:
+                    second = d
+            ok = best < 50 if kf_vs_kf else best <= 50
+            if ok and f32(best) < f32(f32(ratio) * f32(second)):
+                taken[bi] = True
+                if kf_vs_kf:
+                    out[i1] = bi
+                else:
+                    out[bi] = i1
+                nm += 1
+                if check_ori:
+                    hist[rot_bin(angA[i1], angB[bi])].append(i1 if kf_vs_kf else bi)
+    if check_ori:
+        ind = three_maxima([len(h) for h in hist])
+        for b in range(30):
+            if b in ind:
+                continue
+            for i in hist[b]:
+                out[i] = -1
+                nm -= 1
+    return np.array(out, np.int32), nm

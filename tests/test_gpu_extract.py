@@ -1,0 +1,233 @@
+"""GPU parity of the HIP extractor (liborbx.so) against the CPU oracle.
+
+Bar: bit-exact keypoints (x, y, size, angle, response, octave, class_id, and
+their order) and descriptor bytes, plus the stage probes (pyramid levels,
+blurred levels, per-cell FAST candidates). All calls go through the C ABI.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("x", "y", "size", "angle", "response", "octave", "class_id")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def assert_same(kp, desc, rkp, rdesc):
+    assert len(kp) == len(rkp), (len(kp), len(rkp))
+    for f in FIELDS:
+        if not np.array_equal(kp[f], rkp[f]):
+            i = int(np.argmax(kp[f] != rkp[f]))
+            raise AssertionError(f"field {f} differs first at {i}: {kp[i]} vs {rkp[i]}")
+    assert np.array_equal(desc, rdesc), f"descriptor rows differ: {np.nonzero((desc != rdesc).any(1))[0][:10]}"
+
+
+def oracle_cfg(O, nf, W, H, **kw):
+    return O.config(nfeatures=nf, width=W, height=H, scale_mode=1 if kw.get("scale_mode") == "F" else 0,
+                    pattern_mode=1 if kw.get("pattern") == "upstream" else 0,
+                    scale_factor=kw.get("scale_factor", 1.2), nlevels=kw.get("nlevels", 8),
+                    ini_th=kw.get("ini", 20), min_th=kw.get("mn", 7))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 9])
+def test_kitti_full_frame_parity(pkg, O, seed):
+    from orb_slam_cuda_amd.synth import synth_frame
+    W, H = 1241, 376
+    img = synth_frame(seed, W, H)
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H)
+    kp, desc = ext(img)
+    rkp, rdesc = O.extract(oracle_cfg(O, 2000, W, H), img)
+    assert_same(kp, desc, rkp, rdesc)
+    assert 1990 <= len(kp) <= 2016
+
+
+def test_stage_probes(pkg, O):
+    from orb_slam_cuda_amd.synth import synth_frame
+    W, H = 1241, 376
+    img = synth_frame(5, W, H)
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H)
+    ext(img)
+    cfg = oracle_cfg(O, 2000, W, H)
+    for l in range(8):
+        assert np.array_equal(ext.level_image(l), O.pyramid_level(cfg, img, l)), f"pyramid {l}"
+        assert np.array_equal(ext.level_image(l, blurred=True), O.blur_level(cfg, img, l)), f"blur {l}"
+        g, r = ext.fast_candidates(l), O.fast_level(cfg, img, l)
+        assert len(g) == len(r)
+        for f in ("x", "y", "response"):
+            assert np.array_equal(g[f], r[f]), f"fast {l} {f}"
+    pyr = ext.mvImagePyramid
+    assert [p.shape for p in pyr] == [(376, 1241), (313, 1034), (261, 862), (218, 718), (181, 598),
+                                      (151, 499), (126, 416), (105, 346)]
+
+
+@pytest.mark.parametrize("name", ["kitti_s0", "euroc_s3"])
+def test_golden_vectors(pkg, name):
+    from orb_slam_cuda_amd.synth import synth_frame
+    g = np.load(os.path.join(GOLDEN, f"extract_{name}.npz"))
+    W, H = int(g["W"]), int(g["H"])
+    img = synth_frame(int(g["seed"]), W, H)
+    assert sha(img) == str(g["image_sha"])
+    ext = pkg.ORBextractor(int(g["nfeatures"]), 1.2, 8, 20, 7, W, H)
+    kp, desc = ext(img)
+    assert np.array_equal(kp.view(np.uint8).reshape(len(kp), 28), g["keypoints"])
+    assert np.array_equal(desc, g["descriptors"])
+    for l in range(8):
+        assert sha(ext.level_image(l)) == g["pyramid_sha"][l]
+        assert sha(ext.level_image(l, blurred=True)) == g["blur_sha"][l]
+        assert len(ext.fast_candidates(l)) == g["fast_counts"][l]
+
+
+@pytest.mark.parametrize("kw", [
+    dict(nf=4000),                                  # the 2x initialisation extractor (Tracking.cc:133)
+    dict(nf=1000, W=752, H=480),                    # EuRoC
+    dict(nf=500),
+    dict(nf=2000, scale_mode="F"),                  # fork's VX ORB-scale override
+    dict(nf=2000, pattern="upstream"),              # upstream BRIEF table
+    dict(nf=1500, nlevels=4),
+    dict(nf=800, scale_factor=2.0, nlevels=4, W=1280, H=720),  # exact 2x: INTER_AREA path
+    dict(nf=1200, scale_factor=1.5, nlevels=5),
+    dict(nf=2000, ini=30, mn=10),
+    dict(nf=2000, ini=5, mn=12),                    # iniTh < minTh
+    dict(nf=0),                                     # no features requested
+])
+def test_config_parity(pkg, O, kw):
+    from orb_slam_cuda_amd.synth import synth_frame
+    W, H, nf = kw.pop("W", 1241), kw.pop("H", 376), kw.pop("nf")
+    img = synth_frame(21, W, H)
+    extra = {k: kw[k] for k in ("scale_mode", "pattern") if k in kw}
+    ext = pkg.ORBextractor(nf, kw.get("scale_factor", 1.2), kw.get("nlevels", 8), kw.get("ini", 20),
+                           kw.get("mn", 7), W, H, **extra)
+    kp, desc = ext(img)
+    rkp, rdesc = O.extract(oracle_cfg(O, nf, W, H, **kw), img)
+    assert_same(kp, desc, rkp, rdesc)
+
+
+def test_dense_noise_uses_global_quadtree_path(pkg, O):
+    # pure noise: tens of thousands of FAST candidates per level, beyond the LDS key budget
+    rng = np.random.default_rng(4)
+    W, H = 1241, 376
+    img = rng.integers(0, 256, size=(H, W), dtype=np.uint8)
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H)
+    kp, desc = ext(img)
+    assert len(ext.fast_candidates(0)) > 10000
+    rkp, rdesc = O.extract(oracle_cfg(O, 2000, W, H), img)
+    assert_same(kp, desc, rkp, rdesc)
+
+
+def test_edge_images(pkg, O):
+    W, H = 640, 360
+    ext = pkg.ORBextractor(1000, 1.2, 8, 20, 7, W, H)
+    cfg = oracle_cfg(O, 1000, W, H)
+    flat = np.full((H, W), 128, np.uint8)
+    kp, desc = ext(flat)
+    assert len(kp) == 0 and desc.shape == (0, 32)
+    # one bright square: only a handful of corners, few quadtree nodes
+    sq = flat.copy()
+    sq[100:140, 200:260] = 250
+    kp, desc = ext(sq)
+    rkp, rdesc = O.extract(cfg, sq)
+    assert_same(kp, desc, rkp, rdesc)
+    assert 0 < len(kp) < 50
+    # saturated extremes
+    ext_img = (np.indices((H, W)).sum(0) % 7 == 0).astype(np.uint8) * 255
+    kp, desc = ext(ext_img)
+    rkp, rdesc = O.extract(cfg, ext_img)
+    assert_same(kp, desc, rkp, rdesc)
+    # empty image: outputs untouched / empty (src/ORBextractor.cc:1542-1543)
+    kp, desc = ext(np.zeros((0, 0), np.uint8))
+    assert len(kp) == 0
+
+
+def test_strided_input_and_replan(pkg, O):
+    from orb_slam_cuda_amd.synth import synth_frame
+    big = synth_frame(8, 1400, 500)
+    view = big[40:40 + 376, 100:100 + 1241]  # non-contiguous rows
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, 1241, 376)
+    kp, desc = ext(view)
+    rkp, rdesc = O.extract(oracle_cfg(O, 2000, 1241, 376), np.ascontiguousarray(view))
+    assert_same(kp, desc, rkp, rdesc)
+    # a different image size on the same handle re-plans (the reference accepts any size)
+    img2 = synth_frame(9, 800, 600)
+    kp, desc = ext(img2)
+    rkp, rdesc = O.extract(oracle_cfg(O, 2000, 800, 600), img2)
+    assert_same(kp, desc, rkp, rdesc)
+    assert ext.levels_info()["w"][0] == 800
+
+
+def test_invalid_inputs_raise(pkg):
+    with pytest.raises(pkg.OrbxError):
+        pkg.ORBextractor(2000, 1.0, 8, 20, 7, 1241, 376)       # scaleFactor must be > 1
+    with pytest.raises(pkg.OrbxError):
+        pkg.ORBextractor(2000, 1.2, 8, 20, 7, 100, 60)         # top levels smaller than one cell
+    ext = pkg.ORBextractor(500, 1.2, 4, 20, 7, 320, 240)
+    with pytest.raises(pkg.OrbxError):
+        ext(np.zeros((240, 320, 3), np.uint8))                 # not CV_8UC1
+
+
+def test_batch_api_matches_single_calls(pkg):
+    from orb_slam_cuda_amd import _lib
+    from orb_slam_cuda_amd.synth import SynthSequence
+    W, H, B = 1241, 376, 6
+    frames = SynthSequence(31, W, H).frames(B)
+    single = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H)
+    ref = [single(f) for f in frames]
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H, max_batch=B)
+    cap = ext.frame_capacity
+    pitch = 1280
+    host = np.zeros((B, H, pitch), np.uint8)
+    host[:, :, :W] = frames
+    d_in = _lib.DeviceArray(host.nbytes)
+    d_in.upload(host)
+    d_kp, d_desc, d_n = _lib.DeviceArray(B * cap * 28), _lib.DeviceArray(B * cap * 32), _lib.DeviceArray(B * 4)
+    s = _lib.Stream()
+    ext.extract_batch_device(d_in.ptr, B, H * pitch, pitch, d_kp.ptr, d_desc.ptr, d_n.ptr, s)
+    s.synchronize()
+    n = d_n.download(B, np.int32)
+    kps = d_kp.download(B * cap, pkg.KP_DTYPE).reshape(B, cap)
+    descs = d_desc.download((B, cap, 32), np.uint8)
+    for i in range(B):
+        assert n[i] == len(ref[i][0])
+        assert np.array_equal(kps[i, :n[i]].view(np.uint8), ref[i][0].view(np.uint8))
+        assert np.array_equal(descs[i, :n[i]], ref[i][1])
+    # determinism across repeated launches
+    ext.extract_batch_device(d_in.ptr, B, H * pitch, pitch, d_kp.ptr, d_desc.ptr, d_n.ptr, s)
+    s.synchronize()
+    assert np.array_equal(d_desc.download((B, cap, 32), np.uint8), descs)
+
+
+def test_full_batch_properties(pkg):
+    """At the bench's full batch size: counts within [N-?, N+16], keypoints inside the
+    image and sorted by octave, descriptors distinct, results invariant to batch position."""
+    from orb_slam_cuda_amd import _lib
+    from orb_slam_cuda_amd.synth import SynthSequence
+    W, H, B = 1241, 376, 64
+    frames = SynthSequence(77, W, H).frames(B)
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H, max_batch=B)
+    cap = ext.frame_capacity
+    host = np.ascontiguousarray(frames)
+    d_in = _lib.DeviceArray(host.nbytes)
+    d_in.upload(host)
+    d_kp, d_desc, d_n = _lib.DeviceArray(B * cap * 28), _lib.DeviceArray(B * cap * 32), _lib.DeviceArray(B * 4)
+    s = _lib.Stream()
+    ext.extract_batch_device(d_in.ptr, B, H * W, W, d_kp.ptr, d_desc.ptr, d_n.ptr, s)
+    s.synchronize()
+    n = d_n.download(B, np.int32)
+    kps = d_kp.download(B * cap, pkg.KP_DTYPE).reshape(B, cap)
+    assert (n >= 1900).all() and (n <= 2016).all()
+    for i in range(B):
+        k = kps[i, :n[i]]
+        assert (np.diff(k["octave"]) >= 0).all()
+        assert (k["x"] >= 0).all() and (k["x"] < W).all() and (k["y"] >= 0).all() and (k["y"] < H).all()
+        assert ((k["angle"] >= 0) & (k["angle"] < 360)).all()
+    # frame 10 alone == frame 10 inside the batch
+    one = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H)
+    kp10, _ = one(frames[10])
+    assert np.array_equal(kps[10, :n[10]].view(np.uint8), kp10.view(np.uint8))

@@ -1,0 +1,58 @@
+"""CPU checks of the C-ABI library: it loads, exports every declared symbol,
+matches the header's struct layouts, and fails loudly without a GPU."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_function():
+    import orb_slam_cuda_amd as pkg
+    L = pkg.lib()
+    names = pkg.header_functions()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_so_is_gfx950_code_object():
+    so = os.path.join(ROOT, "orb_slam_cuda_amd", "liborbx.so")
+    blob = open(so, "rb").read()
+    # the .hip_fatbin bundle names its device code object by target triple
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in blob
+
+
+def test_struct_layouts_match_header():
+    from orb_slam_cuda_amd._lib import KP_DTYPE, GridBounds, OrbxConfig
+    assert KP_DTYPE.itemsize == 28  # cv::KeyPoint
+    assert C.sizeof(OrbxConfig) == 16 * 4
+    assert C.sizeof(GridBounds) == 16
+    hdr = open(os.path.join(ROOT, "include", "orbx_c.h")).read()
+    body = re.search(r"typedef struct orbx_config \{(.*?)\} orbx_config;", hdr, re.S).group(1)
+    ints = sum(int(n) if n else 1 for n in re.findall(r"(?:int|float)\s+[a-z_, ]+?(?:\[(\d+)\])?;", body))
+    assert ints >= 12
+
+
+def test_descriptor_distance_is_host_exact():
+    import numpy as np
+
+    import orb_slam_cuda_amd as pkg
+    D = np.load(os.path.join(ROOT, "tests", "golden", "mapyml_descriptors.npy"))
+    for i in range(0, 775, 37):
+        j = (i * 7 + 3) % 775
+        assert pkg.ORBmatcher.DescriptorDistance(D[i], D[j]) == int(np.unpackbits(D[i] ^ D[j]).sum())
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="only meaningful without a GPU")
+def test_no_gpu_fails_loudly():
+    import orb_slam_cuda_amd as pkg
+    with pytest.raises(pkg.OrbxError):
+        pkg.ORBextractor(2000, 1.2, 8, 20, 7, 1241, 376)
+    with pytest.raises(pkg.OrbxError):
+        pkg.ORBmatcher(0.9, True)
