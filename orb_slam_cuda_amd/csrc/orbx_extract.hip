@@ -98,13 +98,17 @@ __global__ __launch_bounds__(256) void pyr_resize_kernel(
 }
 
 // ------------------------------------------------------------ blur
-// Separable 7-tap fixed-point Gaussian with BORDER_REFLECT_101 at the level
-// edges; tile 64 x 16 outputs per 256-thread block, input tile in LDS.
-constexpr int kBlurTW = 64, kBlurTH = 16;
+// Separable 7-tap fixed-point Gaussian, BORDER_REFLECT_101 at the level edges.
+// Tile = 128 x 32 outputs per 256-thread block. The input tile (+3 halo, 16-B
+// aligned: columns [x0-16, x0+144)) is staged with 16-byte loads (byte loads
+// with reflection only where a chunk leaves the image); the row pass keeps
+// u16 sums (max 257*255 = 65535); each thread then produces a 4 x 4 output
+// block from a sliding column window and stores 4 bytes per row.
+constexpr int kBlurTW = 128, kBlurTH = 32, kBlurInW = kBlurTW + 32;
 __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp, uint8_t* __restrict__ blur) {
-  __shared__ uint8_t in[kBlurTH + 6][kBlurTW + 8];
-  __shared__ int tmp[kBlurTH + 6][kBlurTW];
-  const int f = blockIdx.y;
+  __shared__ __attribute__((aligned(16))) uint8_t in[kBlurTH + 6][kBlurInW];
+  __shared__ __attribute__((aligned(16))) uint16_t tmp[kBlurTH + 6][kBlurTW];
+  const int f = blockIdx.y, tid = threadIdx.x;
   int t = blockIdx.x, l = 0;
   for (; l < P.L; ++l) {
     const LevelGeom& g = P.lv[l];
@@ -114,35 +118,91 @@ __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp
   }
   if (l >= P.L) return;
   const LevelGeom& g = P.lv[l];
-  const int tx = (g.w + kBlurTW - 1) / kBlurTW;
+  const int W = g.w, H = g.h;
+  const int tx = (W + kBlurTW - 1) / kBlurTW;
   const int x0 = (t % tx) * kBlurTW, y0 = (t / tx) * kBlurTH;
   const uint8_t* S = lp.base[l] + f * lp.fstride[l];
   const int pitch = lp.pitch[l];
-  for (int i = threadIdx.x; i < (kBlurTH + 6) * (kBlurTW + 6); i += 256) {
-    const int r = i / (kBlurTW + 6), c = i % (kBlurTW + 6);
-    int gy = y0 + r - 3, gx = x0 + c - 3;
-    gy = min(max(gy, -(g.h - 1)), 2 * g.h - 2);
-    gx = min(max(gx, -(g.w - 1)), 2 * g.w - 2);
-    in[r][c] = S[(long long)reflect101(gy, g.h) * pitch + reflect101(gx, g.w)];
+  // stage rows y0-3 .. y0+TH+2, columns x0-16 .. x0+TW+15
+  constexpr int kChunks = kBlurInW / 16;
+  for (int i = tid; i < (kBlurTH + 6) * kChunks; i += 256) {
+    const int r = i / kChunks, ch = i - r * kChunks;
+    const int gy = reflect101(min(max(y0 + r - 3, -(H - 1)), 2 * H - 2), H);
+    const int gx = x0 - 16 + ch * 16;
+    const uint8_t* src = S + (long long)gy * pitch;
+    uint4 v;
+    if (gx >= 0 && gx + 16 <= W && (((uintptr_t)(src + gx)) & 15) == 0) {
+      v = *(const uint4*)(src + gx);
+    } else {
+      uint8_t b[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int xx = min(max(gx + k, -(W - 1)), 2 * W - 2);
+        b[k] = src[reflect101(xx, W)];
+      }
+      v = *(const uint4*)b;
+    }
+    *(uint4*)&in[r][ch * 16] = v;
   }
   __syncthreads();
   const int* k = P.gauss;
-  for (int i = threadIdx.x; i < (kBlurTH + 6) * kBlurTW; i += 256) {
-    const int r = i / kBlurTW, c = i % kBlurTW;
-    int acc = 0;
+  // row pass: 4 outputs per item, input bytes [x+13, x+23) of the staged row
+  for (int i = tid; i < (kBlurTH + 6) * (kBlurTW / 4); i += 256) {
+    const int r = i / (kBlurTW / 4), x = (i - r * (kBlurTW / 4)) * 4;
+    const uint32_t w0 = *(const uint32_t*)&in[r][x + 12];
+    const uint32_t w1 = *(const uint32_t*)&in[r][x + 16];
+    const uint32_t w2 = *(const uint32_t*)&in[r][x + 20];
+    int px[12];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) acc += k[j] * in[r][c + j];
-    tmp[r][c] = acc;
+    for (int j = 0; j < 4; ++j) {
+      px[j] = (w0 >> (8 * j)) & 255;
+      px[4 + j] = (w1 >> (8 * j)) & 255;
+      px[8 + j] = (w2 >> (8 * j)) & 255;
+    }
+    uint32_t o01 = 0, o23 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int acc = 0;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) acc += k[j] * px[q + 1 + j];
+      if (q < 2) o01 |= (uint32_t)acc << (16 * q);
+      else o23 |= (uint32_t)acc << (16 * (q - 2));
+    }
+    *(uint2*)&tmp[r][x] = make_uint2(o01, o23);
   }
   __syncthreads();
-  uint8_t* D = blur + g.off + f * g.plane;
-  for (int i = threadIdx.x; i < kBlurTH * kBlurTW; i += 256) {
-    const int r = i / kBlurTW, c = i % kBlurTW;
-    if (y0 + r >= g.h || x0 + c >= g.w) continue;
-    int acc = 0;
+  // column pass: thread -> 4 columns x 4 rows
+  const int cx = (tid & 31) * 4, ry = (tid >> 5) * 4;
+  int col[10][4];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) acc += k[j] * tmp[r + j][c];
-    D[(long long)(y0 + r) * g.pitch + x0 + c] = (uint8_t)sat_u8((acc + (1 << 15)) >> 16);
+  for (int j = 0; j < 10; ++j) {
+    const uint2 v = *(const uint2*)&tmp[ry + j][cx];
+    col[j][0] = v.x & 0xFFFF;
+    col[j][1] = v.x >> 16;
+    col[j][2] = v.y & 0xFFFF;
+    col[j][3] = v.y >> 16;
+  }
+  uint8_t* D = blur + g.off + f * g.plane;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int y = y0 + ry + rr;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int acc = 0;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) acc += k[j] * col[rr + j][q];
+      packed |= (uint32_t)sat_u8((acc + (1 << 15)) >> 16) << (8 * q);
+    }
+    if (y < H) {
+      const int x = x0 + cx;
+      uint8_t* dst = D + (long long)y * g.pitch + x;
+      if (x + 4 <= W) {
+        *(uint32_t*)dst = packed;
+      } else {
+        for (int q = 0; q < 4 && x + q < W; ++q) dst[q] = (uint8_t)(packed >> (8 * q));
+      }
+    }
   }
 }
 
@@ -191,19 +251,25 @@ __device__ __forceinline__ bool has_arc9(uint32_t m) {
   return (a & 0xFFFFu) != 0;
 }
 
-// One wavefront per (frame, grid cell): the cell ROI (<= 65 x 65 with the
-// 3-px FAST halo) is staged in LDS; every band pixel gets its FAST score at
-// t_low (one score map serves both thresholds: detected-at-t <=> score >= t);
-// non-max suppression sees only the cell's own band (neighbours outside it
-// are 0), exactly like cv::FAST run on the ROI; the iniThFAST pass falls back
-// to minThFAST when it finds nothing. Survivors are compacted in row-major
-// order with ballots into the cell's fixed slot range.
+// One wavefront per (frame, grid cell). The cell ROI (<= 65 x 65 with the
+// 3-px FAST halo) is staged in LDS; lanes cover the detection band as
+// 2 rows x 32 columns (band width <= 32, every KITTI/EuRoC level) or
+// 1 row x 64 columns. Every band pixel gets its FAST score at t_low (one
+// score map serves both thresholds: detected-at-t <=> score >= t); a pixel
+// fails fast unless two of the four compass ring pixels agree (any 9-arc
+// covers two of them). Non-max suppression sees only the cell's own band
+// (neighbours outside it are 0), exactly like cv::FAST on the ROI; one pass
+// records the survivors at iniThFAST and at minThFAST as row-major ballots,
+// the cell keeps the iniThFAST set unless it is empty, and the survivors are
+// written in row-major order into the cell's fixed slot range.
+constexpr int kMaxBallots = 64;
 __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPtrs lp,
                                                         const CellGeom* __restrict__ cells,
                                                         uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_counts) {
   __shared__ uint8_t roi[kMaxRoi * kMaxRoi];
   __shared__ uint8_t sc[(kMaxRoi - 4) * (kMaxRoi - 4)];
+  __shared__ uint64_t s_ball[2][kMaxBallots];
   const int cell = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
   const CellGeom cg = cells[cell];
   int* cnt = cell_counts + (long long)f * P.ncells_total + cell;
@@ -215,65 +281,93 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
   }
   const int l = cg.level;
   const LevelGeom& g = P.lv[l];
-  const uint8_t* S = lp.base[l] + f * lp.fstride[l] + (long long)cg.r0 * lp.pitch[l] + cg.c0;
   const int pitch = lp.pitch[l];
-  for (int i = lane; i < rw * rh; i += 64) {
-    const int r = i / rw, c = i - r * rw;
-    roi[i] = S[(long long)r * pitch + c];
+  const uint8_t* S = lp.base[l] + f * lp.fstride[l] + (long long)cg.r0 * pitch + cg.c0;
+  // stage the ROI: lanes = columns
+#pragma unroll 4
+  for (int r = 0; r < rh; ++r) {
+    if (lane < rw) roi[r * rw + lane] = S[(long long)r * pitch + lane];
+    if (lane + 64 < rw) roi[r * rw + lane + 64] = S[(long long)r * pitch + lane + 64];
   }
   const int sw = bw + 2;  // score map with a zero ring
   for (int i = lane; i < sw * (bh + 2); i += 64) sc[i] = 0;
   __syncthreads();
+  const bool two = bw <= 32;
+  const int lr = two ? (lane >> 5) : 0, lc = two ? (lane & 31) : lane;
+  const int rstep = two ? 2 : 1;
   const int t = P.t_low;
-  for (int p = lane; p < bw * bh; p += 64) {
-    const int by = p / bw, bx = p - by * bw;
-    const uint8_t* c0 = roi + (by + 3) * rw + (bx + 3);
+  for (int by = lr; by < bh; by += rstep) {
+    if (lc >= bw) continue;
+    const uint8_t* c0 = roi + (by + 3) * rw + (lc + 3);
     const int v = c0[0];
-    int d[16];
-    uint32_t dark = 0, bright = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      constexpr int rx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-      constexpr int ry[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-      const int x = c0[ry[k] * rw + rx[k]];
-      d[k] = v - x;
-      dark |= (uint32_t)(x < v - t) << k;
-      bright |= (uint32_t)(x > v + t) << k;
-    }
+    // compass points k = 0, 4, 8, 12: (0,3) (3,0) (0,-3) (-3,0)
+    const int n0 = c0[3 * rw], n4 = c0[3], n8 = c0[-3 * rw], n12 = c0[-3];
+    const int lo = v - t, hi = v + t;
+    const int nd = (n0 < lo) + (n4 < lo) + (n8 < lo) + (n12 < lo);
+    const int nb = (n0 > hi) + (n4 > hi) + (n8 > hi) + (n12 > hi);
     int s = 0;
-    if (has_arc9(dark) || has_arc9(bright)) s = corner_score16(d, t);
-    sc[(by + 1) * sw + bx + 1] = (uint8_t)s;
+    if (nd >= 2 || nb >= 2) {
+      int d[16];
+      uint32_t dark = 0, bright = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        constexpr int rx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+        constexpr int ry[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+        const int x = c0[ry[k] * rw + rx[k]];
+        d[k] = v - x;
+        dark |= (uint32_t)(x < lo) << k;
+        bright |= (uint32_t)(x > hi) << k;
+      }
+      if (has_arc9(dark) || has_arc9(bright)) s = corner_score16(d, t);
+    }
+    sc[(by + 1) * sw + lc + 1] = (uint8_t)s;
   }
   __syncthreads();
-  // NMS at a threshold: neighbours below it count as 0 (not detected there).
-  auto is_kp = [&](int p, int th) -> bool {
-    const int by = p / bw, bx = p - by * bw;
-    const uint8_t* q = sc + (by + 1) * sw + bx + 1;
-    const int s = q[0];
-    if (s < th || s == 0) return false;
-    auto nb = [&](int o) { const int x = q[o]; return x >= th ? x : 0; };
-    return s > nb(-1) && s > nb(1) && s > nb(-sw - 1) && s > nb(-sw) && s > nb(-sw + 1) &&
-           s > nb(sw - 1) && s > nb(sw) && s > nb(sw + 1);
-  };
+  // NMS at both thresholds in one pass; neighbours below a threshold count as 0
+  const int ti = P.t_ini, tm = P.t_min;
+  const int nit = (bh + rstep - 1) / rstep;
   int n_ini = 0;
-  for (int p0 = 0; p0 < bw * bh; p0 += 64) {
-    const int p = p0 + lane;
-    const bool k = p < bw * bh && is_kp(p, P.t_ini);
-    n_ini += __popcll(__ballot(k));
+  for (int it = 0; it < nit; ++it) {
+    const int by = it * rstep + lr;
+    bool ki = false, km = false;
+    if (by < bh && lc < bw) {
+      const uint8_t* q = sc + (by + 1) * sw + lc + 1;
+      const int s = q[0];
+      if (s > 0) {
+        int m = 0;  // max neighbour
+        const int nbv[8] = {q[-1], q[1], q[-sw - 1], q[-sw], q[-sw + 1], q[sw - 1], q[sw], q[sw + 1]};
+        bool gi = s >= ti, gm = s >= tm;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int x = nbv[j];
+          if (x >= ti && x >= s) gi = false;
+          if (x >= tm && x >= s) gm = false;
+          m = max(m, x);
+        }
+        (void)m;
+        ki = gi;
+        km = gm;
+      }
+    }
+    const uint64_t bi = __ballot(ki), bm = __ballot(km);
+    if (lane == 0) {
+      s_ball[0][it] = bi;
+      s_ball[1][it] = bm;
+    }
+    n_ini += __popcll(bi);
   }
-  const int th = n_ini > 0 ? P.t_ini : P.t_min;
+  __syncthreads();
+  const int which = n_ini > 0 ? 0 : 1;
   uint32_t* out = slots + (long long)f * P.slots_per_frame + cg.slot_off;
   int base = 0;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int p0 = 0; p0 < bw * bh; p0 += 64) {
-    const int p = p0 + lane;
-    const bool k = p < bw * bh && is_kp(p, th);
-    const uint64_t m = __ballot(k);
-    if (k) {
-      const int by = p / bw, bx = p - by * bw;
+  for (int it = 0; it < nit; ++it) {
+    const uint64_t m = s_ball[which][it];
+    if ((m >> lane) & 1ull) {
+      const int by = it * rstep + lr;
       const int pos = base + __popcll(m & lt);
-      const int x = cg.c0 + 3 + bx - g.minBX, y = cg.r0 + 3 + by - g.minBY;
-      const int score = sc[(by + 1) * sw + bx + 1];
+      const int x = cg.c0 + 3 + lc - g.minBX, y = cg.r0 + 3 + by - g.minBY;
+      const int score = sc[(by + 1) * sw + lc + 1];
       if (pos < cg.cap) out[pos] = pack_key(x, y, score);
     }
     base += __popcll(m);

@@ -135,11 +135,15 @@ struct InitParams {
   float nnratio;
   int check_ori;
   int kp_pitch;
-  int sortn;       // pow2 >= kp_pitch
-  long long cand_cap;
+  int sortn;        // pow2 >= kp_pitch (LDS sort capacity)
+  int cand_lds;     // candidate entries kept in LDS
+  long long cand_cap;  // global candidate entries per pair (fallback)
 };
 
-// Frame::PosInGrid (src/Frame.cc:381-391)
+constexpr int kInitThreads = 512;
+constexpr int kInitWaves = kInitThreads / 64;
+
+// Frame::PosInGrid (src/Frame.cc:381-391): round() of a float (half away from zero)
 __device__ __forceinline__ bool pos_in_grid(float x, float y, const InitParams& P, int* gx, int* gy) {
   const int px = (int)roundf(__fmul_rn(__fsub_rn(x, P.minX), P.invW));
   const int py = (int)roundf(__fmul_rn(__fsub_rn(y, P.minY), P.invH));
@@ -148,9 +152,10 @@ __device__ __forceinline__ bool pos_in_grid(float x, float y, const InitParams& 
   return !(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows);
 }
 
-__device__ int block_scan_excl256(int* a, int n, int* s_tmp) {
+template <int NT>
+__device__ int block_scan_excl(int* a, int n, int* s_tmp) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int per = (n + 255) / 256;
+  const int per = (n + NT - 1) / NT;
   const int b = min(tid * per, n), e = min(b + per, n);
   int sum = 0;
   for (int i = b; i < e; ++i) sum += a[i];
@@ -164,7 +169,7 @@ __device__ int block_scan_excl256(int* a, int n, int* s_tmp) {
   __syncthreads();
   int wpre = 0, total = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NT / 64; ++i) {
     const int v = s_tmp[i];
     if (i < w) wpre += v;
     total += v;
@@ -179,15 +184,73 @@ __device__ int block_scan_excl256(int* a, int n, int* s_tmp) {
   return total;
 }
 
-__global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const orbx_kp* __restrict__ kp1_all,
-                                                          const uint8_t* __restrict__ desc1_all,
-                                                          const int* __restrict__ n1_all,
-                                                          const orbx_kp* __restrict__ kp2_all,
-                                                          const uint8_t* __restrict__ desc2_all,
-                                                          const int* __restrict__ n2_all, float* __restrict__ prev_all,
-                                                          uint32_t* __restrict__ cand_all, int* __restrict__ coff_all,
-                                                          int* __restrict__ matches_all, int* __restrict__ nmatches,
-                                                          int* err) {
+// The candidate window of one query, flattened: per grid column ix in
+// [cx0, cx1] the sorted-grid range of cells [cy0, cy1] is contiguous, so a
+// candidate is (column, offset). Lanes 0..ncol-1 hold one column each.
+struct Window {
+  bool ok;
+  float x, y;
+  int cx0, ncol, total;
+  int col_start;  // per lane: first sorted position of its column
+  int col_pre;    // per lane: inclusive prefix of column lengths
+};
+
+__device__ __forceinline__ Window make_window(float x, float y, const InitParams& P, const int* s_cell) {
+  Window w;
+  w.ok = false;
+  w.x = x;
+  w.y = y;
+  w.total = 0;
+  const float r = P.r;
+  const int lane = threadIdx.x & 63;
+  const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, P.minX), r), P.invW)));
+  const int nMaxCellX = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, P.minX), r), P.invW)));
+  const int nMinCellY = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, P.minY), r), P.invH)));
+  const int nMaxCellY = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, P.minY), r), P.invH)));
+  if (nMinCellX >= kGridCols || nMaxCellX < 0 || nMinCellY >= kGridRows || nMaxCellY < 0) return w;
+  w.ok = true;
+  w.cx0 = nMinCellX;
+  w.ncol = max(0, nMaxCellX - nMinCellX + 1);
+  int len = 0;
+  w.col_start = 0;
+  if (lane < w.ncol) {
+    const int ix = nMinCellX + lane;
+    w.col_start = s_cell[ix * kGridRows + nMinCellY];
+    len = max(0, s_cell[ix * kGridRows + nMaxCellY + 1] - w.col_start);
+  }
+  int x2 = len;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(x2, off, 64);
+    if (lane >= off) x2 += t;
+  }
+  w.col_pre = x2;
+  w.total = __shfl(x2, 63, 64);
+  return w;
+}
+
+// sorted-grid position of flat candidate f (0 <= f < total)
+__device__ __forceinline__ int window_pos(const Window& w, int f) {
+  // column c = number of columns whose inclusive prefix <= f
+  int c = 0;
+#pragma unroll 1
+  for (int step = 32; step > 0; step >>= 1) {
+    const int probe = c + step - 1;
+    const int pre = __shfl(w.col_pre, min(probe, 63), 64);
+    if (probe < w.ncol && pre <= f) c += step;
+  }
+  // every lane must take part in a cross-lane read (the source lane of a
+  // bpermute must be active), so no shuffle sits under a lane-varying branch
+  const int pre_prev = __shfl(w.col_pre, max(c - 1, 0), 64);
+  const int start = __shfl(w.col_start, c, 64);
+  return start + (f - (c ? pre_prev : 0));
+}
+
+__global__ __launch_bounds__(kInitThreads) void search_init_kernel(
+    InitParams P, const orbx_kp* __restrict__ kp1_all, const uint8_t* __restrict__ desc1_all,
+    const int* __restrict__ n1_all, const orbx_kp* __restrict__ kp2_all, const uint8_t* __restrict__ desc2_all,
+    const int* __restrict__ n2_all, float* __restrict__ prev_all, uint32_t* __restrict__ cand_all,
+    int* __restrict__ matches_all, int* __restrict__ nmatches, int* err) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n1 = n1_all[pr], n2 = n2_all[pr];
@@ -198,46 +261,54 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
   // prev_all == nullptr: windows centred on F1's own keypoints, the initial
   // mvbPrevMatched of Tracking::MonocularInitialization (src/Tracking.cc:645-647)
   float* prev = prev_all ? prev_all + (long long)pr * P.kp_pitch * 2 : nullptr;
-  auto px = [&](int i) { return prev ? prev[2 * i] : kp1[i].x; };
-  auto py = [&](int i) { return prev ? prev[2 * i + 1] : kp1[i].y; };
   int* m12 = matches_all + (long long)pr * P.kp_pitch;
-  int* coff = coff_all + (long long)pr * (P.kp_pitch + 1);
-  uint32_t* cand = cand_all + (long long)pr * P.cand_cap;
 
   unsigned char* sp = smem;
   auto take = [&](size_t bytes) { unsigned char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
-  uint32_t* s_sort = (uint32_t*)take(4ull * P.sortn);
-  int* s_cell = (int*)take(4ull * (kGridCols * kGridRows + 1));  // first sorted entry of each cell
-  int* s_md = (int*)take(4ull * P.kp_pitch);                      // vMatchedDistance
-  int* s_m21 = (int*)take(4ull * P.kp_pitch);                     // vnMatches21
-  int* s_bin = (int*)take(4ull * P.kp_pitch);                     // rotation bin per i1 or -1
+  uint32_t* s_sort = (uint32_t*)take(4ull * P.sortn);   // (cell << 16 | compact idx), sorted
+  float2* s_xy = (float2*)take(8ull * P.kp_pitch);      // F2 keypoint positions (octave 0)
+  int* s_cell = (int*)take(4ull * (kGridCols * kGridRows + 1));
+  int* s_md = (int*)take(4ull * P.kp_pitch);            // vMatchedDistance
+  int* s_m21 = (int*)take(4ull * P.kp_pitch);           // vnMatches21
+  int* s_bin = (int*)take(4ull * P.kp_pitch);           // rotation bin per i1 or -1
+  int* s_coff = (int*)take(4ull * (P.kp_pitch + 1));    // candidate offsets per i1
   int* s_tmp = (int*)take(64);
   int* s_var = (int*)take(64);
   int* s_hist = (int*)take(4 * 32);
+  uint32_t* s_cand = (uint32_t*)take(4ull * P.cand_lds);
 
-  // ---- grid of F2 restricted to octave 0 (the only level SearchForInitialization asks for)
-  for (int i = tid; i < P.sortn; i += 256) {
-    uint32_t key = 0xFFFFFFFFu;
-    if (i < n2) {
-      const orbx_kp k = kp2[i];
-      int gx, gy;
-      if (k.octave == 0 && pos_in_grid(k.x, k.y, P, &gx, &gy)) key = ((uint32_t)(gx * kGridRows + gy) << 16) | (uint32_t)i;
-    }
-    s_sort[i] = key;
-  }
-  for (int i = tid; i < n2; i += 256) {
+  // ---- octave-0 keypoints of F2 with a valid grid cell (the only ones
+  // GetFeaturesInArea(.., 0, 0) can return); slot order is irrelevant because
+  // the keys (cell << 16 | index) are sorted next.
+  if (tid == 0) s_var[5] = 0;
+  for (int i = tid; i < n2; i += kInitThreads) {
     s_md[i] = INT_MAX;
     s_m21[i] = -1;
   }
-  for (int i = tid; i < n1; i += 256) {
+  for (int i = tid; i < n1; i += kInitThreads) {
     s_bin[i] = -1;
     m12[i] = -1;
   }
   if (tid < 32) s_hist[tid] = 0;
   __syncthreads();
-  for (int kk = 2; kk <= P.sortn; kk <<= 1) {
+  for (int i = tid; i < n2; i += kInitThreads) {
+    const orbx_kp k = kp2[i];
+    int gx, gy;
+    if (k.octave == 0 && pos_in_grid(k.x, k.y, P, &gx, &gy)) {
+      s_xy[i] = make_float2(k.x, k.y);
+      s_sort[atomicAdd(&s_var[5], 1)] = ((uint32_t)(gx * kGridRows + gy) << 16) | (uint32_t)i;
+    }
+  }
+  __syncthreads();
+  const int n0 = s_var[5];
+  int sortn = 1;
+  while (sortn < n0) sortn <<= 1;
+  for (int i = n0 + tid; i < sortn; i += kInitThreads) s_sort[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  // bitonic sort of n0 keys (ascending): grid order cell-major, then index
+  for (int kk = 2; kk <= sortn; kk <<= 1) {
     for (int j = kk >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < P.sortn; i += 256) {
+      for (int i = tid; i < sortn; i += kInitThreads) {
         const int ixj = i ^ j;
         if (ixj > i) {
           const uint32_t a = s_sort[i], b = s_sort[ixj];
@@ -252,8 +323,8 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
     }
   }
   // s_cell[c] = first sorted position with cell >= c (lower bound)
-  for (int c = tid; c <= kGridCols * kGridRows; c += 256) {
-    int lo = 0, hi = P.sortn;
+  for (int c = tid; c <= kGridCols * kGridRows; c += kInitThreads) {
+    int lo = 0, hi = n0;
     const uint32_t key = (uint32_t)c << 16;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -264,89 +335,89 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
   }
   __syncthreads();
 
-  // ---- candidate windows (Frame::GetFeaturesInArea, minLevel = maxLevel = 0)
-  auto window = [&](int i1, int* cx0, int* cx1, int* cy0, int* cy1) -> bool {
-    const float x = px(i1), y = py(i1), r = P.r;
-    const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, P.minX), r), P.invW)));
-    if (nMinCellX >= kGridCols) return false;
-    const int nMaxCellX = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, P.minX), r), P.invW)));
-    if (nMaxCellX < 0) return false;
-    const int nMinCellY = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, P.minY), r), P.invH)));
-    if (nMinCellY >= kGridRows) return false;
-    const int nMaxCellY = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, P.minY), r), P.invH)));
-    if (nMaxCellY < 0) return false;
-    *cx0 = nMinCellX;
-    *cx1 = nMaxCellX;
-    *cy0 = nMinCellY;
-    *cy1 = nMaxCellY;
-    return true;
+  auto center = [&](int i1, float* x, float* y) {
+    if (prev) {
+      *x = prev[2 * i1];
+      *y = prev[2 * i1 + 1];
+    } else {
+      const orbx_kp k = kp1[i1];
+      *x = k.x;
+      *y = k.y;
+    }
   };
-  // enumerate candidate k (0-based, reference order) of query i1 -> sorted position
-  // pass 1: counts
-  for (int i1 = wv; i1 < n1; i1 += 4) {
+  // ---- pass 1: candidate counts per query (Frame::GetFeaturesInArea, octave 0)
+  for (int i1 = wv; i1 < n1; i1 += kInitWaves) {
     int cnt = 0;
-    int cx0, cx1, cy0, cy1;
-    if (kp1[i1].octave == 0 && window(i1, &cx0, &cx1, &cy0, &cy1)) {
-      const float x = px(i1), y = py(i1);
-      for (int ix = cx0; ix <= cx1; ++ix) {
-        const int s0 = s_cell[ix * kGridRows + cy0], s1 = s_cell[ix * kGridRows + cy1 + 1];
-        for (int s = s0 + lane; s < s1; s += 64) {
-          const orbx_kp k = kp2[s_sort[s] & 0xFFFF];
-          cnt += (fabsf(__fsub_rn(k.x, x)) < P.r && fabsf(__fsub_rn(k.y, y)) < P.r) ? 1 : 0;
+    if (kp1[i1].octave == 0) {
+      float x, y;
+      center(i1, &x, &y);
+      const Window w = make_window(x, y, P, s_cell);
+      if (w.ok) {
+        for (int f0 = 0; f0 < w.total; f0 += 64) {
+          const int f = f0 + lane;
+          const int s = window_pos(w, min(f, w.total - 1));
+          if (f < w.total) {
+            const float2 q = s_xy[s_sort[s] & 0xFFFF];
+            cnt += (fabsf(__fsub_rn(q.x, x)) < P.r && fabsf(__fsub_rn(q.y, y)) < P.r) ? 1 : 0;
+          }
         }
       }
     }
     cnt = wave_sum_i(cnt);
-    if (lane == 0) coff[i1] = cnt;
+    if (lane == 0) s_coff[i1] = cnt;
   }
   __syncthreads();
-  if (tid == 0) coff[n1] = 0;
+  if (tid == 0) s_coff[n1] = 0;
   __syncthreads();
-  const int total = block_scan_excl256(coff, n1 + 1, s_tmp);
-  if (total > P.cand_cap) {
+  const int total = block_scan_excl<kInitThreads>(s_coff, n1 + 1, s_tmp);
+  if (total > P.cand_lds && total > P.cand_cap) {
     if (tid == 0) atomicOr(err, 8);
     return;
   }
-  // pass 2: fill (candidate order preserved by ballot compaction) + distances
-  for (int i1 = wv; i1 < n1; i1 += 4) {
-    int cx0, cx1, cy0, cy1;
-    if (!(kp1[i1].octave == 0 && window(i1, &cx0, &cx1, &cy0, &cy1))) continue;
-    const float x = px(i1), y = py(i1);
+  uint32_t* cand = total <= P.cand_lds ? s_cand : cand_all + (long long)pr * P.cand_cap;
+  // ---- pass 2: fill candidates (reference order) with their Hamming distances
+  for (int i1 = wv; i1 < n1; i1 += kInitWaves) {
+    if (s_coff[i1 + 1] == s_coff[i1]) continue;
+    float x, y;
+    center(i1, &x, &y);
+    const Window w = make_window(x, y, P, s_cell);
     const uint4* d1 = (const uint4*)(desc1 + (long long)i1 * 32);
     const uint4 a0 = d1[0], a1 = d1[1];
-    int base = coff[i1];
+    int base = s_coff[i1];
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (int ix = cx0; ix <= cx1; ++ix) {
-      const int s0 = s_cell[ix * kGridRows + cy0], s1 = s_cell[ix * kGridRows + cy1 + 1];
-      for (int sb = s0; sb < s1; sb += 64) {
-        const int s = sb + lane;
-        bool ok = false;
-        int i2 = 0;
-        if (s < s1) {
-          i2 = (int)(s_sort[s] & 0xFFFF);
-          const orbx_kp k = kp2[i2];
-          ok = fabsf(__fsub_rn(k.x, x)) < P.r && fabsf(__fsub_rn(k.y, y)) < P.r;
-        }
-        const uint64_t m = __ballot(ok);
-        if (ok) {
-          const uint4* d2 = (const uint4*)(desc2 + (long long)i2 * 32);
-          const int d = hamming256(a0, a1, d2[0], d2[1]);
-          cand[base + __popcll(m & lt)] = (uint32_t)i2 | ((uint32_t)d << 23);
-        }
-        base += __popcll(m);
+    for (int f0 = 0; f0 < w.total; f0 += 64) {
+      const int f = f0 + lane;
+      const int s = window_pos(w, min(f, w.total - 1));
+      bool ok = false;
+      int i2 = 0;
+      if (f < w.total) {
+        i2 = (int)(s_sort[s] & 0xFFFF);
+        const float2 q = s_xy[i2];
+        ok = fabsf(__fsub_rn(q.x, x)) < P.r && fabsf(__fsub_rn(q.y, y)) < P.r;
       }
+      const uint64_t m = __ballot(ok);
+      if (ok) {
+        const uint4* d2 = (const uint4*)(desc2 + (long long)i2 * 32);
+        const int d = hamming256(a0, a1, d2[0], d2[1]);
+        cand[base + __popcll(m & lt)] = (uint32_t)i2 | ((uint32_t)d << 23);
+      }
+      base += __popcll(m);
     }
   }
   __syncthreads();
-  // pass 3: greedy resolution in i1 order (one wavefront)
+  // ---- pass 3: greedy resolution in i1 order (one wavefront; LDS state)
   if (wv == 0) {
     volatile int* md = s_md;
     volatile int* m21 = s_m21;
     int nm = 0;
     const float factor = 1.0f / kHistoLength;
-    for (int i1 = 0; i1 < n1; ++i1) {
-      const int c0 = coff[i1], c1 = coff[i1 + 1];
-      if (c0 == c1) continue;
+    for (int q0 = 0; q0 < n1; q0 += 64) {
+     // queries of this chunk that have candidates, visited in index order
+     uint64_t todo = __ballot(q0 + lane < n1 && s_coff[q0 + lane + 1] > s_coff[q0 + lane]);
+     while (todo) {
+      const int i1 = q0 + __ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      const int c0 = s_coff[i1], c1 = s_coff[i1 + 1];
       Top2 acc{INT_MAX, -1, INT_MAX};
       for (int cb = c0; cb < c1; cb += 64) {
         const int c = cb + lane;
@@ -359,7 +430,6 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
           valid = !(md[i2] <= dist);
         }
         const Top2 t = wave_top2(valid, dist, i2);
-        // merge chunk (later) into acc (earlier)
         const int nb = min(acc.best, t.best);
         const int npos = (acc.best <= t.best) ? acc.pos : t.pos;
         const int nsec = min(min(max(acc.best, t.best), acc.second), t.second);
@@ -390,13 +460,14 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
       }
+     }
     }
     if (lane == 0) s_var[0] = nm;
   }
   __syncthreads();
   // rotation consistency (ComputeThreeMaxima src/ORBmatcher.cc:1601-1642)
   if (P.check_ori) {
-    for (int i = tid; i < n1; i += 256)
+    for (int i = tid; i < n1; i += kInitThreads)
       if (s_bin[i] >= 0) atomicAdd(&s_hist[s_bin[i]], 1);
     __syncthreads();
     if (tid == 0) {
@@ -423,11 +494,10 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
       s_var[1] = ind1;
       s_var[2] = ind2;
       s_var[3] = ind3;
-      s_var[4] = 0;
     }
     __syncthreads();
     const int ind1 = s_var[1], ind2 = s_var[2], ind3 = s_var[3];
-    for (int i = tid; i < n1; i += 256) {
+    for (int i = tid; i < n1; i += kInitThreads) {
       const int b = s_bin[i];
       if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
       if (m12[i] >= 0) {
@@ -438,7 +508,7 @@ __global__ __launch_bounds__(256) void search_init_kernel(InitParams P, const or
     __syncthreads();
   }
   // vbPrevMatched update
-  for (int i = tid; i < n1 && prev; i += 256) {
+  for (int i = tid; i < n1 && prev; i += kInitThreads) {
     const int j = m12[i];
     if (j >= 0) {
       prev[2 * i] = kp2[j].x;
@@ -592,10 +662,12 @@ int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_c
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
+constexpr size_t kInitLdsBudget = 160 * 1024 - 512;
 static size_t init_lds_bytes(const InitParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-  return r16(4ull * P.sortn) + r16(4ull * (kGridCols * kGridRows + 1)) + 3 * r16(4ull * P.kp_pitch) + 2 * r16(64) +
-         r16(128);
+  return r16(4ull * P.sortn) + r16(8ull * P.kp_pitch) + r16(4ull * (kGridCols * kGridRows + 1)) +
+         3 * r16(4ull * P.kp_pitch) + r16(4ull * (P.kp_pitch + 1)) + 2 * r16(64) + r16(128) +
+         r16(4ull * P.cand_lds);
 }
 
 }  // namespace orbx
@@ -669,12 +741,8 @@ int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out) {
     return mfail(ORBX_ENOMEM, "matcher workspace allocation failed");
   }
   (void)hipMemset(m->err, 0, 16);
-  const int lds = (int)init_lds_bytes(InitParams{0, 0, 0, 0, 0, 0, 0, 0, 0, max_kps, m->sortn, 0});
-  if (lds > 160 * 1024) {
-    orbm_destroy(m);
-    return mfail(ORBX_EINVAL, "max_kps too large for the LDS grid");
-  }
-  (void)hipFuncSetAttribute((const void*)search_init_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  (void)hipFuncSetAttribute((const void*)search_init_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kInitLdsBudget);
   *out = m;
   return ORBX_OK;
 }
@@ -731,9 +799,14 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
   P.sortn = 1;
   while (P.sortn < kp_pitch) P.sortn <<= 1;
   P.cand_cap = m->cand_cap;
-  hipLaunchKernelGGL(search_init_kernel, dim3(pairs), dim3(256), init_lds_bytes(P),
+  P.cand_lds = 0;
+  if (init_lds_bytes(P) > kInitLdsBudget)
+    return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization's LDS grid (max ~5000)",
+                 kp_pitch);
+  P.cand_lds = (int)((kInitLdsBudget - init_lds_bytes(P)) / 4) & ~15;
+  hipLaunchKernelGGL(search_init_kernel, dim3(pairs), dim3(kInitThreads), init_lds_bytes(P),
                      (hipStream_t)stream, P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2,
-                     d_prev_xy, m->cand, m->coff, d_matches12, d_nmatches, m->err);
+                     d_prev_xy, m->cand, d_matches12, d_nmatches, m->err);
   MHIP(hipGetLastError());
   return ORBX_OK;
 }

@@ -82,7 +82,7 @@ class ORBmatcher:
     HISTO_LENGTH = 30  # :39
 
     def __init__(self, nnratio: float = 0.6, checkOri: bool = True, *, device: int = 0,
-                 max_pairs: int = 1, max_kps: int = 8192):
+                 max_pairs: int = 1, max_kps: int = 4096):
         self.mfNNratio = float(nnratio)
         self.mbCheckOrientation = bool(checkOri)
         self.device = device
