@@ -1,0 +1,247 @@
+// orbx_fast.hip — FAST-9/16 per grid cell with per-cell non-max suppression.
+//
+// Reference: ComputeKeyPointsOctTree's FAST stage (src/ORBextractor.cc:1258-1298)
+// calls cv::FAST(ROI, iniThFAST, nonmax) on every cell ROI (cell + 3-px halo
+// on each side) and, if that finds nothing, cv::FAST(ROI, minThFAST). FAST on
+// a ROI only scores pixels in [3, n-3) of the ROI and its 3x3 NMS sees 0 for
+// everything outside that band, so suppression is per cell; cells' bands
+// tile the level exactly.
+//
+// One wavefront per (frame, cell). The ROI is staged in LDS (16-byte loads
+// when the level is 16-byte aligned), then a three-step funnel keeps lanes
+// busy on the pixels that matter:
+//   (a) every band pixel: centre + 4 compass ring pixels; a 9-arc always
+//       covers two compass points, so pixels without two agreeing compass
+//       points cannot be corners at t_low = min(iniTh, minTh);
+//   (b) survivors: full 16-pixel ring test (9 contiguous darker/brighter);
+//   (c) detected pixels: OpenCV's cornerScore<16> (the largest threshold at
+//       which the pixel is still detected, minus 1), written to a score map.
+// One score map serves both thresholds because a pixel is detected at t iff
+// its score is >= t. NMS then visits only detected pixels, records the
+// survivors at iniThFAST and minThFAST as ballots, keeps the iniThFAST set
+// unless it is empty, and writes the keys in row-major order (the order
+// cv::FAST emits them) into the cell's fixed slot range. Every compaction is
+// an ordered ballot compaction, so row-major order is preserved throughout.
+#include "orbx_device.cuh"
+
+namespace orbx {
+
+constexpr int kRoiStride = 80;  // >= 65-px ROI + 15 bytes of 16-B alignment slack
+
+// FAST-9/16 "cornerScore<16>" of OpenCV 3.x, d[k] = v - ring[k].
+__device__ __forceinline__ int corner_score16(const int (&d)[16], int threshold) {
+  auto D = [&](int k) { return d[k & 15]; };
+  int a0 = threshold;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int a = min(D(k + 1), D(k + 2));
+    a = min(a, D(k + 3));
+    if (a <= a0) continue;
+    a = min(a, D(k + 4));
+    a = min(a, D(k + 5));
+    a = min(a, D(k + 6));
+    a = min(a, D(k + 7));
+    a = min(a, D(k + 8));
+    a0 = max(a0, min(a, D(k)));
+    a0 = max(a0, min(a, D(k + 9)));
+  }
+  int b0 = -a0;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int b = max(D(k + 1), D(k + 2));
+    b = max(b, D(k + 3));
+    b = max(b, D(k + 4));
+    b = max(b, D(k + 5));
+    if (b >= b0) continue;
+    b = max(b, D(k + 6));
+    b = max(b, D(k + 7));
+    b = max(b, D(k + 8));
+    b0 = min(b0, max(b, D(k)));
+    b0 = min(b0, max(b, D(k + 9)));
+  }
+  return -b0 - 1;
+}
+
+// 9 contiguous set bits in a circular 16-bit mask
+__device__ __forceinline__ bool has_arc9(uint32_t m) {
+  const uint32_t x = m | (m << 16);
+  uint32_t a = x & (x >> 1);  // runs of 2
+  a &= a >> 2;                // runs of 4
+  a &= a >> 4;                // runs of 8
+  a &= x >> 8;                // runs of 9
+  return (a & 0xFFFFu) != 0;
+}
+
+// Bresenham ring of radius 3, k = 0..15 (cv::makeOffsets, pattern 16)
+__device__ __forceinline__ int ring_off(int k) {
+  constexpr int rx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+  constexpr int ry[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+  return ry[k] * kRoiStride + rx[k];
+}
+
+__device__ __forceinline__ void ring_masks(const uint8_t* c, int lo, int hi, uint32_t* dark, uint32_t* bright) {
+  uint32_t dk = 0, br = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int x = c[ring_off(k)];
+    dk |= (uint32_t)(x < lo) << k;
+    br |= (uint32_t)(x > hi) << k;
+  }
+  *dark = dk;
+  *bright = br;
+}
+
+__global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPtrs lp,
+                                                        const CellGeom* __restrict__ cells,
+                                                        uint32_t* __restrict__ slots,
+                                                        int* __restrict__ cell_counts) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int cell = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+  const CellGeom cg = cells[cell];
+  int* cnt = cell_counts + (long long)f * P.ncells_total + cell;
+  const int rw = cg.c1 - cg.c0, rh = cg.r1 - cg.r0;
+  const int bw = rw - 6, bh = rh - 6;
+  if (cg.cap == 0 || bw <= 0 || bh <= 0) {
+    if (lane == 0) *cnt = 0;
+    return;
+  }
+  unsigned char* sp = smem;
+  auto take = [&](size_t bytes) { unsigned char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
+  uint8_t* roi = (uint8_t*)take((size_t)P.fast_rh_max * kRoiStride);
+  uint8_t* sc = (uint8_t*)take((size_t)(P.fast_bw_max + 2) * (P.fast_bh_max + 2));
+  uint16_t* list = (uint16_t*)take(2ull * P.fast_bw_max * P.fast_bh_max);
+  uint64_t* ball = (uint64_t*)take(16ull * ((P.fast_bw_max * P.fast_bh_max + 63) / 64));
+
+  const int l = cg.level;
+  const LevelGeom& g = P.lv[l];
+  const int pitch = lp.pitch[l];
+  const uint8_t* rows = lp.base[l] + f * lp.fstride[l] + (long long)cg.r0 * pitch;
+  const int a0 = cg.c0 & ~15, ox = cg.c0 - a0;
+  if (lp.aligned16[l]) {
+    const int nch = (cg.c1 - a0 + 15) >> 4;
+    for (int i = lane; i < rh * nch; i += 64) {
+      const int r = i / nch, ch = i - r * nch;
+      *(uint4*)(roi + r * kRoiStride + ch * 16) = *(const uint4*)(rows + (long long)r * pitch + a0 + ch * 16);
+    }
+  } else {
+    for (int r = 0; r < rh; ++r)
+      for (int c = lane; c < rw; c += 64) roi[r * kRoiStride + ox + c] = rows[(long long)r * pitch + cg.c0 + c];
+  }
+  const int sw = bw + 2;  // score map with a zero ring
+  for (int i = lane; i < sw * (bh + 2); i += 64) sc[i] = 0;
+  __syncthreads();
+
+  const int t = P.t_low;
+  const uint64_t lt = lanemask_lt(lane);
+  const bool two = bw <= 32;  // 2 rows x 32 lanes, else 1 row x 64 lanes (bw <= 59)
+  const int lr = two ? (lane >> 5) : 0, lc = two ? (lane & 31) : lane;
+  const int rstep = two ? 2 : 1;
+  const uint8_t* band = roi + 3 * kRoiStride + ox + 3;  // band pixel (0,0)
+
+  // (a) compass pre-test over all band pixels, row-major ordered compaction
+  int n1 = 0;
+  for (int by0 = 0; by0 < bh; by0 += rstep) {
+    const int by = by0 + lr;
+    bool flag = false;
+    if (by < bh && lc < bw) {
+      const uint8_t* c = band + by * kRoiStride + lc;
+      const int v = c[0], lo = v - t, hi = v + t;
+      const int n0 = c[3 * kRoiStride], n4 = c[3], n8 = c[-3 * kRoiStride], n12 = c[-3];
+      const int nd = (n0 < lo) + (n4 < lo) + (n8 < lo) + (n12 < lo);
+      const int nb = (n0 > hi) + (n4 > hi) + (n8 > hi) + (n12 > hi);
+      flag = nd >= 2 || nb >= 2;
+    }
+    const uint64_t m = __ballot(flag);
+    if (flag) list[n1 + __popcll(m & lt)] = (uint16_t)((by << 8) | lc);
+    n1 += __popcll(m);
+  }
+  // (b) full ring test, compacted in place (reads of a chunk precede its writes)
+  int n2 = 0;
+  for (int i0 = 0; i0 < n1; i0 += 64) {
+    const int i = i0 + lane;
+    const int e = i < n1 ? list[i] : 0;
+    bool det = false;
+    if (i < n1) {
+      const uint8_t* c = band + (e >> 8) * kRoiStride + (e & 255);
+      const int v = c[0];
+      uint32_t dk, br;
+      ring_masks(c, v - t, v + t, &dk, &br);
+      det = has_arc9(dk) || has_arc9(br);
+    }
+    const uint64_t m = __ballot(det);
+    if (det) list[n2 + __popcll(m & lt)] = (uint16_t)e;
+    n2 += __popcll(m);
+  }
+  // (c) FAST scores of the detected pixels
+  for (int i = lane; i < n2; i += 64) {
+    const int e = list[i];
+    const uint8_t* c = band + (e >> 8) * kRoiStride + (e & 255);
+    const int v = c[0];
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = v - c[ring_off(k)];
+    sc[((e >> 8) + 1) * sw + (e & 255) + 1] = (uint8_t)corner_score16(d, t);
+  }
+  __syncthreads();
+  // (d) 3x3 NMS at both thresholds (neighbours below a threshold count as 0)
+  const int ti = P.t_ini, tm = P.t_min;
+  const int nch2 = (n2 + 63) >> 6;
+  int n_ini = 0;
+  for (int ch = 0; ch < nch2; ++ch) {
+    const int i = ch * 64 + lane;
+    bool ki = false, km = false;
+    if (i < n2) {
+      const int e = list[i];
+      const uint8_t* q = sc + ((e >> 8) + 1) * sw + (e & 255) + 1;
+      const int s = q[0];
+      bool gi = s >= ti && s > 0, gm = s >= tm && s > 0;
+      const int nbv[8] = {q[-1], q[1], q[-sw - 1], q[-sw], q[-sw + 1], q[sw - 1], q[sw], q[sw + 1]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int x = nbv[j];
+        if (x >= ti && x >= s) gi = false;
+        if (x >= tm && x >= s) gm = false;
+      }
+      ki = gi;
+      km = gm;
+    }
+    const uint64_t bi = __ballot(ki), bm = __ballot(km);
+    if (lane == 0) {
+      ball[2 * ch] = bi;
+      ball[2 * ch + 1] = bm;
+    }
+    n_ini += __popcll(bi);
+  }
+  __syncthreads();
+  const int which = n_ini > 0 ? 0 : 1;
+  uint32_t* out = slots + (long long)f * P.slots_per_frame + cg.slot_off;
+  int base = 0;
+  for (int ch = 0; ch < nch2; ++ch) {
+    const uint64_t m = ball[2 * ch + which];
+    if ((m >> lane) & 1ull) {
+      const int e = list[ch * 64 + lane];
+      const int by = e >> 8, bx = e & 255;
+      const int pos = base + __popcll(m & lt);
+      const int x = cg.c0 + 3 + bx - g.minBX, y = cg.r0 + 3 + by - g.minBY;
+      if (pos < cg.cap) out[pos] = pack_key(x, y, sc[(by + 1) * sw + bx + 1]);
+    }
+    base += __popcll(m);
+  }
+  if (lane == 0) *cnt = min(base, (int)cg.cap);
+}
+
+size_t fast_lds_bytes(const ExtractParams& P) {
+  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  const size_t band = (size_t)P.fast_bw_max * P.fast_bh_max;
+  return r16((size_t)P.fast_rh_max * kRoiStride) + r16((size_t)(P.fast_bw_max + 2) * (P.fast_bh_max + 2)) +
+         r16(2 * band) + r16(16 * ((band + 63) / 64));
+}
+
+int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cells, uint32_t* slots,
+                int* cell_counts, int batch, hipStream_t s) {
+  hipLaunchKernelGGL(fast_cells_kernel, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P, lp, cells,
+                     slots, cell_counts);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+}  // namespace orbx

@@ -255,6 +255,11 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
         cg.r1 = (int16_t)(int)maxY;
         const int bw = cg.c1 - cg.c0 - 6, bh = cg.r1 - cg.r0 - 6;
         cg.cap = (skip || bw <= 0 || bh <= 0) ? 0 : (int16_t)(((bw + 1) / 2) * ((bh + 1) / 2));
+        if (cg.cap) {
+          P.fast_rh_max = std::max(P.fast_rh_max, cg.r1 - cg.r0);
+          P.fast_bw_max = std::max(P.fast_bw_max, bw);
+          P.fast_bh_max = std::max(P.fast_bh_max, bh);
+        }
         cg.slot_off = slot;
         slot += cg.cap;
         pl.cells.push_back(cg);
@@ -281,6 +286,20 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     if (l >= 1) {
       std::vector<int2> xt, yt;
       resize_tables(P.lv[l - 1].w, P.lv[l - 1].h, g.w, g.h, xt, yt, &g.xmax, &g.area2x);
+      // the pyramid kernel stages each 16 x 256 output tile's source footprint
+      // in a 36 x 576 LDS tile (orbx_pyramid.hip): true for scaleFactor <= 2
+      for (int x0 = 0; x0 < g.w; x0 += 256) {
+        const int xe = std::min(x0 + 255, g.w - 1);
+        const int lo = g.area2x ? 2 * x0 : xt[x0].x, hi = g.area2x ? 2 * xe + 1 : xt[xe].x + 1;
+        if (hi - (lo & ~15) + 16 > 576)
+          return fail(ORBX_EINVAL, "scaleFactor %g too large for the pyramid tile (max 2.0)", c.scale_factor);
+      }
+      for (int y0 = 0; y0 < g.h; y0 += 16) {
+        const int ye = std::min(y0 + 15, g.h - 1);
+        const int lo = g.area2x ? 2 * y0 : (yt[y0].x & 0xFFFF), hi = g.area2x ? 2 * ye + 1 : (yt[ye].x >> 16);
+        if (hi - lo + 1 > 36)
+          return fail(ORBX_EINVAL, "scaleFactor %g too large for the pyramid tile (max 2.0)", c.scale_factor);
+      }
       g.xtab = (int)pl.rtab.size();
       pl.rtab.insert(pl.rtab.end(), xt.begin(), xt.end());
       g.ytab = (int)pl.rtab.size();

@@ -60,6 +60,8 @@ struct ExtractParams {
   int maxnodes, sortn;         // quadtree node-table size, bitonic size (pow2)
   int max_cells_level;         // largest ncells of any level
   int kcap_lds;                // quadtree keys kept in LDS up to this count
+  int fast_rh_max;             // largest FAST cell ROI height
+  int fast_bw_max, fast_bh_max;  // largest FAST detection band
   int pattern_upstream;
   int gauss[7];                // 7-tap Gaussian fixed-point kernel (sum 257)
   LevelGeom lv[kMaxLevels];
@@ -70,6 +72,7 @@ struct LevelPtrs {
   const uint8_t* base[kMaxLevels];
   long long fstride[kMaxLevels];  // bytes between frames
   int pitch[kMaxLevels];          // bytes between rows
+  int aligned16[kMaxLevels];      // base, pitch and frame stride all 16-byte aligned
 };
 
 __host__ __device__ inline uint32_t pack_key(int x, int y, int score) {

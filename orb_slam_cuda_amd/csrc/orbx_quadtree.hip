@@ -1,0 +1,331 @@
+// orbx_quadtree.hip — DistributeOctTree (src/ORBextractor.cc:889-1120).
+//
+// The reference keeps the quadtree as a std::list<ExtractorNode>: nIni root
+// columns; then rounds that split every multi-key node in list order,
+// pushing the non-empty children n1..n4 to the FRONT of the list and erasing
+// the parent, until the list holds >= N nodes or a round changes nothing;
+// once the next full round would overshoot N it switches to splitting the
+// previous round's children in (size, heap-address) descending order, again
+// stopping as soon as the list reaches N. Each node finally keeps its
+// max-response key (first in key order on ties).
+//
+// Data-parallel restatement (one 256-thread workgroup per frame x level):
+// the list is a node table indexed by list position; keys never move, each
+// key carries its node index. A round is "split a prefix of the candidate
+// sequence": candidates = nodes with > 1 key, taken in list order (breadth
+// rounds) or sorted by (size desc, creation desc) (sorted rounds; creation
+// order stands in for the reference's heap-pointer tie-break, the same rule
+// the oracle uses); the prefix ends where the running list size reaches N.
+// The new list is [children of the split nodes, last split first, each as
+// n4 n3 n2 n1] followed by the untouched nodes in their old order, which is
+// exactly what the reference's push_front/erase sequence produces.
+#include "orbx_device.cuh"
+
+namespace orbx {
+
+struct QNode {
+  int16_t x0, y0, x1, y1;
+};
+
+__device__ __forceinline__ void halves(const QNode& nd, int* mx, int* my) {
+  // DivideNode: halfX = ceil((UR.x-UL.x)/2) in float (src/ORBextractor.cc:833-834)
+  *mx = nd.x0 + (int)ceilf(__fdiv_rn((float)(nd.x1 - nd.x0), 2.f));
+  *my = nd.y0 + (int)ceilf(__fdiv_rn((float)(nd.y1 - nd.y0), 2.f));
+}
+
+__device__ __forceinline__ int quadrant(const QNode& nd, int kx, int ky) {
+  int mx, my;
+  halves(nd, &mx, &my);
+  return (kx >= mx ? 1 : 0) + (ky >= my ? 2 : 0);  // 0=n1 1=n2 2=n3 3=n4
+}
+
+__device__ __forceinline__ QNode child_box(const QNode& nd, int q) {
+  int mx, my;
+  halves(nd, &mx, &my);
+  QNode c;
+  c.x0 = (q & 1) ? mx : nd.x0;
+  c.x1 = (q & 1) ? nd.x1 : mx;
+  c.y0 = (q & 2) ? my : nd.y0;
+  c.y1 = (q & 2) ? nd.y1 : my;
+  return c;
+}
+
+__device__ __forceinline__ int nonempty(int4 c) { return (c.x > 0) + (c.y > 0) + (c.z > 0) + (c.w > 0); }
+
+__global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, const int* __restrict__ cell_counts,
+                                                              const uint32_t* __restrict__ slots,
+                                                              const CellGeom* __restrict__ cells,
+                                                              uint32_t* __restrict__ qscratch,
+                                                              uint16_t* __restrict__ qnscratch,
+                                                              uint32_t* __restrict__ qkeys,
+                                                              int* __restrict__ qcounts, int* err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+  const LevelGeom& g = P.lv[l];
+  const int MN = P.maxnodes, SN = P.sortn;
+  unsigned char* p = smem;
+  auto take = [&](size_t bytes) { unsigned char* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
+  unsigned long long* s_sort = (unsigned long long*)take(8ull * SN);  // also best-key-per-node
+  QNode* nodeA = (QNode*)take(sizeof(QNode) * MN);
+  QNode* nodeB = (QNode*)take(sizeof(QNode) * MN);
+  int* nkA = (int*)take(4ull * MN);
+  int* nkB = (int*)take(4ull * MN);
+  int* seqA = (int*)take(4ull * MN);
+  int* seqB = (int*)take(4ull * MN);
+  int4* cc = (int4*)take(16ull * MN);  // child key counts, then child list positions
+  int* tA = (int*)take(4ull * (MN + 1));
+  int* tB = (int*)take(4ull * (MN + 1));
+  int* rank = (int*)take(4ull * MN);   // processing rank of a split node, or -1
+  int* ord = (int*)take(4ull * MN);    // processing rank -> node
+  int* coff = (int*)take(4ull * (P.max_cells_level + 1));
+  int* s_tmp = (int*)take(64);
+  int* s_var = (int*)take(64);
+  uint32_t* lkeys = (uint32_t*)take(4ull * P.kcap_lds);
+  uint16_t* lnode = (uint16_t*)take(2ull * P.kcap_lds);
+
+  // ---- the level's FAST keys in reference order (cells row-major, FAST order inside)
+  const int* cntp = cell_counts + (long long)f * P.ncells_total + g.cell0;
+  for (int c = tid; c < g.ncells; c += kQtThreads) coff[c] = cntp[c];
+  __syncthreads();
+  const int K = block_scan_excl<kQtThreads>(coff, g.ncells, s_tmp);
+  uint32_t* keys = lkeys;
+  uint16_t* knode = lnode;
+  if (K > P.kcap_lds) {  // too many for LDS: same algorithm on an L2-resident scratch copy
+    keys = qscratch + (long long)f * P.slots_per_frame + g.slot0;
+    knode = qnscratch + (long long)f * P.slots_per_frame + g.slot0;
+  }
+  const uint32_t* fslots = slots + (long long)f * P.slots_per_frame;
+  {
+    const int wv = tid >> 6, lane = tid & 63;
+    for (int c = wv; c < g.ncells; c += kQtThreads / 64) {
+      const int n = cntp[c], o = coff[c];
+      const uint32_t* src = fslots + cells[g.cell0 + c].slot_off;
+      for (int i = lane; i < n; i += 64) keys[o + i] = src[i];
+    }
+  }
+  // ---- root nodes: nIni columns of width hX (src/ORBextractor.cc:894-936)
+  const int nIni = g.nIni;
+  int* rootCnt = tA;  // nIni <= MN
+  for (int i = tid; i < nIni; i += kQtThreads) rootCnt[i] = 0;
+  __syncthreads();
+  for (int k = tid; k < K; k += kQtThreads) {
+    const int r = (int)__fdiv_rn((float)key_x(keys[k]), g.hX);  // vpIniNodes[kp.pt.x/hX]
+    knode[k] = (uint16_t)r;
+    atomicAdd(&rootCnt[r], 1);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int n = 0;
+    for (int i = 0; i < nIni; ++i) {
+      const int c = rootCnt[i];
+      if (c > 0) {
+        QNode nd;
+        nd.x0 = (int16_t)(int)__fmul_rn(g.hX, (float)i);
+        nd.x1 = (int16_t)(int)__fmul_rn(g.hX, (float)(i + 1));
+        nd.y0 = 0;
+        nd.y1 = (int16_t)g.boxH;
+        nodeA[n] = nd;
+        nkA[n] = c;
+        seqA[n] = 0;
+        rootCnt[i] = n++;
+      } else {
+        rootCnt[i] = -1;  // empty roots are erased
+      }
+    }
+    s_var[0] = n;  // list size
+    s_var[1] = 0;  // sorted-phase flag
+  }
+  __syncthreads();
+  for (int k = tid; k < K; k += kQtThreads) knode[k] = (uint16_t)rootCnt[knode[k]];
+  __syncthreads();
+
+  const int N = g.N;
+  for (int round = 0; round < 64; ++round) {
+    const int size = s_var[0];
+    const bool sorted_phase = s_var[1] != 0;
+    // child key counts of every splittable node
+    for (int n = tid; n < size; n += kQtThreads) cc[n] = make_int4(0, 0, 0, 0);
+    __syncthreads();
+    for (int k = tid; k < K; k += kQtThreads) {
+      const int n = knode[k];
+      if (nkA[n] > 1) {
+        const uint32_t kk = keys[k];
+        atomicAdd(((int*)&cc[n]) + quadrant(nodeA[n], key_x(kk), key_y(kk)), 1);
+      }
+    }
+    __syncthreads();
+    // processing order and cut-off: split while the list size is < N
+    if (!sorted_phase) {
+      for (int n = tid; n < size; n += kQtThreads) {
+        const bool cand = nkA[n] > 1;
+        tA[n] = cand ? nonempty(cc[n]) - 1 : 0;
+        tB[n] = cand ? 1 : 0;
+      }
+      __syncthreads();
+      block_scan_excl<kQtThreads>(tA, size, s_tmp);
+      block_scan_excl<kQtThreads>(tB, size, s_tmp);
+      if (tid == 0) s_var[2] = 0;
+      __syncthreads();
+      for (int n = tid; n < size; n += kQtThreads) {
+        if (nkA[n] > 1 && size + tA[n] < N) {
+          rank[n] = tB[n];
+          ord[tB[n]] = n;
+          atomicAdd(&s_var[2], 1);
+        } else {
+          rank[n] = -1;
+        }
+      }
+    } else {
+      for (int i = tid; i < SN; i += kQtThreads) {
+        unsigned long long key = 0;
+        if (i < size && nkA[i] > 1)
+          key = ((unsigned long long)nkA[i] << 40) | ((unsigned long long)seqA[i] << 16) | (unsigned long long)i;
+        s_sort[i] = key;
+        if (i < size) rank[i] = -1;
+      }
+      if (tid == 0) s_var[3] = 0;
+      __syncthreads();
+      for (int kk = 2; kk <= SN; kk <<= 1) {  // bitonic sort, descending
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+          for (int i = tid; i < SN; i += kQtThreads) {
+            const int ixj = i ^ j;
+            if (ixj > i) {
+              const unsigned long long a = s_sort[i], b = s_sort[ixj];
+              const bool desc = (i & kk) == 0;
+              if (desc ? (a < b) : (a > b)) {
+                s_sort[i] = b;
+                s_sort[ixj] = a;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      for (int j = tid; j < size; j += kQtThreads) {
+        const unsigned long long key = s_sort[j];
+        tA[j] = key ? nonempty(cc[(int)(key & 0xFFFF)]) - 1 : 0;
+        if (key) atomicAdd(&s_var[3], 1);
+      }
+      __syncthreads();
+      const int ncand = s_var[3];
+      block_scan_excl<kQtThreads>(tA, ncand, s_tmp);
+      if (tid == 0) s_var[2] = 0;
+      __syncthreads();
+      for (int j = tid; j < ncand; j += kQtThreads) {
+        if (size + tA[j] < N) {
+          const int n = (int)(s_sort[j] & 0xFFFF);
+          rank[n] = j;
+          ord[j] = n;
+          atomicAdd(&s_var[2], 1);
+        }
+      }
+    }
+    __syncthreads();
+    const int m = s_var[2];  // nodes split this round
+    // children block: processing rank j lands at T - (E_j + C_j) (last split first)
+    for (int j = tid; j < m; j += kQtThreads) tA[j] = nonempty(cc[ord[j]]);
+    __syncthreads();
+    const int T = block_scan_excl<kQtThreads>(tA, m, s_tmp);
+    for (int n = tid; n < size; n += kQtThreads) tB[n] = rank[n] < 0 ? 1 : 0;
+    __syncthreads();
+    const int nKept = block_scan_excl<kQtThreads>(tB, size, s_tmp);
+    const int newSize = T + nKept;
+    if (tid == 0) s_var[4] = 0;
+    __syncthreads();
+    // new node table; cc[n] becomes the list positions of split node n's children
+    for (int n = tid; n < size; n += kQtThreads) {
+      const int j = rank[n];
+      if (j < 0) {
+        const int pos = T + tB[n];
+        nodeB[pos] = nodeA[n];
+        nkB[pos] = nkA[n];
+        seqB[pos] = seqA[n];
+      } else {
+        const int4 c = cc[n];
+        const int cnts[4] = {c.x, c.y, c.z, c.w};
+        const int base = T - (tA[j] + nonempty(c));
+        int pos4[4];
+        int after = 0, expand = 0;
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+          if (cnts[q] > 0) {
+            pos4[q] = base + after++;
+            nodeB[pos4[q]] = child_box(nodeA[n], q);
+            nkB[pos4[q]] = cnts[q];
+            seqB[pos4[q]] = j * 4 + q;  // creation order: split rank, then n1..n4
+            expand += cnts[q] > 1;
+          } else {
+            pos4[q] = -1;
+          }
+        }
+        cc[n] = make_int4(pos4[0], pos4[1], pos4[2], pos4[3]);
+        if (expand) atomicAdd(&s_var[4], expand);
+      }
+    }
+    __syncthreads();
+    // re-home the keys
+    for (int k = tid; k < K; k += kQtThreads) {
+      const int n = knode[k];
+      const int j = rank[n];
+      if (j < 0) {
+        knode[k] = (uint16_t)(T + tB[n]);
+      } else {
+        const uint32_t kk = keys[k];
+        knode[k] = (uint16_t)((const int*)&cc[n])[quadrant(nodeA[n], key_x(kk), key_y(kk))];
+      }
+    }
+    __syncthreads();
+    for (int n = tid; n < newSize; n += kQtThreads) {
+      nodeA[n] = nodeB[n];
+      nkA[n] = nkB[n];
+      seqA[n] = seqB[n];
+    }
+    // finish when the list reached N or a round changed nothing (src/ORBextractor.cc:1011, 1093);
+    // the breadth phase ends once one more full round would overshoot N (:1015)
+    const bool finish = newSize >= N || newSize == size;
+    const int nExp = s_var[4];
+    __syncthreads();
+    if (tid == 0) {
+      if (!finish && !sorted_phase && newSize + 3 * nExp > N) s_var[1] = 1;
+      s_var[0] = newSize;
+    }
+    __syncthreads();
+    if (finish) break;
+    if (round == 63 && tid == 0) atomicOr(err, 2);
+  }
+  // ---- keep the best key per node: max FAST score, first in node (= original) order
+  const int size = s_var[0];
+  for (int n = tid; n < size; n += kQtThreads) s_sort[n] = 0;
+  __syncthreads();
+  for (int k = tid; k < K; k += kQtThreads) {
+    const unsigned long long v =
+        ((unsigned long long)key_score(keys[k]) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)k);
+    atomicMax(&s_sort[knode[k]], v);
+  }
+  __syncthreads();
+  uint32_t* out = qkeys + (long long)f * P.kp_per_frame + g.kbase;
+  for (int n = tid; n < size && n < g.kcap; n += kQtThreads)
+    out[n] = keys[0xFFFFFFFFu - (uint32_t)(s_sort[n] & 0xFFFFFFFFull)];
+  if (tid == 0) {
+    qcounts[f * P.L + l] = min(size, g.kcap);
+    if (size > g.kcap) atomicOr(err, 4);
+  }
+}
+
+size_t quadtree_lds_bytes(const ExtractParams& P) {
+  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  const size_t MN = P.maxnodes, SN = P.sortn;
+  return r16(8 * SN) + 2 * r16(sizeof(QNode) * MN) + 4 * r16(4 * MN) + r16(16 * MN) + 2 * r16(4 * (MN + 1)) +
+         2 * r16(4 * MN) + r16(4 * (P.max_cells_level + 1)) + 2 * r16(64) + r16(4ull * P.kcap_lds) +
+         r16(2ull * P.kcap_lds);
+}
+
+const void* quadtree_kernel_ptr() { return (const void*)quadtree_kernel; }
+
+int launch_quadtree(const ExtractParams& P, const ExtractBuffers& X, int batch, hipStream_t s) {
+  hipLaunchKernelGGL(quadtree_kernel, dim3(P.L, batch), dim3(kQtThreads), quadtree_lds_bytes(P), s, P,
+                     X.cell_counts, X.slots, X.cells, X.qscratch, X.qnode_scratch, X.qkeys, X.qcounts, X.err);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+}  // namespace orbx
