@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "orbx_internal.h"
+#include "orbx_wave.cuh"
 
 namespace orbx {
 
@@ -88,16 +89,8 @@ __global__ __launch_bounds__(256) void hamming_top2_kernel(const uint8_t* __rest
 }
 
 // ------------------------------------------------------------ wave helpers
-__device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
-  return v;
-}
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
+__device__ __forceinline__ int wave_min(int v) { return wave_min_dpp(v); }
+__device__ __forceinline__ int wave_sum_i(int v) { return wave_sum_dpp(v); }
 
 // best / second of the multiset of valid distances, first position wins ties
 // (the sequential "if(d<best){second=best;best=d;idx=i} else if(d<second)"
@@ -118,7 +111,7 @@ __device__ __forceinline__ Top2 wave_top2(bool valid, int dist, int pos) {
     return r;
   }
   const int first_lane = __ffsll((long long)eq) - 1;
-  r.pos = __shfl(pos, first_lane, 64);
+  r.pos = __builtin_amdgcn_readlane(pos, first_lane);
   if (__popcll(eq) >= 2) {
     r.second = b;
   } else {
@@ -138,10 +131,10 @@ struct InitParams {
   int sortn;        // pow2 >= kp_pitch (LDS sort capacity)
   int cand_lds;     // candidate entries kept in LDS
   long long cand_cap;  // global candidate entries per pair (fallback)
+  int stop;            // diagnostics: 0 = full kernel, k = return before pass k
 };
 
-constexpr int kInitThreads = 512;
-constexpr int kInitWaves = kInitThreads / 64;
+constexpr int kInitThreads = 1024;
 
 // Frame::PosInGrid (src/Frame.cc:381-391): round() of a float (half away from zero)
 __device__ __forceinline__ bool pos_in_grid(float x, float y, const InitParams& P, int* gx, int* gy) {
@@ -195,7 +188,8 @@ struct Window {
   int col_pre;    // per lane: inclusive prefix of column lengths
 };
 
-__device__ __forceinline__ Window make_window(float x, float y, const InitParams& P, const int* s_cell) {
+template <typename CellPtr>
+__device__ __forceinline__ Window make_window(float x, float y, const InitParams& P, CellPtr s_cell) {
   Window w;
   w.ok = false;
   w.x = x;
@@ -218,14 +212,9 @@ __device__ __forceinline__ Window make_window(float x, float y, const InitParams
     w.col_start = s_cell[ix * kGridRows + nMinCellY];
     len = max(0, s_cell[ix * kGridRows + nMaxCellY + 1] - w.col_start);
   }
-  int x2 = len;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int t = __shfl_up(x2, off, 64);
-    if (lane >= off) x2 += t;
-  }
+  const int x2 = wave_incl_scan_dpp(len);
   w.col_pre = x2;
-  w.total = __shfl(x2, 63, 64);
+  w.total = __builtin_amdgcn_readlane(x2, 63);
   return w;
 }
 
@@ -246,6 +235,201 @@ __device__ __forceinline__ int window_pos(const Window& w, int f) {
   return start + (f - (c ? pre_prev : 0));
 }
 
+// Passes 2 and 3 of search_init_kernel, instantiated once with the candidate
+// list in LDS and once in global memory, so that each copy addresses a single
+// known memory space (a run-time choice between the two would make the
+// compiler emit flat_* accesses, which wait on both memory counters).
+#define LDS __attribute__((address_space(3)))
+
+struct InitCtx {
+  InitParams P;
+  const orbx_kp* kp1;
+  const orbx_kp* kp2;
+  const uint8_t* desc1;
+  const uint8_t* desc2;
+  const float* prev;
+  uint32_t* s_sort;
+  float2* s_xy;
+  int2* s_queue;
+  int* s_m12;
+  int* s_cell;
+  int* s_md;
+  int* s_m21;
+  int* s_src;
+  int* s_coff;
+  int* s_var;
+  int n1, total;
+  int* err;
+};
+
+template <typename CandPtr>
+__device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
+  const InitParams& P = C.P;
+  const orbx_kp* kp1 = C.kp1;
+  const orbx_kp* kp2 = C.kp2;
+  const uint8_t* desc1 = C.desc1;
+  const uint8_t* desc2 = C.desc2;
+  const float* prev = C.prev;
+  const LDS uint32_t* s_sort = (const LDS uint32_t*)C.s_sort;
+  const LDS float* s_xy = (const LDS float*)C.s_xy;  // (x, y) pairs
+  LDS int* s_queue = (LDS int*)C.s_queue;           // {i1, first candidate} pairs
+  LDS int* s_m12 = (LDS int*)C.s_m12;
+  const LDS int* s_cell = (const LDS int*)C.s_cell;
+  LDS int* s_md = (LDS int*)C.s_md;
+  LDS int* s_m21 = (LDS int*)C.s_m21;
+  LDS int* s_src = (LDS int*)C.s_src;
+  const LDS int* s_coff = (const LDS int*)C.s_coff;
+  LDS int* s_var = (LDS int*)C.s_var;
+  const int n1 = C.n1, total = C.total;
+  int* err = C.err;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  (void)kp2;
+  (void)err;
+  if (P.stop == 2) return;
+  // ---- pass 2: fill candidates (reference order) with their Hamming distances
+  for (int q0 = wv * 64; q0 < n1; q0 += kInitThreads) {
+    const int qi = q0 + lane;
+    float cxl = 0.f, cyl = 0.f;
+    bool has = false;
+    uint4 dl0 = make_uint4(0, 0, 0, 0), dl1 = dl0;
+    if (qi < n1) {
+      has = s_coff[qi + 1] > s_coff[qi];
+      if (has) {
+        const orbx_kp k = kp1[qi];
+        cxl = prev ? prev[2 * qi] : k.x;
+        cyl = prev ? prev[2 * qi + 1] : k.y;
+        const uint4* d1 = (const uint4*)(desc1 + (long long)qi * 32);
+        dl0 = d1[0];
+        dl1 = d1[1];
+      }
+    }
+    uint64_t todo = __ballot(has);
+    while (todo) {
+      const int j = __ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      const float x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxl), j));
+      const float y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cyl), j));
+      const uint4 a0 = make_uint4(__builtin_amdgcn_readlane(dl0.x, j), __builtin_amdgcn_readlane(dl0.y, j),
+                                  __builtin_amdgcn_readlane(dl0.z, j), __builtin_amdgcn_readlane(dl0.w, j));
+      const uint4 a1 = make_uint4(__builtin_amdgcn_readlane(dl1.x, j), __builtin_amdgcn_readlane(dl1.y, j),
+                                  __builtin_amdgcn_readlane(dl1.z, j), __builtin_amdgcn_readlane(dl1.w, j));
+      const Window w = make_window(x, y, P, s_cell);
+      int base = s_coff[q0 + j];
+      const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+      for (int f0 = 0; f0 < w.total; f0 += 64) {
+        const int f = f0 + lane;
+        const int s = window_pos(w, min(f, w.total - 1));
+        bool ok = false;
+        int i2 = 0;
+        if (f < w.total) {
+          i2 = (int)(s_sort[s] & 0xFFFF);
+          ok = fabsf(__fsub_rn(s_xy[2 * i2], x)) < P.r && fabsf(__fsub_rn(s_xy[2 * i2 + 1], y)) < P.r;
+        }
+        const uint64_t m = __ballot(ok);
+        if (ok) {
+          const uint4* d2 = (const uint4*)(desc2 + (long long)i2 * 32);
+          const int d = hamming256(a0, a1, d2[0], d2[1]);
+          cand[base + __popcll(m & lt)] = (uint32_t)i2 | ((uint32_t)d << 23);
+        }
+        base += __popcll(m);
+      }
+    }
+  }
+  __syncthreads();
+  if (P.stop == 3) return;
+  // ---- pass 3: greedy resolution in i1 order (one wavefront, LDS state only)
+  if (wv == 0) {
+    volatile LDS int* md = s_md;
+    volatile LDS int* m21 = s_m21;
+    volatile LDS int* m12 = s_m12;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    // ordered queue of the queries that have candidates: {i1, first candidate};
+    // candidates of entry q end where entry q+1's begin (empty queries between
+    // them own no candidates)
+    int nq = 0;
+    for (int q0 = 0; q0 < n1; q0 += 64) {
+      const int qi = q0 + lane;
+      const bool act = qi < n1 && s_coff[qi + 1] > s_coff[qi];
+      const uint64_t m = __ballot(act);
+      if (qi < n1) m12[qi] = -1;
+      if (act) {
+        const int q = nq + __popcll(m & lt);
+        s_queue[2 * q] = qi;
+        s_queue[2 * q + 1] = s_coff[qi];
+      }
+      nq += __popcll(m);
+    }
+    if (lane == 0) {
+      s_queue[2 * nq] = n1;
+      s_queue[2 * nq + 1] = total;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    int nm = 0;
+    // two-deep prefetch of the greedy-independent data: queue entries q+1, q+2
+    // and the first candidate chunk of query q+1
+    auto qload = [&](int q) { return make_int2(s_queue[2 * q], s_queue[2 * q + 1]); };
+    int2 qa = nq > 0 ? qload(0) : make_int2(0, 0);
+    int2 qb = nq > 0 ? qload(1) : make_int2(0, 0);
+    uint32_t ea = (nq > 0 && qa.y + lane < qb.y) ? cand[qa.y + lane] : 0u;
+    for (int qi = 0; qi < nq; ++qi) {
+      const int i1 = qa.x, c0 = qa.y, c1 = qb.y;
+      const uint32_t e0 = ea;
+      int2 qc = make_int2(0, total);
+      if (qi + 2 <= nq) qc = qload(qi + 2);
+      ea = (qi + 1 < nq && qb.y + lane < qc.y) ? cand[qb.y + lane] : 0u;
+      qa = qb;
+      qb = qc;
+      Top2 acc{INT_MAX, -1, INT_MAX};
+      int owner = -1;  // vnMatches21 of this lane's candidate, read with its distance
+      for (int cb = c0; cb < c1; cb += 64) {
+        const int c = cb + lane;
+        bool valid = false;
+        int dist = 0, i2 = -1, o = -1;
+        if (c < c1) {
+          const uint32_t e = (cb == c0) ? e0 : cand[c];
+          i2 = (int)(e & 0x7FFFFF);
+          dist = (int)(e >> 23);
+          valid = !(md[i2] <= dist);  // vMatchedDistance[i2] <= dist -> skip (:444-445)
+          o = m21[i2];
+        }
+        const Top2 t = wave_top2(valid, dist, i2);
+        const int nb = min(acc.best, t.best);
+        const int npos = (acc.best <= t.best) ? acc.pos : t.pos;
+        const int nsec = min(min(max(acc.best, t.best), acc.second), t.second);
+        if (t.best < acc.best) {
+          const uint64_t eq = __ballot(valid && dist == t.best);
+          owner = __builtin_amdgcn_readlane(o, __ffsll((long long)eq) - 1);
+        }
+        acc.best = nb;
+        acc.pos = npos;
+        acc.second = nsec;
+      }
+      const int bestDist = acc.best, bestDist2 = acc.second, bestIdx2 = acc.pos;
+      if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)bestDist2, P.nnratio)) {
+        if (lane == 0) {
+          if (owner >= 0) {  // steal: the earlier query loses its match (:463-467)
+            m12[owner] = -1;
+            nm--;
+          }
+          m12[i1] = bestIdx2;
+          m21[bestIdx2] = i1;
+          md[bestIdx2] = bestDist;
+          nm++;
+          s_src[i1] = bestIdx2;  // rotHist[bin].push_back(i1), bin from this pair
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (lane == 0) s_var[0] = nm;
+    if (P.stop == 9 && lane == 0) {  // diagnostics: pass-3 cycles, queue length, candidates
+      atomicMax(err + 1, (int)(__builtin_amdgcn_s_memtime() - t_start));
+      atomicMax(err + 2, nq);
+      atomicMax(err + 3, total * 2 + (total <= P.cand_lds ? 1 : 0));
+    }
+  }
+}
+
 __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     InitParams P, const orbx_kp* __restrict__ kp1_all, const uint8_t* __restrict__ desc1_all,
     const int* __restrict__ n1_all, const orbx_kp* __restrict__ kp2_all, const uint8_t* __restrict__ desc2_all,
@@ -261,16 +445,18 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   // prev_all == nullptr: windows centred on F1's own keypoints, the initial
   // mvbPrevMatched of Tracking::MonocularInitialization (src/Tracking.cc:645-647)
   float* prev = prev_all ? prev_all + (long long)pr * P.kp_pitch * 2 : nullptr;
-  int* m12 = matches_all + (long long)pr * P.kp_pitch;
+  int* m12_out = matches_all + (long long)pr * P.kp_pitch;
 
   unsigned char* sp = smem;
   auto take = [&](size_t bytes) { unsigned char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
-  uint32_t* s_sort = (uint32_t*)take(4ull * P.sortn);   // (cell << 16 | compact idx), sorted
-  float2* s_xy = (float2*)take(8ull * P.kp_pitch);      // F2 keypoint positions (octave 0)
+  uint32_t* s_sort = (uint32_t*)take(4ull * P.sortn);   // (cell << 16 | index), sorted
+  float2* s_xy = (float2*)take(8ull * (P.kp_pitch + 1));  // F2 positions (passes 1-2)
+  int2* s_queue = (int2*)s_xy;                          // pass 3: {query, first candidate}
+  int* s_m12 = (int*)s_sort;                            // pass 3: vnMatches12 (sort keys are dead)
   int* s_cell = (int*)take(4ull * (kGridCols * kGridRows + 1));
   int* s_md = (int*)take(4ull * P.kp_pitch);            // vMatchedDistance
   int* s_m21 = (int*)take(4ull * P.kp_pitch);           // vnMatches21
-  int* s_bin = (int*)take(4ull * P.kp_pitch);           // rotation bin per i1 or -1
+  int* s_src = (int*)take(4ull * P.kp_pitch);           // i2 an i1 matched when it entered rotHist, or -1
   int* s_coff = (int*)take(4ull * (P.kp_pitch + 1));    // candidate offsets per i1
   int* s_tmp = (int*)take(64);
   int* s_var = (int*)take(64);
@@ -285,10 +471,7 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     s_md[i] = INT_MAX;
     s_m21[i] = -1;
   }
-  for (int i = tid; i < n1; i += kInitThreads) {
-    s_bin[i] = -1;
-    m12[i] = -1;
-  }
+  for (int i = tid; i < n1; i += kInitThreads) s_src[i] = -1;
   if (tid < 32) s_hist[tid] = 0;
   __syncthreads();
   for (int i = tid; i < n2; i += kInitThreads) {
@@ -305,8 +488,7 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   while (sortn < n0) sortn <<= 1;
   for (int i = n0 + tid; i < sortn; i += kInitThreads) s_sort[i] = 0xFFFFFFFFu;
   __syncthreads();
-  // bitonic sort of n0 keys (ascending): grid order cell-major, then index
-  for (int kk = 2; kk <= sortn; kk <<= 1) {
+  for (int kk = 2; kk <= sortn; kk <<= 1) {  // bitonic sort: grid cell-major, then index
     for (int j = kk >> 1; j > 0; j >>= 1) {
       for (int i = tid; i < sortn; i += kInitThreads) {
         const int ixj = i ^ j;
@@ -322,8 +504,7 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
       __syncthreads();
     }
   }
-  // s_cell[c] = first sorted position with cell >= c (lower bound)
-  for (int c = tid; c <= kGridCols * kGridRows; c += kInitThreads) {
+  for (int c = tid; c <= kGridCols * kGridRows; c += kInitThreads) {  // first sorted position of each cell
     int lo = 0, hi = n0;
     const uint32_t key = (uint32_t)c << 16;
     while (lo < hi) {
@@ -334,24 +515,31 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     s_cell[c] = lo;
   }
   __syncthreads();
+  if (P.stop == 1) return;
 
-  auto center = [&](int i1, float* x, float* y) {
-    if (prev) {
-      *x = prev[2 * i1];
-      *y = prev[2 * i1 + 1];
-    } else {
-      const orbx_kp k = kp1[i1];
-      *x = k.x;
-      *y = k.y;
-    }
-  };
+  // Passes 1 and 2 walk the queries 64 at a time per wave: lane j prefetches
+  // query q0+j's octave, window centre and descriptor words with coalesced
+  // loads, and readlane broadcasts them when query q0+j is processed.
   // ---- pass 1: candidate counts per query (Frame::GetFeaturesInArea, octave 0)
-  for (int i1 = wv; i1 < n1; i1 += kInitWaves) {
-    int cnt = 0;
-    if (kp1[i1].octave == 0) {
-      float x, y;
-      center(i1, &x, &y);
+  for (int q0 = wv * 64; q0 < n1; q0 += kInitThreads) {
+    const int qi = q0 + lane;
+    float cxl = 0.f, cyl = 0.f;
+    bool lvl0 = false;
+    if (qi < n1) {
+      const orbx_kp k = kp1[qi];
+      lvl0 = k.octave == 0;
+      cxl = prev ? prev[2 * qi] : k.x;
+      cyl = prev ? prev[2 * qi + 1] : k.y;
+      s_coff[qi] = 0;
+    }
+    uint64_t todo = __ballot(lvl0);
+    while (todo) {
+      const int j = __ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      const float x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxl), j));
+      const float y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cyl), j));
       const Window w = make_window(x, y, P, s_cell);
+      int cnt = 0;
       if (w.ok) {
         for (int f0 = 0; f0 < w.total; f0 += 64) {
           const int f = f0 + lane;
@@ -362,9 +550,9 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
           }
         }
       }
+      cnt = wave_sum_i(cnt);
+      if (lane == 0) s_coff[q0 + j] = cnt;
     }
-    cnt = wave_sum_i(cnt);
-    if (lane == 0) s_coff[i1] = cnt;
   }
   __syncthreads();
   if (tid == 0) s_coff[n1] = 0;
@@ -374,101 +562,29 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     if (tid == 0) atomicOr(err, 8);
     return;
   }
-  uint32_t* cand = total <= P.cand_lds ? s_cand : cand_all + (long long)pr * P.cand_cap;
-  // ---- pass 2: fill candidates (reference order) with their Hamming distances
-  for (int i1 = wv; i1 < n1; i1 += kInitWaves) {
-    if (s_coff[i1 + 1] == s_coff[i1]) continue;
-    float x, y;
-    center(i1, &x, &y);
-    const Window w = make_window(x, y, P, s_cell);
-    const uint4* d1 = (const uint4*)(desc1 + (long long)i1 * 32);
-    const uint4 a0 = d1[0], a1 = d1[1];
-    int base = s_coff[i1];
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (int f0 = 0; f0 < w.total; f0 += 64) {
-      const int f = f0 + lane;
-      const int s = window_pos(w, min(f, w.total - 1));
-      bool ok = false;
-      int i2 = 0;
-      if (f < w.total) {
-        i2 = (int)(s_sort[s] & 0xFFFF);
-        const float2 q = s_xy[i2];
-        ok = fabsf(__fsub_rn(q.x, x)) < P.r && fabsf(__fsub_rn(q.y, y)) < P.r;
-      }
-      const uint64_t m = __ballot(ok);
-      if (ok) {
-        const uint4* d2 = (const uint4*)(desc2 + (long long)i2 * 32);
-        const int d = hamming256(a0, a1, d2[0], d2[1]);
-        cand[base + __popcll(m & lt)] = (uint32_t)i2 | ((uint32_t)d << 23);
-      }
-      base += __popcll(m);
-    }
+  InitCtx ctx{P, kp1, kp2, desc1, desc2, prev, s_sort, s_xy, s_queue, s_m12, s_cell, s_md, s_m21, s_src, s_coff,
+              s_var, n1, total, err};
+  if (total <= P.cand_lds) {
+    init_pass23(ctx, (LDS uint32_t*)s_cand);
+  } else {
+    init_pass23(ctx, cand_all + (long long)pr * P.cand_cap);
   }
   __syncthreads();
-  // ---- pass 3: greedy resolution in i1 order (one wavefront; LDS state)
-  if (wv == 0) {
-    volatile int* md = s_md;
-    volatile int* m21 = s_m21;
-    int nm = 0;
-    const float factor = 1.0f / kHistoLength;
-    for (int q0 = 0; q0 < n1; q0 += 64) {
-     // queries of this chunk that have candidates, visited in index order
-     uint64_t todo = __ballot(q0 + lane < n1 && s_coff[q0 + lane + 1] > s_coff[q0 + lane]);
-     while (todo) {
-      const int i1 = q0 + __ffsll((long long)todo) - 1;
-      todo &= todo - 1;
-      const int c0 = s_coff[i1], c1 = s_coff[i1 + 1];
-      Top2 acc{INT_MAX, -1, INT_MAX};
-      for (int cb = c0; cb < c1; cb += 64) {
-        const int c = cb + lane;
-        bool valid = false;
-        int dist = 0, i2 = -1;
-        if (c < c1) {
-          const uint32_t e = cand[c];
-          i2 = (int)(e & 0x7FFFFF);
-          dist = (int)(e >> 23);
-          valid = !(md[i2] <= dist);
-        }
-        const Top2 t = wave_top2(valid, dist, i2);
-        const int nb = min(acc.best, t.best);
-        const int npos = (acc.best <= t.best) ? acc.pos : t.pos;
-        const int nsec = min(min(max(acc.best, t.best), acc.second), t.second);
-        acc.best = nb;
-        acc.pos = npos;
-        acc.second = nsec;
-      }
-      const int bestDist = acc.best, bestDist2 = acc.second, bestIdx2 = acc.pos;
-      if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)bestDist2, P.nnratio)) {
-        if (lane == 0) {
-          const int old = m21[bestIdx2];
-          if (old >= 0) {
-            m12[old] = -1;
-            nm--;
-          }
-          m12[i1] = bestIdx2;
-          m21[bestIdx2] = i1;
-          md[bestIdx2] = bestDist;
-          nm++;
-          if (P.check_ori) {
-            float rot = __fsub_rn(kp1[i1].angle, kp2[bestIdx2].angle);
-            if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-            int bin = (int)roundf(__fmul_rn(rot, factor));
-            if (bin == kHistoLength) bin = 0;
-            s_bin[i1] = bin;
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-      }
-     }
-    }
-    if (lane == 0) s_var[0] = nm;
-  }
-  __syncthreads();
-  // rotation consistency (ComputeThreeMaxima src/ORBmatcher.cc:1601-1642)
+  // rotation consistency (src/ORBmatcher.cc:473-512, ComputeThreeMaxima :1601-1642)
+  const float factor = 1.0f / kHistoLength;
   if (P.check_ori) {
-    for (int i = tid; i < n1; i += kInitThreads)
-      if (s_bin[i] >= 0) atomicAdd(&s_hist[s_bin[i]], 1);
+    for (int i = tid; i < n1; i += kInitThreads) {
+      const int j = s_src[i];
+      int bin = -1;
+      if (j >= 0) {
+        float rot = __fsub_rn(kp1[i].angle, kp2[j].angle);
+        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+        bin = (int)roundf(__fmul_rn(rot, factor));
+        if (bin == kHistoLength) bin = 0;
+        atomicAdd(&s_hist[bin], 1);
+      }
+      s_src[i] = bin;
+    }
     __syncthreads();
     if (tid == 0) {
       int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
@@ -498,19 +614,20 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     __syncthreads();
     const int ind1 = s_var[1], ind2 = s_var[2], ind3 = s_var[3];
     for (int i = tid; i < n1; i += kInitThreads) {
-      const int b = s_bin[i];
+      const int b = s_src[i];
       if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
-      if (m12[i] >= 0) {
-        m12[i] = -1;
+      if (s_m12[i] >= 0) {
+        s_m12[i] = -1;
         atomicSub(&s_var[0], 1);
       }
     }
     __syncthreads();
   }
-  // vbPrevMatched update
-  for (int i = tid; i < n1 && prev; i += kInitThreads) {
-    const int j = m12[i];
-    if (j >= 0) {
+  // outputs: vnMatches12 and the vbPrevMatched update (:515-517)
+  for (int i = tid; i < n1; i += kInitThreads) {
+    const int j = s_m12[i];
+    m12_out[i] = j;
+    if (prev && j >= 0) {
       prev[2 * i] = kp2[j].x;
       prev[2 * i + 1] = kp2[j].y;
     }
@@ -665,7 +782,7 @@ int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_c
 constexpr size_t kInitLdsBudget = 160 * 1024 - 512;
 static size_t init_lds_bytes(const InitParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-  return r16(4ull * P.sortn) + r16(8ull * P.kp_pitch) + r16(4ull * (kGridCols * kGridRows + 1)) +
+  return r16(4ull * P.sortn) + r16(8ull * (P.kp_pitch + 1)) + r16(4ull * (kGridCols * kGridRows + 1)) +
          3 * r16(4ull * P.kp_pitch) + r16(4ull * (P.kp_pitch + 1)) + 2 * r16(64) + r16(128) +
          r16(4ull * P.cand_lds);
 }
@@ -799,6 +916,10 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
   P.sortn = 1;
   while (P.sortn < kp_pitch) P.sortn <<= 1;
   P.cand_cap = m->cand_cap;
+  {
+    const char* st = getenv("ORBX_INIT_STOP");  // diagnostics only
+    P.stop = st ? atoi(st) : 0;
+  }
   P.cand_lds = 0;
   if (init_lds_bytes(P) > kInitLdsBudget)
     return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization's LDS grid (max ~5000)",
@@ -808,6 +929,14 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
                      (hipStream_t)stream, P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2,
                      d_prev_xy, m->cand, d_matches12, d_nmatches, m->err);
   MHIP(hipGetLastError());
+  if (P.stop == 9) {  // diagnostics only
+    int e[4] = {0, 0, 0, 0};
+    MHIP(hipStreamSynchronize((hipStream_t)stream));
+    MHIP(hipMemcpy(e, m->err, 16, hipMemcpyDeviceToHost));
+    fprintf(stderr, "search_init pass3: max cycles %d, max queue %d, max candidates %d (lds %d, cand_lds %d)\n", e[1],
+            e[2], e[3] / 2, e[3] & 1, P.cand_lds);
+    MHIP(hipMemset(m->err, 0, 16));
+  }
   return ORBX_OK;
 }
 
