@@ -135,6 +135,7 @@ struct InitParams {
 };
 
 constexpr int kInitThreads = 1024;
+constexpr int kInitMaxRounds = 48;
 
 // Frame::PosInGrid (src/Frame.cc:381-391): round() of a float (half away from zero)
 __device__ __forceinline__ bool pos_in_grid(float x, float y, const InitParams& P, int* gx, int* gy) {
@@ -241,6 +242,17 @@ __device__ __forceinline__ int window_pos(const Window& w, int f) {
 // compiler emit flat_* accesses, which wait on both memory counters).
 #define LDS __attribute__((address_space(3)))
 
+// workgroup-scope LDS atomics (the atomicAdd family takes generic pointers)
+__device__ __forceinline__ int lds_add(LDS int* p, int v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int lds_exch(LDS int* p, int v) {
+  return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int lds_max(LDS int* p, int v) {
+  return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 struct InitCtx {
   InitParams P;
   const orbx_kp* kp1;
@@ -258,7 +270,7 @@ struct InitCtx {
   int* s_src;
   int* s_coff;
   int* s_var;
-  int n1, total;
+  int n1, n2, total;
   int* err;
 };
 
@@ -337,16 +349,136 @@ __device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
   }
   __syncthreads();
   if (P.stop == 3) return;
-  // ---- pass 3: greedy resolution in i1 order (one wavefront, LDS state only)
-  if (wv == 0) {
+  // ---- pass 3: greedy resolution (src/ORBmatcher.cc:436-470)
+  // The reference resolves the queries one after another in i1 order: query
+  // i1 skips every candidate i2 whose vMatchedDistance[i2] (the distance of
+  // the latest earlier query that accepted i2) is <= its own distance. Each
+  // query's outcome is therefore a function of the outcomes of the queries
+  // before it -- a triangular system. It is solved here by Jacobi rounds:
+  // every query recomputes its top-2 from a snapshot of all accepted
+  // outcomes, keeping only claims by earlier queries; a round that changes no
+  // outcome is a fixed point, and the triangular system has exactly one --
+  // the sequential result. Rounds needed = length of the longest chain of
+  // outcome dependencies (a handful in practice); past kInitMaxRounds the
+  // sequential wavefront below finishes the job instead.
+  LDS int* res = s_m12;                  // per i1: -1, or bestIdx2 << 9 | bestDist
+  LDS int* head = (LDS int*)C.s_xy;      // per i2: latest claiming i1 of the snapshot, or -1
+  LDS int* nxt = head + P.kp_pitch;      // per i1: (next claimer + 1) << 9 | its distance
+  LDS int* queue = s_md;                 // queries that have candidates (unordered)
+  const int n2 = C.n2;
+  for (int i = tid; i < n1; i += kInitThreads) res[i] = -1;
+  for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
+  if (tid == 0) {
+    s_var[0] = 0;
+    s_var[6] = 1;
+    s_var[7] = 0;
+  }
+  __syncthreads();
+  for (int i = tid; i < n1; i += kInitThreads)
+    if (s_coff[i + 1] > s_coff[i]) queue[lds_add(&s_var[7], 1)] = i;
+  __syncthreads();
+  const int nq = s_var[7];
+  int rounds = 0;
+  bool converged = false;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  (void)lt;
+  while (rounds < kInitMaxRounds) {
+    // s_var[6] = "an outcome changed" of the previous round; read, then reset
+    if (s_var[6] == 0) {
+      converged = true;
+      break;
+    }
+    __syncthreads();
+    if (tid == 0) s_var[6] = 0;
+    ++rounds;
+    for (int qq = wv; qq < nq; qq += kInitThreads / 64) {
+      const int i1 = queue[qq];
+      const int c0 = s_coff[i1], c1 = s_coff[i1 + 1];
+      Top2 acc{INT_MAX, -1, INT_MAX};
+      for (int cb = c0; cb < c1; cb += 64) {
+        const int c = cb + lane;
+        bool valid = false;
+        int dist = 0, i2 = -1;
+        if (c < c1) {
+          const uint32_t e = cand[c];
+          i2 = (int)(e & 0x7FFFFF);
+          dist = (int)(e >> 23);
+          int md = INT_MAX;
+          for (int h = head[i2]; h >= 0;) {
+            const int x = nxt[h];
+            if (h < i1) md = min(md, x & 511);
+            h = (x >> 9) - 1;
+          }
+          valid = !(md <= dist);  // vMatchedDistance[i2] <= dist -> skip (:444-445)
+        }
+        const Top2 t = wave_top2(valid, dist, i2);
+        const int npos = (acc.best <= t.best) ? acc.pos : t.pos;
+        acc.second = min(min(max(acc.best, t.best), acc.second), t.second);
+        acc.best = min(acc.best, t.best);
+        acc.pos = npos;
+      }
+      const bool ok = acc.best <= kThLow && (float)acc.best < __fmul_rn((float)acc.second, P.nnratio);
+      const int r = ok ? (acc.pos << 9 | acc.best) : -1;
+      if (lane == 0 && res[i1] != r) {
+        res[i1] = r;
+        s_var[6] = 1;
+      }
+    }
+    __syncthreads();
+    // snapshot of this round's outcomes as per-i2 claim lists
+    for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
+    __syncthreads();
+    for (int qq = tid; qq < nq; qq += kInitThreads) {
+      const int i1 = queue[qq];
+      const int r = res[i1];
+      if (r >= 0) nxt[i1] = ((lds_exch(&head[r >> 9], i1) + 1) << 9) | (r & 511);
+    }
+    __syncthreads();
+  }
+  if (converged) {
+    // the latest accepting query keeps each i2 (earlier ones were stolen
+    // from, :463-467); every accepted query entered rotHist (:469-470)
+    for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
+    __syncthreads();
+    for (int qq = tid; qq < nq; qq += kInitThreads) {
+      const int i1 = queue[qq];
+      const int r = res[i1];
+      if (r >= 0) lds_max(&head[r >> 9], i1);
+    }
+    __syncthreads();
+    int kept = 0;
+    for (int i = tid; i < n1; i += kInitThreads) {
+      const int r = res[i];
+      const int best = r >= 0 ? (r >> 9) : -1;
+      const bool keep = r >= 0 && head[best] == i;
+      s_src[i] = best;
+      res[i] = keep ? best : -1;  // res aliases vnMatches12
+      kept += keep ? 1 : 0;
+    }
+    kept = wave_sum_dpp(kept);
+    if (lane == 0 && kept) lds_add(&s_var[0], kept);
+  } else {
+    // sequential fallback state: vMatchedDistance, vnMatches21 (queue is dead)
+    for (int i = tid; i < n2; i += kInitThreads) {
+      s_md[i] = INT_MAX;
+      s_m21[i] = -1;
+    }
+  }
+  if (P.stop == 9 && tid == 0) {  // diagnostics: rounds, queue length, candidates
+    atomicMax(err + 1, rounds + (converged ? 0 : 1000));
+    atomicMax(err + 2, nq);
+    atomicMax(err + 3, total * 2 + (total <= P.cand_lds ? 1 : 0));
+  }
+  __syncthreads();
+  // sequential greedy in i1 order (one wavefront, LDS state only)
+  if (!converged && wv == 0) {
     volatile LDS int* md = s_md;
     volatile LDS int* m21 = s_m21;
     volatile LDS int* m12 = s_m12;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     // ordered queue of the queries that have candidates: {i1, first candidate};
     // candidates of entry q end where entry q+1's begin (empty queries between
     // them own no candidates)
-    int nq = 0;
+    int nq = 0;  // shadows the unordered queue count
     for (int q0 = 0; q0 < n1; q0 += 64) {
       const int qi = q0 + lane;
       const bool act = qi < n1 && s_coff[qi + 1] > s_coff[qi];
@@ -364,7 +496,6 @@ __device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
       s_queue[2 * nq + 1] = total;
     }
     __builtin_amdgcn_wave_barrier();
-    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     int nm = 0;
     // two-deep prefetch of the greedy-independent data: queue entries q+1, q+2
     // and the first candidate chunk of query q+1
@@ -422,11 +553,6 @@ __device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
       }
     }
     if (lane == 0) s_var[0] = nm;
-    if (P.stop == 9 && lane == 0) {  // diagnostics: pass-3 cycles, queue length, candidates
-      atomicMax(err + 1, (int)(__builtin_amdgcn_s_memtime() - t_start));
-      atomicMax(err + 2, nq);
-      atomicMax(err + 3, total * 2 + (total <= P.cand_lds ? 1 : 0));
-    }
   }
 }
 
@@ -563,7 +689,7 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     return;
   }
   InitCtx ctx{P, kp1, kp2, desc1, desc2, prev, s_sort, s_xy, s_queue, s_m12, s_cell, s_md, s_m21, s_src, s_coff,
-              s_var, n1, total, err};
+              s_var, n1, n2, total, err};
   if (total <= P.cand_lds) {
     init_pass23(ctx, (LDS uint32_t*)s_cand);
   } else {

@@ -193,3 +193,70 @@ def test_search_by_bow_golden(pkg, O):
                                                                                       to_dict(fb)), out)
     assert nm == int(g["bow_nmatches"]) and np.array_equal(np.array(out, np.int32), g["bow_kf_f"])
     assert feature_vector_csr(to_dict(fa))[0].tolist() == fa[0].tolist()
+
+
+def _kps(pkg, xs, ys, angles=None):
+    k = np.zeros(len(xs), pkg.KP_DTYPE)
+    k["x"], k["y"], k["size"], k["response"] = xs, ys, 31.0, 1.0
+    k["angle"] = 0.0 if angles is None else angles
+    return k
+
+
+def _flip(rng, base, nbits):
+    d = base.copy()
+    for b in rng.choice(256, nbits, replace=False):
+        d[b // 8] ^= np.uint8(1 << (b % 8))
+    return d
+
+
+@pytest.mark.parametrize("n", [20, 70])
+def test_search_for_initialization_steal_chain(pkg, O, n):
+    """A chain of greedy dependencies as long as the query list: query i (i>=1)
+    sees targets t_i and t_i+1 at equal distance (ambiguous -> rejected) unless
+    query i-1 took t_i, which it does only when query i-2 took t_i-1, and so
+    on down to query 0, whose window holds t_1 alone. Resolution order matters
+    at every link (the n=70 chain exceeds the parallel rounds' cap and runs
+    the sequential path)."""
+    W, H = 1241, 376
+    rng = np.random.default_rng(3)
+    base = rng.integers(0, 256, 32, dtype=np.uint8)
+    tdesc = _flip(rng, base, 30)
+    tx = 20.0 + 16.0 * np.arange(n + 1)
+    k2 = _kps(pkg, tx, np.full(n + 1, 100.0))
+    qx = np.concatenate([[tx[1]], tx[1:n] + 8.0])
+    k1 = _kps(pkg, qx, np.full(n, 100.0))
+    d1 = np.repeat(base[None], n, 0)
+    d2 = np.repeat(tdesc[None], n + 1, 0)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    m = pkg.ORBmatcher(0.9, True, max_kps=4096)
+    v12 = []
+    nm = m.SearchForInitialization(pkg.Frame.from_extraction(k1, d1, W, H), pkg.Frame.from_extraction(k2, d2, W, H),
+                                   prev, v12, 12)
+    r12, rnm, rprev = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), np.stack([k1["x"], k1["y"]], 1),
+                                                  12, 0.9, True)
+    assert rnm == n and np.array_equal(r12, np.arange(1, n + 1, dtype=np.int32))
+    assert nm == rnm and np.array_equal(np.array(v12, np.int32), r12) and np.array_equal(prev, rprev)
+
+
+@pytest.mark.parametrize("seed,ratio", [(0, 0.9), (1, 0.7), (2, 1.0)])
+def test_search_for_initialization_contention(pkg, O, seed, ratio):
+    """Heavy contention: 600 queries and 500 targets crowded into one window,
+    descriptors a few bits from a common base, so most queries compete for
+    the same targets and steals cascade."""
+    W, H = 1241, 376
+    rng = np.random.default_rng(100 + seed)
+    base = rng.integers(0, 256, 32, dtype=np.uint8)
+    n1, n2 = 600, 500
+    k1 = _kps(pkg, rng.uniform(300, 360, n1), rng.uniform(150, 210, n1), rng.uniform(0, 360, n1))
+    k2 = _kps(pkg, rng.uniform(300, 360, n2), rng.uniform(150, 210, n2), rng.uniform(0, 360, n2))
+    d1 = np.stack([_flip(rng, base, int(rng.integers(0, 20))) for _ in range(n1)])
+    d2 = np.stack([_flip(rng, base, int(rng.integers(0, 20))) for _ in range(n2)])
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    for ori in (True, False):
+        m = pkg.ORBmatcher(ratio, ori, max_kps=4096)
+        p = prev.copy()
+        v12 = []
+        nm = m.SearchForInitialization(pkg.Frame.from_extraction(k1, d1, W, H),
+                                       pkg.Frame.from_extraction(k2, d2, W, H), p, v12, 100)
+        r12, rnm, rprev = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), prev, 100, ratio, ori)
+        assert nm == rnm and np.array_equal(np.array(v12, np.int32), r12) and np.array_equal(p, rprev)
