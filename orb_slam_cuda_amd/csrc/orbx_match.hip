@@ -12,9 +12,11 @@
 // steal a frame feature from an earlier one, SearchForInitialization
 // :444-445,463-470; matched features drop out of SearchByBoW :205-210). The
 // kernels keep that order exactly: candidate lists and all 256-bit distances
-// are computed in parallel, the order-dependent resolution runs as one
-// wavefront walking the queries in reference order with the per-query
-// best/second reduction done across lanes.
+// are computed in parallel; SearchForInitialization's order-dependent
+// resolution is solved as a triangular fixed point by parallel rounds (with
+// a sequential wavefront as the fallback), SearchByBoW's per-node greedy
+// loops run one wavefront per node with the best/second reduction across
+// lanes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
