@@ -17,8 +17,9 @@ constexpr int kBlurTW = 128, kBlurTH = 32, kBlurInW = kBlurTW + 32;
 __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp, uint8_t* __restrict__ blur) {
   __shared__ __attribute__((aligned(16))) uint8_t in[kBlurTH + 6][kBlurInW];
   __shared__ __attribute__((aligned(16))) uint16_t tmp[kBlurTH + 6][kBlurTW];
-  const int f = blockIdx.y, tid = threadIdx.x;
-  int t = blockIdx.x, l = 0;
+  const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+  const int f = wg / gridDim.x, tid = threadIdx.x;
+  int t = wg % gridDim.x, l = 0;
   for (; l < P.L; ++l) {
     const LevelGeom& g = P.lv[l];
     const int n = ((g.w + kBlurTW - 1) / kBlurTW) * ((g.h + kBlurTH - 1) / kBlurTH);

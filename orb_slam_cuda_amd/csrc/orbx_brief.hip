@@ -28,10 +28,11 @@ __global__ __launch_bounds__(256) void orient_brief_kernel(ExtractParams P, Leve
                                                            orbx_kp* __restrict__ out_kps,
                                                            uint8_t* __restrict__ out_desc,
                                                            int* __restrict__ out_counts) {
-  const int f = blockIdx.y, lane = threadIdx.x & 63;
-  const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+  const int bx = wg % gridDim.x, f = wg / gridDim.x, lane = threadIdx.x & 63;
+  const int slot = bx * 4 + (threadIdx.x >> 6);
   const int* cnt = qcounts + f * P.L;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (bx == 0 && threadIdx.x == 0) {
     int tot = 0;
     for (int i = 0; i < P.L; ++i) tot += cnt[i];
     out_counts[f] = tot;

@@ -34,6 +34,17 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
+// XCD-aware workgroup order. Workgroups are dealt round-robin over the 8
+// XCDs (each with its own L2), so consecutive linear ids land on different
+// L2s and neighbouring tiles' shared halo lines are fetched once per XCD.
+// This bijection hands each XCD a contiguous run of logical tiles instead
+// (q = n/8, r = n%8; MI355X_MICROARCH.md "Workgroup dispatch"). Speed only:
+// any placement is correct.
+__device__ __forceinline__ int xcd_remap(int orig, int n) {
+  const int q = n >> 3, r = n & 7, x = orig & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
 // cv::fastAtan2 (OpenCV 3.x polynomial), float arithmetic without contraction.

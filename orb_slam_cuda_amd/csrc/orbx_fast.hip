@@ -96,7 +96,8 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
                                                         uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_counts) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int cell = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+  const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+  const int cell = wg % P.ncells_total, f = wg / P.ncells_total, lane = threadIdx.x;
   const CellGeom cg = cells[cell];
   int* cnt = cell_counts + (long long)f * P.ncells_total + cell;
   const int rw = cg.c1 - cg.c0, rh = cg.r1 - cg.r0;

@@ -28,8 +28,10 @@ __global__ __launch_bounds__(256) void pyr_resize_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t tile[kPyrMaxSrcH][kPyrMaxSrcW];
   __shared__ int2 s_xt[kPyrTW];
   __shared__ int2 s_yt[kPyrTH];
-  const int f = blockIdx.z, tid = threadIdx.x;
-  const int x0 = blockIdx.x * kPyrTW, y0 = blockIdx.y * kPyrTH;
+  const int wg = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                           gridDim.x * gridDim.y * gridDim.z);
+  const int f = wg / (gridDim.x * gridDim.y), tid = threadIdx.x;
+  const int x0 = (wg % gridDim.x) * kPyrTW, y0 = ((wg / gridDim.x) % gridDim.y) * kPyrTH;
   const int nx = min(kPyrTW, dw - x0), ny = min(kPyrTH, dh - y0);
   const uint8_t* S = src + f * src_fs;
   // source footprint of the tile
