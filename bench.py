@@ -12,6 +12,11 @@ One step = one batch of B frames resident in HBM:
 Frame t-1 of the first frame of a batch is the last frame of the previous
 batch (carried on device), so every step does B extractions + B matches.
 
+Two streams: the matching of batch k (a few wide workgroups per frame pair)
+runs on its own stream, overlapping the extraction of batch k+1; outputs are
+triple-buffered and ordered by events (see step()). --serial runs everything
+on one stream.
+
 Multi-GPU: one process per GPU, frames sharded by rank (each rank streams its
 own synthetic sequence), no data-path collective ("weak" scaling). The
 barrier and the max-over-ranks of the timed region go through
@@ -83,6 +88,7 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--cpu-sample", type=int, default=24, help="frames in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-match", action="store_true", help="extract only (C2)")
+    ap.add_argument("--serial", action="store_true", help="one stream: no overlap of matching with the next extraction")
     args = ap.parse_args()
 
     from orb_slam_cuda_amd import sharding
@@ -111,77 +117,97 @@ def main():
     ext = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=B)
     cap = ext.frame_capacity
     KP, DS = 28, 32
-    d_kps = _lib.DeviceArray((B + 1) * cap * KP)
-    d_desc = _lib.DeviceArray((B + 1) * cap * DS)
-    d_counts = _lib.DeviceArray((B + 1) * 4)
-    d_counts.zero()
+    # three output sets: batch k writes set k % 3, slots 1..B, and then copies
+    # its last frame into slot 0 of set (k+1) % 3 (frame t-1 of the next
+    # batch's first frame). Set k % 3 is free again once matching k-3 is done.
+    NS = 3
+    d_kps = [_lib.DeviceArray((B + 1) * cap * KP) for _ in range(NS)]
+    d_desc = [_lib.DeviceArray((B + 1) * cap * DS) for _ in range(NS)]
+    d_counts = [_lib.DeviceArray((B + 1) * 4) for _ in range(NS)]
+    for d in d_counts:
+        d.zero()
     matcher = pkg.ORBmatcher(0.9, True, device=local, max_pairs=B, max_kps=cap)
     d_bi, d_bd, d_sd = (_lib.DeviceArray(B * cap * 4) for _ in range(3))
     d_m12 = _lib.DeviceArray(B * cap * 4)
     d_nm = _lib.DeviceArray(B * 4)
-    stream = _lib.Stream()
+    s_ext = _lib.Stream()
+    s_match = _lib.Stream() if not args.serial else s_ext
     bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
     vp = lambda a: C.c_void_p(a)
+    n_ev = 9  # 6 extraction stage marks (extract stream) + 3 matching marks (match stream)
 
-    def step(evs=None):
-        if evs is not None:
-            arr = (C.c_void_p * 6)(*[e.e.value for e in evs[:6]])
-            check(L.orbx_set_stage_events(ext.handle, arr))
+    def step(k, evs, ev_ext, ev_done):
+        """Batch k: extraction + carry copy on s_ext; matching of the same
+        batch on s_match, overlapping the extraction of batch k+1 (--serial:
+        one stream, no overlap). Before the carry into set (k+1) % 3 the
+        extraction stream waits for matching k-2 (the last reader of that
+        set); matching k waits for extraction k."""
+        b, nb = k % NS, (k + 1) % NS
+        arr = (C.c_void_p * 6)(*[e.e.value for e in evs[:6]])
+        check(L.orbx_set_stage_events(ext.handle, arr))
         check(L.orbx_extract_batch(ext.handle, vp(d_frames.ptr), B, H * pitch, pitch,
-                                   vp(d_kps.ptr + cap * KP), vp(d_desc.ptr + cap * DS), vp(d_counts.ptr + 4),
-                                   stream.s))
+                                   vp(d_kps[b].ptr + cap * KP), vp(d_desc[b].ptr + cap * DS),
+                                   vp(d_counts[b].ptr + 4), s_ext.s))
+        ev_ext[k].record(s_ext)
+        if k >= 2 and not args.serial:
+            s_ext.wait(ev_done[k - 2])
+        check(L.orbx_memcpy_dtod_async(vp(d_kps[nb].ptr), vp(d_kps[b].ptr + B * cap * KP), cap * KP, s_ext.s))
+        check(L.orbx_memcpy_dtod_async(vp(d_desc[nb].ptr), vp(d_desc[b].ptr + B * cap * DS), cap * DS, s_ext.s))
+        check(L.orbx_memcpy_dtod_async(vp(d_counts[nb].ptr), vp(d_counts[b].ptr + B * 4), 4, s_ext.s))
+        if not args.serial:
+            s_match.wait(ev_ext[k])
+        evs[6].record(s_match)
         if not args.no_match:
             # query = frame t (slots 1..B), candidates = frame t-1 (slots 0..B-1)
-            check(L.orbm_hamming_top2(matcher.handle, vp(d_desc.ptr + cap * DS), cap * DS, vp(d_counts.ptr + 4),
-                                      cap, vp(d_desc.ptr), cap * DS, vp(d_counts.ptr), B, vp(d_bi.ptr),
-                                      vp(d_bd.ptr), vp(d_sd.ptr), stream.s), matcher=True)
-            if evs is not None:
-                evs[6].record(stream)
+            check(L.orbm_hamming_top2(matcher.handle, vp(d_desc[b].ptr + cap * DS), cap * DS,
+                                      vp(d_counts[b].ptr + 4), cap, vp(d_desc[b].ptr), cap * DS,
+                                      vp(d_counts[b].ptr), B, vp(d_bi.ptr), vp(d_bd.ptr), vp(d_sd.ptr),
+                                      s_match.s), matcher=True)
+            evs[7].record(s_match)
             check(L.orbm_search_for_initialization_batch(
-                matcher.handle, vp(d_kps.ptr), vp(d_desc.ptr), vp(d_counts.ptr), vp(d_kps.ptr + cap * KP),
-                vp(d_desc.ptr + cap * DS), vp(d_counts.ptr + 4), cap, B, bounds, None, 100, C.c_float(0.9), 1,
-                vp(d_m12.ptr), vp(d_nm.ptr), stream.s), matcher=True)
-            if evs is not None:
-                evs[7].record(stream)
-        # carry frame B-1 into slot 0 as the next batch's frame t-1
-        check(L.orbx_memcpy_dtod_async(vp(d_kps.ptr), vp(d_kps.ptr + B * cap * KP), cap * KP, stream.s))
-        check(L.orbx_memcpy_dtod_async(vp(d_desc.ptr), vp(d_desc.ptr + B * cap * DS), cap * DS, stream.s))
-        check(L.orbx_memcpy_dtod_async(vp(d_counts.ptr), vp(d_counts.ptr + B * 4), 4, stream.s))
+                matcher.handle, vp(d_kps[b].ptr), vp(d_desc[b].ptr), vp(d_counts[b].ptr),
+                vp(d_kps[b].ptr + cap * KP), vp(d_desc[b].ptr + cap * DS), vp(d_counts[b].ptr + 4), cap, B,
+                bounds, None, 100, C.c_float(0.9), 1, vp(d_m12.ptr), vp(d_nm.ptr), s_match.s), matcher=True)
+        evs[8].record(s_match)
+        ev_done[k].record(s_match)
 
-    for _ in range(args.warmup):
-        step()
-    stream.synchronize()
-    counts = d_counts.download(B + 1, np.int32)[1:]
-    nkp_mean = float(counts.mean())
-
-    evsets = [[_lib.Event() for _ in range(8)] for _ in range(args.steps)]
-    t_start, t_end = _lib.Event(), _lib.Event()
+    total_steps = args.warmup + args.steps
+    evsets = [[_lib.Event() for _ in range(n_ev)] for _ in range(total_steps)]
+    ev_ext = [_lib.Event() for _ in range(total_steps)]
+    ev_done = [_lib.Event() for _ in range(total_steps)]
+    for k in range(args.warmup):
+        step(k, evsets[k], ev_ext, ev_done)
+    s_ext.synchronize()
+    s_match.synchronize()
     if dist is not None:
         dist.barrier()
-    stream.synchronize()
+    s_ext.synchronize()
+    s_match.synchronize()
     t0 = time.perf_counter()
-    t_start.record(stream)
-    for k in range(args.steps):
-        step(evsets[k])
-    t_end.record(stream)
-    stream.synchronize()
+    for k in range(args.warmup, total_steps):
+        step(k, evsets[k], ev_ext, ev_done)
+    s_ext.synchronize()
+    s_match.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
     wall = sharding.max_over_ranks(t1 - t0, dist)
-    ev_ms = t_start.elapsed_ms(t_end)
+    timed = evsets[args.warmup:]
+    ev_ms = timed[0][0].elapsed_ms(timed[-1][8])
 
-    # per-stage average durations over the timed steps (ms per launch-group, B frames)
+    # per-stage average durations over the timed steps (ms per launch-group, B frames),
+    # each bracketed by events on the stream its kernels run on
     st = {s: 0.0 for s in STAGES}
-    for evs in evsets:
+    for evs in timed:
         for i, s in enumerate(STAGES[:5]):
             st[s] += evs[i].elapsed_ms(evs[i + 1])
         if not args.no_match:
-            st["hamming_top2"] += evs[5].elapsed_ms(evs[6])
-            st["search_init"] += evs[6].elapsed_ms(evs[7])
+            st["hamming_top2"] += evs[6].elapsed_ms(evs[7])
+            st["search_init"] += evs[7].elapsed_ms(evs[8])
     st = {s: v / args.steps for s, v in st.items()}
 
     nm = d_nm.download(B, np.int32)
+    nkp_mean = float(d_counts[(total_steps - 1) % NS].download(B + 1, np.int32)[1:].mean())
     frames_total = B * args.steps * world
     value = frames_total / wall
     ab = algorithmic_bytes(W, H, nkp_mean)
@@ -219,7 +245,8 @@ def main():
             "data": "synthetic (seeded shapes + noise sequence, orb_slam_cuda_amd/synth.py)",
             "config": {"workload": cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only",
                        "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
-                       "frames_per_step_per_gpu": B, "parallelism": f"frame-sharded x{world}, no collectives"},
+                       "frames_per_step_per_gpu": B, "parallelism": f"frame-sharded x{world}, no collectives",
+                       "streams": 1 if args.serial else 2},
             "roofline": roof,
             "cpu_baseline": cpu,
             "pyr_fast_pass_hbm_gbs": round(pf_gbs, 1),

@@ -234,6 +234,9 @@ int orbx_stream_synchronize(void* stream);
 int orbx_event_create(void** ev);
 int orbx_event_destroy(void* ev);
 int orbx_event_record(void* ev, void* stream);
+/* Make `stream` wait (on the device) for the work recorded in `ev`, so a
+ * host can pipeline extraction and matching on two streams. */
+int orbx_stream_wait_event(void* stream, void* ev);
 int orbx_event_elapsed_ms(void* start, void* stop, float* ms);
 
 #ifdef __cplusplus

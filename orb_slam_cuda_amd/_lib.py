@@ -104,6 +104,7 @@ def lib() -> C.CDLL:
         L.orbx_event_destroy.argtypes = [C.c_void_p]
         L.orbx_event_record.argtypes = [C.c_void_p, C.c_void_p]
         L.orbx_event_elapsed_ms.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]
+        L.orbx_stream_wait_event.argtypes = [C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -171,6 +172,9 @@ class Stream:
 
     def synchronize(self) -> None:
         check(lib().orbx_stream_synchronize(self.s))
+
+    def wait(self, event: "Event") -> None:
+        check(lib().orbx_stream_wait_event(self.s, event.e))
 
     def __del__(self):
         if getattr(self, "s", None) and self.s.value and _lib is not None:

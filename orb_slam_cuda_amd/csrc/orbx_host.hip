@@ -398,10 +398,9 @@ int orbx_create(const orbx_config* cfg, orbx_handle* out) {
   compute_scales(h);
   int rc = build_plan(h, c.width, c.height, c.max_batch);
   if (rc) { delete h; return rc; }
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete h;
-    return fail(ORBX_EDEVICE, "hipStreamCreate failed");
-  }
+  // h->stream (the synchronous API's stream) is created on first use: an idle
+  // stream would still take one of the process's few hardware queues, and a
+  // host that pipelines on its own streams wants those on distinct queues
   const char* t = getenv("ORBX_TIMING");
   h->timing = t && t[0] == '1';
   if (h->timing)
@@ -464,6 +463,7 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
     return rc;
   if (h->d_desc.n < (size_t)cap_frame * 32 && (rc = h->d_desc.alloc((size_t)cap_frame * 32))) return rc;
   if (h->d_counts.n < 4 && (rc = h->d_counts.alloc(4))) return rc;
+  if (!h->stream) HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   HIP_OK(hipMemcpy2DAsync(h->d_in.p, pitch, img, stride, w, hh, hipMemcpyHostToDevice, h->stream));
   rc = orbx_extract_batch(h, h->d_in.as<uint8_t>(), 1, pitch * hh, pitch, h->d_kps.as<orbx_kp>(),
                           h->d_desc.as<uint8_t>(), h->d_counts.as<int>(), h->stream);
@@ -510,7 +510,7 @@ int orbx_get_level(orbx_handle h, int frame, int level, int blurred, uint8_t* ou
   if (level < 0 || level >= pl.P.L || frame < 0 || frame >= h->last_batch)
     return fail(ORBX_EINVAL, "no such frame/level");
   HIP_OK(hipSetDevice(h->cfg.device));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(hipDeviceSynchronize());  // the last extraction may have run on a caller stream
   const LevelGeom& g = pl.P.lv[level];
   const ExtractBuffers X = buffers_of(pl);
   const uint8_t* src;
@@ -535,7 +535,7 @@ int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out, 
   if (level < 0 || level >= pl.P.L || frame < 0 || frame >= h->last_batch)
     return fail(ORBX_EINVAL, "no such frame/level");
   HIP_OK(hipSetDevice(h->cfg.device));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(hipDeviceSynchronize());  // the last extraction may have run on a caller stream
   const LevelGeom& g = pl.P.lv[level];
   std::vector<int> cnt(g.ncells);
   std::vector<uint32_t> slots(std::max(g.nslots, 1));
@@ -603,6 +603,10 @@ int orbx_stream_synchronize(void* s) { HIP_OK(hipStreamSynchronize((hipStream_t)
 int orbx_event_create(void** e) { HIP_OK(hipEventCreate((hipEvent_t*)e)); return ORBX_OK; }
 int orbx_event_destroy(void* e) { HIP_OK(hipEventDestroy((hipEvent_t)e)); return ORBX_OK; }
 int orbx_event_record(void* e, void* s) { HIP_OK(hipEventRecord((hipEvent_t)e, (hipStream_t)s)); return ORBX_OK; }
+int orbx_stream_wait_event(void* s, void* e) {
+  HIP_OK(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0));
+  return ORBX_OK;
+}
 int orbx_event_elapsed_ms(void* a, void* b, float* ms) {
   HIP_OK(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
   return ORBX_OK;

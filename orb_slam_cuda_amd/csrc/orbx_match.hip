@@ -946,7 +946,6 @@ struct orbx_matcher {
   int sortn = 1;
   long long cand_cap = 0;
   uint32_t* cand = nullptr;
-  int* coff = nullptr;
   int* err = nullptr;
   hipStream_t stream = nullptr;
   // staging for the synchronous entry points
@@ -979,9 +978,7 @@ int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out) {
   // below this; overflow is reported (ORBX_ECAPACITY), never truncated.
   m->cand_cap = std::min<long long>((long long)max_kps * max_kps, 4ll << 20);
   if (hipMalloc(&m->cand, (size_t)max_pairs * m->cand_cap * 4) != hipSuccess ||
-      hipMalloc(&m->coff, (size_t)max_pairs * (max_kps + 1) * 4) != hipSuccess ||
-      hipMalloc(&m->err, 16) != hipSuccess ||
-      hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
+      hipMalloc(&m->err, 16) != hipSuccess) {
     orbm_destroy(m);
     return mfail(ORBX_ENOMEM, "matcher workspace allocation failed");
   }
@@ -997,7 +994,6 @@ int orbm_destroy(orbm_handle m) {
   (void)hipSetDevice(m->device);
   if (m->stream) (void)hipStreamSynchronize(m->stream);
   if (m->cand) (void)hipFree(m->cand);
-  if (m->coff) (void)hipFree(m->coff);
   if (m->err) (void)hipFree(m->err);
   if (m->stage) (void)hipFree(m->stage);
   if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -1088,6 +1084,7 @@ int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1, const uint
   float* dprev = (float*)(dd2 + db);
   int* dm = (int*)(dprev + 2 * pitch);
   int* dn = dm + pitch;  // n1, n2, nmatches
+  if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));  // created on first use
   hipStream_t st = m->stream;
   const int hn[2] = {n1, n2};
   if (n1) {
@@ -1159,6 +1156,7 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
     d[i] = p;
     p += sz[i];
   }
+  if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));  // created on first use
   hipStream_t st = m->stream;
   auto up = [&](void* dst, const void* src, size_t n) -> int {
     if (n && src) MHIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));

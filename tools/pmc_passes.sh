@@ -2,7 +2,8 @@
 # PMC counter passes over the benchmark (one rocprofv3 run per counter group;
 # counters never combined with runtime/sys tracing). Usage: tools/pmc_passes.sh OUTDIR [bench args]
 set -e
-OUT=$1; shift
+OUT=$GRAFT_REPO_ROOT/$1; shift
+mkdir -p $OUT
 cd /tmp; export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
 ARGS="--steps 3 --warmup 1 --cpu-sample 0 $*"
 i=0
