@@ -25,6 +25,8 @@
 namespace orbx {
 size_t quadtree_lds_bytes(const ExtractParams& P);
 extern const void* quadtree_kernel_ptr();
+size_t pyr_band_lds_bytes(const ExtractParams& P);
+extern const void* pyr_band_kernel_ptr();
 }  // namespace orbx
 
 using namespace orbx;
@@ -192,6 +194,72 @@ static void resize_tables(int sw, int sh, int dw, int dh, std::vector<int2>& xt,
   }
 }
 
+// Row bands of the one-launch pyramid (orbx_pyramid.hip pyr_band_kernel).
+// Bands of R rows partition the last level; walking down, a band's rows at
+// level l start at the first source row of its first row at level l+1, and it
+// OWNS (writes) the rows up to where the next band's start; it COMPUTES its
+// own rows plus every source row its level-(l+1) rows read. Level 0 rows are
+// only read. R shrinks until the two LDS row buffers fit; if even R = 1 does
+// not, the per-level kernel is used.
+static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
+  P.pyr_fused = 0;
+  const int L = P.L;
+  if (L < 2) return;
+  for (int l = 0; l < L; ++l) P.lv[l].lpitch = (P.lv[l].w + 8 + 15) & ~15;
+  auto src_lo = [&](int l, int y) { return P.lv[l].area2x ? 2 * y : (rtab[P.lv[l].ytab + y].x & 0xFFFF); };
+  auto src_hi = [&](int l, int y) { return P.lv[l].area2x ? 2 * y + 1 : (rtab[P.lv[l].ytab + y].x >> 16); };
+  const int HL = P.lv[L - 1].h;
+  // prefer bands small enough for two workgroups per CU (the kernel is
+  // latency-bound: more resident waves beat less halo recompute)
+  const size_t budgets[2] = {78 * 1024, 160 * 1024 - 1024};
+  const int R0 = std::max(1, (HL + 17) / 18);
+  for (int pass = 0; pass < 2; ++pass)
+  for (int R = R0; R >= std::max(1, R0 / 3); --R) {
+    const size_t budget = budgets[pass];
+    const int nb = (HL + R - 1) / R;
+    std::vector<int> lo((size_t)nb * L), chi((size_t)nb * L), ohi((size_t)nb * L);
+    for (int b = 0; b < nb; ++b) {
+      lo[b * L + L - 1] = b * R;
+      chi[b * L + L - 1] = ohi[b * L + L - 1] = std::min((b + 1) * R, HL) - 1;
+    }
+    for (int l = L - 2; l >= 0; --l)
+      for (int b = 0; b < nb; ++b) lo[b * L + l] = b == 0 ? 0 : src_lo(l + 1, lo[b * L + l + 1]);
+    for (int l = L - 2; l >= 0; --l)
+      for (int b = 0; b < nb; ++b) {
+        const int own_hi = b + 1 < nb ? lo[(b + 1) * L + l] - 1 : P.lv[l].h - 1;
+        ohi[b * L + l] = own_hi;
+        chi[b * L + l] = std::max(src_hi(l + 1, chi[b * L + l + 1]), l > 0 ? own_hi : 0);
+      }
+    size_t need[2] = {0, 0};
+    for (int l = 0; l < L; ++l) {
+      int rows = 0;
+      for (int b = 0; b < nb; ++b) rows = std::max(rows, chi[b * L + l] - lo[b * L + l] + 1);
+      need[l & 1] = std::max(need[l & 1], (size_t)rows * P.lv[l].lpitch);
+    }
+    need[0] = (need[0] + 15) & ~(size_t)15;
+    need[1] = (need[1] + 15) & ~(size_t)15;
+    size_t ybytes = 0;
+    for (int b = 0; b < nb; ++b) {
+      size_t s = 0;
+      for (int l = 1; l < L; ++l) s += (size_t)(chi[b * L + l] - lo[b * L + l] + 1) * 8;
+      ybytes = std::max(ybytes, s);
+    }
+    if (need[0] + need[1] + ybytes + 16 > budget) continue;
+    P.pyr_fused = 1;
+    P.pyr_nbands = nb;
+    P.pyr_lds_a = (int)need[0];
+    P.pyr_lds_b = (int)need[1];
+    P.pyr_lds_y = (int)ybytes;
+    P.pyr_bands = (int)rtab.size();
+    for (int b = 0; b < nb; ++b)
+      for (int l = 0; l < L; ++l) {
+        rtab.push_back(make_int2(lo[b * L + l], chi[b * L + l]));
+        rtab.push_back(make_int2(lo[b * L + l], ohi[b * L + l]));
+      }
+    return;
+  }
+}
+
 static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   Plan& pl = h->plan;
   const orbx_config& c = h->cfg;
@@ -304,8 +372,18 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
       pl.rtab.insert(pl.rtab.end(), xt.begin(), xt.end());
       g.ytab = (int)pl.rtab.size();
       pl.rtab.insert(pl.rtab.end(), yt.begin(), yt.end());
+      // band-pyramid column table: columns at or past xmax replicate S[sx]
+      // (x2048), the same as coefficients {2048, 0}
+      g.xtab2 = (int)pl.rtab.size();
+      for (int dx = 0; dx < g.w; ++dx) {
+        int2 e = xt[dx];
+        if (g.area2x) e = make_int2(2 * dx, 0);
+        else if (dx >= g.xmax) e.y = 2048;
+        pl.rtab.push_back(e);
+      }
     }
   }
+  plan_band_pyramid(P, pl.rtab);
   if (maxnodes > 65000) return fail(ORBX_EINVAL, "nfeatures too large for the quadtree node table");
   P.slots_per_frame = slot;
   P.ncells_total = (int)pl.cells.size();
@@ -344,6 +422,9 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   HIP_OK(hipMemcpy(pl.cells_d.p, pl.cells.data(), pl.cells.size() * sizeof(CellGeom), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(pl.umax_d.p, h->umax, 16 * sizeof(int), hipMemcpyHostToDevice));
   HIP_OK(hipMemset(pl.err.p, 0, 16));
+  if (P.pyr_fused)
+    HIP_OK(hipFuncSetAttribute(pyr_band_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)pyr_band_lds_bytes(P)));
   HIP_OK(hipFuncSetAttribute(quadtree_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)quadtree_lds_bytes(P)));
   return ORBX_OK;

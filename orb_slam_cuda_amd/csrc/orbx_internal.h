@@ -27,7 +27,8 @@ constexpr int kMaxLevelDim = 4096;      // packed key coordinates are 12 bits
 constexpr int kQtThreads = 256;
 
 struct LevelGeom {
-  int w, h, pitch, pad0;
+  int w, h, pitch;
+  int lpitch;        // LDS row pitch of this level in the band pyramid kernel
   long long plane;   // bytes of one frame's plane (h * pitch)
   long long off;     // byte offset of this level's planes in the pyramid / blur buffers
   // INTER_LINEAR resize from level l-1 (l >= 1): offsets into the resize table
@@ -43,7 +44,7 @@ struct LevelGeom {
   int kcap, kbase;       // quadtree output slots of this level inside a frame
   float scale;           // mvScaleFactor[l]
   float size;            // (float)(int)(PATCH_SIZE * mvScaleFactor[l])
-  int pad1;
+  int xtab2;             // band pyramid column table: {sx, a0 | a1 << 16}, replicate folded in
 };
 
 struct CellGeom {
@@ -63,6 +64,12 @@ struct ExtractParams {
   int fast_rh_max;             // largest FAST cell ROI height
   int fast_bw_max, fast_bh_max;  // largest FAST detection band
   int pattern_upstream;
+  // band pyramid (orbx_pyramid.hip): one workgroup per (frame, band of rows)
+  int pyr_fused;               // 0 = one launch per level instead
+  int pyr_nbands;              // bands per frame
+  int pyr_bands;               // int2 offset in the resize table: per (band, level) {comp_lo, comp_hi}, {own_lo, own_hi}
+  int pyr_lds_a, pyr_lds_b;    // LDS bytes of the even-level and odd-level row buffers
+  int pyr_lds_y;               // LDS bytes of the band's staged row coefficients
   int gauss[7];                // 7-tap Gaussian fixed-point kernel (sum 257)
   LevelGeom lv[kMaxLevels];
 };

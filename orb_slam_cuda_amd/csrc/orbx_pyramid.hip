@@ -9,10 +9,15 @@
 // mean, as cv::resize does. The 19-px border the reference pads each level
 // with is never read by extraction and is not built.
 //
-// One launch per level (each level depends on the previous). A 256-thread
+// pyr_resize_kernel: one launch per level (each level depends on the
+// previous), used when a level's band does not fit LDS. A 256-thread
 // block produces a 16-row x 256-column output tile: the source rows/columns
 // the tile touches are staged in LDS with 16-byte loads, then each thread
 // computes a 4x4 output block from LDS and writes 4 x 32-bit stores.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 #include "orbx_device.cuh"
 
 namespace orbx {
@@ -122,7 +127,196 @@ __global__ __launch_bounds__(256) void pyr_resize_kernel(
   }
 }
 
+// ---------------------------------------------------------------- band pyramid
+// All levels in ONE launch: a workgroup owns a band of rows of the last
+// level and, walking the chain back, the rows of every level that band
+// depends on. It stages the level-0 rows once (16-byte loads, all in flight),
+// then builds level 1, 2, ... in LDS, each from the previous level's rows in
+// LDS, and writes to HBM only the rows it owns at each level (bands partition
+// every level's rows; the few source rows two bands share are recomputed by
+// both instead of exchanged). Row ranges per (band, level) come from the host
+// (orbx_host.hip build_plan): comp = rows computed, own = rows written.
+constexpr int kPyrBandThreads = 512;
+
+// Rows of one level for one thread: all 32 source bytes of a row pair are
+// read before any is used, so one LDS wait covers them.
+template <bool AREA2X>
+__device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtrs& lp, int l, int f,
+                                          const uint8_t* src, uint8_t* dst, const int2* yt_rows, int src_lo,
+                                          int2 cd, int2 own, int r0, int rstep, int xa, int xb, const int (&sx)[8],
+                                          const int (&a0v)[8], const int (&a1v)[8]) {
+  const LevelGeom& g = P.lv[l];
+  const int spitch = P.lv[l - 1].lpitch, w = g.w;
+  uint8_t* G0 = (uint8_t*)lp.base[l] + f * lp.fstride[l];
+  for (int r = cd.x + r0; r <= cd.y; r += rstep) {
+    const int2 yt = yt_rows[r - cd.x];
+    const uint8_t* s0 = src + ((yt.x & 0xFFFF) - src_lo) * spitch;
+    const uint8_t* s1 = src + ((yt.x >> 16) - src_lo) * spitch;
+    int p00[8], p01[8], p10[8], p11[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      p00[q] = s0[sx[q]];
+      p01[q] = s0[sx[q] + 1];
+      p10[q] = s1[sx[q]];
+      p11[q] = s1[sx[q] + 1];
+    }
+    int v[8];
+    if (AREA2X) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = (p00[q] + p01[q] + p10[q] + p11[q] + 2) >> 2;
+    } else {
+      const int b0 = (short)(yt.y & 0xFFFF), b1 = (short)(yt.y >> 16);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int D0 = p00[q] * a0v[q] + p01[q] * a1v[q];
+        const int D1 = p10[q] * a0v[q] + p11[q] * a1v[q];
+        v[q] = sat_u8((D0 * b0 + D1 * b1 + (1 << 21)) >> 22);
+      }
+    }
+    const uint32_t pa = pack4_u8(v[0], v[1], v[2], v[3]), pb = pack4_u8(v[4], v[5], v[6], v[7]);
+    uint8_t* lrow = dst + (r - cd.x) * g.lpitch;
+    *(uint32_t*)(lrow + xa) = pa;
+    *(uint32_t*)(lrow + xb) = pb;
+    if (r >= own.x && r <= own.y) {
+      uint8_t* drow = G0 + (long long)r * lp.pitch[l];
+      // level pitch and xa, xb are multiples of 4
+      if (xa + 4 <= w) *(uint32_t*)(drow + xa) = pa;
+      else for (int q = 0; xa + q < w; ++q) drow[xa + q] = (uint8_t)(pa >> (8 * q));
+      if (xb + 4 <= w) *(uint32_t*)(drow + xb) = pb;
+      else for (int q = 0; xb + q < w; ++q) drow[xb + q] = (uint8_t)(pb >> (8 * q));
+    }
+  }
+}
+
+__global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams P, LevelPtrs lp,
+                                                                   const int2* __restrict__ rtab, int* dbg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+  const int nb = P.pyr_nbands, L = P.L, tid = threadIdx.x;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int f = wg / nb, band = wg - f * nb;
+  const int2* bt = rtab + P.pyr_bands + (long long)band * L * 2;  // {comp}, {own} per level
+  uint8_t* const bufA = smem;
+  uint8_t* const bufB = smem + P.pyr_lds_a;
+  // the band's row coefficients of every level, staged once: a global load
+  // per output row would put one memory latency on every row iteration
+  int2* const s_yt = (int2*)(smem + P.pyr_lds_a + P.pyr_lds_b);
+  for (int l = 1, off = 0; l < L; ++l) {
+    const LevelGeom& g = P.lv[l];
+    const int2 cd = bt[2 * l];
+    const int n = cd.y - cd.x + 1;
+    for (int i = tid; i < n; i += kPyrBandThreads) {
+      const int r = cd.x + i;
+      s_yt[off + i] = g.area2x ? make_int2((2 * r) | ((2 * r + 1) << 16), 0) : rtab[g.ytab + r];
+    }
+    off += n;
+  }
+
+  // ---- stage level-0 rows [comp_lo, comp_hi], full width, 4 loads in flight per thread
+  {
+    const int2 c0 = bt[0];
+    const int rows = c0.y - c0.x + 1, W0 = P.lv[0].w, lp0 = P.lv[0].lpitch, pitch = lp.pitch[0];
+    const uint8_t* S = lp.base[0] + f * lp.fstride[0] + (long long)c0.x * pitch;
+    if (lp.aligned16[0]) {
+      const int nch = (W0 + 15) >> 4, total = rows * nch;
+      auto ld = [&](int i) -> uint4 {
+        if (i >= total) return make_uint4(0, 0, 0, 0);
+        const int r = i / nch, ch = i - r * nch;
+        return *(const uint4*)(S + (long long)r * pitch + ch * 16);
+      };
+      auto st = [&](int i, const uint4& v) {
+        if (i >= total) return;
+        const int r = i / nch, ch = i - r * nch;
+        *(uint4*)(bufA + r * lp0 + ch * 16) = v;
+      };
+      for (int i0 = tid; i0 < total; i0 += 4 * kPyrBandThreads) {
+        const uint4 v0 = ld(i0), v1 = ld(i0 + kPyrBandThreads), v2 = ld(i0 + 2 * kPyrBandThreads),
+                    v3 = ld(i0 + 3 * kPyrBandThreads);
+        st(i0, v0);
+        st(i0 + kPyrBandThreads, v1);
+        st(i0 + 2 * kPyrBandThreads, v2);
+        st(i0 + 3 * kPyrBandThreads, v3);
+      }
+    } else {
+      for (int r = 0; r < rows; ++r)
+        for (int c = tid; c < W0; c += kPyrBandThreads) bufA[r * lp0 + c] = S[(long long)r * pitch + c];
+    }
+  }
+
+  // column coefficients: level l+1's are fetched while level l is computed
+  int2 nxt[8];
+  // a thread's 8 columns are two runs of 4, [4g, 4g+4) and [4(g+G), 4(g+G)+4)
+  // with G = ceil(w/8): neighbouring lanes then read source bytes ~5 apart,
+  // which keeps each LDS byte read within few dwords per bank group
+  auto fetch_cols = [&](int l) {
+    const LevelGeom& g = P.lv[l];
+    const int G = (g.w + 7) >> 3, gi = tid % G;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) nxt[q] = rtab[g.xtab2 + min(4 * (gi + (q >> 2) * G) + (q & 3), g.w - 1)];
+  };
+  fetch_cols(1);
+  __syncthreads();
+  if (dbg && tid == 0) dbg[blockIdx.x * 16] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
+
+  // ---- levels 1 .. L-1: thread -> 8 output columns (two runs of 4), rows strided
+  int yoff = 0;
+  for (int l = 1; l < L; ++l) {
+    const LevelGeom& g = P.lv[l];
+    const uint8_t* src = (l & 1) ? bufA : bufB;
+    uint8_t* dst = (l & 1) ? bufB : bufA;
+    const int2 cs = bt[2 * (l - 1)], cd = bt[2 * l], own = bt[2 * l + 1];
+    const int G = (g.w + 7) >> 3, rstep = kPyrBandThreads / G;
+    const int gi = tid % G, r0 = tid / G;
+    const int xa = 4 * gi, xb = 4 * (gi + G);
+    int sx[8], a0v[8], a1v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      sx[q] = nxt[q].x;
+      a0v[q] = (short)(nxt[q].y & 0xFFFF);
+      a1v[q] = (short)(nxt[q].y >> 16);
+    }
+    if (l + 1 < L) fetch_cols(l + 1);
+    if (r0 < rstep) {
+      if (g.area2x)
+        band_rows<true>(P, lp, l, f, src, dst, s_yt + yoff, cs.x, cd, own, r0, rstep, xa, xb, sx, a0v, a1v);
+      else
+        band_rows<false>(P, lp, l, f, src, dst, s_yt + yoff, cs.x, cd, own, r0, rstep, xa, xb, sx, a0v, a1v);
+    }
+    yoff += cd.y - cd.x + 1;
+    __syncthreads();
+    if (dbg && tid == 0) dbg[blockIdx.x * 16 + l] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
+  }
+}
+
+size_t pyr_band_lds_bytes(const ExtractParams& P) { return (size_t)P.pyr_lds_a + P.pyr_lds_b + P.pyr_lds_y + 16; }
+const void* pyr_band_kernel_ptr() { return (const void*)pyr_band_kernel; }
+
 int launch_pyramid(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab, int batch, hipStream_t s) {
+  if (P.L < 2) return ORBX_OK;
+  if (P.pyr_fused) {
+    static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_PYR_PROF=1)
+    static const bool prof = getenv("ORBX_PYR_PROF") && getenv("ORBX_PYR_PROF")[0] == '1';
+    const int nwg = P.pyr_nbands * batch;
+    if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)nwg * 16 * 4);
+    hipLaunchKernelGGL(pyr_band_kernel, dim3(nwg), dim3(kPyrBandThreads), pyr_band_lds_bytes(P), s, P, lp, rtab,
+                       prof ? dbg : nullptr);
+    if (prof) {
+      std::vector<int> h((size_t)nwg * 16);
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpy(h.data(), dbg, h.size() * 4, hipMemcpyDeviceToHost);
+      double avg[16] = {0};
+      int mx[16] = {0};
+      for (int w = 0; w < nwg; ++w)
+        for (int k = 0; k < P.L; ++k) {
+          avg[k] += h[w * 16 + k];
+          mx[k] = std::max(mx[k], h[w * 16 + k]);
+        }
+      fprintf(stderr, "pyr_band: %d WGs; phase cycles avg/max:", nwg);
+      for (int k = 0; k < P.L; ++k) fprintf(stderr, " [%d] %.0f/%d", k, avg[k] / nwg, mx[k]);
+      fprintf(stderr, "\n");
+    }
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+  }
   for (int l = 1; l < P.L; ++l) {
     const LevelGeom& sg = P.lv[l - 1];
     const LevelGeom& d = P.lv[l];
