@@ -2,7 +2,7 @@
 //
 //   hamming_top2_kernel   dense best/second search (the inner loop shared by
 //                         every ORBmatcher search), lane-per-query, candidate
-//                         rows broadcast from LDS, 4 x v_bcnt per pair
+//                         rows in SGPRs via scalar loads, 8 x v_bcnt per pair
 //   search_init_kernel    SearchForInitialization   src/ORBmatcher.cc:405-520
 //                         + Frame::AssignFeaturesToGrid / GetFeaturesInArea
 //                         src/Frame.cc:229-244, 326-391
@@ -44,50 +44,89 @@ __device__ __forceinline__ int hamming256(const uint4& a0, const uint4& a1, cons
 }
 
 // ------------------------------------------------------------ dense top-2
-constexpr int kTopChunk = 256;
-__global__ __launch_bounds__(256) void hamming_top2_kernel(const uint8_t* __restrict__ A, long long a_pitch,
-                                                           const int* __restrict__ nA, int a_cap,
-                                                           const uint8_t* __restrict__ B, long long b_pitch,
-                                                           const int* __restrict__ nB, int* __restrict__ best_idx,
-                                                           int* __restrict__ best, int* __restrict__ second) {
-  __shared__ uint4 sB[kTopChunk][2];
-  const int p = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const int na = nA[p], nb = nB[p];
-  if (blockIdx.x * 256 >= na) return;
+constexpr int kTopQueries = 256;  // queries per workgroup (lane per query)
+constexpr int kTopSplit = 4;      // candidate quarters per query (one wave set each)
+constexpr int kTopThreads = kTopQueries * kTopSplit;
+// popcount(x) + acc as ONE v_bcnt_u32_b32 (the compiler otherwise splits the
+// chain into bcnt(x, 0) and v_add3)
+__device__ __forceinline__ int bcnt_acc(uint32_t x, int acc) {
+  int r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+  return r;
+}
+__device__ __forceinline__ int med3_i32(int a, int b, int c) {
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Lane per query; the candidate rows are wave-uniform, so they are read with
+// scalar loads (32 bytes straight into SGPRs, no LDS) and each pair costs
+// 8 v_xor + 8 v_bcnt + 4 top-2 updates: b2 = med3(d, b1, b2) (b1 <= b2
+// always), b1 = min(d, b1), index by compare. The candidates are split in
+// kTopSplit contiguous ranges, one per wave set, so that enough waves are
+// resident to cover the scalar-load latency; the partial results are merged
+// in range order (earlier range wins ties, as the sequential scan would).
+__global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t* __restrict__ A, long long a_pitch,
+                                                                   const int* __restrict__ nA, int a_cap,
+                                                                   const uint8_t* __restrict__ B, long long b_pitch,
+                                                                   const int* __restrict__ nB,
+                                                                   int* __restrict__ best_idx, int* __restrict__ best,
+                                                                   int* __restrict__ second) {
+  __shared__ int3 part[kTopSplit][kTopQueries];
+  const int p = blockIdx.y, q = threadIdx.x % kTopQueries, k = threadIdx.x / kTopQueries;
+  const int i = blockIdx.x * kTopQueries + q;
+  const int na = nA[p], nb = __builtin_amdgcn_readfirstlane(nB[p]);
+  if (blockIdx.x * kTopQueries >= na) return;
   const uint4* Ap = (const uint4*)(A + p * a_pitch);
-  const uint4* Bp = (const uint4*)(B + p * b_pitch);
+  const uint32_t* Bp = (const uint32_t*)(B + p * b_pitch);
   uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
   if (i < na) {
     a0 = Ap[2 * i];
     a1 = Ap[2 * i + 1];
   }
+  const int per = ((nb + kTopSplit - 1) / kTopSplit + 3) & ~3;
+  const int jb = __builtin_amdgcn_readfirstlane(min(k * per, nb)), je = min(jb + per, nb);
   int b1d = 256, b2d = 256, bi = -1;
-  for (int j0 = 0; j0 < nb; j0 += kTopChunk) {
-    const int n = min(kTopChunk, nb - j0);
-    __syncthreads();
-    if (threadIdx.x < n) {
-      sB[threadIdx.x][0] = Bp[2 * (j0 + threadIdx.x)];
-      sB[threadIdx.x][1] = Bp[2 * (j0 + threadIdx.x) + 1];
-    }
-    __syncthreads();
-    for (int j = 0; j < n; ++j) {
-      const int d = hamming256(a0, a1, sB[j][0], sB[j][1]);
-      if (d < b1d) {
-        b2d = b1d;
-        b1d = d;
-        bi = j0 + j;
-      } else if (d < b2d) {
-        b2d = d;
-      }
+  auto score = [&](const uint32_t* r, int j) {
+    int d = bcnt_acc(a0.x ^ r[0], 0);
+    d = bcnt_acc(a0.y ^ r[1], d);
+    d = bcnt_acc(a0.z ^ r[2], d);
+    d = bcnt_acc(a0.w ^ r[3], d);
+    d = bcnt_acc(a1.x ^ r[4], d);
+    d = bcnt_acc(a1.y ^ r[5], d);
+    d = bcnt_acc(a1.z ^ r[6], d);
+    d = bcnt_acc(a1.w ^ r[7], d);
+    bi = d < b1d ? j : bi;
+    b2d = med3_i32(d, b1d, b2d);
+    b1d = min(d, b1d);
+  };
+  // four candidate rows per step: their scalar loads are issued together
+  int j = jb;
+  for (; j + 4 <= je; j += 4) {
+    uint32_t r[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) r[t] = Bp[8 * j + t];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) score(r + 8 * t, j + t);
+  }
+  for (; j < je; ++j) score(Bp + 8 * j, j);
+  part[k][q] = make_int3(b1d, bi, b2d);
+  __syncthreads();
+  if (k != 0 || i >= na) return;
+#pragma unroll
+  for (int s = 1; s < kTopSplit; ++s) {
+    const int3 o = part[s][q];
+    b2d = min(min(max(b1d, o.x), b2d), o.z);
+    if (o.x < b1d) {
+      b1d = o.x;
+      bi = o.y;
     }
   }
-  if (i < na) {
-    const long long o = (long long)p * a_cap + i;
-    best_idx[o] = bi;
-    best[o] = b1d;
-    second[o] = b2d;
-  }
+  const long long o = (long long)p * a_cap + i;
+  best_idx[o] = bi;
+  best[o] = b1d;
+  second[o] = b2d;
 }
 
 // ------------------------------------------------------------ wave helpers
@@ -901,8 +940,8 @@ __global__ __launch_bounds__(256) void search_bow_kernel(
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap, const uint8_t* B,
                         size_t b_pitch, const int* nB, int pairs, int* best_idx, int* best, int* second,
                         void* stream) {
-  dim3 grid((a_cap + 255) / 256, pairs);
-  hipLaunchKernelGGL(hamming_top2_kernel, grid, dim3(256), 0, (hipStream_t)stream, A, (long long)a_pitch, nA, a_cap,
+  dim3 grid((a_cap + kTopQueries - 1) / kTopQueries, pairs);
+  hipLaunchKernelGGL(hamming_top2_kernel, grid, dim3(kTopThreads), 0, (hipStream_t)stream, A, (long long)a_pitch, nA, a_cap,
                      B, (long long)b_pitch, nB, best_idx, best, second);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
