@@ -142,6 +142,12 @@ int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap,
 #define ORBX_STAGE_EVENTS 6
 int orbx_set_stage_events(orbx_handle h, void** events);
 
+/* The descriptor rotation's sin/cos (src/ORBextractor.cc:199-200: glibc
+ * sinf/cosf on a float argument) exactly as the kernels compute it, on the
+ * host: s[i] = sinf(x[i]), c[i] = cosf(x[i]) for |x| < 120. For checking the
+ * restatement against a host libm. */
+int orbx_sincosf_glibc(const float* x, int n, float* s, float* c);
+
 /* ------------------------------------------------------------- matcher */
 typedef struct orbx_matcher* orbm_handle;
 

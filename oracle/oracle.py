@@ -42,6 +42,7 @@ def lib():
         _lib = C.CDLL(LIB_PATH)
         _lib.orc_fast_atan2.restype = C.c_float
         _lib.orc_fast_atan2.argtypes = [C.c_float, C.c_float]
+        _lib.orc_sincosf.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     return _lib
 
 
@@ -163,3 +164,11 @@ def search_by_bow(descA, angleA, mpA, fvA, descB, angleB, mpB, fvB, nnratio, che
                             _p(fb[2]), len(fb[0]), C.c_float(nnratio), int(check_ori),
                             int(kf_vs_kf), _p(out), C.byref(nm))
     return out, nm.value
+
+
+def sincosf(x):
+    """Host libm sinf/cosf of a float32 array (returns sin, cos)."""
+    x = np.ascontiguousarray(x, np.float32)
+    s, c = np.empty_like(x), np.empty_like(x)
+    lib().orc_sincosf(x.ctypes.data, len(x), s.ctypes.data, c.ctypes.data)
+    return s, c

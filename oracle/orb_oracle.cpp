@@ -895,6 +895,12 @@ int orc_distribute(const orc_kp* keys, int nkeys, int minX, int maxX, int minY, 
 int orc_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
 
 float orc_fast_atan2(float y, float x) { return fast_atan2(y, x); }
+void orc_sincosf(const float* x, int n, float* s, float* c) {
+  for (int i = 0; i < n; ++i) {
+    s[i] = sinf(x[i]);
+    c[i] = cosf(x[i]);
+  }
+}
 
 void orc_hamming_top2(const uint8_t* A, int nA, const uint8_t* B, int nB, int* best_idx,
                       int* best_dist, int* second_dist) {

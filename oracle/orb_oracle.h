@@ -98,6 +98,8 @@ int orc_search_by_bow(
 
 /* Elementary OpenCV restatements, exported for unit tests. */
 float orc_fast_atan2(float y, float x);
+/* The host libm's sinf/cosf (what computeOrbDescriptor calls, :199-200). */
+void orc_sincosf(const float* x, int n, float* s, float* c);
 
 #ifdef __cplusplus
 }

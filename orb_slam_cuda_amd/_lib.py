@@ -105,6 +105,7 @@ def lib() -> C.CDLL:
         L.orbx_event_record.argtypes = [C.c_void_p, C.c_void_p]
         L.orbx_event_elapsed_ms.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]
         L.orbx_stream_wait_event.argtypes = [C.c_void_p, C.c_void_p]
+        L.orbx_sincosf_glibc.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 

@@ -14,6 +14,7 @@
 // straight into the 32 descriptor bytes (bit j of byte i = test 8i+j).
 #include "orbx_device.cuh"
 #include "orbx_pattern.h"
+#include "orbx_sincosf.h"
 
 namespace orbx {
 
@@ -73,9 +74,11 @@ __global__ __launch_bounds__(256) void orient_brief_kernel(ExtractParams P, Leve
   const float angle = fast_atan2_dev((float)m01, (float)m10);
 
   // computeOrbDescriptor: a = (float)cos(angle*pi/180), b = (float)sin(...)
+  // with glibc's cosf/sinf (orbx_sincosf.h)
   const float factorPI = (float)(M_PI / 180.f);
   const float ang = __fmul_rn(angle, factorPI);
-  const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+  float a, b;
+  glibc_sincosf(ang, &b, &a);
   const uint8_t* bc = blur + g.off + f * g.plane + (long long)y * g.pitch + x;
   const int step = g.pitch;
   uint64_t words[4];

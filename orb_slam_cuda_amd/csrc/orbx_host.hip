@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "orbx_internal.h"
+#include "orbx_sincosf.h"
 
 namespace orbx {
 size_t quadtree_lds_bytes(const ExtractParams& P);
@@ -684,6 +685,11 @@ int orbx_stream_synchronize(void* s) { HIP_OK(hipStreamSynchronize((hipStream_t)
 int orbx_event_create(void** e) { HIP_OK(hipEventCreate((hipEvent_t*)e)); return ORBX_OK; }
 int orbx_event_destroy(void* e) { HIP_OK(hipEventDestroy((hipEvent_t)e)); return ORBX_OK; }
 int orbx_event_record(void* e, void* s) { HIP_OK(hipEventRecord((hipEvent_t)e, (hipStream_t)s)); return ORBX_OK; }
+int orbx_sincosf_glibc(const float* x, int n, float* s, float* c) {
+  if (n < 0 || (n && (!x || !s || !c))) return fail(ORBX_EINVAL, "bad argument");
+  for (int i = 0; i < n; ++i) glibc_sincosf(x[i], s + i, c + i);
+  return ORBX_OK;
+}
 int orbx_stream_wait_event(void* s, void* e) {
   HIP_OK(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0));
   return ORBX_OK;

@@ -56,3 +56,25 @@ def test_no_gpu_fails_loudly():
         pkg.ORBextractor(2000, 1.2, 8, 20, 7, 1241, 376)
     with pytest.raises(pkg.OrbxError):
         pkg.ORBmatcher(0.9, True)
+
+
+def test_descriptor_sincosf_matches_host_libm():
+    """The kernels' sin/cos of the descriptor rotation (glibc sinf/cosf
+    restated, csrc/orbx_sincosf.h) against this host's libm on 2M samples of
+    [0, 2pi) plus the quadrant edges. (tools/check_sincosf.cpp runs all
+    1,086,918,619 floats of [0, 2pi): 0 mismatches.)"""
+    import numpy as np
+
+    import orb_slam_cuda_amd as pkg
+    from oracle import oracle as O
+    rng = np.random.default_rng(11)
+    x = rng.uniform(0, 2 * np.pi, 2_000_000).astype(np.float32)
+    edges = np.float32(np.pi / 4) * np.arange(0, 9, dtype=np.float32)
+    near = np.concatenate([np.nextafter(edges, np.float32(-1)), edges, np.nextafter(edges, np.float32(9))])
+    x = np.concatenate([x, near[near >= 0], np.float32([0.0, 0.75, 2.0 ** -12, 6.2831855])]).astype(np.float32)
+    s, c = np.empty_like(x), np.empty_like(x)
+    from orb_slam_cuda_amd._lib import check
+    check(pkg.lib().orbx_sincosf_glibc(x.ctypes.data, len(x), s.ctypes.data, c.ctypes.data))
+    rs, rc = O.sincosf(x)
+    assert np.array_equal(s.view(np.uint32), rs.view(np.uint32))
+    assert np.array_equal(c.view(np.uint32), rc.view(np.uint32))
