@@ -8,97 +8,141 @@
 // size = (int)(31 * scale), octave = level, class_id = -1, output in
 // level-major order.
 //
-// One wavefront per keypoint: IC moments over the r=15 circular patch with
-// lanes = patch columns (wave-reduced), cv::fastAtan2 in float without
-// contraction, then 4 rBRIEF tests per lane packed by four 64-bit ballots
-// straight into the 32 descriptor bytes (bit j of byte i = test 8i+j).
+// Two keypoints per wavefront, 32 lanes each. Every global access of a
+// keypoint is issued in one burst after its key is known: the 31 rows of the
+// IC patch (lane = patch column, one byte load per row, coalesced across the
+// lanes) and the 39 x 64-byte blurred patch that the rotated BRIEF pattern
+// can reach (radius <= 19), staged in LDS with 16-byte loads. Moments are
+// reduced across the 32 lanes with DPP, cv::fastAtan2 and glibc sin/cos are
+// evaluated per lane, and 8 tests per lane (test t = lane + 32k) give, by
+// one ballot per k, descriptor dword k of both keypoints at once
+// (bit j of byte i = test 8i + j).
 #include "orbx_device.cuh"
 #include "orbx_pattern.h"
 #include "orbx_sincosf.h"
+#include "orbx_wave.cuh"
 
 namespace orbx {
 
-__constant__ signed char c_brief_x[512];
-__constant__ signed char c_brief_y[512];
+// packed test t: {x0, y0, x1, y1} as signed bytes (fork and upstream tables)
+__constant__ int c_brief_tests[2][256];
 
-__global__ __launch_bounds__(256) void orient_brief_kernel(ExtractParams P, LevelPtrs lp,
-                                                           const uint8_t* __restrict__ blur,
-                                                           const uint32_t* __restrict__ qkeys,
-                                                           const int* __restrict__ qcounts,
-                                                           const int* __restrict__ umax,
-                                                           orbx_kp* __restrict__ out_kps,
-                                                           uint8_t* __restrict__ out_desc,
-                                                           int* __restrict__ out_counts) {
+constexpr int kObThreads = 256;              // 4 waves, 8 keypoints
+constexpr int kObKps = kObThreads / 32;
+constexpr int kObRadius = 19;                // |rotated pattern offset| <= 18.4, rounded
+constexpr int kObRows = 2 * kObRadius + 1;   // 39
+constexpr int kObStride = 64;                // 4 x 16-byte chunks per staged row
+
+// sum over the 32 lanes of each half-wave; the half's total is returned to all its lanes
+__device__ __forceinline__ int half_sum(int v) {
+  v += dpp_i<kDppQuad1032>(0, v);
+  v += dpp_i<kDppQuad2301>(0, v);
+  v += dpp_i<kDppHalfMirror>(0, v);
+  v += dpp_i<kDppMirror>(0, v);
+  v += dpp_i<kDppBcast15, 0xa>(0, v);
+  const int lo = __builtin_amdgcn_readlane(v, 31), hi = __builtin_amdgcn_readlane(v, 63);
+  return (threadIdx.x & 32) ? hi : lo;
+}
+
+__global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams P, LevelPtrs lp,
+                                                                  const uint8_t* __restrict__ blur,
+                                                                  const uint32_t* __restrict__ qkeys,
+                                                                  const int* __restrict__ qcounts,
+                                                                  const int* __restrict__ /*umax*/,
+                                                                  orbx_kp* __restrict__ out_kps,
+                                                                  uint8_t* __restrict__ out_desc,
+                                                                  int* __restrict__ out_counts) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_patch[kObKps][kObRows * kObStride];
+  __shared__ int s_tests[256];
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-  const int bx = wg % gridDim.x, f = wg / gridDim.x, lane = threadIdx.x & 63;
-  const int slot = bx * 4 + (threadIdx.x >> 6);
+  const int bx = wg % gridDim.x, f = wg / gridDim.x, tid = threadIdx.x;
+  const int lane = tid & 31, hk = tid >> 5;  // keypoint of this half-wave within the workgroup
+  const int slot = bx * kObKps + hk;
   const int* cnt = qcounts + f * P.L;
-  if (bx == 0 && threadIdx.x == 0) {
+  if (bx == 0 && tid == 0) {
     int tot = 0;
     for (int i = 0; i < P.L; ++i) tot += cnt[i];
     out_counts[f] = tot;
   }
-  if (slot >= P.kp_per_frame) return;
+  s_tests[tid] = c_brief_tests[P.pattern_upstream ? 1 : 0][tid];
+
+  // ---- the keypoint of this half-wave
   int l = 0;
   while (l + 1 < P.L && slot >= P.lv[l + 1].kbase) ++l;
   const LevelGeom& g = P.lv[l];
   const int idx = slot - g.kbase;
-  if (idx >= cnt[l]) return;
-  int outpos = idx;
-  for (int i = 0; i < l; ++i) outpos += cnt[i];
-  const uint32_t key = qkeys[(long long)f * P.kp_per_frame + slot];
-  const int x = key_x(key) + g.minBX, y = key_y(key) + g.minBY;
+  const bool valid = slot < P.kp_per_frame && idx < cnt[l];
+  uint32_t key = 0;
+  if (valid) key = qkeys[(long long)f * P.kp_per_frame + slot];
+  // an empty slot works on a dummy keypoint at the level centre (never stored)
+  const int x = valid ? key_x(key) + g.minBX : g.w / 2, y = valid ? key_y(key) + g.minBY : g.h / 2;
 
-  // IC_Angle: lanes 0..30 -> column u = lane-15, rows v = 0 (centre) and 1..7;
-  //           lanes 32..62 -> u = lane-47, rows v = 8..15.
+  // ---- one burst of loads: blurred patch -> LDS, IC rows -> registers
+  const int c0 = (x - kObRadius) & ~15;
+  if (valid) {
+    const uint8_t* brow = blur + g.off + f * g.plane + (long long)(y - kObRadius) * g.pitch + c0;
+    uint8_t* dst = s_patch[hk];
+    for (int i = lane; i < kObRows * 4; i += 32) {
+      const int r = i >> 2, ch = i & 3;
+      if (c0 + ch * 16 + 16 <= g.pitch)
+        *(uint4*)(dst + r * kObStride + ch * 16) = *(const uint4*)(brow + (long long)r * g.pitch + ch * 16);
+    }
+  }
   const int pitch = lp.pitch[l];
   const uint8_t* center = lp.base[l] + f * lp.fstride[l] + (long long)y * pitch + x;
   int m10 = 0, m01 = 0;
-  {
-    const int half = lane >> 5, u = (lane & 31) - 15;
-    if ((lane & 31) < 31) {
-      if (half == 0) m10 += u * center[u];
-      const int vb = half ? 8 : 1, ve = half ? 15 : 7;
-      for (int v = vb; v <= ve; ++v) {
-        const int d = umax[v];
-        if (u >= -d && u <= d) {
-          const int vp = center[u + v * pitch], vm = center[u - v * pitch];
-          m01 += v * (vp - vm);
-          m10 += u * (vp + vm);
-        }
-      }
+  // umax of the r = 15 circle (ORBextractor ctor :540-555; PATCH_SIZE is fixed)
+  constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+  if (valid && lane < 31) {
+    // every (u, v) of the 31 x 31 square is inside the level for a valid
+    // keypoint, so the 31 row loads are issued unconditionally and the circle
+    // applied as a weight
+    const int u = lane - 15, au = u < 0 ? -u : u;
+    int I[31];
+#pragma unroll
+    for (int v = -15; v <= 15; ++v) I[v + 15] = center[u + v * pitch];
+#pragma unroll
+    for (int v = -15; v <= 15; ++v) {
+      const int w = au <= kUmax[v < 0 ? -v : v] ? I[v + 15] : 0;
+      m10 += u * w;
+      m01 += v * w;
     }
   }
-  m10 = wave_sum(m10);
-  m01 = wave_sum(m01);
+  m10 = half_sum(m10);
+  m01 = half_sum(m01);
   const float angle = fast_atan2_dev((float)m01, (float)m10);
 
-  // computeOrbDescriptor: a = (float)cos(angle*pi/180), b = (float)sin(...)
-  // with glibc's cosf/sinf (orbx_sincosf.h)
+  // computeOrbDescriptor: a = cosf(angle*pi/180), b = sinf(...), glibc's (orbx_sincosf.h)
   const float factorPI = (float)(M_PI / 180.f);
-  const float ang = __fmul_rn(angle, factorPI);
   float a, b;
-  glibc_sincosf(ang, &b, &a);
-  const uint8_t* bc = blur + g.off + f * g.plane + (long long)y * g.pitch + x;
-  const int step = g.pitch;
-  uint64_t words[4];
+  glibc_sincosf(__fmul_rn(angle, factorPI), &b, &a);
+  __syncthreads();  // staged patches and test table
+
+  // GET_VALUE(idx): center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)]
+  const uint8_t* pc = s_patch[hk] + kObRadius * kObStride + (x - c0);
+  uint32_t dword[8];
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const int test = w * 64 + lane;
-    int px0 = c_brief_x[2 * test];
-    const int py0 = c_brief_y[2 * test];
-    const int px1 = c_brief_x[2 * test + 1], py1 = c_brief_y[2 * test + 1];
-    if (P.pattern_upstream && 2 * test == kBriefForkPoint) px0 = kBriefUpstreamX;
-    // GET_VALUE(idx): center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)]
-    const int ry0 = __float2int_rn(__fadd_rn(__fmul_rn((float)px0, b), __fmul_rn((float)py0, a)));
-    const int rx0 = __float2int_rn(__fsub_rn(__fmul_rn((float)px0, a), __fmul_rn((float)py0, b)));
-    const int ry1 = __float2int_rn(__fadd_rn(__fmul_rn((float)px1, b), __fmul_rn((float)py1, a)));
-    const int rx1 = __float2int_rn(__fsub_rn(__fmul_rn((float)px1, a), __fmul_rn((float)py1, b)));
-    words[w] = __ballot(bc[ry0 * step + rx0] < bc[ry1 * step + rx1]);
+  for (int k = 0; k < 8; ++k) {
+    const int t = s_tests[lane + 32 * k];
+    const float px0 = (float)(signed char)(t & 0xFF), py0 = (float)(signed char)((t >> 8) & 0xFF);
+    const float px1 = (float)(signed char)((t >> 16) & 0xFF), py1 = (float)(t >> 24);
+    const int ry0 = __float2int_rn(__fadd_rn(__fmul_rn(px0, b), __fmul_rn(py0, a)));
+    const int rx0 = __float2int_rn(__fsub_rn(__fmul_rn(px0, a), __fmul_rn(py0, b)));
+    const int ry1 = __float2int_rn(__fadd_rn(__fmul_rn(px1, b), __fmul_rn(py1, a)));
+    const int rx1 = __float2int_rn(__fsub_rn(__fmul_rn(px1, a), __fmul_rn(py1, b)));
+    const uint64_t m = __ballot(pc[ry0 * kObStride + rx0] < pc[ry1 * kObStride + rx1]);
+    dword[k] = (uint32_t)((tid & 32) ? (m >> 32) : m);
   }
+
+  if (!valid) return;
+  int outpos = idx;
+  for (int i = 0; i < l; ++i) outpos += cnt[i];
   const long long o = (long long)f * P.kp_per_frame + outpos;
-  if (lane < 4) ((uint64_t*)(out_desc + o * 32))[lane] = words[lane];
-  if (lane == 0) {
+  if (lane < 2) {
+    uint4* d = (uint4*)(out_desc + o * 32) + lane;
+    *d = lane ? make_uint4(dword[4], dword[5], dword[6], dword[7])
+              : make_uint4(dword[0], dword[1], dword[2], dword[3]);
+  } else if (lane == 2) {
     orbx_kp kp;
     float fxp = (float)x, fyp = (float)y;
     if (l != 0) {
@@ -121,13 +165,20 @@ static bool g_pattern_uploaded = false;
 int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const ExtractBuffers& X, orbx_kp* kps,
                         uint8_t* desc, int* counts, int batch, hipStream_t s) {
   if (!g_pattern_uploaded) {
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_x), kBriefPointX, 512) != hipSuccess) return ORBX_EDEVICE;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_y), kBriefPointY, 512) != hipSuccess) return ORBX_EDEVICE;
+    int t[2][256];
+    for (int m = 0; m < 2; ++m)
+      for (int i = 0; i < 256; ++i) {
+        int x0 = kBriefPointX[2 * i];
+        if (m == 1 && 2 * i == kBriefForkPoint) x0 = kBriefUpstreamX;
+        const int y0 = kBriefPointY[2 * i], x1 = kBriefPointX[2 * i + 1], y1 = kBriefPointY[2 * i + 1];
+        t[m][i] = (x0 & 0xFF) | ((y0 & 0xFF) << 8) | ((x1 & 0xFF) << 16) | ((y1 & 0xFF) << 24);
+      }
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_tests), t, sizeof(t)) != hipSuccess) return ORBX_EDEVICE;
     g_pattern_uploaded = true;
   }
-  dim3 grid((P.kp_per_frame + 3) / 4, batch);
-  hipLaunchKernelGGL(orient_brief_kernel, grid, dim3(256), 0, s, P, lp, X.blur, X.qkeys, X.qcounts, X.umax, kps, desc,
-                     counts);
+  dim3 grid((P.kp_per_frame + kObKps - 1) / kObKps, batch);
+  hipLaunchKernelGGL(orient_brief_kernel, grid, dim3(kObThreads), 0, s, P, lp, X.blur, X.qkeys, X.qcounts, X.umax,
+                     kps, desc, counts);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
