@@ -22,6 +22,10 @@
 // unless it is empty, and writes the keys in row-major order (the order
 // cv::FAST emits them) into the cell's fixed slot range. Every compaction is
 // an ordered ballot compaction, so row-major order is preserved throughout.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 #include "orbx_device.cuh"
 
 namespace orbx {
@@ -94,8 +98,13 @@ __device__ __forceinline__ void ring_masks(const uint8_t* c, int lo, int hi, uin
 __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPtrs lp,
                                                         const CellGeom* __restrict__ cells,
                                                         uint32_t* __restrict__ slots,
-                                                        int* __restrict__ cell_counts) {
+                                                        int* __restrict__ cell_counts, int* dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](int k) {
+    if (dbg && threadIdx.x == 0)
+      dbg[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + k] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
+  };
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
   const int cell = wg % P.ncells_total, f = wg / P.ncells_total, lane = threadIdx.x;
   const CellGeom cg = cells[cell];
@@ -119,8 +128,26 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
   const uint8_t* rows = lp.base[l] + f * lp.fstride[l] + (long long)cg.r0 * pitch;
   const int a0 = cg.c0 & ~15, ox = cg.c0 - a0;
   if (lp.aligned16[l]) {
-    const int nch = (cg.c1 - a0 + 15) >> 4;
-    for (int i = lane; i < rh * nch; i += 64) {
+    // the ROI's 16-byte chunks in flight at once (4 per lane; tall cells loop for the rest)
+    const int nch = (cg.c1 - a0 + 15) >> 4, total = rh * nch;
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = lane + 64 * k;
+      if (i < total) {
+        const int r = i / nch, ch = i - r * nch;
+        v[k] = *(const uint4*)(rows + (long long)r * pitch + a0 + ch * 16);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = lane + 64 * k;
+      if (i < total) {
+        const int r = i / nch, ch = i - r * nch;
+        *(uint4*)(roi + r * kRoiStride + ch * 16) = v[k];
+      }
+    }
+    for (int i = lane + 256; i < total; i += 64) {
       const int r = i / nch, ch = i - r * nch;
       *(uint4*)(roi + r * kRoiStride + ch * 16) = *(const uint4*)(rows + (long long)r * pitch + a0 + ch * 16);
     }
@@ -129,8 +156,9 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
       for (int c = lane; c < rw; c += 64) roi[r * kRoiStride + ox + c] = rows[(long long)r * pitch + cg.c0 + c];
   }
   const int sw = bw + 2;  // score map with a zero ring
-  for (int i = lane; i < sw * (bh + 2); i += 64) sc[i] = 0;
+  for (int i = lane; i < (sw * (bh + 2) + 3) >> 2; i += 64) ((uint32_t*)sc)[i] = 0;
   __syncthreads();
+  stamp(0);
 
   const int t = P.t_low;
   const uint64_t lt = lanemask_lt(lane);
@@ -139,23 +167,30 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
   const int rstep = two ? 2 : 1;
   const uint8_t* band = roi + 3 * kRoiStride + ox + 3;  // band pixel (0,0)
 
-  // (a) compass pre-test over all band pixels, row-major ordered compaction
+  // (a) compass pre-test over all band pixels, row-major ordered compaction;
+  // four row groups per step so their LDS reads are in flight together
   int n1 = 0;
-  for (int by0 = 0; by0 < bh; by0 += rstep) {
-    const int by = by0 + lr;
-    bool flag = false;
-    if (by < bh && lc < bw) {
-      const uint8_t* c = band + by * kRoiStride + lc;
+  for (int by0 = 0; by0 < bh; by0 += 4 * rstep) {
+    bool fl[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int by = by0 + q * rstep + lr;
+      const uint8_t* c = band + min(by, bh - 1) * kRoiStride + min(lc, bw - 1);
       const int v = c[0], lo = v - t, hi = v + t;
       const int n0 = c[3 * kRoiStride], n4 = c[3], n8 = c[-3 * kRoiStride], n12 = c[-3];
       const int nd = (n0 < lo) + (n4 < lo) + (n8 < lo) + (n12 < lo);
       const int nb = (n0 > hi) + (n4 > hi) + (n8 > hi) + (n12 > hi);
-      flag = nd >= 2 || nb >= 2;
+      fl[q] = by < bh && lc < bw && (nd >= 2 || nb >= 2);
     }
-    const uint64_t m = __ballot(flag);
-    if (flag) list[n1 + __popcll(m & lt)] = (uint16_t)((by << 8) | lc);
-    n1 += __popcll(m);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int by = by0 + q * rstep + lr;
+      const uint64_t m = __ballot(fl[q]);
+      if (fl[q]) list[n1 + __popcll(m & lt)] = (uint16_t)((by << 8) | lc);
+      n1 += __popcll(m);
+    }
   }
+  stamp(1);
   // (b) full ring test, compacted in place (reads of a chunk precede its writes)
   int n2 = 0;
   for (int i0 = 0; i0 < n1; i0 += 64) {
@@ -173,6 +208,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
     if (det) list[n2 + __popcll(m & lt)] = (uint16_t)e;
     n2 += __popcll(m);
   }
+  stamp(2);
   // (c) FAST scores of the detected pixels
   for (int i = lane; i < n2; i += 64) {
     const int e = list[i];
@@ -184,6 +220,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
     sc[((e >> 8) + 1) * sw + (e & 255) + 1] = (uint8_t)corner_score16(d, t);
   }
   __syncthreads();
+  stamp(3);
   // (d) 3x3 NMS at both thresholds (neighbours below a threshold count as 0)
   const int ti = P.t_ini, tm = P.t_min;
   const int nch2 = (n2 + 63) >> 6;
@@ -229,6 +266,11 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
     base += __popcll(m);
   }
   if (lane == 0) *cnt = min(base, (int)cg.cap);
+  stamp(4);
+  if (dbg && lane == 0) {
+    dbg[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + 5] = n1;
+    dbg[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + 6] = n2;
+  }
 }
 
 size_t fast_lds_bytes(const ExtractParams& P) {
@@ -240,8 +282,28 @@ size_t fast_lds_bytes(const ExtractParams& P) {
 
 int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cells, uint32_t* slots,
                 int* cell_counts, int batch, hipStream_t s) {
+  static int* dbg = nullptr;  // diagnostics only: per-cell phase cycles (ORBX_FAST_PROF=1)
+  static const bool prof = getenv("ORBX_FAST_PROF") && getenv("ORBX_FAST_PROF")[0] == '1';
+  const int nwg = P.ncells_total * batch;
+  if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)nwg * 32);
+  if (prof) (void)hipMemsetAsync(dbg, 0, (size_t)nwg * 32, s);
   hipLaunchKernelGGL(fast_cells_kernel, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P, lp, cells,
-                     slots, cell_counts);
+                     slots, cell_counts, prof ? dbg : nullptr);
+  if (prof) {
+    std::vector<int> h((size_t)nwg * 8);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), dbg, h.size() * 4, hipMemcpyDeviceToHost);
+    double t[8] = {0};
+    int n = 0;
+    for (int w = 0; w < nwg; ++w) {
+      if (h[w * 8 + 4] == 0) continue;  // skipped cell
+      ++n;
+      for (int k = 0; k < 7; ++k) t[k] += h[w * 8 + k];
+    }
+    n = n ? n : 1;
+    fprintf(stderr, "fast: %d cells; avg cycles at stage end: staged %.0f compass %.0f ring %.0f score %.0f done %.0f; avg n1 %.1f n2 %.1f\n",
+            n, t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6] / n);
+  }
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
