@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=24, help="frames in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-match", action="store_true", help="extract only (C2)")
     ap.add_argument("--serial", action="store_true", help="one stream: no overlap of matching with the next extraction")
+    ap.add_argument("--split", type=int, default=1, help="extraction launches (and streams) per batch")
     args = ap.parse_args()
 
     from orb_slam_cuda_amd import sharding
@@ -114,7 +115,12 @@ def main():
     check(L.orbx_set_device(local))
     d_frames.upload(host)
 
-    ext = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=B)
+    S = args.split
+    if S < 1 or B % S:
+        raise SystemExit("--split must divide --batch")
+    BS = B // S  # frames per extraction launch
+    exts = [pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=BS) for _ in range(S)]
+    ext = exts[0]
     cap = ext.frame_capacity
     KP, DS = 28, 32
     # three output sets: batch k writes set k % 3, slots 1..B, and then copies
@@ -130,7 +136,8 @@ def main():
     d_bi, d_bd, d_sd = (_lib.DeviceArray(B * cap * 4) for _ in range(3))
     d_m12 = _lib.DeviceArray(B * cap * 4)
     d_nm = _lib.DeviceArray(B * 4)
-    s_ext = _lib.Stream()
+    s_exts = [_lib.Stream() for _ in range(S)]
+    s_ext = s_exts[0]
     s_match = _lib.Stream() if not args.serial else s_ext
     bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
     vp = lambda a: C.c_void_p(a)
@@ -143,11 +150,21 @@ def main():
         extraction stream waits for matching k-2 (the last reader of that
         set); matching k waits for extraction k."""
         b, nb = k % NS, (k + 1) % NS
-        arr = (C.c_void_p * 6)(*[e.e.value for e in evs[:6]])
-        check(L.orbx_set_stage_events(ext.handle, arr))
-        check(L.orbx_extract_batch(ext.handle, vp(d_frames.ptr), B, H * pitch, pitch,
-                                   vp(d_kps[b].ptr + cap * KP), vp(d_desc[b].ptr + cap * DS),
-                                   vp(d_counts[b].ptr + 4), s_ext.s))
+        # the batch is cut into S contiguous parts, one extractor and stream each
+        for h, (ex, se) in enumerate(zip(exts, s_exts)):
+            if h == 0:
+                arr = (C.c_void_p * 6)(*[e.e.value for e in evs[:6]])
+                check(L.orbx_set_stage_events(ex.handle, arr))
+            elif not args.serial and k >= 3:
+                se.wait(ev_done[k - 3])  # matching k-3 was the last reader of set k % 3
+            sv = se if not args.serial else s_ext
+            check(L.orbx_extract_batch(ex.handle, vp(d_frames.ptr + h * BS * H * pitch), BS, H * pitch, pitch,
+                                       vp(d_kps[b].ptr + (1 + h * BS) * cap * KP),
+                                       vp(d_desc[b].ptr + (1 + h * BS) * cap * DS),
+                                       vp(d_counts[b].ptr + 4 * (1 + h * BS)), sv.s))
+            if h > 0 and not args.serial:
+                ev_part[k][h].record(se)
+                s_ext.wait(ev_part[k][h])
         ev_ext[k].record(s_ext)
         if k >= 2 and not args.serial:
             s_ext.wait(ev_done[k - 2])
@@ -175,19 +192,22 @@ def main():
     evsets = [[_lib.Event() for _ in range(n_ev)] for _ in range(total_steps)]
     ev_ext = [_lib.Event() for _ in range(total_steps)]
     ev_done = [_lib.Event() for _ in range(total_steps)]
+    ev_part = [[_lib.Event() for _ in range(S)] for _ in range(total_steps)]
+    def sync_all():
+        for se in s_exts:
+            se.synchronize()
+        s_match.synchronize()
+
     for k in range(args.warmup):
         step(k, evsets[k], ev_ext, ev_done)
-    s_ext.synchronize()
-    s_match.synchronize()
+    sync_all()
     if dist is not None:
         dist.barrier()
-    s_ext.synchronize()
-    s_match.synchronize()
+    sync_all()
     t0 = time.perf_counter()
     for k in range(args.warmup, total_steps):
         step(k, evsets[k], ev_ext, ev_done)
-    s_ext.synchronize()
-    s_match.synchronize()
+    sync_all()
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
@@ -215,7 +235,7 @@ def main():
     dominant = max(STAGES, key=lambda s: st[s])
     # roofline of the pyramid+FAST pass and of the dominant kernel
     pf_ms = st["pyramid"] + st["fast_grid"]
-    pf_gbs = ab["pyr_fast_pass"] * B / (pf_ms * 1e-3) / 1e9
+    pf_gbs = ab["pyr_fast_pass"] * BS / (pf_ms * 1e-3) / 1e9
     roof = None
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
                   "orient_brief": ab["orient_brief"]}
@@ -227,10 +247,10 @@ def main():
             traffic = json.load(open(pmc_path)).get(KERNELS[rk].split(" ")[0], {}).get("bytes_per_launch")
         except Exception:
             traffic = None
-    ach = hbm_stages[rk] * B / (st[rk] * 1e-3) / 1e9
+    ach = hbm_stages[rk] * BS / (st[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "algorithmic_bytes_per_launch": int(hbm_stages[rk] * B),
+            "algorithmic_bytes_per_launch": int(hbm_stages[rk] * BS),
             "avg_launch_ms": round(st[rk], 4)}
 
     cpu = None
@@ -246,13 +266,13 @@ def main():
             "config": {"workload": cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only",
                        "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
                        "frames_per_step_per_gpu": B, "parallelism": f"frame-sharded x{world}, no collectives",
-                       "streams": 1 if args.serial else 2},
+                       "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS},
             "roofline": roof,
             "cpu_baseline": cpu,
             "pyr_fast_pass_hbm_gbs": round(pf_gbs, 1),
             "dominant_kernel": KERNELS[dominant],
             "stage_ms_per_step": {s: round(v, 4) for s, v in st.items()},
-            "extract_only_frames_per_s": round(B / (extract_ms * 1e-3), 1),
+            "extract_only_frames_per_s": round(BS / (extract_ms * 1e-3), 1),
             "event_ms_per_step": round(ev_ms / args.steps, 4),
             "keypoints_per_frame": round(nkp_mean, 1),
             "init_matches_per_pair": round(float(nm[1:].mean()), 1),
