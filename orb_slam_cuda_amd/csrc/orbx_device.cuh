@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "orbx_internal.h"
+#include "orbx_wave.cuh"
 
 namespace orbx {
 
@@ -80,12 +81,7 @@ __device__ int block_scan_excl(int* a, int n, int* s_tmp) {
   const int b = min(tid * per, n), e = min(b + per, n);
   int sum = 0;
   for (int i = b; i < e; ++i) sum += a[i];
-  int x = sum;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
+  const int x = wave_incl_scan_dpp(sum);
   if (lane == 63) s_tmp[w] = x;
   __syncthreads();
   int wpre = 0, total = 0;

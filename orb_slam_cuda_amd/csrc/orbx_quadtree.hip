@@ -19,6 +19,11 @@
 // The new list is [children of the split nodes, last split first, each as
 // n4 n3 n2 n1] followed by the untouched nodes in their old order, which is
 // exactly what the reference's push_front/erase sequence produces.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 #include "orbx_device.cuh"
 
 namespace orbx {
@@ -58,8 +63,16 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
                                                               uint32_t* __restrict__ qscratch,
                                                               uint16_t* __restrict__ qnscratch,
                                                               uint32_t* __restrict__ qkeys,
-                                                              int* __restrict__ qcounts, int* err) {
+                                                              int* __restrict__ qcounts, int* err, int* dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+  int dbg_rounds = 0, dbg_sorted = 0;
+  unsigned long long dbg_ph[5] = {0, 0, 0, 0, 0}, dbg_t = 0;
+  auto ph = [&](int k) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (k >= 0) dbg_ph[k] += t - dbg_t;
+    dbg_t = t;
+  };
   const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
   const LevelGeom& g = P.lv[l];
   const int MN = P.maxnodes, SN = P.sortn;
@@ -78,6 +91,7 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   int* rank = (int*)take(4ull * MN);   // processing rank of a split node, or -1
   int* ord = (int*)take(4ull * MN);    // processing rank -> node
   int* coff = (int*)take(4ull * (P.max_cells_level + 1));
+  int* s_soff = (int*)take(4ull * (P.max_cells_level + 1));  // cell slot offsets
   int* s_tmp = (int*)take(64);
   int* s_var = (int*)take(64);
   uint32_t* lkeys = (uint32_t*)take(4ull * P.kcap_lds);
@@ -96,11 +110,19 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   }
   const uint32_t* fslots = slots + (long long)f * P.slots_per_frame;
   {
-    const int wv = tid >> 6, lane = tid & 63;
-    for (int c = wv; c < g.ncells; c += kQtThreads / 64) {
-      const int n = cntp[c], o = coff[c];
-      const uint32_t* src = fslots + cells[g.cell0 + c].slot_off;
-      for (int i = lane; i < n; i += 64) keys[o + i] = src[i];
+    // gather the K keys with independent loads: key k lives in cell c with
+    // coff[c] <= k < coff[c+1] (binary search in LDS), at slot_off(c) + k - coff[c]
+    for (int c = tid; c < g.ncells; c += kQtThreads) s_soff[c] = cells[g.cell0 + c].slot_off;
+    if (tid == 0) coff[g.ncells] = K;
+    __syncthreads();
+    for (int k = tid; k < K; k += kQtThreads) {
+      int lo = 0, hi = g.ncells - 1;  // last c with coff[c] <= k
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (coff[mid] <= k) lo = mid;
+        else hi = mid - 1;
+      }
+      keys[k] = fslots[s_soff[lo] + k - coff[lo]];
     }
   }
   // ---- root nodes: nIni columns of width hX (src/ORBextractor.cc:894-936)
@@ -143,6 +165,7 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   for (int round = 0; round < 64; ++round) {
     const int size = s_var[0];
     const bool sorted_phase = s_var[1] != 0;
+    ph(-1);
     // child key counts of every splittable node
     for (int n = tid; n < size; n += kQtThreads) cc[n] = make_int4(0, 0, 0, 0);
     __syncthreads();
@@ -154,6 +177,7 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
       }
     }
     __syncthreads();
+    ph(0);
     // processing order and cut-off: split while the list size is < N
     if (!sorted_phase) {
       for (int n = tid; n < size; n += kQtThreads) {
@@ -176,31 +200,27 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
         }
       }
     } else {
-      for (int i = tid; i < SN; i += kQtThreads) {
-        unsigned long long key = 0;
-        if (i < size && nkA[i] > 1)
-          key = ((unsigned long long)nkA[i] << 40) | ((unsigned long long)seqA[i] << 16) | (unsigned long long)i;
-        s_sort[i] = key;
-        if (i < size) rank[i] = -1;
+      // descending order of the candidates by (size, creation): each candidate
+      // counts the larger keys (keys are distinct), no sorting network
+      unsigned long long* s_key = (unsigned long long*)nodeB;  // free until the table phase
+      for (int i = tid; i < size; i += kQtThreads) {
+        s_key[i] = nkA[i] > 1
+                       ? ((unsigned long long)nkA[i] << 40) | ((unsigned long long)seqA[i] << 16) | (unsigned long long)i
+                       : 0ull;
+        s_sort[i] = 0;
+        rank[i] = -1;
       }
       if (tid == 0) s_var[3] = 0;
       __syncthreads();
-      for (int kk = 2; kk <= SN; kk <<= 1) {  // bitonic sort, descending
-        for (int j = kk >> 1; j > 0; j >>= 1) {
-          for (int i = tid; i < SN; i += kQtThreads) {
-            const int ixj = i ^ j;
-            if (ixj > i) {
-              const unsigned long long a = s_sort[i], b = s_sort[ixj];
-              const bool desc = (i & kk) == 0;
-              if (desc ? (a < b) : (a > b)) {
-                s_sort[i] = b;
-                s_sort[ixj] = a;
-              }
-            }
-          }
-          __syncthreads();
+      for (int i = tid; i < size; i += kQtThreads) {
+        const unsigned long long ki = s_key[i];
+        if (ki) {
+          int r = 0;
+          for (int j = 0; j < size; ++j) r += s_key[j] > ki ? 1 : 0;
+          s_sort[r] = ki;
         }
       }
+      __syncthreads();
       for (int j = tid; j < size; j += kQtThreads) {
         const unsigned long long key = s_sort[j];
         tA[j] = key ? nonempty(cc[(int)(key & 0xFFFF)]) - 1 : 0;
@@ -221,6 +241,7 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
       }
     }
     __syncthreads();
+    ph(sorted_phase ? 4 : 1);
     const int m = s_var[2];  // nodes split this round
     // children block: processing rank j lands at T - (E_j + C_j) (last split first)
     for (int j = tid; j < m; j += kQtThreads) tA[j] = nonempty(cc[ord[j]]);
@@ -263,6 +284,7 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
       }
     }
     __syncthreads();
+    ph(2);
     // re-home the keys
     for (int k = tid; k < K; k += kQtThreads) {
       const int n = knode[k];
@@ -290,9 +312,13 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
       s_var[0] = newSize;
     }
     __syncthreads();
+    ph(3);
+    dbg_rounds++;
+    dbg_sorted += sorted_phase;
     if (finish) break;
     if (round == 63 && tid == 0) atomicOr(err, 2);
   }
+  const unsigned long long t_rounds = __builtin_amdgcn_s_memtime();
   // ---- keep the best key per node: max FAST score, first in node (= original) order
   const int size = s_var[0];
   for (int n = tid; n < size; n += kQtThreads) s_sort[n] = 0;
@@ -310,21 +336,57 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     qcounts[f * P.L + l] = min(size, g.kcap);
     if (size > g.kcap) atomicOr(err, 4);
   }
+  if (dbg && tid == 0) {  // diagnostics only (ORBX_QT_PROF=1)
+    int* d = dbg + (blockIdx.y * gridDim.x + blockIdx.x) * 8;
+    d[0] = (int)(t_rounds - t_begin);
+    d[1] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
+    d[2] = dbg_rounds;
+    d[3] = dbg_sorted;
+    d[4] = K;
+    d[5] = size;
+    for (int k = 0; k < 5; ++k) dbg[gridDim.x * gridDim.y * 8 + (blockIdx.y * gridDim.x + blockIdx.x) * 8 + k] = (int)dbg_ph[k];
+  }
 }
 
 size_t quadtree_lds_bytes(const ExtractParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t MN = P.maxnodes, SN = P.sortn;
   return r16(8 * SN) + 2 * r16(sizeof(QNode) * MN) + 4 * r16(4 * MN) + r16(16 * MN) + 2 * r16(4 * (MN + 1)) +
-         2 * r16(4 * MN) + r16(4 * (P.max_cells_level + 1)) + 2 * r16(64) + r16(4ull * P.kcap_lds) +
+         2 * r16(4 * MN) + 2 * r16(4 * (P.max_cells_level + 1)) + 2 * r16(64) + r16(4ull * P.kcap_lds) +
          r16(2ull * P.kcap_lds);
 }
 
 const void* quadtree_kernel_ptr() { return (const void*)quadtree_kernel; }
 
 int launch_quadtree(const ExtractParams& P, const ExtractBuffers& X, int batch, hipStream_t s) {
+  static int* dbg = nullptr;  // diagnostics only: per-(frame, level) cycles and rounds (ORBX_QT_PROF=1)
+  static const bool prof = getenv("ORBX_QT_PROF") && getenv("ORBX_QT_PROF")[0] == '1';
+  const int nwg = P.L * batch;
+  if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)nwg * 64);
   hipLaunchKernelGGL(quadtree_kernel, dim3(P.L, batch), dim3(kQtThreads), quadtree_lds_bytes(P), s, P,
-                     X.cell_counts, X.slots, X.cells, X.qscratch, X.qnode_scratch, X.qkeys, X.qcounts, X.err);
+                     X.cell_counts, X.slots, X.cells, X.qscratch, X.qnode_scratch, X.qkeys, X.qcounts, X.err,
+                     prof ? dbg : nullptr);
+  if (prof) {
+    std::vector<int> h((size_t)nwg * 16);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), dbg, h.size() * 4, hipMemcpyDeviceToHost);
+    for (int l = 0; l < P.L; ++l) {
+      double a[6] = {0};
+      int mx = 0;
+      for (int f = 0; f < batch; ++f)
+        for (int k = 0; k < 6; ++k) {
+          a[k] += h[(f * P.L + l) * 8 + k];
+          if (k == 1) mx = std::max(mx, h[(f * P.L + l) * 8 + 1]);
+        }
+      double q[5] = {0};
+      for (int f = 0; f < batch; ++f)
+        for (int k = 0; k < 5; ++k) q[k] += h[(size_t)nwg * 8 + (f * P.L + l) * 8 + k];
+      fprintf(stderr, "quadtree L%d: avg cycles rounds %.0f total %.0f (max %d) rounds %.1f sorted %.1f K %.0f out %.0f"
+              " | count %.0f order %.0f sortorder %.0f table %.0f rehome %.0f\n",
+              l, a[0] / batch, a[1] / batch, mx, a[2] / batch, a[3] / batch, a[4] / batch, a[5] / batch,
+              q[0] / batch, q[1] / batch, q[4] / batch, q[2] / batch, q[3] / batch);
+    }
+  }
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
