@@ -10,13 +10,26 @@ namespace orbx {
 // Separable 7-tap fixed-point Gaussian, BORDER_REFLECT_101 at the level edges.
 // Tile = 128 x 32 outputs per 256-thread block. The input tile (+3 halo, 16-B
 // aligned: columns [x0-16, x0+144)) is staged with 16-byte loads (byte loads
-// with reflection only where a chunk leaves the image); the row pass keeps
-// u16 sums (max 257*255 = 65535); each thread then produces a 4 x 4 output
-// block from a sliding column window and stores 4 bytes per row.
+// with reflection only where a chunk leaves the image).
+//   row pass:    v_dot4_u32_u8 of a pixel dword with a tap dword: 10 dot4 per
+//                4 outputs (sums <= 257*255 = 65535 fit u16); the sums of two
+//                vertically adjacent rows are packed into one dword,
+//   column pass: v_dot2_u32_u16 of such a row pair with a tap pair: 4 dot2
+//                per output, then (acc + 2^15) >> 16.
 constexpr int kBlurTW = 128, kBlurTH = 32, kBlurInW = kBlurTW + 32;
+constexpr int kBlurPairs = (kBlurTH + 6 + 1) / 2;  // 19 staged row pairs
+
+typedef unsigned short us2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot4(uint32_t px, uint32_t taps, uint32_t acc) {
+  return __builtin_amdgcn_udot4(px, taps, acc, false);
+}
+__device__ __forceinline__ uint32_t dot2(uint32_t pair, uint32_t taps, uint32_t acc) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(us2_t, pair), __builtin_bit_cast(us2_t, taps), acc, false);
+}
+
 __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp, uint8_t* __restrict__ blur) {
-  __shared__ __attribute__((aligned(16))) uint8_t in[kBlurTH + 6][kBlurInW];
-  __shared__ __attribute__((aligned(16))) uint16_t tmp[kBlurTH + 6][kBlurTW];
+  __shared__ __attribute__((aligned(16))) uint8_t in[kBlurPairs * 2][kBlurInW];
+  __shared__ __attribute__((aligned(16))) uint32_t tmp[kBlurPairs][kBlurTW];  // {row 2p, row 2p+1} u16 sums
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
   const int f = wg / gridDim.x, tid = threadIdx.x;
   int t = wg % gridDim.x, l = 0;
@@ -56,56 +69,54 @@ __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp
   }
   __syncthreads();
   const int* k = P.gauss;
-  // row pass: 4 outputs per item, input bytes [x+13, x+23) of the staged row
-  for (int i = tid; i < (kBlurTH + 6) * (kBlurTW / 4); i += 256) {
-    const int r = i / (kBlurTW / 4), x = (i - r * (kBlurTW / 4)) * 4;
-    const uint32_t w0 = *(const uint32_t*)&in[r][x + 12];
-    const uint32_t w1 = *(const uint32_t*)&in[r][x + 16];
-    const uint32_t w2 = *(const uint32_t*)&in[r][x + 20];
-    int px[12];
+  // tap dwords of the row pass: output x reads staged bytes [x+13, x+20)
+  // from dwords A = [x+12, x+16), B = [x+16, x+20), C = [x+20, x+24)
+  const uint32_t kA0 = (k[0] << 8) | (k[1] << 16) | (k[2] << 24), kB0 = k[3] | (k[4] << 8) | (k[5] << 16) | (k[6] << 24);
+  const uint32_t kA1 = (k[0] << 16) | (k[1] << 24), kB1 = k[2] | (k[3] << 8) | (k[4] << 16) | (k[5] << 24), kC1 = k[6];
+  const uint32_t kA2 = k[0] << 24, kB2 = k[1] | (k[2] << 8) | (k[3] << 16) | (k[4] << 24), kC2 = k[5] | (k[6] << 8);
+  const uint32_t kB3 = k[0] | (k[1] << 8) | (k[2] << 16) | (k[3] << 24), kC3 = k[4] | (k[5] << 8) | (k[6] << 16);
+  // row pass: item = (row pair, 4 columns)
+  for (int i = tid; i < kBlurPairs * (kBlurTW / 4); i += 256) {
+    const int pr = i / (kBlurTW / 4), x = (i - pr * (kBlurTW / 4)) * 4;
+    uint32_t o[2][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      px[j] = (w0 >> (8 * j)) & 255;
-      px[4 + j] = (w1 >> (8 * j)) & 255;
-      px[8 + j] = (w2 >> (8 * j)) & 255;
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t* row = (const uint32_t*)in[2 * pr + h];
+      const uint32_t A = row[(x + 12) >> 2], B = row[(x + 16) >> 2], C = row[(x + 20) >> 2];
+      o[h][0] = dot4(B, kB0, dot4(A, kA0, 0));
+      o[h][1] = dot4(C, kC1, dot4(B, kB1, dot4(A, kA1, 0)));
+      o[h][2] = dot4(C, kC2, dot4(B, kB2, dot4(A, kA2, 0)));
+      o[h][3] = dot4(C, kC3, dot4(B, kB3, 0));
     }
-    uint32_t o01 = 0, o23 = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      int acc = 0;
-#pragma unroll
-      for (int j = 0; j < 7; ++j) acc += k[j] * px[q + 1 + j];
-      if (q < 2) o01 |= (uint32_t)acc << (16 * q);
-      else o23 |= (uint32_t)acc << (16 * (q - 2));
-    }
-    *(uint2*)&tmp[r][x] = make_uint2(o01, o23);
+    *(uint4*)&tmp[pr][x] = make_uint4(o[0][0] | (o[1][0] << 16), o[0][1] | (o[1][1] << 16),
+                                      o[0][2] | (o[1][2] << 16), o[0][3] | (o[1][3] << 16));
   }
   __syncthreads();
-  // column pass: thread -> 4 columns x 4 rows
-  const int cx = (tid & 31) * 4, ry = (tid >> 5) * 4;
-  int col[10][4];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    const uint2 v = *(const uint2*)&tmp[ry + j][cx];
-    col[j][0] = v.x & 0xFFFF;
-    col[j][1] = v.x >> 16;
-    col[j][2] = v.y & 0xFFFF;
-    col[j][3] = v.y >> 16;
-  }
+  // column pass: thread -> 2 output rows (o, o+1) x 4 columns, reading row pairs o/2 .. o/2+3
+  const uint32_t t01 = k[0] | (k[1] << 16), t23 = k[2] | (k[3] << 16), t45 = k[4] | (k[5] << 16), t6 = k[6];
+  const uint32_t u0 = k[0] << 16, u12 = k[1] | (k[2] << 16), u34 = k[3] | (k[4] << 16), u56 = k[5] | (k[6] << 16);
   uint8_t* D = blur + g.off + f * g.plane;
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int y = y0 + ry + rr;
-    uint32_t packed = 0;
+  for (int i = tid; i < (kBlurTH / 2) * (kBlurTW / 4); i += 256) {
+    const int rp = i / (kBlurTW / 4), cx = (i - rp * (kBlurTW / 4)) * 4;
+    const uint4 q0 = *(const uint4*)&tmp[rp][cx], q1 = *(const uint4*)&tmp[rp + 1][cx];
+    const uint4 q2 = *(const uint4*)&tmp[rp + 2][cx], q3 = *(const uint4*)&tmp[rp + 3][cx];
+    const uint32_t P0[4] = {q0.x, q0.y, q0.z, q0.w}, P1[4] = {q1.x, q1.y, q1.z, q1.w};
+    const uint32_t P2[4] = {q2.x, q2.y, q2.z, q2.w}, P3[4] = {q3.x, q3.y, q3.z, q3.w};
+    int va[4], vb[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      int acc = 0;
-#pragma unroll
-      for (int j = 0; j < 7; ++j) acc += k[j] * col[rr + j][q];
-      packed |= (uint32_t)sat_u8((acc + (1 << 15)) >> 16) << (8 * q);
+      const uint32_t a = dot2(P3[q], t6, dot2(P2[q], t45, dot2(P1[q], t23, dot2(P0[q], t01, 1u << 15))));
+      const uint32_t b = dot2(P3[q], u56, dot2(P2[q], u34, dot2(P1[q], u12, dot2(P0[q], u0, 1u << 15))));
+      va[q] = min((int)(a >> 16), 255);
+      vb[q] = min((int)(b >> 16), 255);
     }
-    if (y < H) {
-      const int x = x0 + cx;
+    const uint32_t pa = pack4_u8(va[0], va[1], va[2], va[3]), pb = pack4_u8(vb[0], vb[1], vb[2], vb[3]);
+    const int x = x0 + cx;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int y = y0 + 2 * rp + h;
+      if (y >= H) break;
+      const uint32_t packed = h ? pb : pa;
       uint8_t* dst = D + (long long)y * g.pitch + x;
       if (x + 4 <= W) {
         *(uint32_t*)dst = packed;

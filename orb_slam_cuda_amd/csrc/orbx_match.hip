@@ -260,21 +260,17 @@ __device__ __forceinline__ Window make_window(float x, float y, const InitParams
   return w;
 }
 
-// sorted-grid position of flat candidate f (0 <= f < total)
+// sorted-grid position of flat candidate f (0 <= f < total): a scan over the
+// window's few columns with wave-uniform readlanes (no LDS round trips)
 __device__ __forceinline__ int window_pos(const Window& w, int f) {
-  // column c = number of columns whose inclusive prefix <= f
-  int c = 0;
-#pragma unroll 1
-  for (int step = 32; step > 0; step >>= 1) {
-    const int probe = c + step - 1;
-    const int pre = __shfl(w.col_pre, min(probe, 63), 64);
-    if (probe < w.ncol && pre <= f) c += step;
+  int s = 0, prev = 0;
+  for (int c = 0; c < w.ncol; ++c) {
+    const int pre = __builtin_amdgcn_readlane(w.col_pre, c);
+    const int st = __builtin_amdgcn_readlane(w.col_start, c);
+    if (f >= prev && f < pre) s = st + (f - prev);
+    prev = pre;
   }
-  // every lane must take part in a cross-lane read (the source lane of a
-  // bpermute must be active), so no shuffle sits under a lane-varying branch
-  const int pre_prev = __shfl(w.col_pre, max(c - 1, 0), 64);
-  const int start = __shfl(w.col_start, c, 64);
-  return start + (f - (c ? pre_prev : 0));
+  return s;
 }
 
 // Passes 2 and 3 of search_init_kernel, instantiated once with the candidate
@@ -294,6 +290,9 @@ __device__ __forceinline__ int lds_max(LDS int* p, int v) {
   return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+__device__ __forceinline__ int lds_add_g(int* p, int v) { return lds_add((LDS int*)p, v); }
+__device__ __forceinline__ uint64_t lanemask_lt_w(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
 struct InitCtx {
   InitParams P;
   const orbx_kp* kp1;
@@ -303,6 +302,8 @@ struct InitCtx {
   const float* prev;
   uint32_t* s_sort;
   float2* s_xy;
+  float2* s_pos;
+  uint4* s_d0;
   int2* s_queue;
   int* s_m12;
   int* s_cell;
@@ -312,10 +313,11 @@ struct InitCtx {
   int* s_coff;
   int* s_var;
   int n1, n2, total;
+  int qb, qe;  // this wave's range of the octave-0 query list
   int* err;
 };
 
-template <typename CandPtr>
+template <typename CandPtr, bool DESC_LDS>
 __device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
   const InitParams& P = C.P;
   const orbx_kp* kp1 = C.kp1;
@@ -324,8 +326,9 @@ __device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
   const uint8_t* desc2 = C.desc2;
   const float* prev = C.prev;
   const LDS uint32_t* s_sort = (const LDS uint32_t*)C.s_sort;
-  const LDS float* s_xy = (const LDS float*)C.s_xy;  // (x, y) pairs
-  LDS int* s_queue = (LDS int*)C.s_queue;           // {i1, first candidate} pairs
+  const LDS float* s_pos = (const LDS float*)C.s_pos;  // (x, y) by sorted position (passes 1-2)
+  const LDS uint32_t* s_d0 = (const LDS uint32_t*)C.s_d0;  // descriptors by sorted position (DESC_LDS)
+  LDS int* s_queue = (LDS int*)C.s_queue;             // {i1, first candidate} pairs
   LDS int* s_m12 = (LDS int*)C.s_m12;
   const LDS int* s_cell = (const LDS int*)C.s_cell;
   LDS int* s_md = (LDS int*)C.s_md;
@@ -340,12 +343,14 @@ __device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
   (void)err;
   if (P.stop == 2) return;
   // ---- pass 2: fill candidates (reference order) with their Hamming distances
-  for (int q0 = wv * 64; q0 < n1; q0 += kInitThreads) {
-    const int qi = q0 + lane;
+  const LDS int* s_qlist = (const LDS int*)C.s_src;  // octave-0 queries (pass 1)
+  for (int q0 = C.qb; q0 < C.qe; q0 += 64) {
+    const int e = q0 + lane;
+    const int qi = e < C.qe ? s_qlist[e] : 0;
     float cxl = 0.f, cyl = 0.f;
     bool has = false;
     uint4 dl0 = make_uint4(0, 0, 0, 0), dl1 = dl0;
-    if (qi < n1) {
+    if (e < C.qe) {
       has = s_coff[qi + 1] > s_coff[qi];
       if (has) {
         const orbx_kp k = kp1[qi];
@@ -367,21 +372,28 @@ __device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
       const uint4 a1 = make_uint4(__builtin_amdgcn_readlane(dl1.x, j), __builtin_amdgcn_readlane(dl1.y, j),
                                   __builtin_amdgcn_readlane(dl1.z, j), __builtin_amdgcn_readlane(dl1.w, j));
       const Window w = make_window(x, y, P, s_cell);
-      int base = s_coff[q0 + j];
+      int base = s_coff[__builtin_amdgcn_readlane(qi, j)];
       const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
       for (int f0 = 0; f0 < w.total; f0 += 64) {
         const int f = f0 + lane;
-        const int s = window_pos(w, min(f, w.total - 1));
+        const int s = window_pos(w, f);
         bool ok = false;
-        int i2 = 0;
-        if (f < w.total) {
-          i2 = (int)(s_sort[s] & 0xFFFF);
-          ok = fabsf(__fsub_rn(s_xy[2 * i2], x)) < P.r && fabsf(__fsub_rn(s_xy[2 * i2 + 1], y)) < P.r;
-        }
+        if (f < w.total)
+          ok = fabsf(__fsub_rn(s_pos[2 * s], x)) < P.r && fabsf(__fsub_rn(s_pos[2 * s + 1], y)) < P.r;
         const uint64_t m = __ballot(ok);
         if (ok) {
-          const uint4* d2 = (const uint4*)(desc2 + (long long)i2 * 32);
-          const int d = hamming256(a0, a1, d2[0], d2[1]);
+          const int i2 = (int)(s_sort[s] & 0xFFFF);
+          uint4 b0, b1;
+          if (DESC_LDS) {
+            const LDS uint32_t* w = s_d0 + 8 * s;
+            b0 = make_uint4(w[0], w[1], w[2], w[3]);
+            b1 = make_uint4(w[4], w[5], w[6], w[7]);
+          } else {
+            const uint4* d2 = (const uint4*)(desc2 + (long long)i2 * 32);
+            b0 = d2[0];
+            b1 = d2[1];
+          }
+          const int d = hamming256(a0, a1, b0, b1);
           cand[base + __popcll(m & lt)] = (uint32_t)i2 | ((uint32_t)d << 23);
         }
         base += __popcll(m);
@@ -499,11 +511,12 @@ __device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
     kept = wave_sum_dpp(kept);
     if (lane == 0 && kept) lds_add(&s_var[0], kept);
   } else {
-    // sequential fallback state: vMatchedDistance, vnMatches21 (queue is dead)
+    // sequential fallback state: vMatchedDistance, vnMatches21, rotHist entries (queue is dead)
     for (int i = tid; i < n2; i += kInitThreads) {
       s_md[i] = INT_MAX;
       s_m21[i] = -1;
     }
+    for (int i = tid; i < n1; i += kInitThreads) s_src[i] = -1;
   }
   if (P.stop == 9 && tid == 0) {  // diagnostics: rounds, queue length, candidates
     atomicMax(err + 1, rounds + (converged ? 0 : 1000));
@@ -634,11 +647,6 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   // GetFeaturesInArea(.., 0, 0) can return); slot order is irrelevant because
   // the keys (cell << 16 | index) are sorted next.
   if (tid == 0) s_var[5] = 0;
-  for (int i = tid; i < n2; i += kInitThreads) {
-    s_md[i] = INT_MAX;
-    s_m21[i] = -1;
-  }
-  for (int i = tid; i < n1; i += kInitThreads) s_src[i] = -1;
   if (tid < 32) s_hist[tid] = 0;
   __syncthreads();
   for (int i = tid; i < n2; i += kInitThreads) {
@@ -684,25 +692,66 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   __syncthreads();
   if (P.stop == 1) return;
 
+  // F2's level-0 positions, and its descriptors when they fit beside the
+  // candidate list, copied in sorted-grid order: a window's candidates are
+  // then contiguous LDS entries
+  float2* s_pos = (float2*)s_md;  // s_md / s_m21 (adjacent) are free until pass 3
+  const bool d0_lds = 8 * n0 <= P.cand_lds / 2;
+  uint4* s_d0 = (uint4*)s_cand;
+  for (int s = tid; s < n0; s += kInitThreads) {
+    const int i2 = (int)(s_sort[s] & 0xFFFF);
+    s_pos[s] = s_xy[i2];
+    if (d0_lds) {
+      const uint4* d = (const uint4*)(desc2 + (long long)i2 * 32);
+      s_d0[2 * s] = d[0];
+      s_d0[2 * s + 1] = d[1];
+    }
+  }
+  const int cand_off = d0_lds ? 8 * n0 : 0;  // uint32 entries of s_cand taken by s_d0
+  const int cand_lds = P.cand_lds - cand_off;
+  // the octave-0 queries, compacted so that every wave gets an equal share
+  // (keypoints are level-major: they are all at the front); order is
+  // irrelevant, results are indexed by query
+  int* s_qlist = s_src;  // s_src is written in pass 3
+  if (tid == 0) s_var[6] = 0;
+  for (int i = tid; i <= n1; i += kInitThreads) s_coff[i] = 0;
+  __syncthreads();
+  {
+    const uint64_t lt = lanemask_lt_w(lane);
+    for (int i0 = wv * 64; i0 < n1; i0 += kInitThreads) {
+      const int i = i0 + lane;
+      const bool z = i < n1 && kp1[i].octave == 0;
+      const uint64_t mz = __ballot(z);
+      int base = 0;
+      if (lane == 0 && mz) base = lds_add_g(s_var + 6, __popcll(mz));
+      base = __builtin_amdgcn_readlane(base, 0);
+      if (z) s_qlist[base + __popcll(mz & lt)] = i;
+    }
+  }
+  __syncthreads();
+  const int nq0 = s_var[6];
+  const int qper = (nq0 + kInitThreads / 64 - 1) / (kInitThreads / 64);
+  const int qb = min(wv * qper, nq0), qe = min(qb + qper, nq0);
+
   // Passes 1 and 2 walk the queries 64 at a time per wave: lane j prefetches
   // query q0+j's octave, window centre and descriptor words with coalesced
   // loads, and readlane broadcasts them when query q0+j is processed.
   // ---- pass 1: candidate counts per query (Frame::GetFeaturesInArea, octave 0)
-  for (int q0 = wv * 64; q0 < n1; q0 += kInitThreads) {
-    const int qi = q0 + lane;
+  for (int q0 = qb; q0 < qe; q0 += 64) {
+    const int e = q0 + lane;
     float cxl = 0.f, cyl = 0.f;
-    bool lvl0 = false;
-    if (qi < n1) {
+    int qi = 0;
+    if (e < qe) {
+      qi = s_qlist[e];
       const orbx_kp k = kp1[qi];
-      lvl0 = k.octave == 0;
       cxl = prev ? prev[2 * qi] : k.x;
       cyl = prev ? prev[2 * qi + 1] : k.y;
-      s_coff[qi] = 0;
     }
-    uint64_t todo = __ballot(lvl0);
+    uint64_t todo = __ballot(e < qe);
     while (todo) {
       const int j = __ffsll((long long)todo) - 1;
       todo &= todo - 1;
+      const int qj = __builtin_amdgcn_readlane(qi, j);
       const float x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxl), j));
       const float y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cyl), j));
       const Window w = make_window(x, y, P, s_cell);
@@ -710,32 +759,37 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
       if (w.ok) {
         for (int f0 = 0; f0 < w.total; f0 += 64) {
           const int f = f0 + lane;
-          const int s = window_pos(w, min(f, w.total - 1));
+          const int s = window_pos(w, f);
           if (f < w.total) {
-            const float2 q = s_xy[s_sort[s] & 0xFFFF];
+            const float2 q = s_pos[s];
             cnt += (fabsf(__fsub_rn(q.x, x)) < P.r && fabsf(__fsub_rn(q.y, y)) < P.r) ? 1 : 0;
           }
         }
       }
       cnt = wave_sum_i(cnt);
-      if (lane == 0) s_coff[q0 + j] = cnt;
+      if (lane == 0) s_coff[qj] = cnt;
     }
   }
   __syncthreads();
   if (tid == 0) s_coff[n1] = 0;
   __syncthreads();
   const int total = block_scan_excl<kInitThreads>(s_coff, n1 + 1, s_tmp);
-  if (total > P.cand_lds && total > P.cand_cap) {
+  if (total > cand_lds && total > P.cand_cap) {
     if (tid == 0) atomicOr(err, 8);
     return;
   }
-  InitCtx ctx{P, kp1, kp2, desc1, desc2, prev, s_sort, s_xy, s_queue, s_m12, s_cell, s_md, s_m21, s_src, s_coff,
-              s_var, n1, n2, total, err};
-  if (total <= P.cand_lds) {
-    init_pass23(ctx, (LDS uint32_t*)s_cand);
+  InitCtx ctx{P, kp1, kp2, desc1, desc2, prev, s_sort, s_xy, s_pos, s_d0, s_queue, s_m12, s_cell, s_md, s_m21, s_src,
+              s_coff, s_var, n1, n2, total, qb, qe, err};
+  if (total <= cand_lds) {
+    LDS uint32_t* c = (LDS uint32_t*)s_cand + cand_off;
+    if (d0_lds) init_pass23<LDS uint32_t*, true>(ctx, c);
+    else init_pass23<LDS uint32_t*, false>(ctx, c);
   } else {
-    init_pass23(ctx, cand_all + (long long)pr * P.cand_cap);
+    uint32_t* c = cand_all + (long long)pr * P.cand_cap;
+    if (d0_lds) init_pass23<uint32_t*, true>(ctx, c);
+    else init_pass23<uint32_t*, false>(ctx, c);
   }
+  if (P.stop == 2 || P.stop == 3) return;  // diagnostics: the passes were cut short
   __syncthreads();
   // rotation consistency (src/ORBmatcher.cc:473-512, ComputeThreeMaxima :1601-1642)
   const float factor = 1.0f / kHistoLength;
