@@ -32,6 +32,11 @@ namespace orbx {
 
 constexpr int kRoiStride = 80;  // >= 65-px ROI + 15 bytes of 16-B alignment slack
 
+// popcount of the bits of m below this lane
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // FAST-9/16 "cornerScore<16>" of OpenCV 3.x, d[k] = v - ring[k].
 __device__ __forceinline__ int corner_score16(const int (&d)[16], int threshold) {
   auto D = [&](int k) { return d[k & 15]; };
@@ -161,7 +166,6 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
   stamp(0);
 
   const int t = P.t_low;
-  const uint64_t lt = lanemask_lt(lane);
   const bool two = bw <= 32;  // 2 rows x 32 lanes, else 1 row x 64 lanes (bw <= 59)
   const int lr = two ? (lane >> 5) : 0, lc = two ? (lane & 31) : lane;
   const int rstep = two ? 2 : 1;
@@ -176,17 +180,19 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
     for (int q = 0; q < 4; ++q) {
       const int by = by0 + q * rstep + lr;
       const uint8_t* c = band + min(by, bh - 1) * kRoiStride + min(lc, bw - 1);
-      const int v = c[0], lo = v - t, hi = v + t;
+      const int v = c[0];
       const int n0 = c[3 * kRoiStride], n4 = c[3], n8 = c[-3 * kRoiStride], n12 = c[-3];
-      const int nd = (n0 < lo) + (n4 < lo) + (n8 < lo) + (n12 < lo);
-      const int nb = (n0 > hi) + (n4 > hi) + (n8 > hi) + (n12 > hi);
-      fl[q] = by < bh && lc < bw && (nd >= 2 || nb >= 2);
+      // >= 2 of the 4 compass pixels darker than v - t  <=>  their 2nd smallest is;
+      // >= 2 brighter than v + t  <=>  their 2nd largest is
+      const int s1 = min(n0, n4), l1 = max(n0, n4), s2 = min(n8, n12), l2 = max(n8, n12);
+      const int a = max(s1, s2), b = min(l1, l2);
+      fl[q] = by < bh && lc < bw && (min(a, b) < v - t || max(a, b) > v + t);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int by = by0 + q * rstep + lr;
       const uint64_t m = __ballot(fl[q]);
-      if (fl[q]) list[n1 + __popcll(m & lt)] = (uint16_t)((by << 8) | lc);
+      if (fl[q]) list[n1 + mbcnt64(m)] = (uint16_t)((by << 8) | lc);
       n1 += __popcll(m);
     }
   }
@@ -205,7 +211,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
       det = has_arc9(dk) || has_arc9(br);
     }
     const uint64_t m = __ballot(det);
-    if (det) list[n2 + __popcll(m & lt)] = (uint16_t)e;
+    if (det) list[n2 + mbcnt64(m)] = (uint16_t)e;
     n2 += __popcll(m);
   }
   stamp(2);
@@ -259,7 +265,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
     if ((m >> lane) & 1ull) {
       const int e = list[ch * 64 + lane];
       const int by = e >> 8, bx = e & 255;
-      const int pos = base + __popcll(m & lt);
+      const int pos = base + mbcnt64(m);
       const int x = cg.c0 + 3 + bx - g.minBX, y = cg.r0 + 3 + by - g.minBY;
       if (pos < cg.cap) out[pos] = pack_key(x, y, sc[(by + 1) * sw + bx + 1]);
     }
