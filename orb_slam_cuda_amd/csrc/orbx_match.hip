@@ -2,7 +2,7 @@
 //
 //   hamming_top2_kernel   dense best/second search (the inner loop shared by
 //                         every ORBmatcher search), lane-per-query, candidate
-//                         rows in SGPRs via scalar loads, 8 x v_bcnt per pair
+//                         rows broadcast from LDS, 8 x v_bcnt per pair
 //   search_init_kernel    SearchForInitialization   src/ORBmatcher.cc:405-520
 //                         + Frame::AssignFeaturesToGrid / GetFeaturesInArea
 //                         src/Frame.cc:229-244, 326-391
@@ -44,9 +44,10 @@ __device__ __forceinline__ int hamming256(const uint4& a0, const uint4& a1, cons
 }
 
 // ------------------------------------------------------------ dense top-2
-constexpr int kTopQueries = 256;  // queries per workgroup (lane per query)
-constexpr int kTopSplit = 4;      // candidate quarters per query (one wave set each)
-constexpr int kTopThreads = kTopQueries * kTopSplit;
+constexpr int kTopQueries = 256;  // queries per workgroup, two per lane
+constexpr int kTopSplit = 8;      // candidate ranges per query (two waves each)
+constexpr int kTopThreads = 1024;
+constexpr int kTopChunk = kTopThreads / (2 * kTopSplit);  // candidates per range per staged chunk (64)
 // popcount(x) + acc as ONE v_bcnt_u32_b32 (the compiler otherwise splits the
 // chain into bcnt(x, 0) and v_add3)
 __device__ __forceinline__ int bcnt_acc(uint32_t x, int acc) {
@@ -60,73 +61,100 @@ __device__ __forceinline__ int med3_i32(int a, int b, int c) {
   return r;
 }
 
-// Lane per query; the candidate rows are wave-uniform, so they are read with
-// scalar loads (32 bytes straight into SGPRs, no LDS) and each pair costs
-// 8 v_xor + 8 v_bcnt + 4 top-2 updates: b2 = med3(d, b1, b2) (b1 <= b2
-// always), b1 = min(d, b1), index by compare. The candidates are split in
-// kTopSplit contiguous ranges, one per wave set, so that enough waves are
-// resident to cover the scalar-load latency; the partial results are merged
-// in range order (earlier range wins ties, as the sequential scan would).
+struct Top2Acc {
+  uint4 a0, a1;  // query descriptor
+  int b1, b2, bi;
+  __device__ __forceinline__ void score(const uint4& r0, const uint4& r1, int j) {
+    int d = bcnt_acc(a0.x ^ r0.x, 0);
+    d = bcnt_acc(a0.y ^ r0.y, d);
+    d = bcnt_acc(a0.z ^ r0.z, d);
+    d = bcnt_acc(a0.w ^ r0.w, d);
+    d = bcnt_acc(a1.x ^ r1.x, d);
+    d = bcnt_acc(a1.y ^ r1.y, d);
+    d = bcnt_acc(a1.z ^ r1.z, d);
+    d = bcnt_acc(a1.w ^ r1.w, d);
+    bi = d < b1 ? j : bi;
+    b2 = med3_i32(d, b1, b2);
+    b1 = min(d, b1);
+  }
+};
+
+// Two queries per lane against wave-uniform candidate rows. The candidates
+// are split in kTopSplit contiguous ranges, two waves per range (so that 8
+// waves per SIMD are resident); each range stages chunks in LDS (one 16-byte
+// load per thread per chunk) that its lanes read back as broadcast loads, one
+// pair of row reads serving two queries. A pair costs 8 v_xor + 8 v_bcnt + 4
+// top-2 updates: b2 = med3(d, b1, b2) (b1 <= b2 always), b1 = min(d, b1),
+// index by compare. The partial results are merged in range order (earlier
+// range wins ties, as the sequential scan would).
 __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t* __restrict__ A, long long a_pitch,
                                                                    const int* __restrict__ nA, int a_cap,
                                                                    const uint8_t* __restrict__ B, long long b_pitch,
                                                                    const int* __restrict__ nB,
                                                                    int* __restrict__ best_idx, int* __restrict__ best,
                                                                    int* __restrict__ second) {
+  __shared__ uint4 sB[kTopSplit][kTopChunk][2];
   __shared__ int3 part[kTopSplit][kTopQueries];
-  const int p = blockIdx.y, q = threadIdx.x % kTopQueries, k = threadIdx.x / kTopQueries;
-  const int i = blockIdx.x * kTopQueries + q;
-  const int na = nA[p], nb = __builtin_amdgcn_readfirstlane(nB[p]);
-  if (blockIdx.x * kTopQueries >= na) return;
+  const int p = blockIdx.y, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int k = wv >> 1, h = wv & 1;
+  const int qa = h * 64 + lane, qb = 128 + h * 64 + lane;  // this lane's two queries (of 256)
+  const int base = blockIdx.x * kTopQueries;
+  const int na = nA[p], nb = nB[p];
+  if (base >= na) return;
   const uint4* Ap = (const uint4*)(A + p * a_pitch);
-  const uint32_t* Bp = (const uint32_t*)(B + p * b_pitch);
-  uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
-  if (i < na) {
-    a0 = Ap[2 * i];
-    a1 = Ap[2 * i + 1];
+  const uint4* Bp = (const uint4*)(B + p * b_pitch);
+  Top2Acc x{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 256, 256, -1};
+  Top2Acc y = x;
+  if (base + qa < na) {
+    x.a0 = Ap[2 * (base + qa)];
+    x.a1 = Ap[2 * (base + qa) + 1];
   }
-  const int per = ((nb + kTopSplit - 1) / kTopSplit + 3) & ~3;
-  const int jb = __builtin_amdgcn_readfirstlane(min(k * per, nb)), je = min(jb + per, nb);
-  int b1d = 256, b2d = 256, bi = -1;
-  auto score = [&](const uint32_t* r, int j) {
-    int d = bcnt_acc(a0.x ^ r[0], 0);
-    d = bcnt_acc(a0.y ^ r[1], d);
-    d = bcnt_acc(a0.z ^ r[2], d);
-    d = bcnt_acc(a0.w ^ r[3], d);
-    d = bcnt_acc(a1.x ^ r[4], d);
-    d = bcnt_acc(a1.y ^ r[5], d);
-    d = bcnt_acc(a1.z ^ r[6], d);
-    d = bcnt_acc(a1.w ^ r[7], d);
-    bi = d < b1d ? j : bi;
-    b2d = med3_i32(d, b1d, b2d);
-    b1d = min(d, b1d);
-  };
-  // four candidate rows per step: their scalar loads are issued together
-  int j = jb;
-  for (; j + 4 <= je; j += 4) {
-    uint32_t r[32];
-#pragma unroll
-    for (int t = 0; t < 32; ++t) r[t] = Bp[8 * j + t];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) score(r + 8 * t, j + t);
+  if (base + qb < na) {
+    y.a0 = Ap[2 * (base + qb)];
+    y.a1 = Ap[2 * (base + qb) + 1];
   }
-  for (; j < je; ++j) score(Bp + 8 * j, j);
-  part[k][q] = make_int3(b1d, bi, b2d);
-  __syncthreads();
-  if (k != 0 || i >= na) return;
-#pragma unroll
-  for (int s = 1; s < kTopSplit; ++s) {
-    const int3 o = part[s][q];
-    b2d = min(min(max(b1d, o.x), b2d), o.z);
-    if (o.x < b1d) {
-      b1d = o.x;
-      bi = o.y;
+  const int per = (nb + kTopSplit - 1) / kTopSplit;
+  const int jb = min(k * per, nb), je = min(jb + per, nb);
+  // loader role of this thread: range lk, row lr, half lh
+  const int lk = tid / (2 * kTopChunk), lr = (tid >> 1) % kTopChunk, lh = tid & 1;
+  const int ljb = min(lk * per, nb), lje = min(ljb + per, nb);
+  for (int c0 = 0; c0 < per; c0 += kTopChunk) {
+    __syncthreads();
+    if (ljb + c0 + lr < lje) sB[lk][lr][lh] = Bp[2 * (ljb + c0 + lr) + lh];
+    __syncthreads();
+    const int n = __builtin_amdgcn_readfirstlane(min(kTopChunk, je - (jb + c0)));  // wave-uniform
+    int j = 0;
+    for (; j + 2 <= n; j += 2) {  // two rows' LDS reads in flight, then four (row, query) pairs
+      const uint4 r0 = sB[k][j][0], r1 = sB[k][j][1], r2 = sB[k][j + 1][0], r3 = sB[k][j + 1][1];
+      x.score(r0, r1, jb + c0 + j);
+      y.score(r0, r1, jb + c0 + j);
+      x.score(r2, r3, jb + c0 + j + 1);
+      y.score(r2, r3, jb + c0 + j + 1);
+    }
+    if (j < n) {
+      const uint4 r0 = sB[k][j][0], r1 = sB[k][j][1];
+      x.score(r0, r1, jb + c0 + j);
+      y.score(r0, r1, jb + c0 + j);
     }
   }
-  const long long o = (long long)p * a_cap + i;
-  best_idx[o] = bi;
-  best[o] = b1d;
-  second[o] = b2d;
+  part[k][qa] = make_int3(x.b1, x.bi, x.b2);
+  part[k][qb] = make_int3(y.b1, y.bi, y.b2);
+  __syncthreads();
+  if (tid >= kTopQueries || base + tid >= na) return;
+  int3 r = part[0][tid];
+#pragma unroll
+  for (int s = 1; s < kTopSplit; ++s) {
+    const int3 o = part[s][tid];
+    r.z = min(min(max(r.x, o.x), r.z), o.z);
+    if (o.x < r.x) {
+      r.x = o.x;
+      r.y = o.y;
+    }
+  }
+  const long long o = (long long)p * a_cap + base + tid;
+  best_idx[o] = r.y;
+  best[o] = r.x;
+  second[o] = r.z;
 }
 
 // ------------------------------------------------------------ wave helpers
