@@ -82,14 +82,18 @@ def algorithmic_bytes(W, H, nkp):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--cpu-sample", type=int, default=24, help="frames in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-match", action="store_true", help="extract only (C2)")
     ap.add_argument("--serial", action="store_true", help="one stream: no overlap of matching with the next extraction")
-    ap.add_argument("--split", type=int, default=1, help="extraction launches (and streams) per batch")
+    ap.add_argument("--split", type=int, default=2, help="extraction launches (and streams) per batch")
+    ap.add_argument("--priority", action="store_true",
+                    help="high-priority extraction streams, low-priority matching stream")
+    ap.add_argument("--carry", choices=["match", "ext"], default="match",
+                    help="stream that copies a batch's last frame for the next batch's first pair")
     args = ap.parse_args()
 
     from orb_slam_cuda_amd import sharding
@@ -123,9 +127,9 @@ def main():
     ext = exts[0]
     cap = ext.frame_capacity
     KP, DS = 28, 32
-    # three output sets: batch k writes set k % 3, slots 1..B, and then copies
-    # its last frame into slot 0 of set (k+1) % 3 (frame t-1 of the next
-    # batch's first frame). Set k % 3 is free again once matching k-3 is done.
+    # three output sets: batch k writes set k % 3, slots 1..B, and its last
+    # frame is copied into slot 0 of set (k+1) % 3 (frame t-1 of the next
+    # batch's first frame).
     NS = 3
     d_kps = [_lib.DeviceArray((B + 1) * cap * KP) for _ in range(NS)]
     d_desc = [_lib.DeviceArray((B + 1) * cap * DS) for _ in range(NS)]
@@ -136,26 +140,28 @@ def main():
     d_bi, d_bd, d_sd = (_lib.DeviceArray(B * cap * 4) for _ in range(3))
     d_m12 = _lib.DeviceArray(B * cap * 4)
     d_nm = _lib.DeviceArray(B * 4)
-    s_exts = [_lib.Stream() for _ in range(S)]
+    # the extraction stream may ask the dispatcher for priority (--priority):
+    # it is the critical path, matching fills the compute units it leaves idle
+    prio = 1 if args.priority else None
+    s_exts = [_lib.Stream(prio) for _ in range(S)]
     s_ext = s_exts[0]
-    s_match = _lib.Stream() if not args.serial else s_ext
+    s_match = _lib.Stream(0 if args.priority else None) if not args.serial else s_ext
     bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
     vp = lambda a: C.c_void_p(a)
     n_ev = 9  # 6 extraction stage marks (extract stream) + 3 matching marks (match stream)
 
     def step(k, evs, ev_ext, ev_done):
-        """Batch k: extraction + carry copy on s_ext; matching of the same
+        """Batch k: extraction on s_ext; carry copy and matching of the same
         batch on s_match, overlapping the extraction of batch k+1 (--serial:
-        one stream, no overlap). Before the carry into set (k+1) % 3 the
-        extraction stream waits for matching k-2 (the last reader of that
-        set); matching k waits for extraction k."""
+        one stream, no overlap). Extraction k waits for matching k-3 (the
+        last reader of set k % 3); matching k waits for extraction k."""
         b, nb = k % NS, (k + 1) % NS
         # the batch is cut into S contiguous parts, one extractor and stream each
         for h, (ex, se) in enumerate(zip(exts, s_exts)):
             if h == 0:
                 arr = (C.c_void_p * 6)(*[e.e.value for e in evs[:6]])
                 check(L.orbx_set_stage_events(ex.handle, arr))
-            elif not args.serial and k >= 3:
+            if not args.serial and k >= 3:
                 se.wait(ev_done[k - 3])  # matching k-3 was the last reader of set k % 3
             sv = se if not args.serial else s_ext
             check(L.orbx_extract_batch(ex.handle, vp(d_frames.ptr + h * BS * H * pitch), BS, H * pitch, pitch,
@@ -165,14 +171,21 @@ def main():
             if h > 0 and not args.serial:
                 ev_part[k][h].record(se)
                 s_ext.wait(ev_part[k][h])
+        def carry(st):
+            check(L.orbx_memcpy_dtod_async(vp(d_kps[nb].ptr), vp(d_kps[b].ptr + B * cap * KP), cap * KP, st.s))
+            check(L.orbx_memcpy_dtod_async(vp(d_desc[nb].ptr), vp(d_desc[b].ptr + B * cap * DS), cap * DS, st.s))
+            check(L.orbx_memcpy_dtod_async(vp(d_counts[nb].ptr), vp(d_counts[b].ptr + B * 4), 4, st.s))
+
+        if args.carry == "ext" or args.serial:
+            # slot 0 of set (k+1) % 3 was last read by matching k-2
+            if k >= 2 and not args.serial:
+                s_ext.wait(ev_done[k - 2])
+            carry(s_ext)
         ev_ext[k].record(s_ext)
-        if k >= 2 and not args.serial:
-            s_ext.wait(ev_done[k - 2])
-        check(L.orbx_memcpy_dtod_async(vp(d_kps[nb].ptr), vp(d_kps[b].ptr + B * cap * KP), cap * KP, s_ext.s))
-        check(L.orbx_memcpy_dtod_async(vp(d_desc[nb].ptr), vp(d_desc[b].ptr + B * cap * DS), cap * DS, s_ext.s))
-        check(L.orbx_memcpy_dtod_async(vp(d_counts[nb].ptr), vp(d_counts[b].ptr + B * 4), 4, s_ext.s))
         if not args.serial:
             s_match.wait(ev_ext[k])
+        if args.carry == "match" and not args.serial:
+            carry(s_match)  # in order after matching k-2, the last reader of set (k+1) % 3
         evs[6].record(s_match)
         if not args.no_match:
             # query = frame t (slots 1..B), candidates = frame t-1 (slots 0..B-1)

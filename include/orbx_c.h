@@ -235,6 +235,9 @@ int orbx_memcpy_dtoh(void* dst, const void* src, size_t bytes);
 int orbx_memset(void* dst, int value, size_t bytes);
 int orbx_memcpy_dtod_async(void* dst, const void* src, size_t bytes, void* stream);
 int orbx_stream_create(void** stream);
+/* A stream whose work the dispatcher prefers (high = 1) or defers (high = 0)
+ * when both compete for compute units (hipStreamCreateWithPriority). */
+int orbx_stream_create_priority(void** stream, int high);
 int orbx_stream_destroy(void* stream);
 int orbx_stream_synchronize(void* stream);
 int orbx_event_create(void** ev);

@@ -98,6 +98,7 @@ def lib() -> C.CDLL:
         L.orbx_memset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
         L.orbx_memcpy_dtod_async.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.orbx_stream_create.argtypes = [C.POINTER(C.c_void_p)]
+        L.orbx_stream_create_priority.argtypes = [C.POINTER(C.c_void_p), C.c_int]
         L.orbx_stream_destroy.argtypes = [C.c_void_p]
         L.orbx_stream_synchronize.argtypes = [C.c_void_p]
         L.orbx_event_create.argtypes = [C.POINTER(C.c_void_p)]
@@ -167,9 +168,13 @@ class DeviceArray:
 
 
 class Stream:
-    def __init__(self):
+    def __init__(self, priority: int | None = None):
+        """priority None: default; 1: preferred by the dispatcher; 0: deferred."""
         self.s = C.c_void_p(0)
-        check(lib().orbx_stream_create(C.byref(self.s)))
+        if priority is None:
+            check(lib().orbx_stream_create(C.byref(self.s)))
+        else:
+            check(lib().orbx_stream_create_priority(C.byref(self.s), int(priority)))
 
     def synchronize(self) -> None:
         check(lib().orbx_stream_synchronize(self.s))

@@ -680,6 +680,12 @@ int orbx_memcpy_dtod_async(void* d, const void* s, size_t b, void* st) {
   return ORBX_OK;
 }
 int orbx_stream_create(void** s) { HIP_OK(hipStreamCreateWithFlags((hipStream_t*)s, hipStreamNonBlocking)); return ORBX_OK; }
+int orbx_stream_create_priority(void** s, int high) {
+  int least = 0, greatest = 0;
+  HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  HIP_OK(hipStreamCreateWithPriority((hipStream_t*)s, hipStreamNonBlocking, high ? greatest : least));
+  return ORBX_OK;
+}
 int orbx_stream_destroy(void* s) { HIP_OK(hipStreamDestroy((hipStream_t)s)); return ORBX_OK; }
 int orbx_stream_synchronize(void* s) { HIP_OK(hipStreamSynchronize((hipStream_t)s)); return ORBX_OK; }
 int orbx_event_create(void** e) { HIP_OK(hipEventCreate((hipEvent_t*)e)); return ORBX_OK; }
