@@ -43,6 +43,10 @@ def lib():
         _lib.orc_fast_atan2.restype = C.c_float
         _lib.orc_fast_atan2.argtypes = [C.c_float, C.c_float]
         _lib.orc_sincosf.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        _lib.orc_compute_stereo_matches.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_float,
+            C.c_float, C.c_void_p, C.c_void_p]
     return _lib
 
 
@@ -147,6 +151,33 @@ def search_for_initialization(kp1, desc1, kp2, desc2, bounds, prev_xy, window=10
         C.c_float(bounds[0]), C.c_float(bounds[1]), C.c_float(bounds[2]), C.c_float(bounds[3]),
         _p(prev), window, C.c_float(nnratio), int(check_ori), _p(m12), C.byref(nm))
     return m12, nm.value, prev
+
+
+def pyramid(cfg: OrcConfig, img: np.ndarray) -> list:
+    """All levels of ComputePyramid as packed 2-D arrays (level 0 = the image)."""
+    return [np.ascontiguousarray(img, np.uint8)] + [pyramid_level(cfg, img, l) for l in range(1, cfg.nlevels)]
+
+
+def compute_stereo_matches(kpL, descL, kpR, descR, pyrL, pyrR, scale, inv_scale, mb, mbf):
+    """Frame::ComputeStereoMatches. pyrL/pyrR: lists of per-level 2-D u8 arrays.
+    Returns (mvuRight, mvDepth, kept)."""
+    kpL = np.ascontiguousarray(kpL, KP_DTYPE); kpR = np.ascontiguousarray(kpR, KP_DTYPE)
+    descL = np.ascontiguousarray(descL, np.uint8); descR = np.ascontiguousarray(descR, np.uint8)
+    L = len(pyrL)
+    pl = [np.ascontiguousarray(a, np.uint8) for a in pyrL]
+    pr = [np.ascontiguousarray(a, np.uint8) for a in pyrR]
+    ptrL = (C.c_void_p * L)(*[a.ctypes.data for a in pl])
+    ptrR = (C.c_void_p * L)(*[a.ctypes.data for a in pr])
+    sL = np.array([a.strides[0] for a in pl], np.uint64)
+    sR = np.array([a.strides[0] for a in pr], np.uint64)
+    lw = np.array([a.shape[1] for a in pl], np.int32)
+    lh = np.array([a.shape[0] for a in pl], np.int32)
+    sc = np.ascontiguousarray(scale, np.float32); isc = np.ascontiguousarray(inv_scale, np.float32)
+    uR = np.zeros(len(kpL), np.float32); dep = np.zeros(len(kpL), np.float32)
+    kept = lib().orc_compute_stereo_matches(_p(kpL), _p(descL), len(kpL), _p(kpR), _p(descR), len(kpR),
+                                            ptrL, _p(sL), ptrR, _p(sR), _p(lw), _p(lh), L, _p(sc), _p(isc),
+                                            C.c_float(mb), C.c_float(mbf), _p(uR), _p(dep))
+    return uR, dep, kept
 
 
 def search_by_bow(descA, angleA, mpA, fvA, descB, angleB, mpB, fvB, nnratio, check_ori,

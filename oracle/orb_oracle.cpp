@@ -894,6 +894,132 @@ int orc_distribute(const orc_kp* keys, int nkeys, int minX, int maxX, int minY, 
 
 int orc_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
 
+
+int orc_compute_stereo_matches(const orc_kp* kpL, const uint8_t* descL, int nL, const orc_kp* kpR,
+                               const uint8_t* descR, int nR, const uint8_t* const* pyrL, const size_t* strideL,
+                               const uint8_t* const* pyrR, const size_t* strideR, const int* level_w,
+                               const int* level_h, int nlevels, const float* scale, const float* inv_scale,
+                               float mb, float mbf, float* uRight, float* depth) {
+  // src/Frame.cc:465-639
+  for (int i = 0; i < nL; i++) {
+    uRight[i] = -1.0f;
+    depth[i] = -1.0f;
+  }
+  const int TH_HIGH = 100, TH_LOW = 50;  // src/ORBmatcher.cc:37-38
+  const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
+  const int nRows = level_h[0];
+  // row table: right keypoint iR is a candidate on rows [floor(y - r), ceil(y + r)] (:477-491)
+  std::vector<std::vector<size_t>> vRowIndices(nRows);
+  for (int iR = 0; iR < nR; iR++) {
+    const orc_kp& kp = kpR[iR];
+    const float kpY = kp.y;
+    const float r = 2.0f * scale[kp.octave];
+    const int maxr = (int)std::ceil(kpY + r);
+    const int minr = (int)std::floor(kpY - r);
+    for (int yi = minr; yi <= maxr; yi++)
+      if (yi >= 0 && yi < nRows) vRowIndices[yi].push_back(iR);  // (rows off the image: UB in the reference)
+  }
+  const float minZ = mb;
+  const float minD = 0;
+  const float maxD = mbf / minZ;
+  std::vector<std::pair<int, int>> vDistIdx;
+  vDistIdx.reserve(nL);
+  auto level_px = [&](const uint8_t* const* pyr, const size_t* stride, int l, int y, int x) {
+    return (float)pyr[l][(size_t)y * stride[l] + x];
+  };
+  for (int iL = 0; iL < nL; iL++) {
+    const orc_kp& kpL_ = kpL[iL];
+    const int levelL = kpL_.octave;
+    const float vL = kpL_.y;
+    const float uL = kpL_.x;
+    const size_t row = (size_t)vL;  // vRowIndices[vL]: float -> size_t
+    if (row >= (size_t)nRows) continue;
+    const std::vector<size_t>& vCandidates = vRowIndices[row];
+    if (vCandidates.empty()) continue;
+    const float minU = uL - maxD;
+    const float maxU = uL - minD;
+    if (maxU < 0) continue;
+    int bestDist = TH_HIGH;
+    size_t bestIdxR = 0;
+    const uint8_t* dL = descL + (size_t)iL * 32;
+    for (size_t iC = 0; iC < vCandidates.size(); iC++) {
+      const size_t iR = vCandidates[iC];
+      const orc_kp& kpR_ = kpR[iR];
+      if (kpR_.octave < levelL - 1 || kpR_.octave > levelL + 1) continue;
+      const float uR = kpR_.x;
+      if (uR >= minU && uR <= maxU) {
+        const int dist = descriptor_distance(dL, descR + iR * 32);
+        if (dist < bestDist) {
+          bestDist = dist;
+          bestIdxR = iR;
+        }
+      }
+    }
+    if (bestDist >= thOrbDist) continue;
+    // subpixel match by correlation (:549-606)
+    const float uR0 = kpR[bestIdxR].x;
+    const float scaleFactor = inv_scale[levelL];
+    const float scaleduL = std::round(kpL_.x * scaleFactor);
+    const float scaledvL = std::round(kpL_.y * scaleFactor);
+    const float scaleduR0 = std::round(uR0 * scaleFactor);
+    const int w = 5, L = 5;
+    const int vl = (int)scaledvL, ul = (int)scaleduL;
+    float IL[11][11];
+    const float cL = level_px(pyrL, strideL, levelL, vl, ul);
+    for (int r = -w; r <= w; r++)
+      for (int c = -w; c <= w; c++) IL[r + w][c + w] = level_px(pyrL, strideL, levelL, vl + r, ul + c) - cL;
+    int bestDist2 = INT_MAX;
+    int bestincR = 0;
+    float vDists[2 * L + 1];
+    const float iniu = scaleduR0 + L - w;
+    const float endu = scaleduR0 + L + w + 1;
+    if (iniu < 0 || endu >= level_w[levelL]) continue;
+    const int ur0 = (int)scaleduR0;
+    for (int incR = -L; incR <= +L; incR++) {
+      const float cR = level_px(pyrR, strideR, levelL, vl, ur0 + incR);
+      float dist = 0;  // cv::norm(IL, IR, NORM_L1): a sum of integers below 2^24, exact in any order
+      for (int r = -w; r <= w; r++)
+        for (int c = -w; c <= w; c++)
+          dist += std::fabs(IL[r + w][c + w] - (level_px(pyrR, strideR, levelL, vl + r, ur0 + incR + c) - cR));
+      if (dist < bestDist2) {
+        bestDist2 = (int)dist;
+        bestincR = incR;
+      }
+      vDists[L + incR] = dist;
+    }
+    if (bestincR == -L || bestincR == L) continue;
+    const float dist1 = vDists[L + bestincR - 1];
+    const float dist2 = vDists[L + bestincR];
+    const float dist3 = vDists[L + bestincR + 1];
+    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+    if (deltaR < -1 || deltaR > 1) continue;
+    float bestuR = scale[levelL] * ((float)scaleduR0 + (float)bestincR + deltaR);
+    float disparity = (uL - bestuR);
+    if (disparity >= minD && disparity < maxD) {
+      if (disparity <= 0) {
+        disparity = 0.01;
+        bestuR = uL - 0.01;
+      }
+      depth[iL] = mbf / disparity;
+      uRight[iL] = bestuR;
+      vDistIdx.push_back(std::pair<int, int>(bestDist2, iL));
+    }
+  }
+  // outlier rejection by the median SAD (:620-638)
+  if (vDistIdx.empty()) return 0;  // (the reference indexes an empty vector here)
+  std::sort(vDistIdx.begin(), vDistIdx.end());
+  const float median = vDistIdx[vDistIdx.size() / 2].first;
+  const float thDist = 1.5f * 1.4f * median;
+  int kept = (int)vDistIdx.size();
+  for (int i = (int)vDistIdx.size() - 1; i >= 0; i--) {
+    if (vDistIdx[i].first < thDist) break;
+    uRight[vDistIdx[i].second] = -1;
+    depth[vDistIdx[i].second] = -1;
+    --kept;
+  }
+  return kept;
+}
+
 float orc_fast_atan2(float y, float x) { return fast_atan2(y, x); }
 void orc_sincosf(const float* x, int n, float* s, float* c) {
   for (int i = 0; i < n; ++i) {

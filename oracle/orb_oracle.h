@@ -97,6 +97,20 @@ int orc_search_by_bow(
     float nnratio, int check_ori, int kf_vs_kf, int* out, int* nmatches);
 
 /* Elementary OpenCV restatements, exported for unit tests. */
+/* Frame::ComputeStereoMatches (src/Frame.cc:465-639) for a rectified pair.
+ * Left/right keypoints + descriptors as extracted; the two image pyramids
+ * per level (pointer, row stride; both images share level sizes level_w x
+ * level_h); scale / inv_scale = mvScaleFactors / mvInvScaleFactors; mb =
+ * baseline, mbf = baseline * fx. Writes mvuRight and mvDepth (nL floats,
+ * -1 where no match survives). Returns the number of matches kept. */
+int orc_compute_stereo_matches(const orc_kp* kpL, const uint8_t* descL, int nL,
+                               const orc_kp* kpR, const uint8_t* descR, int nR,
+                               const uint8_t* const* pyrL, const size_t* strideL,
+                               const uint8_t* const* pyrR, const size_t* strideR,
+                               const int* level_w, const int* level_h, int nlevels,
+                               const float* scale, const float* inv_scale, float mb,
+                               float mbf, float* uRight, float* depth);
+
 float orc_fast_atan2(float y, float x);
 /* The host libm's sinf/cosf (what computeOrbDescriptor calls, :199-200). */
 void orc_sincosf(const float* x, int n, float* s, float* c);

@@ -109,11 +109,13 @@ class SynthSequence:
 
 
 def stereo_pair(seed: int, W: int = KITTI_WH[0], H: int = KITTI_WH[1]) -> tuple[np.ndarray, np.ndarray]:
-    """Left/right pair: right = left content shifted left by a disparity in [5, 40]."""
+    """Rectified left/right pair: the right image sees the scene shifted left
+    by a disparity d in [5, 40] (a point at column u in the left image is at
+    u - d in the right one), plus independent noise."""
     rng = np.random.default_rng(seed)
     canvas = _paint_canvas(rng, W + 48, H)
     disp = int(rng.integers(5, 41))
-    left = canvas[:, 48:48 + W]
-    right = canvas[:, 48 - disp:48 - disp + W]
+    left = canvas[:, :W]
+    right = canvas[:, disp:disp + W]
     n = lambda a: np.clip(np.rint(a + rng.integers(-6, 7, size=a.shape)), 0, 255).astype(np.uint8)
     return n(left), n(right)
