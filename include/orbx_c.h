@@ -33,6 +33,8 @@
  *                          include/ORBmatcher.h:66, src/ORBmatcher.cc:522-655
  *   orbm_hamming_top2      the best/second Hamming inner loop shared by every
  *                          matcher (dense, device-resident, batched)
+ *   orbm_compute_stereo_matches  Frame::ComputeStereoMatches (mvuRight, mvDepth)
+ *                          include/Frame.h:82, src/Frame.cc:465-639
  *
  * Error behaviour: every call returns ORBX_OK or a negative code; the
  * message of the last failure on the calling thread is orbx_last_error().
@@ -222,6 +224,37 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
                        const float* angleB, const uint8_t* mp_validB, int nB,
                        orbm_feature_vector fvB, float nnratio, int check_ori,
                        int kf_vs_kf, int* out, int* nmatches);
+
+/* Frame::ComputeStereoMatches (src/Frame.cc:465-639) on host buffers
+ * (synchronous). kpL/descL = mvKeys/mDescriptors of the left image, kpR/descR
+ * = mvKeysRight/mDescriptorsRight; the SAD refinement reads mvImagePyramid of
+ * the two extractors, i.e. the pyramid of frame 0 of each handle's last
+ * extraction (`left` and `right` may be one handle only if it is re-run, as
+ * each extraction replaces its pyramid). mb = baseline (m), mbf = baseline x
+ * fx. Outputs uRight/depth (nL floats, -1 where no match: mvuRight, mvDepth)
+ * and the number of kept matches. A block-match window reaching off the
+ * pyramid level (an OpenCV range assertion in the reference) rejects that
+ * keypoint. */
+int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle right,
+                                const orbx_kp* kpL, const uint8_t* descL, int nL,
+                                const orbx_kp* kpR, const uint8_t* descR, int nR,
+                                float mb, float mbf, float* uRight, float* depth,
+                                int* nkept);
+
+/* Batched device-resident variant: pair p = left frame (left_frame0 + p) of
+ * `left`'s last orbx_extract_batch and right frame (right_frame0 + p) of
+ * `right`'s (the same handle may hold both when one batch extracted left and
+ * right frames together); keypoints/descriptors at d_kpL + p*kp_pitch,
+ * d_descL + p*kp_pitch*32, d_nL[p] (right likewise). Outputs d_uRight /
+ * d_depth: pairs x kp_pitch floats; d_nkept: pairs. Run it on the stream
+ * that extracted (or after it) and before the next extraction on either
+ * handle, which overwrites the pyramid. */
+int orbm_compute_stereo_matches_batch(
+    orbm_handle m, orbx_handle left, int left_frame0, orbx_handle right,
+    int right_frame0, const orbx_kp* d_kpL, const uint8_t* d_descL,
+    const int* d_nL, const orbx_kp* d_kpR, const uint8_t* d_descR,
+    const int* d_nR, int kp_pitch, int pairs, float mb, float mbf,
+    float* d_uRight, float* d_depth, int* d_nkept, void* stream);
 
 /* --------------------------------------------- device plumbing for hosts
  * Thin wrappers so a host without its own HIP binding (ctypes, cgo, JNI)

@@ -964,6 +964,9 @@ int orc_compute_stereo_matches(const orc_kp* kpL, const uint8_t* descL, int nL, 
     const float scaleduR0 = std::round(uR0 * scaleFactor);
     const int w = 5, L = 5;
     const int vl = (int)scaledvL, ul = (int)scaleduL;
+    // a window reaching off the level is an OpenCV range assertion in the
+    // reference (Mat::rowRange/colRange); here that keypoint gets no match
+    if ((int)scaleduR0 < 10 || ul < 5 || ul + 5 >= level_w[levelL] || vl < 5 || vl + 5 >= level_h[levelL]) continue;
     float IL[11][11];
     const float cL = level_px(pyrL, strideL, levelL, vl, ul);
     for (int r = -w; r <= w; r++)

@@ -7,7 +7,7 @@ host-side mirror of the reference classes in Python.
 """
 from ._lib import KP_DTYPE, OrbxError, device_count, header_functions, lib  # noqa: F401
 from .extractor import ORBextractor  # noqa: F401
-from .matcher import Frame, KeyFrame, ORBmatcher  # noqa: F401
+from .matcher import ComputeStereoMatches, Frame, KeyFrame, ORBmatcher  # noqa: F401
 
 __all__ = ["ORBextractor", "ORBmatcher", "Frame", "KeyFrame", "KP_DTYPE", "OrbxError",
            "device_count", "header_functions", "lib"]

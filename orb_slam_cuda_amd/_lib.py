@@ -89,6 +89,13 @@ def lib() -> C.CDLL:
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, FeatureVectorC, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_int, FeatureVectorC, C.c_float, C.c_int, C.c_int, C.c_void_p,
             C.POINTER(C.c_int)]
+        L.orbm_compute_stereo_matches.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+            C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
+        L.orbm_compute_stereo_matches_batch.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+            C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_void_p,
+            C.c_void_p, C.c_void_p, C.c_void_p]
         L.orbx_device_count.argtypes = [C.POINTER(C.c_int)]
         L.orbx_set_device.argtypes = [C.c_int]
         L.orbx_malloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]

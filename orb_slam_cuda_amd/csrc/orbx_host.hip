@@ -449,6 +449,37 @@ static ExtractBuffers buffers_of(const Plan& pl) {
   return X;
 }
 
+// The device pyramid (mvImagePyramid) of frames [frame0, frame0 + n) of the
+// last extraction: level 0 is the caller's frames, levels >= 1 the plan's planes.
+int orbx::extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int* w, int* hgt, float* scale,
+                            float* inv_scale, int* L) {
+  if (!h) return fail(ORBX_EINVAL, "null extractor handle");
+  if (frame0 < 0 || n < 1 || frame0 + n > h->last_batch || !h->last_frames)
+    return fail(ORBX_EINVAL, "frames [%d, %d) not in the extractor's last extraction (%d frames)", frame0,
+                frame0 + n, h->last_batch);
+  const ExtractParams& P = h->plan.P;
+  const ExtractBuffers X = buffers_of(h->plan);
+  *L = P.L;
+  for (int l = 0; l < P.L; ++l) {
+    const LevelGeom& g = P.lv[l];
+    if (l == 0) {
+      lp->base[0] = h->last_frames + (long long)frame0 * h->last_fpitch;
+      lp->fstride[0] = (long long)h->last_fpitch;
+      lp->pitch[0] = (int)h->last_rstride;
+    } else {
+      lp->base[l] = X.pyr + g.off + (long long)frame0 * g.plane;
+      lp->fstride[l] = g.plane;
+      lp->pitch[l] = g.pitch;
+    }
+    lp->aligned16[l] = 0;
+    w[l] = g.w;
+    hgt[l] = g.h;
+    scale[l] = h->scale[l];
+    inv_scale[l] = h->inv_scale[l];
+  }
+  return ORBX_OK;
+}
+
 // ------------------------------------------------------------ C ABI
 extern "C" {
 

@@ -132,4 +132,23 @@ int launch_search_bow(const uint8_t* descA, const float* angleA, const uint8_t* 
                       float nnratio, int check_ori, int kf_vs_kf, int* out, int* nmatches,
                       int* scratch, void* stream);
 
+// orbx_stereo.hip — Frame::ComputeStereoMatches over a batch of rectified pairs.
+// Pyramid pointers address pair 0; pair p's level l is at base[l] + p * fstride[l].
+struct StereoParams {
+  LevelPtrs pl, pr;
+  int lw[kMaxLevels], lh[kMaxLevels];
+  float scale[kMaxLevels], inv_scale[kMaxLevels];
+  int L, nrows;        // levels; rows of level 0 (the row table's size)
+  int rwin;            // row half-window that holds every candidate's floor(y)
+  int kp_pitch, groups;
+  float mb, mbf;
+};
+size_t stereo_lds_bytes(int nrows, int kp_pitch);
+int launch_stereo(const StereoParams& P, const orbx_kp* kpL, const uint8_t* descL, const int* nL,
+                  const orbx_kp* kpR, const uint8_t* descR, const int* nR, int pairs, float* uRight,
+                  float* depth, int* sad, int* nkept, void* stream);
+// orbx_host.hip: the pyramid of frames [frame0, frame0 + n) of an extractor's last extraction
+int extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int* w, int* hgt, float* scale,
+                      float* inv_scale, int* L);
+
 }  // namespace orbx

@@ -1068,6 +1068,7 @@ struct orbx_matcher {
   long long cand_cap = 0;
   uint32_t* cand = nullptr;
   int* err = nullptr;
+  int* stereo_sad = nullptr;  // [max_pairs][max_kps] SAD per left keypoint (-1 = none)
   hipStream_t stream = nullptr;
   // staging for the synchronous entry points
   void* stage = nullptr;
@@ -1099,7 +1100,8 @@ int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out) {
   // below this; overflow is reported (ORBX_ECAPACITY), never truncated.
   m->cand_cap = std::min<long long>((long long)max_kps * max_kps, 4ll << 20);
   if (hipMalloc(&m->cand, (size_t)max_pairs * m->cand_cap * 4) != hipSuccess ||
-      hipMalloc(&m->err, 16) != hipSuccess) {
+      hipMalloc(&m->err, 16) != hipSuccess ||
+      hipMalloc(&m->stereo_sad, (size_t)max_pairs * max_kps * 4) != hipSuccess) {
     orbm_destroy(m);
     return mfail(ORBX_ENOMEM, "matcher workspace allocation failed");
   }
@@ -1116,6 +1118,7 @@ int orbm_destroy(orbm_handle m) {
   if (m->stream) (void)hipStreamSynchronize(m->stream);
   if (m->cand) (void)hipFree(m->cand);
   if (m->err) (void)hipFree(m->err);
+  if (m->stereo_sad) (void)hipFree(m->stereo_sad);
   if (m->stage) (void)hipFree(m->stage);
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
@@ -1303,6 +1306,90 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
   if (nout) MHIP(hipMemcpyAsync(out, d[12], (size_t)nout * 4, hipMemcpyDeviceToHost, st));
   MHIP(hipStreamSynchronize(st));
   *nmatches = nm;
+  return ORBX_OK;
+}
+
+int orbm_compute_stereo_matches_batch(orbm_handle m, orbx_handle left, int left_frame0, orbx_handle right,
+                                      int right_frame0, const orbx_kp* d_kpL, const uint8_t* d_descL,
+                                      const int* d_nL, const orbx_kp* d_kpR, const uint8_t* d_descR,
+                                      const int* d_nR, int kp_pitch, int pairs, float mb, float mbf,
+                                      float* d_uRight, float* d_depth, int* d_nkept, void* stream) {
+  if (!m || !left || !right || !d_kpL || !d_descL || !d_nL || !d_kpR || !d_descR || !d_nR || !d_uRight ||
+      !d_depth || !d_nkept || pairs < 1 || kp_pitch < 1)
+    return mfail(ORBX_EINVAL, "bad argument");
+  if (pairs > m->max_pairs || kp_pitch > m->max_kps)
+    return mfail(ORBX_ECAPACITY, "pairs/kp_pitch above the matcher's max_pairs/max_kps");
+  if (!(mb > 0.f)) return mfail(ORBX_EINVAL, "baseline mb must be positive");
+  MHIP(hipSetDevice(m->device));
+  StereoParams P{};
+  int wr[kMaxLevels], hr[kMaxLevels], LR = 0;
+  float sr[kMaxLevels], isr[kMaxLevels];
+  if (extractor_pyramid(left, left_frame0, pairs, &P.pl, P.lw, P.lh, P.scale, P.inv_scale, &P.L) ||
+      extractor_pyramid(right, right_frame0, pairs, &P.pr, wr, hr, sr, isr, &LR))
+    return mfail(ORBX_EINVAL, "stereo pyramid: %s", orbx_last_error());
+  if (LR != P.L) return mfail(ORBX_EINVAL, "left and right extractors have different level counts");
+  for (int l = 0; l < P.L; ++l)
+    if (wr[l] != P.lw[l] || hr[l] != P.lh[l]) return mfail(ORBX_EINVAL, "left and right image sizes differ");
+  P.nrows = P.lh[0];
+  // every candidate of row yi has floor(y) within yi -/+ (ceil(2 * max scale) + 2)
+  P.rwin = (int)std::ceil(2.0f * P.scale[P.L - 1]) + 2;
+  P.kp_pitch = kp_pitch;
+  P.mb = mb;
+  P.mbf = mbf;
+  if (stereo_lds_bytes(P.nrows, kp_pitch) > 150 * 1024)
+    return mfail(ORBX_ECAPACITY, "stereo row table does not fit in LDS (rows %d, kp_pitch %d)", P.nrows, kp_pitch);
+  // ~1024 workgroups over the batch; each re-buckets its pair's right keypoints
+  P.groups = std::max(1, std::min(16, (1024 + pairs - 1) / pairs));
+  return launch_stereo(P, d_kpL, d_descL, d_nL, d_kpR, d_descR, d_nR, pairs, d_uRight, d_depth, m->stereo_sad,
+                       d_nkept, stream) == ORBX_OK
+             ? ORBX_OK
+             : mfail(ORBX_EDEVICE, "stereo launch: %s", hipGetErrorString(hipGetLastError()));
+}
+
+int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle right, const orbx_kp* kpL,
+                                const uint8_t* descL, int nL, const orbx_kp* kpR, const uint8_t* descR, int nR,
+                                float mb, float mbf, float* uRight, float* depth, int* nkept) {
+  if (!m || !nkept || nL < 0 || nR < 0 || (nL && (!kpL || !descL || !uRight || !depth)) || (nR && (!kpR || !descR)))
+    return mfail(ORBX_EINVAL, "bad argument");
+  if (nL > m->max_kps || nR > m->max_kps) return mfail(ORBX_ECAPACITY, "more keypoints than max_kps");
+  if (nR > 65535) return mfail(ORBX_ECAPACITY, "more than 65535 right keypoints");
+  MHIP(hipSetDevice(m->device));
+  const int pitch = std::max(std::max(nL, nR), 1);
+  const size_t kpb = (size_t)pitch * sizeof(orbx_kp), db = (size_t)pitch * 32;
+  const size_t bytes = 2 * kpb + 2 * db + (size_t)pitch * 8 + 64;
+  int rc;
+  if ((rc = stage_reserve(m, bytes))) return rc;
+  uint8_t* s = (uint8_t*)m->stage;
+  orbx_kp* dkl = (orbx_kp*)s;
+  orbx_kp* dkr = (orbx_kp*)(s + kpb);
+  uint8_t* ddl = s + 2 * kpb;
+  uint8_t* ddr = ddl + db;
+  float* du = (float*)(ddr + db);
+  float* dd = du + pitch;
+  int* dn = (int*)(dd + pitch);  // nL, nR, kept
+  if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+  hipStream_t st = m->stream;
+  const int hn[2] = {nL, nR};
+  if (nL) {
+    MHIP(hipMemcpyAsync(dkl, kpL, (size_t)nL * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(ddl, descL, (size_t)nL * 32, hipMemcpyHostToDevice, st));
+  }
+  if (nR) {
+    MHIP(hipMemcpyAsync(dkr, kpR, (size_t)nR * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(ddr, descR, (size_t)nR * 32, hipMemcpyHostToDevice, st));
+  }
+  MHIP(hipMemcpyAsync(dn, hn, 8, hipMemcpyHostToDevice, st));
+  rc = orbm_compute_stereo_matches_batch(m, left, 0, right, 0, dkl, ddl, dn, dkr, ddr, dn + 1, pitch, 1, mb, mbf,
+                                         du, dd, dn + 2, st);
+  if (rc) return rc;
+  int kept = 0;
+  MHIP(hipMemcpyAsync(&kept, dn + 2, 4, hipMemcpyDeviceToHost, st));
+  if (nL) {
+    MHIP(hipMemcpyAsync(uRight, du, (size_t)nL * 4, hipMemcpyDeviceToHost, st));
+    MHIP(hipMemcpyAsync(depth, dd, (size_t)nL * 4, hipMemcpyDeviceToHost, st));
+  }
+  MHIP(hipStreamSynchronize(st));
+  *nkept = kept;
   return ORBX_OK;
 }
 

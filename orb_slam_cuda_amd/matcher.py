@@ -33,6 +33,13 @@ class Frame:
     mnMinY: float = 0.0
     mnMaxY: float = 0.0
     mFeatVec: dict | None = None           # DBoW2::FeatureVector {NodeId: [feature idx]}
+    # stereo (Frame's stereo constructor, src/Frame.cc:43-101)
+    mvKeysRight: np.ndarray | None = None  # KP_DTYPE
+    mDescriptorsRight: np.ndarray | None = None
+    mb: float = 0.0                        # baseline (m)
+    mbf: float = 0.0                       # baseline x fx
+    mvuRight: np.ndarray | None = None     # (N,) float32, -1 = no stereo match
+    mvDepth: np.ndarray | None = None
 
     @property
     def N(self) -> int:
@@ -46,6 +53,26 @@ class Frame:
     def from_extraction(cls, kps, desc, width, height, featvec=None):
         # no distortion: mvKeysUn == mvKeys and bounds = image rectangle (src/Frame.cc:458-461)
         return cls(kps, desc, 0.0, float(width), 0.0, float(height), featvec)
+
+
+def ComputeStereoMatches(F: Frame, extractorLeft, extractorRight, matcher: "ORBmatcher") -> int:
+    """Frame::ComputeStereoMatches (src/Frame.cc:465-639): fills F.mvuRight / F.mvDepth from
+    F.mvKeys/mDescriptors (left) and F.mvKeysRight/mDescriptorsRight, refining with the
+    mvImagePyramid of the two extractors' last extraction (frame 0 of each). Returns the
+    number of stereo matches kept after the median-SAD rejection."""
+    kpL = np.ascontiguousarray(F.mvKeysUn, KP_DTYPE)
+    kpR = np.ascontiguousarray(F.mvKeysRight, KP_DTYPE)
+    dL = np.ascontiguousarray(F.mDescriptors, np.uint8)
+    dR = np.ascontiguousarray(F.mDescriptorsRight, np.uint8)
+    uR = np.full(len(kpL), -1.0, np.float32)
+    dep = np.full(len(kpL), -1.0, np.float32)
+    kept = C.c_int(0)
+    check(lib().orbm_compute_stereo_matches(
+        matcher.handle, extractorLeft.handle, extractorRight.handle, ptr(kpL), ptr(dL), len(kpL),
+        ptr(kpR), ptr(dR), len(kpR), C.c_float(F.mb), C.c_float(F.mbf), ptr(uR), ptr(dep),
+        C.byref(kept)), matcher=True)
+    F.mvuRight, F.mvDepth = uR, dep
+    return kept.value
 
 
 @dataclass

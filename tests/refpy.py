@@ -345,3 +345,95 @@ def search_by_bow(dA, angA, mpA, fvA, dB, angB, mpB, fvB, ratio, check_ori, kf_v
                 out[i] = -1
                 nm -= 1
     return np.array(out, np.int32), nm
+
+
+# -------------------------------------------------------------- stereo
+def _c_round(v) -> float:
+    """std::round on a float: half away from zero."""
+    v = float(v)
+    return math.copysign(math.floor(abs(v) + 0.5), v)
+
+
+def compute_stereo_matches(kpL, dL, kpR, dR, pyrL, pyrR, scale, inv_scale, mb, mbf):
+    """Frame::ComputeStereoMatches (src/Frame.cc:465-639). pyrL/pyrR: per-level 2-D u8.
+    Windows reaching off the level (an OpenCV range assertion there) give no match."""
+    nL = len(kpL)
+    uR_out = np.full(nL, -1.0, np.float32)
+    dep_out = np.full(nL, -1.0, np.float32)
+    nrows = pyrL[0].shape[0]
+    rows = [[] for _ in range(nrows)]
+    for iR in range(len(kpR)):
+        y = f32(kpR["y"][iR])
+        r = f32(f32(2) * f32(scale[int(kpR["octave"][iR])]))
+        for yi in range(int(math.floor(f32(y - r))), int(math.ceil(f32(y + r))) + 1):
+            if 0 <= yi < nrows:
+                rows[yi].append(iR)
+    mb, mbf = f32(mb), f32(mbf)
+    maxD = f32(mbf / mb)
+    acc = []
+    for iL in range(nL):
+        lev = int(kpL["octave"][iL])
+        uL, vL = f32(kpL["x"][iL]), f32(kpL["y"][iL])
+        if not (0 <= vL < nrows):
+            continue
+        cands = rows[int(vL)]
+        minU, maxU = f32(uL - maxD), uL
+        if not cands or maxU < 0:
+            continue
+        best, bi = 100, 0
+        for iR in cands:
+            o = int(kpR["octave"][iR])
+            if o < lev - 1 or o > lev + 1:
+                continue
+            u = f32(kpR["x"][iR])
+            if minU <= u <= maxU:
+                d = hamming(dL[iL], dR[iR])
+                if d < best:
+                    best, bi = d, iR
+        if best >= 75:
+            continue
+        sf = f32(inv_scale[lev])
+        su = _c_round(f32(uL * sf))
+        sv = _c_round(f32(vL * sf))
+        sr = _c_round(f32(f32(kpR["x"][bi]) * sf))
+        A, B = pyrL[lev].astype(np.int64), pyrR[lev].astype(np.int64)
+        h, w = A.shape
+        ul, vl, ur = int(su), int(sv), int(sr)
+        if ur < 10 or ul < 5 or ul + 5 >= w or vl < 5 or vl + 5 >= h:
+            continue
+        if sr < 0 or sr + 11 >= w:  # iniu / endu
+            continue
+        IL = A[vl - 5:vl + 6, ul - 5:ul + 6] - A[vl, ul]
+        dists = []
+        for inc in range(-5, 6):
+            IR = B[vl - 5:vl + 6, ur + inc - 5:ur + inc + 6] - B[vl, ur + inc]
+            dists.append(int(np.abs(IL - IR).sum()))
+        binc = int(np.argmin(dists)) - 5  # first minimum
+        bdist = min(dists)
+        if binc in (-5, 5):
+            continue
+        d1, d2, d3 = (f32(dists[binc + 5 + k]) for k in (-1, 0, 1))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            delta = f32(f32(d1 - d3) / f32(f32(2) * f32(f32(d1 + d3) - f32(f32(2) * d2))))
+        if delta < -1 or delta > 1:
+            continue
+        buR = f32(f32(scale[lev]) * f32(f32(f32(sr) + f32(binc)) + delta))
+        disp = f32(uL - buR)
+        if disp >= 0 and disp < maxD:
+            if disp <= 0:
+                disp = f32(0.01)
+                buR = f32(float(uL) - 0.01)
+            dep_out[iL] = f32(mbf / disp)
+            uR_out[iL] = buR
+            acc.append((bdist, iL))
+    if not acc:
+        return uR_out, dep_out, 0
+    acc.sort()
+    th = f32(f32(f32(1.5) * f32(1.4)) * f32(acc[len(acc) // 2][0]))
+    kept = len(acc)
+    for d, i in reversed(acc):
+        if f32(d) < th:
+            break
+        uR_out[i] = dep_out[i] = -1
+        kept -= 1
+    return uR_out, dep_out, kept

@@ -244,3 +244,55 @@ def test_golden_match(O):
                                               100, 0.9, True)
     assert nm == int(g["nmatches"]) and np.array_equal(m, g["matches12"])
     assert np.array_equal(prev, g["prev_after"])
+
+
+# ----------------------------------------------------------- stereo (§8f row 1)
+def _stereo_inputs(O, seed, W=1241, H=376, nf=2000):
+    from orb_slam_cuda_amd.synth import stereo_pair
+    imL, imR = stereo_pair(seed, W, H)
+    cfg = O.config(nfeatures=nf, width=W, height=H)
+    (kL, dL), (kR, dR) = O.extract(cfg, imL), O.extract(cfg, imR)
+    li = O.level_info(cfg)
+    return kL, dL, kR, dR, O.pyramid(cfg, imL), O.pyramid(cfg, imR), li["scale"], li["inv_scale"]
+
+
+MB, MBF = 0.54, np.float32(0.54 * 718.856)  # KITTI-like baseline / fx
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_stereo_matches_refpy(O, seed):
+    kL, dL, kR, dR, pL, pR, sc, isc = _stereo_inputs(O, seed)
+    uR, dep, kept = O.compute_stereo_matches(kL, dL, kR, dR, pL, pR, sc, isc, MB, MBF)
+    euR, edep, ekept = refpy.compute_stereo_matches(kL, dL, kR, dR, pL, pR, sc, isc, MB, MBF)
+    assert kept == ekept
+    assert np.array_equal(uR, euR) and np.array_equal(dep, edep)
+    # the synthetic pair is a pure horizontal shift: most matches recover it
+    ok = uR >= 0
+    assert kept == ok.sum() and kept > 0.4 * len(kL)
+    disp = kL["x"][ok] - uR[ok]
+    assert abs(np.median(disp) - np.median(disp.round())) < 0.25
+
+
+def test_stereo_matches_edges(O):
+    kL, dL, kR, dR, pL, pR, sc, isc = _stereo_inputs(O, 3, 640, 240, 500)
+    # no right keypoints / no left keypoints
+    uR, dep, kept = O.compute_stereo_matches(kL, dL, kR[:0], dR[:0], pL, pR, sc, isc, MB, MBF)
+    assert kept == 0 and (uR == -1).all() and (dep == -1).all()
+    uR, dep, kept = O.compute_stereo_matches(kL[:0], dL[:0], kR, dR, pL, pR, sc, isc, MB, MBF)
+    assert kept == 0 and len(uR) == 0
+    # identical images: every SAD is 0, so the median is 0 and the rejection
+    # (SAD >= 1.5 * 1.4 * median, :631-637) drops every match
+    uR, dep, kept = O.compute_stereo_matches(kL, dL, kL, dL, pL, pL, sc, isc, MB, MBF)
+    euR, edep, ekept = refpy.compute_stereo_matches(kL, dL, kL, dL, pL, pL, sc, isc, MB, MBF)
+    assert kept == ekept == 0 and (uR == -1).all() and np.array_equal(dep, edep)
+    # zero shift plus noise: disparities around 0 (negative ones rejected, 0 clamped to 0.01)
+    rng = np.random.default_rng(1)
+    pN = [np.clip(a.astype(np.int32) + rng.integers(-3, 4, a.shape), 0, 255).astype(np.uint8) for a in pL]
+    a = O.compute_stereo_matches(kL, dL, kL, dL, pL, pN, sc, isc, MB, MBF)
+    b = refpy.compute_stereo_matches(kL, dL, kL, dL, pL, pN, sc, isc, MB, MBF)
+    assert a[2] == b[2] > 0 and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    # duplicated right descriptors: ties resolved to the lowest iR
+    kR2 = np.concatenate([kR, kR]); dR2 = np.concatenate([dR, dR])
+    a = O.compute_stereo_matches(kL, dL, kR2, dR2, pL, pR, sc, isc, MB, MBF)
+    b = refpy.compute_stereo_matches(kL, dL, kR2, dR2, pL, pR, sc, isc, MB, MBF)
+    assert a[2] == b[2] and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
