@@ -50,6 +50,9 @@ CONFIGS = {
     "kitti": dict(W=1241, H=376, nfeatures=2000,
                   workload="C3: KITTI-shaped 1241x376 mono u8, nFeatures=2000, 8 levels x1.2, "
                            "extract + match vs t-1 (dense 2000x2000 Hamming top-2 + SearchForInitialization)"),
+    "stereo": dict(W=1241, H=376, nfeatures=2000, stereo=True,
+                   workload="C4: stereo_kitti, 2 x 1241x376 u8 per pair, nFeatures=2000 per image, 8 levels x1.2, "
+                            "left/right extraction on separate HIP streams + Frame::ComputeStereoMatches"),
     "euroc": dict(W=752, H=480, nfeatures=1000,
                   workload="C5: EuRoC-shaped 752x480 mono u8, nFeatures=1000, 8 levels x1.2, "
                            "extract + match vs t-1 (dense Hamming top-2 + SearchForInitialization)"),
@@ -107,6 +110,8 @@ def main():
 
     L = _lib.lib()
     cfg = CONFIGS[args.config]
+    if cfg.get("stereo"):
+        return run_stereo(args, cfg, rank, world, local, dist)
     W, H, NF, B = cfg["W"], cfg["H"], cfg["nfeatures"], args.batch
     pitch = (W + 63) & ~63
 
@@ -293,6 +298,156 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+STEREO_METRIC = "stereo pairs/s ORB extract (left+right) + ComputeStereoMatches, 2x1241x376 nFeatures=2000"
+MB, MBF = 0.54, 0.54 * 718.856  # KITTI stereo baseline (m) and baseline x fx
+
+
+def run_stereo(args, cfg, rank, world, local, dist):
+    """C4: per step B rectified pairs resident in HBM; left frames extracted on
+    one stream and right frames on another (two ORBextractor handles, as
+    Frame's mpORBextractorLeft / mpORBextractorRight), then ComputeStereoMatches
+    of the B pairs on the left stream once both are done. Two handle sets
+    alternate between steps so that the stereo matching of step k (which reads
+    step k's pyramids) overlaps the extraction of step k+1."""
+    import orb_slam_cuda_amd as pkg
+    from orb_slam_cuda_amd import _lib, sharding
+    from orb_slam_cuda_amd.synth import stereo_pair
+
+    L = _lib.lib()
+    check = _lib.check
+    W, H, NF, B = cfg["W"], cfg["H"], cfg["nfeatures"], args.batch
+    pitch = (W + 63) & ~63
+    check(L.orbx_set_device(local))
+    base = sharding.sequence_seed(rank)
+    pairs = [stereo_pair(base + i, W, H) for i in range(B)]
+    host = np.zeros((2, B, H, pitch), np.uint8)
+    for i, (a, b) in enumerate(pairs):
+        host[0, i, :, :W] = a
+        host[1, i, :, :W] = b
+    d_frames = _lib.DeviceArray(host.nbytes)
+    d_frames.upload(host)
+    fb = B * H * pitch  # bytes of one side's frames
+    KP, DS, NSET = 28, 32, 2
+    sets = []
+    for _ in range(NSET):
+        eL = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=B)
+        eR = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=B)
+        cap = eL.frame_capacity
+        sets.append(dict(eL=eL, eR=eR, sL=_lib.Stream(), sR=_lib.Stream(),
+                         kps=_lib.DeviceArray(2 * B * cap * KP), desc=_lib.DeviceArray(2 * B * cap * DS),
+                         n=_lib.DeviceArray(2 * B * 4), u=_lib.DeviceArray(B * cap * 4),
+                         d=_lib.DeviceArray(B * cap * 4), kept=_lib.DeviceArray(B * 4)))
+    cap = sets[0]["eL"].frame_capacity
+    matcher = pkg.ORBmatcher(device=local, max_pairs=B, max_kps=cap)
+    vp = lambda a: C.c_void_p(a)
+    total = args.warmup + args.steps
+    # per step: 6 extraction stage marks (left stream) + stereo start/end + right-done + done
+    evs = [[_lib.Event() for _ in range(10)] for _ in range(total)]
+
+    def step(k):
+        st = sets[k % NSET]
+        ev = evs[k]
+        if k >= NSET:
+            st["sR"].wait(evs[k - NSET][9])  # stereo k-2 (left stream) read this set's right pyramid
+        arr = (C.c_void_p * 6)(*[e.e.value for e in ev[:6]])
+        check(L.orbx_set_stage_events(st["eL"].handle, arr))
+        for side, (ex, s) in enumerate(((st["eL"], st["sL"]), (st["eR"], st["sR"]))):
+            check(L.orbx_extract_batch(ex.handle, vp(d_frames.ptr + side * fb), B, H * pitch, pitch,
+                                       vp(st["kps"].ptr + side * B * cap * KP),
+                                       vp(st["desc"].ptr + side * B * cap * DS), vp(st["n"].ptr + side * B * 4), s.s))
+        ev[8].record(st["sR"])
+        st["sL"].wait(ev[8])
+        ev[6].record(st["sL"])
+        check(L.orbm_compute_stereo_matches_batch(
+            matcher.handle, st["eL"].handle, 0, st["eR"].handle, 0, vp(st["kps"].ptr), vp(st["desc"].ptr),
+            vp(st["n"].ptr), vp(st["kps"].ptr + B * cap * KP), vp(st["desc"].ptr + B * cap * DS),
+            vp(st["n"].ptr + B * 4), cap, B, C.c_float(MB), C.c_float(MBF), vp(st["u"].ptr), vp(st["d"].ptr),
+            vp(st["kept"].ptr), st["sL"].s), matcher=True)
+        ev[7].record(st["sL"])
+        ev[9].record(st["sL"])
+
+    def sync_all():
+        for st in sets:
+            st["sL"].synchronize()
+            st["sR"].synchronize()
+
+    for k in range(args.warmup):
+        step(k)
+    sync_all()
+    if dist is not None:
+        dist.barrier()
+    sync_all()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, total):
+        step(k)
+    sync_all()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    wall = sharding.max_over_ranks(t1 - t0, dist)
+    timed = evs[args.warmup:]
+    stages = STAGES[:5] + ["stereo"]
+    sm = {s: 0.0 for s in stages}
+    for ev in timed:
+        for i, s in enumerate(STAGES[:5]):
+            sm[s] += ev[i].elapsed_ms(ev[i + 1])
+        sm["stereo"] += ev[6].elapsed_ms(ev[7])
+    sm = {s: v / args.steps for s, v in sm.items()}
+    last = sets[(total - 1) % NSET]
+    kept = last["kept"].download(B, np.int32)
+    nkp = last["n"].download(2 * B, np.int32)
+    value = B * args.steps * world / wall
+    ab = algorithmic_bytes(W, H, float(nkp.mean()))
+    hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
+                  "orient_brief": ab["orient_brief"]}
+    rk = max(hbm_stages, key=lambda s: sm[s])
+    ach = hbm_stages[rk] * B / (sm[rk] * 1e-3) / 1e9
+    roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "algorithmic_bytes_per_launch": int(hbm_stages[rk] * B), "avg_launch_ms": round(sm[rk], 4)}
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline_stereo(pairs, cfg, max(1, args.cpu_sample // 2))
+    if rank == 0:
+        out = {
+            "metric": STEREO_METRIC, "value": round(value, 2), "unit": "stereo pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic rectified pairs (orb_slam_cuda_amd/synth.py stereo_pair)",
+            "config": {"workload": cfg["workload"], "frame": f"2x{W}x{H}", "nfeatures": NF, "nlevels": 8,
+                       "scale_factor": 1.2, "pairs_per_step_per_gpu": B,
+                       "parallelism": f"pair-sharded x{world}, no collectives", "streams": 2 * NSET,
+                       "mb": MB, "mbf": MBF},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "stage_ms_per_step": {s: round(v, 4) for s, v in sm.items()},
+            "keypoints_per_image": round(float(nkp.mean()), 1),
+            "stereo_matches_per_pair": round(float(kept.mean()), 1),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_stereo(pairs, cfg, n):
+    """The CPU oracle on a bounded sample of pairs: extract left + right, pyramids, ComputeStereoMatches."""
+    from oracle import oracle as O
+    W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
+    oc = O.config(nfeatures=NF, width=W, height=H)
+    li = O.level_info(oc)
+    n = min(n, len(pairs))
+    t0 = time.perf_counter()
+    for a, b in pairs[:n]:
+        kl, dl = O.extract(oc, a)
+        kr, dr = O.extract(oc, b)
+        O.compute_stereo_matches(kl, dl, kr, dr, O.pyramid(oc, a), O.pyramid(oc, b), li["scale"], li["inv_scale"],
+                                 MB, np.float32(MBF))
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "stereo pairs/s", "cores": 1, "kind": "port",
+            "sample": f"{n} synthetic pairs, oracle extract left + right + ComputeStereoMatches "
+                      f"(pyramids rebuilt for the SAD), single thread, {dt:.1f} s"}
 
 
 def cpu_baseline(frames, cfg, n, no_match):
