@@ -89,7 +89,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
-    ap.add_argument("--cpu-sample", type=int, default=24, help="frames in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=200,
+                    help="frames (stereo: 2 x pairs) in the CPU baseline sample, ~10 s on one core (0 = skip)")
     ap.add_argument("--no-match", action="store_true", help="extract only (C2)")
     ap.add_argument("--serial", action="store_true", help="one stream: no overlap of matching with the next extraction")
     ap.add_argument("--split", type=int, default=2, help="extraction launches (and streams) per batch")
@@ -273,7 +274,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(frames, cfg, args.cpu_sample, args.no_match)
+        sample = frames if args.cpu_sample <= len(frames) else seq_cpu(rank, W, H, args.cpu_sample)
+        cpu = cpu_baseline(sample, cfg, args.cpu_sample, args.no_match)
 
     if rank == 0:
         out = {
@@ -331,11 +333,13 @@ def run_stereo(args, cfg, rank, world, local, dist):
     fb = B * H * pitch  # bytes of one side's frames
     KP, DS, NSET = 28, 32, 2
     sets = []
+    s_one = _lib.Stream() if args.serial else None  # --serial: every launch on one stream
     for _ in range(NSET):
         eL = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=B)
         eR = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=B)
         cap = eL.frame_capacity
-        sets.append(dict(eL=eL, eR=eR, sL=_lib.Stream(), sR=_lib.Stream(),
+        sL = s_one or _lib.Stream()
+        sets.append(dict(eL=eL, eR=eR, sL=sL, sR=s_one or _lib.Stream(),
                          kps=_lib.DeviceArray(2 * B * cap * KP), desc=_lib.DeviceArray(2 * B * cap * DS),
                          n=_lib.DeviceArray(2 * B * 4), u=_lib.DeviceArray(B * cap * 4),
                          d=_lib.DeviceArray(B * cap * 4), kept=_lib.DeviceArray(B * 4)))
@@ -418,7 +422,8 @@ def run_stereo(args, cfg, rank, world, local, dist):
             "data": "synthetic rectified pairs (orb_slam_cuda_amd/synth.py stereo_pair)",
             "config": {"workload": cfg["workload"], "frame": f"2x{W}x{H}", "nfeatures": NF, "nlevels": 8,
                        "scale_factor": 1.2, "pairs_per_step_per_gpu": B,
-                       "parallelism": f"pair-sharded x{world}, no collectives", "streams": 2 * NSET,
+                       "parallelism": f"pair-sharded x{world}, no collectives",
+                       "streams": 1 if args.serial else 2 * NSET,
                        "mb": MB, "mbf": MBF},
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -437,17 +442,24 @@ def cpu_baseline_stereo(pairs, cfg, n):
     W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
     oc = O.config(nfeatures=NF, width=W, height=H)
     li = O.level_info(oc)
-    n = min(n, len(pairs))
     t0 = time.perf_counter()
-    for a, b in pairs[:n]:
+    for i in range(n):
+        a, b = pairs[i % len(pairs)]
         kl, dl = O.extract(oc, a)
         kr, dr = O.extract(oc, b)
         O.compute_stereo_matches(kl, dl, kr, dr, O.pyramid(oc, a), O.pyramid(oc, b), li["scale"], li["inv_scale"],
                                  MB, np.float32(MBF))
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 3), "unit": "stereo pairs/s", "cores": 1, "kind": "port",
-            "sample": f"{n} synthetic pairs, oracle extract left + right + ComputeStereoMatches "
+            "sample": f"{n} synthetic pairs (cycling the step's {len(pairs)}), oracle extract left + right + ComputeStereoMatches "
                       f"(pyramids rebuilt for the SAD), single thread, {dt:.1f} s"}
+
+
+def seq_cpu(rank, W, H, n):
+    """The first n frames of the rank's synthetic sequence (the timed batch is its first B)."""
+    from orb_slam_cuda_amd import sharding
+    from orb_slam_cuda_amd.synth import SynthSequence
+    return SynthSequence(sharding.sequence_seed(rank), W, H).frames(n)
 
 
 def cpu_baseline(frames, cfg, n, no_match):

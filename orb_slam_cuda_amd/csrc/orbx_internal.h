@@ -139,11 +139,12 @@ struct StereoParams {
   int lw[kMaxLevels], lh[kMaxLevels];
   float scale[kMaxLevels], inv_scale[kMaxLevels];
   int L, nrows;        // levels; rows of level 0 (the row table's size)
-  int rwin;            // row half-window that holds every candidate's floor(y)
   int kp_pitch, groups;
+  int jobs_cap;        // SAD jobs a workgroup can hold: its share of left keypoints
   float mb, mbf;
+  int stop;            // diagnostics: 1 = return after the row table, 2 = after the Hamming search
 };
-size_t stereo_lds_bytes(int nrows, int kp_pitch);
+size_t stereo_lds_bytes(int nrows, int kp_pitch, int jobs_cap);
 int launch_stereo(const StereoParams& P, const orbx_kp* kpL, const uint8_t* descL, const int* nL,
                   const orbx_kp* kpR, const uint8_t* descR, const int* nR, int pairs, float* uRight,
                   float* depth, int* sad, int* nkept, void* stream);

@@ -24,6 +24,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -1331,15 +1332,19 @@ int orbm_compute_stereo_matches_batch(orbm_handle m, orbx_handle left, int left_
   for (int l = 0; l < P.L; ++l)
     if (wr[l] != P.lw[l] || hr[l] != P.lh[l]) return mfail(ORBX_EINVAL, "left and right image sizes differ");
   P.nrows = P.lh[0];
-  // every candidate of row yi has floor(y) within yi -/+ (ceil(2 * max scale) + 2)
-  P.rwin = (int)std::ceil(2.0f * P.scale[P.L - 1]) + 2;
   P.kp_pitch = kp_pitch;
   P.mb = mb;
   P.mbf = mbf;
-  if (stereo_lds_bytes(P.nrows, kp_pitch) > 150 * 1024)
+  // ~256 workgroups (one per CU) over the batch; each stages its pair's right
+  // keypoints and descriptors in LDS
+  P.groups = std::max(1, std::min(8, (256 + pairs - 1) / pairs));
+  if (const char* e = getenv("ORBX_STEREO_GROUPS")) P.groups = std::max(1, atoi(e));  // tuning experiments
+  P.stop = 0;
+  if (const char* e = getenv("ORBX_STEREO_STOP")) P.stop = atoi(e);
+  // workgroup g takes left keypoints iL = g + groups * m: at most this many
+  P.jobs_cap = (kp_pitch + P.groups - 1) / P.groups;
+  if (stereo_lds_bytes(P.nrows, kp_pitch, P.jobs_cap) > 156 * 1024)
     return mfail(ORBX_ECAPACITY, "stereo row table does not fit in LDS (rows %d, kp_pitch %d)", P.nrows, kp_pitch);
-  // ~1024 workgroups over the batch; each re-buckets its pair's right keypoints
-  P.groups = std::max(1, std::min(16, (1024 + pairs - 1) / pairs));
   return launch_stereo(P, d_kpL, d_descL, d_nL, d_kpR, d_descR, d_nR, pairs, d_uRight, d_depth, m->stereo_sad,
                        d_nkept, stream) == ORBX_OK
              ? ORBX_OK
