@@ -47,6 +47,9 @@ def lib():
             C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_float,
             C.c_float, C.c_void_p, C.c_void_p]
+        _lib.orc_voc_load_text.argtypes = [C.c_char_p] + [C.c_void_p] * 5 + [C.c_int] + [C.c_void_p] * 4
+        _lib.orc_voc_transform.argtypes = ([C.c_int] * 5 + [C.c_void_p] * 5 + [C.c_int, C.c_int]
+                                           + [C.c_void_p] * 10)
     return _lib
 
 
@@ -203,3 +206,39 @@ def sincosf(x):
     s, c = np.empty_like(x), np.empty_like(x)
     lib().orc_sincosf(x.ctypes.data, len(x), s.ctypes.data, c.ctypes.data)
     return s, c
+
+
+# ------------------------------------------------------------ DBoW2 vocabulary
+def voc_load_text(path: str, cap: int = 2_000_000) -> dict:
+    """TemplatedVocabulary::loadFromTextFile -> node arrays in file order."""
+    k, L, sc, wt, n = (C.c_int(0) for _ in range(5))
+    parent = np.zeros(cap, np.int32); leaf = np.zeros(cap, np.uint8)
+    desc = np.zeros((cap, 32), np.uint8); weight = np.zeros(cap, np.float64)
+    rc = lib().orc_voc_load_text(path.encode(), C.byref(k), C.byref(L), C.byref(sc), C.byref(wt), C.byref(n),
+                                 cap, _p(parent), _p(leaf), _p(desc), _p(weight))
+    if rc:
+        raise ValueError(f"vocabulary load failed ({rc})")
+    m = n.value
+    return dict(k=k.value, L=L.value, scoring=sc.value, weighting=wt.value, parent=parent[:m].copy(),
+                leaf=leaf[:m].copy(), desc=desc[:m].copy(), weight=weight[:m].copy())
+
+
+def voc_transform(voc: dict, desc: np.ndarray, levelsup: int = 4) -> dict:
+    """TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup).
+    Returns per-feature word/nid/weight and the BowVector / FeatureVector (CSR)."""
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    n = len(desc)
+    parent = np.ascontiguousarray(voc["parent"], np.int32)
+    leaf = np.ascontiguousarray(voc["leaf"], np.uint8)
+    nd = np.ascontiguousarray(voc["desc"], np.uint8)
+    nw = np.ascontiguousarray(voc["weight"], np.float64)
+    word = np.zeros(n, np.uint32); nid = np.zeros(n, np.uint32); w = np.zeros(n, np.float64)
+    bw = np.zeros(max(n, 1), np.uint32); bv = np.zeros(max(n, 1), np.float64)
+    fn = np.zeros(max(n, 1), np.uint32); fo = np.zeros(n + 1, np.int32); fi = np.zeros(max(n, 1), np.int32)
+    nb, nf = C.c_int(0), C.c_int(0)
+    lib().orc_voc_transform(voc["k"], voc["L"], voc["weighting"], voc["scoring"], len(parent), _p(parent),
+                            _p(leaf), _p(nd), _p(nw), _p(desc), n, levelsup, _p(word), _p(nid), _p(w), _p(bw),
+                            _p(bv), C.byref(nb), _p(fn), _p(fo), _p(fi), C.byref(nf))
+    b, f = nb.value, nf.value
+    return dict(word=word, nid=nid, weight=w, bow_words=bw[:b].copy(), bow_values=bv[:b].copy(),
+                fv_nodes=fn[:f].copy(), fv_off=fo[:f + 1].copy(), fv_idx=fi[:fo[f]].copy())

@@ -115,6 +115,15 @@ float orc_fast_atan2(float y, float x);
 /* The host libm's sinf/cosf (what computeOrbDescriptor calls, :199-200). */
 void orc_sincosf(const float* x, int n, float* s, float* c);
 
+/* DBoW2 vocabulary (orb_vocab.cpp). Nodes in file order, node 0 = root:
+ * parent[n], leaf flag, 32-byte descriptor, weight. */
+int orc_voc_load_text(const char* path, int* k, int* L, int* scoring, int* weighting, int* n_nodes, int cap,
+                      int* parent, uint8_t* leaf, uint8_t* desc, double* weight);
+int orc_voc_transform(int k, int L, int weighting, int scoring, int n_nodes, const int* parent, const uint8_t* leaf,
+                      const uint8_t* node_desc, const double* node_weight, const uint8_t* desc, int n, int levelsup,
+                      uint32_t* word_out, uint32_t* nid_out, double* w_out, uint32_t* bow_words,
+                      double* bow_values, int* bow_n, uint32_t* fv_nodes, int* fv_off, int* fv_idx, int* fv_n);
+
 #ifdef __cplusplus
 }
 #endif

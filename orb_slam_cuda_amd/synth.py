@@ -119,3 +119,48 @@ def stereo_pair(seed: int, W: int = KITTI_WH[0], H: int = KITTI_WH[1]) -> tuple[
     right = canvas[:, disp:disp + W]
     n = lambda a: np.clip(np.rint(a + rng.integers(-6, 7, size=a.shape)), 0, 255).astype(np.uint8)
     return n(left), n(right)
+
+
+def synthetic_vocabulary(k: int = 10, L: int = 6, seed: int = 0, flip: float = 0.2,
+                         scoring: int = 0, weighting: int = 0) -> dict:
+    """A DBoW2-shaped ORB vocabulary (no ORBvoc.txt in this environment): a full
+    k-ary tree of depth L in breadth-first file order (node 0 = root), each
+    child's descriptor its parent's with a fraction `flip` of the bits flipped
+    (a hierarchical clustering look-alike), leaves flagged as words with an
+    idf-like weight log(N / n_i) > 0, inner nodes weight 0. Defaults follow
+    ORB-SLAM2's ORBvoc.txt header (k 10, L 6, L1 scoring, TF-IDF)."""
+    rng = np.random.default_rng(seed)
+    counts = [k ** d for d in range(L + 1)]
+    n = sum(counts)
+    parent = np.zeros(n, np.int32)
+    leaf = np.zeros(n, np.uint8)
+    desc = np.zeros((n, 32), np.uint8)
+    weight = np.zeros(n, np.float64)
+    desc[0] = rng.integers(0, 256, 32, dtype=np.uint8)
+    start = 1
+    prev0 = 0
+    for d in range(1, L + 1):
+        m = counts[d]
+        par = prev0 + np.arange(m) // k
+        parent[start:start + m] = par
+        bits = (rng.random((m, 256)) < flip).astype(np.uint8)
+        desc[start:start + m] = desc[par] ^ np.packbits(bits, axis=1, bitorder="little")
+        prev0 = start
+        start += m
+    nleaf = counts[L]
+    leaf[n - nleaf:] = 1
+    ni = rng.integers(1, 10000, nleaf)
+    weight[n - nleaf:] = np.log(1e4 / ni) + 1e-3
+    return dict(k=k, L=L, scoring=scoring, weighting=weighting, parent=parent, leaf=leaf, desc=desc,
+                weight=weight)
+
+
+def write_vocabulary_text(path: str, voc: dict) -> None:
+    """DBoW2 text format (TemplatedVocabulary::saveToTextFile layout): header
+    "k L scoring weighting", then one line per node after the root:
+    "parent isLeaf d0 ... d31 weight" (weights written round-trip exact)."""
+    with open(path, "w") as f:
+        f.write(f"{voc['k']} {voc['L']} {voc['scoring']} {voc['weighting']}\n")
+        for i in range(1, len(voc["parent"])):
+            d = " ".join(str(int(b)) for b in voc["desc"][i])
+            f.write(f"{int(voc['parent'][i])} {int(voc['leaf'][i])} {d} {float(voc['weight'][i])!r}\n")

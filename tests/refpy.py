@@ -437,3 +437,65 @@ def compute_stereo_matches(kpL, dL, kpR, dR, pyrL, pyrR, scale, inv_scale, mb, m
         uR_out[i] = dep_out[i] = -1
         kept -= 1
     return uR_out, dep_out, kept
+
+
+# -------------------------------------------------------------- DBoW2 transform
+def voc_transform(voc, desc, levelsup):
+    """TemplatedVocabulary::transform(features, v, fv, levelsup)
+    (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1127-1256, BowVector.cpp,
+    FeatureVector.cpp). Returns (words, nids, weights, bow dict, fv dict)."""
+    n_nodes = len(voc["parent"])
+    children = [[] for _ in range(n_nodes)]
+    word_id = [0] * n_nodes
+    nw = 0
+    for i in range(1, n_nodes):
+        children[int(voc["parent"][i])].append(i)
+        if voc["leaf"][i]:
+            word_id[i] = nw
+            nw += 1
+    nd = voc["desc"]
+    words, nids, ws = [], [], []
+    bow, fv = {}, {}
+    if nw == 0:
+        return words, nids, ws, bow, fv
+    nid_level = voc["L"] - levelsup
+    tf = voc["weighting"] in (0, 1)
+    for i, f in enumerate(np.asarray(desc, np.uint8).reshape(-1, 32)):
+        node, level, nid = 0, 0, 0
+        while True:
+            level += 1
+            ch = children[node]
+            dists = [hamming(f, nd[c]) for c in ch]
+            node = ch[int(np.argmin(dists))]  # first minimum
+            if level == nid_level:
+                nid = node
+            if not children[node]:
+                break
+        if nid_level > level:
+            nid = node
+        w = float(voc["weight"][node])
+        words.append(word_id[node]); nids.append(nid); ws.append(w)
+        if w > 0:
+            if tf:
+                bow[word_id[node]] = bow.get(word_id[node], 0.0) + w
+            else:
+                bow.setdefault(word_id[node], w)
+            fv.setdefault(nid, []).append(i)
+    must = voc["scoring"] != 5
+    if tf and bow and not must:
+        nb = float(len(bow))
+        bow = {k: v / nb for k, v in bow.items()}
+    if must:
+        keys = sorted(bow)
+        if voc["scoring"] == 1:
+            norm = 0.0
+            for k in keys:
+                norm += bow[k] * bow[k]
+            norm = math.sqrt(norm)
+        else:
+            norm = 0.0
+            for k in keys:
+                norm += abs(bow[k])
+        if norm > 0.0:
+            bow = {k: bow[k] / norm for k in keys}
+    return words, nids, ws, bow, fv

@@ -296,3 +296,61 @@ def test_stereo_matches_edges(O):
     a = O.compute_stereo_matches(kL, dL, kR2, dR2, pL, pR, sc, isc, MB, MBF)
     b = refpy.compute_stereo_matches(kL, dL, kR2, dR2, pL, pR, sc, isc, MB, MBF)
     assert a[2] == b[2] and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+# ----------------------------------------------------------- DBoW2 transform (§8f row 2)
+def _voc_cmp(r, e):
+    words, nids, ws, bow, fv = e
+    assert list(r["word"]) == words and list(r["nid"]) == nids and list(r["weight"]) == ws
+    assert list(r["bow_words"]) == sorted(bow) and list(r["bow_values"]) == [bow[k] for k in sorted(bow)]
+    assert list(r["fv_nodes"]) == sorted(fv)
+    for j, k in enumerate(sorted(fv)):
+        assert list(r["fv_idx"][r["fv_off"][j]:r["fv_off"][j + 1]]) == fv[k]
+
+
+@pytest.mark.parametrize("k,L,levelsup,scoring,weighting", [(5, 4, 2, 0, 0), (4, 5, 4, 1, 0), (6, 3, 1, 5, 1),
+                                                            (3, 4, 9, 0, 2), (7, 3, 2, 2, 3)])
+def test_voc_transform_matches_refpy(O, k, L, levelsup, scoring, weighting):
+    from orb_slam_cuda_amd.synth import synthetic_vocabulary
+    voc = synthetic_vocabulary(k, L, seed=k * 10 + L, scoring=scoring, weighting=weighting)
+    rng = np.random.default_rng(k)
+    # descriptors near the vocabulary's leaves (plus noise) and a few exact duplicates
+    leaves = voc["desc"][voc["leaf"] == 1]
+    d = leaves[rng.integers(0, len(leaves), 300)] ^ rng.integers(0, 2, (300, 32), dtype=np.uint8)
+    d[::7] = d[0]
+    r = O.voc_transform(voc, d, levelsup)
+    _voc_cmp(r, refpy.voc_transform(voc, d, levelsup))
+    if scoring == 0:
+        assert abs(r["bow_values"].sum() - 1.0) < 1e-12
+
+
+def test_voc_irregular_tree(O):
+    """Uneven tree: shallow leaves (the node id falls back to the leaf), a
+    childless non-word node (word 0, its weight), zero-weight (stopped) words,
+    tied children (first wins)."""
+    rng = np.random.default_rng(3)
+    parent = [0, 0, 0, 0, 1, 1, 2, 2, 2, 4, 4]
+    leaf = [0, 0, 0, 1, 0, 1, 1, 1, 0, 1, 1]
+    n = len(parent)
+    desc = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    desc[7] = desc[6]  # tie under node 2
+    weight = np.array([0, 0, 0, 0.5, 0, 0.25, 0.0, 1.5, 0.75, 2.0, 0.125])
+    voc = dict(k=3, L=3, scoring=0, weighting=0, parent=np.array(parent, np.int32), leaf=np.array(leaf, np.uint8),
+               desc=desc, weight=weight)
+    d = np.concatenate([desc[[3, 5, 6, 7, 8, 9, 10]], rng.integers(0, 256, (200, 32), dtype=np.uint8)])
+    for levelsup in (0, 1, 2, 3):
+        _voc_cmp(O.voc_transform(voc, d, levelsup), refpy.voc_transform(voc, d, levelsup))
+
+
+def test_voc_text_roundtrip(O, tmp_path):
+    from orb_slam_cuda_amd.synth import synthetic_vocabulary, write_vocabulary_text
+    voc = synthetic_vocabulary(6, 3, seed=2)
+    path = str(tmp_path / "voc.txt")
+    write_vocabulary_text(path, voc)
+    with open(path, "a") as f:
+        f.write("\n")  # a trailing empty line (skipped, see DESIGN.md)
+    v2 = O.voc_load_text(path, 10000)
+    assert (v2["k"], v2["L"], v2["scoring"], v2["weighting"]) == (6, 3, 0, 0)
+    for key in ("parent", "leaf", "weight"):
+        assert np.array_equal(voc[key], v2[key])
+    assert np.array_equal(voc["desc"][1:], v2["desc"][1:])  # the root has no descriptor in the file
