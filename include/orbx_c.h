@@ -35,6 +35,12 @@
  *                          matcher (dense, device-resident, batched)
  *   orbm_compute_stereo_matches  Frame::ComputeStereoMatches (mvuRight, mvDepth)
  *                          include/Frame.h:82, src/Frame.cc:465-639
+ *   orbv_load_text / orbv_create  ORBVocabulary::loadFromTextFile
+ *                          (DBoW2 TemplatedVocabulary, include/ORBVocabulary.h:30,
+ *                          Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1418)
+ *   orbv_transform         Frame::ComputeBoW  src/Frame.cc:394-401 ->
+ *                          TemplatedVocabulary::transform(features, BowVector,
+ *                          FeatureVector, levelsup)  TemplatedVocabulary.h:1127-1256
  *
  * Error behaviour: every call returns ORBX_OK or a negative code; the
  * message of the last failure on the calling thread is orbx_last_error().
@@ -255,6 +261,51 @@ int orbm_compute_stereo_matches_batch(
     const int* d_nL, const orbx_kp* d_kpR, const uint8_t* d_descR,
     const int* d_nR, int kp_pitch, int pairs, float mb, float mbf,
     float* d_uRight, float* d_depth, int* d_nkept, void* stream);
+
+/* ------------------------------------------------------ vocabulary (DBoW2) */
+typedef struct orbv_vocabulary* orbv_handle;
+
+const char* orbv_last_error(void);
+
+/* TemplatedVocabulary::loadFromTextFile: header "k L scoring weighting", then
+ * one line per node "parent isLeaf d0..d31 weight" (node ids in line order,
+ * the root is node 0). Lines without tokens are skipped. The tree is kept on
+ * `device`. */
+int orbv_load_text(const char* path, int device, orbv_handle* out);
+
+/* The same from arrays in file order (node 0 = root; parent[i] < i for i > 0;
+ * is_leaf marks words, numbered in node order; desc n_nodes x 32 bytes;
+ * weight per node). scoring: L1 0, L2 1, CHI_SQUARE 2, KL 3, BHATTACHARYYA 4,
+ * DOT_PRODUCT 5; weighting: TF_IDF 0, TF 1, IDF 2, BINARY 3. */
+int orbv_create(int k, int L, int scoring, int weighting, int n_nodes,
+                const int* parent, const uint8_t* is_leaf, const uint8_t* desc,
+                const double* weight, int device, orbv_handle* out);
+int orbv_destroy(orbv_handle v);
+int orbv_info(orbv_handle v, int* k, int* L, int* scoring, int* weighting,
+              int* n_nodes, int* n_words);
+
+/* transform(features, BowVector, FeatureVector, levelsup) on host buffers
+ * (synchronous), n <= 8192 descriptors of 32 bytes. BowVector: bow_n words
+ * ascending with their values (capacity n). FeatureVector as CSR: fv_n node
+ * ids ascending (file node ids), fv_off[fv_n + 1], fv_idx feature indices
+ * (capacity n each; fv_off capacity n + 1). word_ids / node_ids / weights:
+ * optional per-feature outputs (NULL to skip). */
+int orbv_transform(orbv_handle v, const uint8_t* desc, int n, int levelsup,
+                   uint32_t* bow_words, double* bow_values, int* bow_n,
+                   uint32_t* fv_nodes, int* fv_off, int* fv_idx, int* fv_n,
+                   uint32_t* word_ids, uint32_t* node_ids, double* weights);
+
+/* Batched device-resident variant: frame f's descriptors at d_desc +
+ * f*desc_pitch, d_n[f] of them (<= cap <= 8192). Outputs per frame at pitch
+ * cap (fv_off: cap + 1): d_bow_words/d_bow_values/d_bow_n,
+ * d_fv_nodes/d_fv_off/d_fv_idx/d_fv_n; per-feature d_word_ids/d_node_ids/
+ * d_weights (frames x cap) or all three NULL to use an internal workspace. */
+int orbv_transform_batch(orbv_handle v, const uint8_t* d_desc, size_t desc_pitch,
+                         const int* d_n, int frames, int cap, int levelsup,
+                         uint32_t* d_bow_words, double* d_bow_values, int* d_bow_n,
+                         uint32_t* d_fv_nodes, int* d_fv_off, int* d_fv_idx,
+                         int* d_fv_n, uint32_t* d_word_ids, uint32_t* d_node_ids,
+                         double* d_weights, void* stream);
 
 /* --------------------------------------------- device plumbing for hosts
  * Thin wrappers so a host without its own HIP binding (ctypes, cgo, JNI)

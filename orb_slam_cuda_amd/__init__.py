@@ -8,6 +8,8 @@ host-side mirror of the reference classes in Python.
 from ._lib import KP_DTYPE, OrbxError, device_count, header_functions, lib  # noqa: F401
 from .extractor import ORBextractor  # noqa: F401
 from .matcher import ComputeStereoMatches, Frame, KeyFrame, ORBmatcher  # noqa: F401
+from .vocabulary import ComputeBoW, ORBVocabulary  # noqa: F401
 
-__all__ = ["ORBextractor", "ORBmatcher", "Frame", "KeyFrame", "KP_DTYPE", "OrbxError",
+__all__ = ["ORBextractor", "ORBmatcher", "ORBVocabulary", "Frame", "KeyFrame", "ComputeBoW",
+           "ComputeStereoMatches", "KP_DTYPE", "OrbxError",
            "device_count", "header_functions", "lib"]

@@ -96,6 +96,14 @@ def lib() -> C.CDLL:
             C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orbv_last_error.restype = C.c_char_p
+        L.orbv_load_text.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
+        L.orbv_create.argtypes = [C.c_int] * 5 + [C.c_void_p] * 4 + [C.c_int, C.POINTER(C.c_void_p)]
+        L.orbv_destroy.argtypes = [C.c_void_p]
+        L.orbv_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 6
+        L.orbv_transform.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 10
+        L.orbv_transform_batch.argtypes = ([C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int, C.c_int,
+                                            C.c_int] + [C.c_void_p] * 11)
         L.orbx_device_count.argtypes = [C.POINTER(C.c_int)]
         L.orbx_set_device.argtypes = [C.c_int]
         L.orbx_malloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
@@ -118,10 +126,11 @@ def lib() -> C.CDLL:
     return _lib
 
 
-def check(rc: int, matcher: bool = False) -> None:
+def check(rc: int, matcher: bool = False, vocabulary: bool = False) -> None:
     if rc != ORBX_OK:
         L = lib()
-        msg = (L.orbm_last_error() if matcher else L.orbx_last_error()) or b""
+        msg = (L.orbv_last_error() if vocabulary else
+               L.orbm_last_error() if matcher else L.orbx_last_error()) or b""
         raise OrbxError(rc, msg.decode(errors="replace"))
 
 
@@ -129,7 +138,7 @@ def header_functions(path: str = HEADER) -> list[str]:
     """Names of every function declared in include/orbx_c.h."""
     src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b((?:orbx|orbm)_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b((?:orbx|orbm|orbv)_[a-z0-9_]+)\s*\(", src)))
 
 
 def ptr(a) -> C.c_void_p:

@@ -33,6 +33,7 @@ class Frame:
     mnMinY: float = 0.0
     mnMaxY: float = 0.0
     mFeatVec: dict | None = None           # DBoW2::FeatureVector {NodeId: [feature idx]}
+    mBowVec: dict | None = None            # DBoW2::BowVector {WordId: value}
     # stereo (Frame's stereo constructor, src/Frame.cc:43-101)
     mvKeysRight: np.ndarray | None = None  # KP_DTYPE
     mDescriptorsRight: np.ndarray | None = None
