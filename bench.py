@@ -42,7 +42,7 @@ sys.path.insert(0, ROOT)
 METRIC = "frames/s ORB extract+match, 1241×376 mono nFeatures=2000; achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_top2", "search_init"]
-KERNELS = {"pyramid": "pyr_resize_kernel (x7)", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
+KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
            "hamming_top2": "hamming_top2_kernel", "search_init": "search_init_kernel"}
 
@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--split", type=int, default=2, help="extraction launches (and streams) per batch")
     ap.add_argument("--priority", action="store_true",
                     help="high-priority extraction streams, low-priority matching stream")
+    ap.add_argument("--bow", action="store_true",
+                    help="also Frame::ComputeBoW every frame (synthetic ORBvoc-shaped vocabulary, k 10 L 6)")
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
                     help="stream that copies a batch's last frame for the next batch's first pair")
     args = ap.parse_args()
@@ -154,7 +156,17 @@ def main():
     s_match = _lib.Stream(0 if args.priority else None) if not args.serial else s_ext
     bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
     vp = lambda a: C.c_void_p(a)
-    n_ev = 9  # 6 extraction stage marks (extract stream) + 3 matching marks (match stream)
+    n_ev = 11  # 6 extraction stage marks (extract stream) + 3 matching marks + 2 BoW marks (match stream)
+    voc = None
+    if args.bow:
+        from orb_slam_cuda_amd.synth import synthetic_vocabulary
+        voc = pkg.ORBVocabulary.from_arrays(synthetic_vocabulary(10, 6, seed=1), device=local)
+        d_bw, d_bn, d_fn, d_fi, d_fnn = (_lib.DeviceArray(B * cap * 4), _lib.DeviceArray(B * 4),
+                                         _lib.DeviceArray(B * cap * 4), _lib.DeviceArray(B * cap * 4),
+                                         _lib.DeviceArray(B * 4))
+        d_bv = _lib.DeviceArray(B * cap * 8)
+        d_fo = _lib.DeviceArray(B * (cap + 1) * 4)
+        d_vw = (_lib.DeviceArray(B * cap * 4), _lib.DeviceArray(B * cap * 4), _lib.DeviceArray(B * cap * 8))
 
     def step(k, evs, ev_ext, ev_done):
         """Batch k: extraction on s_ext; carry copy and matching of the same
@@ -192,6 +204,14 @@ def main():
             s_match.wait(ev_ext[k])
         if args.carry == "match" and not args.serial:
             carry(s_match)  # in order after matching k-2, the last reader of set (k+1) % 3
+        if voc is not None:
+            evs[9].record(s_match)
+            # Frame::ComputeBoW of the batch's frames (slots 1..B), levelsup 4 (src/Frame.cc:398)
+            check(L.orbv_transform_batch(voc.handle, vp(d_desc[b].ptr + cap * DS), cap * DS, vp(d_counts[b].ptr + 4),
+                                         B, cap, 4, vp(d_bw.ptr), vp(d_bv.ptr), vp(d_bn.ptr), vp(d_fn.ptr),
+                                         vp(d_fo.ptr), vp(d_fi.ptr), vp(d_fnn.ptr), vp(d_vw[0].ptr), vp(d_vw[1].ptr),
+                                         vp(d_vw[2].ptr), s_match.s), vocabulary=True)
+            evs[10].record(s_match)
         evs[6].record(s_match)
         if not args.no_match:
             # query = frame t (slots 1..B), candidates = frame t-1 (slots 0..B-1)
@@ -233,13 +253,16 @@ def main():
     wall = sharding.max_over_ranks(t1 - t0, dist)
     timed = evsets[args.warmup:]
     ev_ms = timed[0][0].elapsed_ms(timed[-1][8])
+    STAGES_RUN = STAGES + (["bow_transform"] if args.bow else [])
 
     # per-stage average durations over the timed steps (ms per launch-group, B frames),
     # each bracketed by events on the stream its kernels run on
-    st = {s: 0.0 for s in STAGES}
+    st = {s: 0.0 for s in STAGES_RUN}
     for evs in timed:
         for i, s in enumerate(STAGES[:5]):
             st[s] += evs[i].elapsed_ms(evs[i + 1])
+        if args.bow:
+            st["bow_transform"] += evs[9].elapsed_ms(evs[10])
         if not args.no_match:
             st["hamming_top2"] += evs[6].elapsed_ms(evs[7])
             st["search_init"] += evs[7].elapsed_ms(evs[8])
@@ -251,7 +274,7 @@ def main():
     value = frames_total / wall
     ab = algorithmic_bytes(W, H, nkp_mean)
     extract_ms = sum(st[s] for s in STAGES[:5])
-    dominant = max(STAGES, key=lambda s: st[s])
+    dominant = max(STAGES_RUN, key=lambda s: st[s])
     # roofline of the pyramid+FAST pass and of the dominant kernel
     pf_ms = st["pyramid"] + st["fast_grid"]
     pf_gbs = ab["pyr_fast_pass"] * BS / (pf_ms * 1e-3) / 1e9
@@ -283,7 +306,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded shapes + noise sequence, orb_slam_cuda_amd/synth.py)",
-            "config": {"workload": cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only",
+            "config": {"workload": (cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only")
+                                   + (" + Frame::ComputeBoW (synthetic k10 L6 vocabulary)" if args.bow else ""),
                        "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
                        "frames_per_step_per_gpu": B, "parallelism": f"frame-sharded x{world}, no collectives",
                        "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS},

@@ -478,6 +478,8 @@ int orbv_transform_batch(orbv_handle v, const uint8_t* d_desc, size_t desc_pitch
     }
     VHIP(hipGetLastError());
   }
+  if (const char* e = getenv("ORBX_VOC_STOP"))  // diagnostics: 1 = descend only
+    if (atoi(e) == 1) return ORBX_OK;
   int S = 1;
   while (S < cap) S <<= 1;
   const size_t lds = (size_t)S * 12;
