@@ -47,6 +47,9 @@ def lib():
             C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_float,
             C.c_float, C.c_void_p, C.c_void_p]
+        _lib.orc_search_by_projection.argtypes = ([C.c_void_p] * 2 + [C.c_int, C.c_void_p] + [C.c_float] * 4
+                                                  + [C.c_void_p] * 4 + [C.c_int, C.c_float, C.c_float]
+                                                  + [C.c_void_p] * 2)
         _lib.orc_voc_load_text.argtypes = [C.c_char_p] + [C.c_void_p] * 5 + [C.c_int] + [C.c_void_p] * 4
         _lib.orc_voc_transform.argtypes = ([C.c_int] * 5 + [C.c_void_p] * 5 + [C.c_int, C.c_int]
                                            + [C.c_void_p] * 10)
@@ -242,3 +245,24 @@ def voc_transform(voc: dict, desc: np.ndarray, levelsup: int = 4) -> dict:
     b, f = nb.value, nf.value
     return dict(word=word, nid=nid, weight=w, bow_words=bw[:b].copy(), bow_values=bv[:b].copy(),
                 fv_nodes=fn[:f].copy(), fv_off=fo[:f + 1].copy(), fv_idx=fi[:fo[f]].copy())
+
+
+# ------------------------------------------------------------ SearchByProjection
+MP_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+                     ("predicted_level", "<i4"), ("track_in_view", "u1"), ("obs_positive", "u1"),
+                     ("pad", "u1", (2,))])
+
+
+def search_by_projection(kps, desc, uright, bounds, scale, blocked, mps, mpdesc, th=1.0, nnratio=0.8):
+    """ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th). Returns (out, nmatches):
+    out[idx] = index of the map point the keypoint got in this call, -1 if none."""
+    kps = np.ascontiguousarray(kps, KP_DTYPE); desc = np.ascontiguousarray(desc, np.uint8)
+    ur = None if uright is None else np.ascontiguousarray(uright, np.float32)
+    sc = np.ascontiguousarray(scale, np.float32); bl = np.ascontiguousarray(blocked, np.uint8)
+    mps = np.ascontiguousarray(mps, MP_DTYPE); mpd = np.ascontiguousarray(mpdesc, np.uint8)
+    out = np.zeros(max(len(kps), 1), np.int32)
+    nm = C.c_int(0)
+    lib().orc_search_by_projection(_p(kps), _p(desc), len(kps), None if ur is None else _p(ur),
+                                   *[C.c_float(b) for b in bounds], _p(sc), _p(bl), _p(mps), _p(mpd), len(mps),
+                                   C.c_float(th), C.c_float(nnratio), _p(out), C.byref(nm))
+    return out[:len(kps)].copy(), nm.value

@@ -717,6 +717,7 @@ Mat8 wrap_image(const uint8_t* img, int w, int h, size_t stride) {
 
 // ------------------------------------------------------------------ matcher
 const int TH_LOW = 50;
+const int TH_HIGH = 100;  // src/ORBmatcher.cc:37
 const int HISTO_LENGTH = 30;
 
 int descriptor_distance(const uint8_t* a, const uint8_t* b) {
@@ -1202,6 +1203,62 @@ int orc_search_by_bow(const uint8_t* descA, const float* angleA, const uint8_t* 
       }
     }
   }
+  *out_nmatches = nmatches;
+  return 0;
+}
+
+// ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
+// (src/ORBmatcher.cc:45-118) with RadiusByViewingCos (:120-126). The MapPoint
+// fields it reads are passed per point (orc_map_point_proj); the Frame's
+// mvpMapPoints[idx] "has a MapPoint with Observations() > 0" state is
+// `blocked`. out[idx] = index in vpMapPoints of the point the keypoint got in
+// this call (the last one to write it), -1 if none.
+int orc_search_by_projection(const orc_kp* kps, const uint8_t* desc, int n, const float* uright, float min_x,
+                             float max_x, float min_y, float max_y, const float* scale, const uint8_t* blocked,
+                             const orc_map_point_proj* mps, const uint8_t* mpdesc, int nmp, float th,
+                             float mfNNratio, int* out, int* out_nmatches) {
+  GridFrame F(kps, desc, n, min_x, max_x, min_y, max_y);
+  std::vector<int> mp_of(n, -1);          // this call's assignments
+  std::vector<uint8_t> blk(blocked, blocked + n);
+  int nmatches = 0;
+  const bool bFactor = th != 1.0;
+  for (int iMP = 0; iMP < nmp; iMP++) {
+    const orc_map_point_proj& pMP = mps[iMP];
+    if (!pMP.track_in_view) continue;     // mbTrackInView (isBad() folded in by the caller)
+    const int& nPredictedLevel = pMP.predicted_level;
+    float r = pMP.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos
+    if (bFactor) r *= th;
+    const std::vector<size_t> vIndices = F.features_in_area(pMP.proj_x, pMP.proj_y, r * scale[nPredictedLevel],
+                                                            nPredictedLevel - 1, nPredictedLevel);
+    if (vIndices.empty()) continue;
+    const uint8_t* MPdescriptor = mpdesc + (size_t)iMP * 32;
+    int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+    for (size_t idx : vIndices) {
+      if (blk[idx]) continue;  // F.mvpMapPoints[idx] && Observations() > 0
+      if (uright && uright[idx] > 0) {
+        const float er = fabs(pMP.proj_xr - uright[idx]);
+        if (er > r * scale[nPredictedLevel]) continue;
+      }
+      const int dist = descriptor_distance(MPdescriptor, desc + 32 * idx);
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestLevel2 = bestLevel;
+        bestLevel = kps[idx].octave;
+        bestIdx = (int)idx;
+      } else if (dist < bestDist2) {
+        bestLevel2 = kps[idx].octave;
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= TH_HIGH) {
+      if (bestLevel == bestLevel2 && bestDist > mfNNratio * bestDist2) continue;
+      mp_of[bestIdx] = iMP;                     // F.mvpMapPoints[bestIdx] = pMP
+      blk[bestIdx] = pMP.obs_positive ? 1 : 0;  // later points see its Observations()
+      nmatches++;
+    }
+  }
+  for (int i = 0; i < n; ++i) out[i] = mp_of[i];
   *out_nmatches = nmatches;
   return 0;
 }

@@ -124,6 +124,20 @@ int orc_voc_transform(int k, int L, int weighting, int scoring, int n_nodes, con
                       uint32_t* word_out, uint32_t* nid_out, double* w_out, uint32_t* bow_words,
                       double* bow_values, int* bow_n, uint32_t* fv_nodes, int* fv_off, int* fv_idx, int* fv_n);
 
+/* MapPoint fields read by ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th):
+ * mTrackProjX/Y/XR, mTrackViewCos, mnTrackScaleLevel, mbTrackInView && !isBad(),
+ * Observations() > 0. */
+typedef struct orc_map_point_proj {
+  float proj_x, proj_y, proj_xr, view_cos;
+  int32_t predicted_level;
+  uint8_t track_in_view, obs_positive, pad[2];
+} orc_map_point_proj;
+
+int orc_search_by_projection(const orc_kp* kps, const uint8_t* desc, int n, const float* uright, float min_x,
+                             float max_x, float min_y, float max_y, const float* scale, const uint8_t* blocked,
+                             const orc_map_point_proj* mps, const uint8_t* mpdesc, int nmp, float th,
+                             float mfNNratio, int* out, int* out_nmatches);
+
 #ifdef __cplusplus
 }
 #endif

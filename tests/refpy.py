@@ -499,3 +499,87 @@ def voc_transform(voc, desc, levelsup):
         if norm > 0.0:
             bow = {k: bow[k] / norm for k in keys}
     return words, nids, ws, bow, fv
+
+
+# -------------------------------------------------------------- SearchByProjection
+def features_in_area(kps, cells, bounds, x, y, r, minLevel, maxLevel):
+    """Frame::GetFeaturesInArea (src/Frame.cc:326-379) over a prebuilt 64 x 48 grid."""
+    minX, maxX, minY, maxY = (f32(b) for b in bounds)
+    invW = f32(f32(64) / f32(maxX - minX))
+    invH = f32(f32(48) / f32(maxY - minY))
+    x, y, r = f32(x), f32(y), f32(r)
+    cx0 = max(0, int(math.floor(f32(f32(f32(x - minX) - r) * invW))))
+    if cx0 >= 64:
+        return []
+    cx1 = min(63, int(math.ceil(f32(f32(f32(x - minX) + r) * invW))))
+    if cx1 < 0:
+        return []
+    cy0 = max(0, int(math.floor(f32(f32(f32(y - minY) - r) * invH))))
+    if cy0 >= 48:
+        return []
+    cy1 = min(47, int(math.ceil(f32(f32(f32(y - minY) + r) * invH))))
+    if cy1 < 0:
+        return []
+    check = minLevel > 0 or maxLevel >= 0
+    out = []
+    for ix in range(cx0, cx1 + 1):
+        for iy in range(cy0, cy1 + 1):
+            for j in cells.get((ix, iy), []):
+                o = int(kps["octave"][j])
+                if check and (o < minLevel or (maxLevel >= 0 and o > maxLevel)):
+                    continue
+                if abs(f32(f32(kps["x"][j]) - x)) < r and abs(f32(f32(kps["y"][j]) - y)) < r:
+                    out.append(j)
+    return out
+
+
+def grid_cells(kps, bounds):
+    """Frame::AssignFeaturesToGrid / PosInGrid (src/Frame.cc:228-243, 381-391)."""
+    minX, maxX, minY, maxY = (f32(b) for b in bounds)
+    invW = f32(f32(64) / f32(maxX - minX))
+    invH = f32(f32(48) / f32(maxY - minY))
+    cells = {}
+    for i in range(len(kps)):
+        px = _c_round(f32(f32(f32(kps["x"][i]) - minX) * invW))
+        py = _c_round(f32(f32(f32(kps["y"][i]) - minY) * invH))
+        if 0 <= px < 64 and 0 <= py < 48:
+            cells.setdefault((int(px), int(py)), []).append(i)
+    return cells
+
+
+def search_by_projection(kps, desc, uright, bounds, scale, blocked, mps, mpdesc, th, ratio):
+    """ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) (src/ORBmatcher.cc:45-118)."""
+    cells = grid_cells(kps, bounds)
+    blk = [bool(b) for b in blocked]
+    out = [-1] * len(kps)
+    nm = 0
+    th = f32(th)
+    for j in range(len(mps)):
+        mp = mps[j]
+        if not mp["track_in_view"]:
+            continue
+        lvl = int(mp["predicted_level"])
+        r = f32(2.5) if float(f32(mp["view_cos"])) > 0.998 else f32(4.0)
+        if float(th) != 1.0:
+            r = f32(r * th)
+        rad = f32(r * f32(scale[lvl]))
+        idxs = features_in_area(kps, cells, bounds, mp["proj_x"], mp["proj_y"], rad, lvl - 1, lvl)
+        best, bl, best2, bl2, bi = 256, -1, 256, -1, -1
+        for i in idxs:
+            if blk[i]:
+                continue
+            if uright is not None and uright[i] > 0:
+                if abs(f32(f32(mp["proj_xr"]) - f32(uright[i]))) > rad:
+                    continue
+            d = hamming(mpdesc[j], desc[i])
+            if d < best:
+                best2, best, bl2, bl, bi = best, d, bl, int(kps["octave"][i]), i
+            elif d < best2:
+                bl2, best2 = int(kps["octave"][i]), d
+        if best <= 100:
+            if bl == bl2 and f32(best) > f32(f32(ratio) * f32(best2)):
+                continue
+            out[bi] = j
+            blk[bi] = bool(mp["obs_positive"])
+            nm += 1
+    return np.array(out, np.int32), nm

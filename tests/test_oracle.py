@@ -354,3 +354,15 @@ def test_voc_text_roundtrip(O, tmp_path):
     for key in ("parent", "leaf", "weight"):
         assert np.array_equal(voc[key], v2[key])
     assert np.array_equal(voc["desc"][1:], v2["desc"][1:])  # the root has no descriptor in the file
+
+
+# ----------------------------------------------------------- SearchByProjection (§8f row 3)
+@pytest.mark.parametrize("seed,th,ratio,stereo", [(1, 1.0, 0.8, False), (2, 3.0, 0.9, True), (3, 1.5, 0.6, False)])
+def test_search_by_projection_matches_refpy(O, seed, th, ratio, stereo):
+    from projcase import projection_case
+    kps, desc, ur, bounds, scale, blocked, mps, mpd = projection_case(O, seed, 640, 240, 600, 900, stereo)
+    out, nm = O.search_by_projection(kps, desc, ur, bounds, scale, blocked, mps, mpd, th, ratio)
+    eout, enm = refpy.search_by_projection(kps, desc, ur, bounds, scale, blocked, mps, mpd, th, ratio)
+    assert nm == enm and np.array_equal(out, eout)
+    assert nm > 50
+    assert (out[blocked == 1] == -1).all()
