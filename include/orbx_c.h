@@ -35,6 +35,9 @@
  *                          matcher (dense, device-resident, batched)
  *   orbm_compute_stereo_matches  Frame::ComputeStereoMatches (mvuRight, mvDepth)
  *                          include/Frame.h:82, src/Frame.cc:465-639
+ *   orbm_search_by_projection  ORBmatcher::SearchByProjection(Frame&,
+ *                          const vector<MapPoint*>&, th)  include/ORBmatcher.h:48,
+ *                          src/ORBmatcher.cc:45-126 (Tracking::SearchLocalPoints)
  *   orbv_load_text / orbv_create  ORBVocabulary::loadFromTextFile
  *                          (DBoW2 TemplatedVocabulary, include/ORBVocabulary.h:30,
  *                          Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1418)
@@ -208,6 +211,43 @@ int orbm_search_for_initialization_batch(
     const int* d_n2, int kp_pitch, int pairs, orbm_grid_bounds bounds,
     float* d_prev_xy, int window, float nnratio, int check_ori,
     int* d_matches12, int* d_nmatches, void* stream);
+
+/* The MapPoint fields ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>,
+ * th) reads (filled by Frame::isInFrustum, src/Frame.cc:277-324):
+ * mTrackProjX/Y/XR, mTrackViewCos, mnTrackScaleLevel; track_in_view =
+ * mbTrackInView && !isBad(); obs_positive = Observations() > 0. 24 bytes. */
+typedef struct orbm_map_point_proj {
+  float proj_x, proj_y, proj_xr, view_cos;
+  int32_t predicted_level;
+  uint8_t track_in_view, obs_positive, pad[2];
+} orbm_map_point_proj;
+
+/* SearchByProjection(Frame&, vpMapPoints, th) on host buffers (synchronous).
+ * Frame: mvKeysUn (kps), mDescriptors, N; uright = mvuRight (NULL for a
+ * monocular frame); bounds = mnMinX/MaxX/MinY/MaxY; scale = mvScaleFactors
+ * (nlevels); blocked[idx] = mvpMapPoints[idx] && Observations() > 0 on entry.
+ * Map points in vpMapPoints order with their descriptors (GetDescriptor()).
+ * out[idx] = index into vpMapPoints of the point assigned to keypoint idx by
+ * this call (the shim stores vpMapPoints[out[idx]] into mvpMapPoints[idx]),
+ * -1 where the keypoint was not assigned. Up to 8192 map points. */
+int orbm_search_by_projection(orbm_handle m, const orbx_kp* kps, const uint8_t* desc,
+                              int n, const float* uright, orbm_grid_bounds bounds,
+                              const float* scale, int nlevels, const uint8_t* blocked,
+                              const orbm_map_point_proj* mps, const uint8_t* mpdesc,
+                              int nmp, float th, float nnratio, int* out,
+                              int* nmatches);
+
+/* Batched device-resident variant: frame f's keypoints at d_kps + f*kp_pitch
+ * (d_n[f] of them; descriptors, uright (or NULL), blocked and out likewise at
+ * kp_pitch), its map points at d_mps + f*mp_pitch (d_nmp[f]; descriptors
+ * likewise). All frames share the grid bounds and scale factors. */
+int orbm_search_by_projection_batch(
+    orbm_handle m, const orbx_kp* d_kps, const uint8_t* d_desc, const int* d_n,
+    int kp_pitch, const float* d_uright, orbm_grid_bounds bounds,
+    const float* scale, int nlevels, const uint8_t* d_blocked,
+    const orbm_map_point_proj* d_mps, const uint8_t* d_mpdesc, const int* d_nmp,
+    int mp_pitch, int frames, float th, float nnratio, int* d_out,
+    int* d_nmatches, void* stream);
 
 /* DBoW2::FeatureVector as CSR: nodes[k] ascending NodeIds; the feature
  * indices of node k are idx[off[k] .. off[k+1]). Each feature index appears

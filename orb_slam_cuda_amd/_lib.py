@@ -96,6 +96,12 @@ def lib() -> C.CDLL:
             C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orbm_search_by_projection.argtypes = ([C.c_void_p] * 3 + [C.c_int, C.c_void_p, GridBounds, C.c_void_p,
+                                                 C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float,
+                                                 C.c_float, C.c_void_p, C.POINTER(C.c_int)])
+        L.orbm_search_by_projection_batch.argtypes = ([C.c_void_p] * 4 + [C.c_int, C.c_void_p, GridBounds,
+                                                       C.c_void_p, C.c_int] + [C.c_void_p] * 4
+                                                      + [C.c_int, C.c_int, C.c_float, C.c_float] + [C.c_void_p] * 3)
         L.orbv_last_error.restype = C.c_char_p
         L.orbv_load_text.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
         L.orbv_create.argtypes = [C.c_int] * 5 + [C.c_void_p] * 4 + [C.c_int, C.POINTER(C.c_void_p)]
@@ -124,6 +130,12 @@ def lib() -> C.CDLL:
         L.orbx_sincosf_glibc.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
+
+
+# orbm_map_point_proj (include/orbx_c.h), 24 bytes
+MAP_POINT_PROJ_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+                                 ("predicted_level", "<i4"), ("track_in_view", "u1"), ("obs_positive", "u1"),
+                                 ("pad", "u1", (2,))])
 
 
 def check(rc: int, matcher: bool = False, vocabulary: bool = False) -> None:

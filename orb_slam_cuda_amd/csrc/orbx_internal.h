@@ -148,6 +148,19 @@ size_t stereo_lds_bytes(int nrows, int kp_pitch, int jobs_cap);
 int launch_stereo(const StereoParams& P, const orbx_kp* kpL, const uint8_t* descL, const int* nL,
                   const orbx_kp* kpR, const uint8_t* descR, const int* nR, int pairs, float* uRight,
                   float* depth, int* sad, int* nkept, void* stream);
+// orbx_project.hip — SearchByProjection(Frame&, vector<MapPoint*>, th), one frame per workgroup
+struct ProjParams {
+  float minX, maxX, minY, maxY, invW, invH;  // Frame grid bounds, FRAME_GRID_COLS/ROWS over their extent
+  float scale[kMaxLevels];                   // mvScaleFactors
+  float th, nnratio;
+  int kp_pitch, mp_pitch, has_uright;
+  int max_rounds;                            // fixed-point rounds before the sequential pass
+  long long* prof;                           // diagnostics: per-frame phase clocks, or null
+};
+size_t proj_lds_bytes(int kp_pitch);
+int launch_search_proj(const ProjParams& P, const orbx_kp* kps, const uint8_t* desc, const int* n,
+                       const float* uright, const uint8_t* blocked, const orbm_map_point_proj* mps,
+                       const uint8_t* mpdesc, const int* nmp, int frames, int* out, int* nmatches, void* stream);
 // orbx_host.hip: the pyramid of frames [frame0, frame0 + n) of an extractor's last extraction
 int extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int* w, int* hgt, float* scale,
                       float* inv_scale, int* L);

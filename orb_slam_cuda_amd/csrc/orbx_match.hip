@@ -1398,4 +1398,101 @@ int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle rig
   return ORBX_OK;
 }
 
+int orbm_search_by_projection_batch(orbm_handle m, const orbx_kp* d_kps, const uint8_t* d_desc, const int* d_n,
+                                    int kp_pitch, const float* d_uright, orbm_grid_bounds b, const float* scale,
+                                    int nlevels, const uint8_t* d_blocked, const orbm_map_point_proj* d_mps,
+                                    const uint8_t* d_mpdesc, const int* d_nmp, int mp_pitch, int frames, float th,
+                                    float nnratio, int* d_out, int* d_nmatches, void* stream) {
+  if (!m || !d_kps || !d_desc || !d_n || !scale || !d_blocked || !d_mps || !d_mpdesc || !d_nmp || !d_out ||
+      !d_nmatches || frames < 1 || kp_pitch < 1 || mp_pitch < 1 || nlevels < 1 || nlevels > kMaxLevels)
+    return mfail(ORBX_EINVAL, "bad argument");
+  if (mp_pitch > 8192) return mfail(ORBX_ECAPACITY, "more than 8192 map points per frame");
+  if (!(b.max_x > b.min_x) || !(b.max_y > b.min_y)) return mfail(ORBX_EINVAL, "empty grid bounds");
+  if (proj_lds_bytes(kp_pitch) > 156 * 1024) return mfail(ORBX_ECAPACITY, "kp_pitch %d too large", kp_pitch);
+  MHIP(hipSetDevice(m->device));
+  ProjParams P{};
+  P.minX = b.min_x;
+  P.maxX = b.max_x;
+  P.minY = b.min_y;
+  P.maxY = b.max_y;
+  // mfGridElementWidthInv = FRAME_GRID_COLS / (mnMaxX - mnMinX)  (src/Frame.cc:154-155)
+  P.invW = 64.0f / (b.max_x - b.min_x);
+  P.invH = 48.0f / (b.max_y - b.min_y);
+  for (int l = 0; l < kMaxLevels; ++l) P.scale[l] = scale[std::min(l, nlevels - 1)];
+  P.th = th;
+  P.nnratio = nnratio;
+  P.kp_pitch = kp_pitch;
+  P.mp_pitch = mp_pitch;
+  P.has_uright = d_uright != nullptr;
+  P.max_rounds = 32;
+  if (const char* e = getenv("ORBX_PROJ_ROUNDS")) P.max_rounds = atoi(e);  // tests: force the sequential pass
+  static long long* prof = nullptr;  // ORBX_PROJ_PROF: phase clocks of frame 0 printed after the call
+  const bool do_prof = getenv("ORBX_PROJ_PROF") != nullptr;
+  if (do_prof) {
+    if (!prof) MHIP(hipMalloc(&prof, (size_t)frames * 64 * 8));
+    MHIP(hipMemset(prof, 0, (size_t)frames * 64 * 8));
+    P.prof = prof;
+  }
+  if (launch_search_proj(P, d_kps, d_desc, d_n, d_uright, d_blocked, d_mps, d_mpdesc, d_nmp, frames, d_out,
+                         d_nmatches, stream))
+    return mfail(ORBX_EDEVICE, "search_proj launch: %s", hipGetErrorString(hipGetLastError()));
+  if (do_prof) {
+    long long h[64];
+    MHIP(hipStreamSynchronize((hipStream_t)stream));
+    MHIP(hipMemcpy(h, prof, sizeof h, hipMemcpyDeviceToHost));
+    fprintf(stderr, "proj prof frame 0:");
+    for (int i = 1; i < 42 && h[i]; ++i) fprintf(stderr, " r%d=%lld", i - 1, h[i] - h[0]);
+    fprintf(stderr, "\n");
+  }
+  return ORBX_OK;
+}
+
+int orbm_search_by_projection(orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n, const float* uright,
+                              orbm_grid_bounds b, const float* scale, int nlevels, const uint8_t* blocked,
+                              const orbm_map_point_proj* mps, const uint8_t* mpdesc, int nmp, float th,
+                              float nnratio, int* out, int* nmatches) {
+  if (!m || !nmatches || n < 0 || nmp < 0 || (n && (!kps || !desc || !blocked || !out)) ||
+      (nmp && (!mps || !mpdesc)))
+    return mfail(ORBX_EINVAL, "bad argument");
+  if (nmp > 8192) return mfail(ORBX_ECAPACITY, "more than 8192 map points");
+  MHIP(hipSetDevice(m->device));
+  const int kp = std::max(n, 1), mp = std::max(nmp, 1);
+  const size_t sz[] = {(size_t)kp * sizeof(orbx_kp), (size_t)kp * 32, (size_t)kp * 4, (size_t)kp,
+                       (size_t)mp * sizeof(orbm_map_point_proj), (size_t)mp * 32, (size_t)kp * 4, 16};
+  size_t off[8], tot = 0;
+  for (int i = 0; i < 8; ++i) {
+    off[i] = tot;
+    tot += (sz[i] + 255) & ~(size_t)255;
+  }
+  int rc;
+  if ((rc = stage_reserve(m, tot))) return rc;
+  uint8_t* s = (uint8_t*)m->stage;
+  if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+  hipStream_t st = m->stream;
+  int* cnt = (int*)(s + off[7]);  // n, nmp, nmatches
+  const int hn[2] = {n, nmp};
+  if (n) {
+    MHIP(hipMemcpyAsync(s + off[0], kps, (size_t)n * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(s + off[1], desc, (size_t)n * 32, hipMemcpyHostToDevice, st));
+    if (uright) MHIP(hipMemcpyAsync(s + off[2], uright, (size_t)n * 4, hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(s + off[3], blocked, (size_t)n, hipMemcpyHostToDevice, st));
+  }
+  if (nmp) {
+    MHIP(hipMemcpyAsync(s + off[4], mps, (size_t)nmp * sizeof(orbm_map_point_proj), hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(s + off[5], mpdesc, (size_t)nmp * 32, hipMemcpyHostToDevice, st));
+  }
+  MHIP(hipMemcpyAsync(cnt, hn, 8, hipMemcpyHostToDevice, st));
+  rc = orbm_search_by_projection_batch(m, (const orbx_kp*)(s + off[0]), s + off[1], cnt, kp,
+                                       uright ? (const float*)(s + off[2]) : nullptr, b, scale, nlevels, s + off[3],
+                                       (const orbm_map_point_proj*)(s + off[4]), s + off[5], cnt + 1, mp, 1, th,
+                                       nnratio, (int*)(s + off[6]), cnt + 2, st);
+  if (rc) return rc;
+  int nm = 0;
+  MHIP(hipMemcpyAsync(&nm, cnt + 2, 4, hipMemcpyDeviceToHost, st));
+  if (n) MHIP(hipMemcpyAsync(out, s + off[6], (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  MHIP(hipStreamSynchronize(st));
+  *nmatches = nm;
+  return ORBX_OK;
+}
+
 }  // extern "C"

@@ -20,7 +20,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import KP_DTYPE, FeatureVectorC, GridBounds, check, lib, ptr
+from ._lib import KP_DTYPE, MAP_POINT_PROJ_DTYPE, FeatureVectorC, GridBounds, check, lib, ptr
 
 
 @dataclass
@@ -41,6 +41,8 @@ class Frame:
     mbf: float = 0.0                       # baseline x fx
     mvuRight: np.ndarray | None = None     # (N,) float32, -1 = no stereo match
     mvDepth: np.ndarray | None = None
+    mvScaleFactors: np.ndarray | None = None  # (nlevels,) float32 (ORBextractor::GetScaleFactors)
+    mvpMapPoints: np.ndarray | None = None    # (N,) int: map point index, -1 = NULL
 
     @property
     def N(self) -> int:
@@ -160,6 +162,36 @@ class ORBmatcher:
         if vnMatches12 is not None:
             vnMatches12[:] = m12.tolist()
         self.last_matches12 = m12
+        return nm.value
+
+    def SearchByProjection(self, F: Frame, mps: np.ndarray, mp_desc: np.ndarray, th: float = 3.0,
+                           blocked: np.ndarray | None = None) -> int:
+        """SearchByProjection(Frame&, const vector<MapPoint*>&, th) (src/ORBmatcher.cc:45-118).
+        mps: MAP_POINT_PROJ_DTYPE per map point (Frame::isInFrustum's mTrackProj*, view cos,
+        predicted level, in-view and Observations() > 0 flags), mp_desc their descriptors.
+        blocked[idx]: keypoint idx already holds a map point with observations (default:
+        F.mvpMapPoints >= 0). Assigned keypoints get the map point's index in F.mvpMapPoints."""
+        kps = np.ascontiguousarray(F.mvKeysUn, KP_DTYPE)
+        d = np.ascontiguousarray(F.mDescriptors, np.uint8)
+        n = len(kps)
+        if F.mvpMapPoints is None:
+            F.mvpMapPoints = np.full(n, -1, np.int32)
+        if blocked is None:
+            blocked = F.mvpMapPoints >= 0
+        bl = np.ascontiguousarray(blocked, np.uint8)
+        ur = None if F.mvuRight is None else np.ascontiguousarray(F.mvuRight, np.float32)
+        sc = np.ascontiguousarray(F.mvScaleFactors, np.float32)
+        mp = np.ascontiguousarray(mps, MAP_POINT_PROJ_DTYPE)
+        md = np.ascontiguousarray(mp_desc, np.uint8)
+        out = np.full(max(n, 1), -1, np.int32)
+        nm = C.c_int(0)
+        b = GridBounds(F.mnMinX, F.mnMaxX, F.mnMinY, F.mnMaxY)
+        check(lib().orbm_search_by_projection(self._h, ptr(kps), ptr(d), n, ptr(ur), b, ptr(sc), len(sc), ptr(bl),
+                                              ptr(mp), ptr(md), len(mp), C.c_float(th), C.c_float(self.mfNNratio),
+                                              ptr(out), C.byref(nm)), matcher=True)
+        hit = out[:n] >= 0
+        F.mvpMapPoints[hit] = out[:n][hit]
+        self.last_projection = out[:n].copy()
         return nm.value
 
     def SearchByBoW(self, A: KeyFrame, B, out: list | None = None) -> int:

@@ -547,8 +547,9 @@ def grid_cells(kps, bounds):
     return cells
 
 
-def search_by_projection(kps, desc, uright, bounds, scale, blocked, mps, mpdesc, th, ratio):
-    """ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) (src/ORBmatcher.cc:45-118)."""
+def search_by_projection(kps, desc, uright, bounds, scale, blocked, mps, mpdesc, th, ratio, independent=False):
+    """ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) (src/ORBmatcher.cc:45-118).
+    independent=True drops the blocking by earlier points (a test of the test data only)."""
     cells = grid_cells(kps, bounds)
     blk = [bool(b) for b in blocked]
     out = [-1] * len(kps)
@@ -580,6 +581,7 @@ def search_by_projection(kps, desc, uright, bounds, scale, blocked, mps, mpdesc,
             if bl == bl2 and f32(best) > f32(f32(ratio) * f32(best2)):
                 continue
             out[bi] = j
-            blk[bi] = bool(mp["obs_positive"])
+            if not independent:
+                blk[bi] = bool(mp["obs_positive"])
             nm += 1
     return np.array(out, np.int32), nm

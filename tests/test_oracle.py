@@ -366,3 +366,13 @@ def test_search_by_projection_matches_refpy(O, seed, th, ratio, stereo):
     assert nm == enm and np.array_equal(out, eout)
     assert nm > 50
     assert (out[blocked == 1] == -1).all()
+
+
+def test_projection_cases_exercise_blocking(O):
+    """The synthetic cases contain points whose match depends on earlier points'
+    assignments (the order-dependent part the GPU resolves as a fixed point)."""
+    from projcase import projection_case
+    kps, desc, ur, bounds, scale, blocked, mps, mpd = projection_case(O, 2, 640, 240, 600, 900, True)
+    seq = refpy.search_by_projection(kps, desc, ur, bounds, scale, blocked, mps, mpd, 3.0, 0.9)
+    ind = refpy.search_by_projection(kps, desc, ur, bounds, scale, blocked, mps, mpd, 3.0, 0.9, independent=True)
+    assert seq[1] != ind[1] or not np.array_equal(seq[0], ind[0])
