@@ -33,6 +33,10 @@ constexpr int kObRadius = 19;                // |rotated pattern offset| <= 18.4
 constexpr int kObRows = 2 * kObRadius + 1;   // 39
 constexpr int kObStride = 64;                // 4 x 16-byte chunks per staged row
 
+// IC_Angle coefficient dwords per |v| (0..15): byte j of dword k is column
+// u = 4k + j - 15; {u if 0 < u <= umax[|v|]}, {-u if -umax <= u < 0}, {1 if |u| <= umax}
+__constant__ uint32_t c_ic_coef[16 * 24];
+
 // sum over the 32 lanes of each half-wave; the half's total is returned to all its lanes
 __device__ __forceinline__ int half_sum(int v) {
   v += dpp_i<kDppQuad1032>(0, v);
@@ -54,6 +58,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
                                                                   int* __restrict__ out_counts) {
   __shared__ __attribute__((aligned(16))) uint8_t s_patch[kObKps][kObRows * kObStride];
   __shared__ int s_tests[256];
+  __shared__ uint32_t s_ictab[16 * 24];
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
   const int bx = wg % gridDim.x, f = wg / gridDim.x, tid = threadIdx.x;
   const int lane = tid & 31, hk = tid >> 5;  // keypoint of this half-wave within the workgroup
@@ -65,6 +70,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
     out_counts[f] = tot;
   }
   s_tests[tid] = c_brief_tests[P.pattern_upstream ? 1 : 0][tid];
+  for (int i = tid; i < 16 * 24; i += kObThreads) s_ictab[i] = c_ic_coef[i];
 
   // ---- the keypoint of this half-wave
   int l = 0;
@@ -77,8 +83,13 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   // an empty slot works on a dummy keypoint at the level centre (never stored)
   const int x = valid ? key_x(key) + g.minBX : g.w / 2, y = valid ? key_y(key) + g.minBY : g.h / 2;
 
-  // ---- one burst of loads: blurred patch -> LDS, IC rows -> registers
+  // ---- one burst of loads: blurred patch -> LDS (16-byte chunks), IC rows ->
+  // registers (lane v - 15 = patch row: the row's 31 pixels as 9 dwords)
   const int c0 = (x - kObRadius) & ~15;
+  const int pitch = lp.pitch[l];
+  const uint8_t* lrow = lp.base[l] + f * lp.fstride[l] + (long long)(y - kHalfPatch) * pitch + (x - kHalfPatch);
+  uint32_t w[9] = {};
+  int sh = 0;
   if (valid) {
     const uint8_t* brow = blur + g.off + f * g.plane + (long long)(y - kObRadius) * g.pitch + c0;
     uint8_t* dst = s_patch[hk];
@@ -87,26 +98,42 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
       if (c0 + ch * 16 + 16 <= g.pitch)
         *(uint4*)(dst + r * kObStride + ch * 16) = *(const uint4*)(brow + (long long)r * g.pitch + ch * 16);
     }
-  }
-  const int pitch = lp.pitch[l];
-  const uint8_t* center = lp.base[l] + f * lp.fstride[l] + (long long)y * pitch + x;
-  int m10 = 0, m01 = 0;
-  // umax of the r = 15 circle (ORBextractor ctor :540-555; PATCH_SIZE is fixed)
-  constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
-  if (valid && lane < 31) {
-    // every (u, v) of the 31 x 31 square is inside the level for a valid
-    // keypoint, so the 31 row loads are issued unconditionally and the circle
-    // applied as a weight
-    const int u = lane - 15, au = u < 0 ? -u : u;
-    int I[31];
+    if (lane < kPatchSize) {
+      const uint8_t* rp = lrow + (long long)lane * pitch;
+      if (lp.aligned16[l]) {
+        // dword loads covering [x - 15, x + 16], at most byte x + 18 (< w: the
+        // keypoints keep EDGE_THRESHOLD = 19 from the border)
+        const uint32_t* q = (const uint32_t*)((uintptr_t)rp & ~(uintptr_t)3);
+        sh = (int)((uintptr_t)rp & 3);
 #pragma unroll
-    for (int v = -15; v <= 15; ++v) I[v + 15] = center[u + v * pitch];
+        for (int k = 0; k < 9; ++k) w[k] = q[k];
+      } else {
 #pragma unroll
-    for (int v = -15; v <= 15; ++v) {
-      const int w = au <= kUmax[v < 0 ? -v : v] ? I[v + 15] : 0;
-      m10 += u * w;
-      m01 += v * w;
+        for (int k = 0; k < 8; ++k)
+          w[k] = (uint32_t)rp[4 * k] | ((uint32_t)rp[4 * k + 1] << 8) | ((uint32_t)rp[4 * k + 2] << 16) |
+                 ((uint32_t)rp[4 * k + 3] << 24);
+      }
     }
+  }
+  __syncthreads();  // staged patch, test table, IC coefficient table
+
+  // ---- IC_Angle (:164-191): per row, the pixels weighted with v_dot4_u32_u8
+  // against coefficient dwords (u for u > 0 / -u for u < 0 / 1, inside the
+  // circle umax[|v|]); the 31 row sums are reduced over the half-wave
+  int m10 = 0, m01 = 0;
+  if (valid && lane < kPatchSize) {
+    const int v = lane - kHalfPatch, av = v < 0 ? -v : v;
+    const uint32_t* tp = s_ictab + av * 24;
+    uint32_t pos = 0, neg = 0, sum = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t d = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+      pos = __builtin_amdgcn_udot4(d, tp[k], pos, false);
+      neg = __builtin_amdgcn_udot4(d, tp[8 + k], neg, false);
+      sum = __builtin_amdgcn_udot4(d, tp[16 + k], sum, false);
+    }
+    m10 = (int)pos - (int)neg;
+    m01 = v * (int)sum;
   }
   m10 = half_sum(m10);
   m01 = half_sum(m01);
@@ -116,7 +143,6 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   const float factorPI = (float)(M_PI / 180.f);
   float a, b;
   glibc_sincosf(__fmul_rn(angle, factorPI), &b, &a);
-  __syncthreads();  // staged patches and test table
 
   // GET_VALUE(idx): center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)]
   const uint8_t* pc = s_patch[hk] + kObRadius * kObStride + (x - c0);
@@ -174,6 +200,19 @@ int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const Extra
         t[m][i] = (x0 & 0xFF) | ((y0 & 0xFF) << 8) | ((x1 & 0xFF) << 16) | ((y1 & 0xFF) << 24);
       }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_tests), t, sizeof(t)) != hipSuccess) return ORBX_EDEVICE;
+    // umax of the r = 15 circle (ORBextractor ctor :540-555; PATCH_SIZE is fixed at 31)
+    constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+    uint32_t coef[16 * 24] = {};
+    for (int av = 0; av < 16; ++av)
+      for (int b = 0; b < 32; ++b) {
+        const int u = b - kHalfPatch, au = u < 0 ? -u : u;
+        if (au > kUmax[av] || b >= kPatchSize) continue;
+        const int k = b >> 2, sh = 8 * (b & 3);
+        if (u > 0) coef[av * 24 + k] |= (uint32_t)u << sh;
+        if (u < 0) coef[av * 24 + 8 + k] |= (uint32_t)(-u) << sh;
+        coef[av * 24 + 16 + k] |= 1u << sh;
+      }
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_ic_coef), coef, sizeof(coef)) != hipSuccess) return ORBX_EDEVICE;
     g_pattern_uploaded = true;
   }
   dim3 grid((P.kp_per_frame + kObKps - 1) / kObKps, batch);
