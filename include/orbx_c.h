@@ -38,6 +38,19 @@
  *   orbm_search_by_projection  ORBmatcher::SearchByProjection(Frame&,
  *                          const vector<MapPoint*>&, th)  include/ORBmatcher.h:48,
  *                          src/ORBmatcher.cc:45-126 (Tracking::SearchLocalPoints)
+ *   orbm_search_by_projection_last_frame  ORBmatcher::SearchByProjection(
+ *                          Frame& CurrentFrame, const Frame& LastFrame, th,
+ *                          bMono)  include/ORBmatcher.h:52, src/ORBmatcher.cc:1328-1470
+ *                          (Tracking::TrackWithMotionModel)
+ *   orbm_search_by_projection_keyframe  ORBmatcher::SearchByProjection(
+ *                          Frame&, KeyFrame*, const set<MapPoint*>&, th,
+ *                          ORBdist)  include/ORBmatcher.h:56,
+ *                          src/ORBmatcher.cc:1472-1599 (Tracking::Relocalization)
+ *   orbm_search_by_projection_sim3  ORBmatcher::SearchByProjection(KeyFrame*,
+ *                          cv::Mat Scw, const vector<MapPoint*>&,
+ *                          vector<MapPoint*>&, th)  include/ORBmatcher.h:60,
+ *                          src/ORBmatcher.cc:290-403 (LoopClosing::ComputeSim3)
+ *   orbm_search_by_projection_pose_batch  the three above, batched on device
  *   orbv_load_text / orbv_create  ORBVocabulary::loadFromTextFile
  *                          (DBoW2 TemplatedVocabulary, include/ORBVocabulary.h:30,
  *                          Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1418)
@@ -247,6 +260,112 @@ int orbm_search_by_projection_batch(
     const float* scale, int nlevels, const uint8_t* d_blocked,
     const orbm_map_point_proj* d_mps, const uint8_t* d_mpdesc, const int* d_nmp,
     int mp_pitch, int frames, float th, float nnratio, int* d_out,
+    int* d_nmatches, void* stream);
+
+/* ---------------------------------------- pose-projection search overloads
+ * The SearchByProjection overloads that project MapPoint world positions
+ * with a pose inside the matcher. Frame/KeyFrame camera fields: fx, fy, cx,
+ * cy, mb, mbf and rows 0..2 of mTcw, row-major (the Sim3 overload passes
+ * Scw rows 0..2 here). */
+typedef struct orbm_camera {
+  float fx, fy, cx, cy, mb, mbf;
+  float Tcw[12];
+} orbm_camera;
+
+/* A MapPoint as these overloads read it: GetWorldPos(), GetNormal() (Sim3
+ * overload), mfMinDistance / mfMaxDistance (GetMin/MaxDistanceInvariance
+ * scale them by 0.8f / 1.2f; PredictScale reads mfMaxDistance), the angle
+ * and octave of the keypoint that holds the point in the source frame
+ * (LastFrame.mvKeysUn[i].angle / mvKeys[i].octave; pKF->mvKeysUn[i].angle),
+ * valid = the point is searched (LastFrame: pMP && !mvbOutlier[i]; KeyFrame:
+ * pMP && !isBad() && !sAlreadyFound.count(pMP); Sim3: !isBad() && not in
+ * vpMatched), obs_positive = Observations() > 0. 48 bytes. */
+typedef struct orbm_map_point_world {
+  float pos[3], normal[3];
+  float min_distance, max_distance, angle;
+  int32_t octave;
+  uint8_t valid, obs_positive, pad[6];
+} orbm_map_point_world;
+
+#define ORBM_PROJ_LAST_FRAME 1 /* src/ORBmatcher.cc:1328-1470 */
+#define ORBM_PROJ_KEYFRAME 2   /* src/ORBmatcher.cc:1472-1599 */
+#define ORBM_PROJ_SIM3 3       /* src/ORBmatcher.cc:290-403   */
+
+/* Per-frame projection prepared on the host from a camera (the scalar
+ * cv::Mat work each overload does once per call): Rt = the 3x4 transform
+ * applied to world points (Sim3: sRcw/scw | tcw/scw), Ow = -R^T t (camera
+ * centre), level_mode (last-frame overload: 0 = levels lo-1..lo+1,
+ * 1 = bForward: lo.., 2 = bBackward: 0..lo). 84 bytes. */
+typedef struct orbm_pose {
+  float Rt[12];
+  float Ow[3];
+  float fx, fy, cx, cy, mbf;
+  int32_t level_mode;
+} orbm_pose;
+
+/* Fill *out for `mode`. Tlw: LastFrame.mTcw rows 0..2 (ORBM_PROJ_LAST_FRAME
+ * only, else NULL); mono = bMono. Host only (no device call). */
+int orbm_prepare_pose(int mode, const orbm_camera* cam, const float* Tlw, int mono,
+                      orbm_pose* out);
+
+/* MapPoint::PredictScale(dist, Frame* or KeyFrame*) (src/MapPoint.cc:390-422)
+ * as the kernels evaluate it: the level is the number of thresholds
+ * thr[0..nlevels-2] the ratio mfMaxDistance/dist reaches, thr[k-1] = the
+ * least float ratio with ceil(logf(ratio)/logf(scale_factor)) >= k, found
+ * on the host with the host's logf. Host only. */
+int orbm_predict_scale_thresholds(float scale_factor, int nlevels, float* thr);
+int orbm_predict_scale(float max_distance, float dist, float scale_factor, int nlevels);
+
+/* SearchByProjection(CurrentFrame, LastFrame, th, bMono), host buffers,
+ * synchronous. Current frame as for orbm_search_by_projection (uright NULL
+ * for monocular); blocked[i2] = mvpMapPoints[i2] && Observations() > 0 on
+ * entry; cur = CurrentFrame camera and pose; Tlw = LastFrame.mTcw rows 0..2;
+ * one map point record + descriptor per LastFrame keypoint. out[i2] = index
+ * of the LastFrame keypoint whose point this call stored in
+ * CurrentFrame.mvpMapPoints[i2]; -1 = not touched; -2 = stored and then
+ * cleared (NULL) by the rotation consistency check. */
+int orbm_search_by_projection_last_frame(
+    orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n, const float* uright,
+    orbm_grid_bounds bounds, const float* scale, int nlevels, const uint8_t* blocked,
+    const orbm_camera* cur, const float* Tlw, const orbm_map_point_world* mps,
+    const uint8_t* mpdesc, int nmp, float th, int mono, int check_ori, int* out,
+    int* nmatches);
+
+/* SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist):
+ * has_mp[i2] = CurrentFrame.mvpMapPoints[i2] != NULL on entry; one record
+ * per pKF->GetMapPointMatches() entry; scale_factor = mfScaleFactor (for
+ * PredictScale). out as above. */
+int orbm_search_by_projection_keyframe(
+    orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n, orbm_grid_bounds bounds,
+    const float* scale, int nlevels, float scale_factor, const uint8_t* has_mp,
+    const orbm_camera* cur, const orbm_map_point_world* mps, const uint8_t* mpdesc, int nmp,
+    float th, int orb_dist, int check_ori, int* out, int* nmatches);
+
+/* SearchByProjection(pKF, Scw, vpPoints, vpMatched, th): pKF's keypoints,
+ * grid bounds, mvScaleFactors and mfScaleFactor; kf->Tcw = Scw rows 0..2;
+ * matched[idx] >= 0 where vpMatched[idx] is set on entry (NULL: none).
+ * out[idx] = index into vpPoints stored in vpMatched[idx] by this call, -1
+ * otherwise. */
+int orbm_search_by_projection_sim3(
+    orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n, orbm_grid_bounds bounds,
+    const float* scale, int nlevels, float scale_factor, const orbm_camera* kf,
+    const orbm_map_point_world* mps, const uint8_t* mpdesc, int nmp, int th,
+    const int* matched, int* out, int* nmatches);
+
+/* Batched device-resident variant of the three: frame f's keypoints at
+ * d_kps + f*kp_pitch (d_n[f]; descriptors, d_uright (LAST_FRAME, or NULL),
+ * d_blocked and d_out likewise), its points at d_mps + f*mp_pitch (d_nmp[f];
+ * descriptors likewise), d_poses[f] from orbm_prepare_pose. d_blocked: the
+ * blocking state on entry of the mode (LAST_FRAME: a point with
+ * observations; KEYFRAME: any point; SIM3: vpMatched set). dist_th: TH_HIGH
+ * (100) / ORBdist / TH_LOW (50); th: the window factor (Sim3: its int th).
+ * All frames share grid bounds, scale factors and scale_factor. */
+int orbm_search_by_projection_pose_batch(
+    orbm_handle m, int mode, const orbx_kp* d_kps, const uint8_t* d_desc, const int* d_n,
+    int kp_pitch, const float* d_uright, orbm_grid_bounds bounds, const float* scale,
+    int nlevels, float scale_factor, const uint8_t* d_blocked, const orbm_pose* d_poses,
+    const orbm_map_point_world* d_mps, const uint8_t* d_mpdesc, const int* d_nmp,
+    int mp_pitch, int frames, float th, int dist_th, int check_ori, int* d_out,
     int* d_nmatches, void* stream);
 
 /* DBoW2::FeatureVector as CSR: nodes[k] ascending NodeIds; the feature

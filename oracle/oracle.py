@@ -266,3 +266,83 @@ def search_by_projection(kps, desc, uright, bounds, scale, blocked, mps, mpdesc,
                                    *[C.c_float(b) for b in bounds], _p(sc), _p(bl), _p(mps), _p(mpd), len(mps),
                                    C.c_float(th), C.c_float(nnratio), _p(out), C.byref(nm))
     return out[:len(kps)].copy(), nm.value
+
+
+# ------------------------------------------------ SearchByProjection, pose overloads
+MPW_DTYPE = np.dtype([("pos", "<f4", (3,)), ("normal", "<f4", (3,)), ("min_distance", "<f4"),
+                      ("max_distance", "<f4"), ("angle", "<f4"), ("octave", "<i4"), ("valid", "u1"),
+                      ("obs_positive", "u1"), ("pad", "u1", (6,))])
+assert MPW_DTYPE.itemsize == 48
+
+
+class OrcCamera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("mb", C.c_float), ("mbf", C.c_float), ("Tcw", C.c_float * 12)]
+
+
+def camera(fx, fy, cx, cy, mb, mbf, Tcw) -> OrcCamera:
+    T = np.asarray(Tcw, np.float32).reshape(-1)[:12]
+    return OrcCamera(fx, fy, cx, cy, mb, mbf, (C.c_float * 12)(*T.tolist()))
+
+
+def predict_scale(max_distance, dist, scale_factor=1.2, nlevels=8):
+    lib().orc_predict_scale.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int]
+    return lib().orc_predict_scale(max_distance, dist, scale_factor, nlevels)
+
+
+def predict_scale_ratios(ratios, scale_factor=1.2, nlevels=8):
+    r = np.ascontiguousarray(ratios, np.float32)
+    out = np.zeros(len(r), np.int32)
+    f = lib().orc_predict_scale_ratios
+    f.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p]
+    f(_p(r), len(r), scale_factor, nlevels, _p(out))
+    return out
+
+
+def _pose_common(kps, desc, mps, mpdesc):
+    kps = np.ascontiguousarray(kps, KP_DTYPE); desc = np.ascontiguousarray(desc, np.uint8)
+    mps = np.ascontiguousarray(mps, MPW_DTYPE); mpd = np.ascontiguousarray(mpdesc, np.uint8)
+    return kps, desc, mps, mpd, np.zeros(max(len(kps), 1), np.int32), C.c_int(0)
+
+
+def search_by_projection_last_frame(kps, desc, uright, bounds, scale, blocked, cam, Tlw, mps, mpdesc, th,
+                                    mono, check_ori=True):
+    """SearchByProjection(CurrentFrame, LastFrame, th, bMono). Returns (out, nmatches): out[i2] =
+    last-frame index whose point the keypoint got, -1 untouched, -2 cleared by the rotation check."""
+    kps, desc, mps, mpd, out, nm = _pose_common(kps, desc, mps, mpdesc)
+    ur = None if uright is None else np.ascontiguousarray(uright, np.float32)
+    sc = np.ascontiguousarray(scale, np.float32); bl = np.ascontiguousarray(blocked, np.uint8)
+    T = np.ascontiguousarray(Tlw, np.float32).reshape(-1)
+    f = lib().orc_search_by_projection_last_frame
+    f.argtypes = ([C.c_void_p] * 2 + [C.c_int, C.c_void_p] + [C.c_float] * 4 + [C.c_void_p] * 6
+                  + [C.c_int, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p])
+    f(_p(kps), _p(desc), len(kps), None if ur is None else _p(ur), *[C.c_float(b) for b in bounds], _p(sc),
+      _p(bl), C.byref(cam), _p(T), _p(mps), _p(mpd), len(mps), th, int(mono), int(check_ori), _p(out),
+      C.byref(nm))
+    return out[:len(kps)].copy(), nm.value
+
+
+def search_by_projection_keyframe(kps, desc, bounds, scale, scale_factor, has_mp, cam, mps, mpdesc, th, orb_dist,
+                                  check_ori=True):
+    """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (relocalization)."""
+    kps, desc, mps, mpd, out, nm = _pose_common(kps, desc, mps, mpdesc)
+    sc = np.ascontiguousarray(scale, np.float32); hm = np.ascontiguousarray(has_mp, np.uint8)
+    f = lib().orc_search_by_projection_keyframe
+    f.argtypes = ([C.c_void_p] * 2 + [C.c_int] + [C.c_float] * 4 + [C.c_void_p, C.c_int, C.c_float]
+                  + [C.c_void_p] * 4 + [C.c_int, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p])
+    f(_p(kps), _p(desc), len(kps), *[C.c_float(b) for b in bounds], _p(sc), len(sc), scale_factor, _p(hm),
+      C.byref(cam), _p(mps), _p(mpd), len(mps), th, int(orb_dist), int(check_ori), _p(out), C.byref(nm))
+    return out[:len(kps)].copy(), nm.value
+
+
+def search_by_projection_sim3(kps, desc, bounds, scale, scale_factor, cam, mps, mpdesc, th, matched=None):
+    """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (loop closing); cam.Tcw = Scw."""
+    kps, desc, mps, mpd, out, nm = _pose_common(kps, desc, mps, mpdesc)
+    sc = np.ascontiguousarray(scale, np.float32)
+    mt = None if matched is None else np.ascontiguousarray(matched, np.int32)
+    f = lib().orc_search_by_projection_sim3
+    f.argtypes = ([C.c_void_p] * 2 + [C.c_int] + [C.c_float] * 4 + [C.c_void_p, C.c_int, C.c_float]
+                  + [C.c_void_p] * 3 + [C.c_int, C.c_int] + [C.c_void_p] * 3)
+    f(_p(kps), _p(desc), len(kps), *[C.c_float(b) for b in bounds], _p(sc), len(sc), scale_factor,
+      C.byref(cam), _p(mps), _p(mpd), len(mps), int(th), None if mt is None else _p(mt), _p(out), C.byref(nm))
+    return out[:len(kps)].copy(), nm.value

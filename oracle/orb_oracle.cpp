@@ -1263,4 +1263,304 @@ int orc_search_by_projection(const orc_kp* kps, const uint8_t* desc, int n, cons
   return 0;
 }
 
+// ======================================================= pose projection
+// The SearchByProjection overloads that project world points with a pose
+// (src/ORBmatcher.cc:290-403, 1328-1470, 1472-1599) and the cv::Mat
+// arithmetic they run, restated from OpenCV 3.x (Appendix-A style, not
+// vendored, PARITY UNPINNED at this boundary):
+//  * R*x + t (MatExpr -> gemm(R, x, 1, t, 1), 3x3 times 3x1 float): gemm's
+//    small-matrix path: t_r = a0*x0 + a1*x1 + a2*x2 summed in float, then
+//    d_r = (float)(t_r*1.0 + c_r*1.0) in double (alpha = beta = 1.0).
+//  * -R.t()*t (gemm with GEMM_1_T, alpha -1): the general path,
+//    GEMMSingleMul<float,double>: double products summed in order, (float)(-s).
+//  * cv::norm(v) (NORM_L2 of 3 floats): std::sqrt of the double sum of the
+//    squares; Mat::dot of 3 floats: the double sum of double products.
+//  * Mat / s: convertTo(alpha = 1/s): v * (float)(1.0/s) + 0.0f in float.
+//  * log(float) in MapPoint::PredictScale and Frame's mfLogScaleFactor: the
+//    float overload (glibc logf).
+}  // extern "C"
+
+namespace {
+
+struct PoseMath {
+  // R*x + t through gemm's small-matrix path
+  static void rx_plus_t(const float* T, const float* x, float* d) {
+    for (int r = 0; r < 3; ++r) {
+      const float t = T[4 * r] * x[0] + T[4 * r + 1] * x[1] + T[4 * r + 2] * x[2];
+      d[r] = (float)((double)t * 1.0 + (double)T[4 * r + 3] * 1.0);
+    }
+  }
+  // -R.t()*t through the general gemm path
+  static void neg_rt_t(const float* T, float* d) {
+    for (int r = 0; r < 3; ++r) {
+      double s = 0;
+      for (int k = 0; k < 3; ++k) s += (double)T[4 * k + r] * (double)T[4 * k + 3];
+      d[r] = (float)(s * -1.0);
+    }
+  }
+  static double norm3(const float* v) {
+    double s = 0;
+    for (int k = 0; k < 3; ++k) { double e = v[k]; s += e * e; }
+    return std::sqrt(s);
+  }
+  static double dot3(const float* a, const float* b) {
+    double s = 0;
+    for (int k = 0; k < 3; ++k) s += (double)a[k] * b[k];
+    return s;
+  }
+};
+
+// MapPoint::PredictScale (src/MapPoint.cc:407-422). ceil(log(ratio)/mfLogScaleFactor)
+// converted to int; a non-finite quotient converts like x86 cvttss2si (INT_MIN).
+int predict_scale(float mfMaxDistance, float currentDist, float mfLogScaleFactor, int mnScaleLevels) {
+  const float ratio = mfMaxDistance / currentDist;
+  const float q = std::ceil(std::log(ratio) / mfLogScaleFactor);
+  int nScale = (q >= -2147483648.0f && q < 2147483648.0f) ? (int)q : INT_MIN;
+  if (nScale < 0)
+    nScale = 0;
+  else if (nScale >= mnScaleLevels)
+    nScale = mnScaleLevels - 1;
+  return nScale;
+}
+
+// Rotation consistency of the motion-model / relocalization overloads
+// (src/ORBmatcher.cc:1423-1466, 1577-1596): assignments in bins outside the three
+// largest are cleared (mvpMapPoints[i2] = NULL, recorded as -2).
+void rotation_filter(std::vector<int>* rotHist, int* out, int& nmatches) {
+  int ind1 = -1, ind2 = -1, ind3 = -1;
+  compute_three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+  for (int i = 0; i < HISTO_LENGTH; i++) {
+    if (i != ind1 && i != ind2 && i != ind3) {
+      for (size_t j = 0, jend = rotHist[i].size(); j < jend; j++) {
+        out[rotHist[i][j]] = -2;
+        nmatches--;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int orc_predict_scale(float max_distance, float current_dist, float scale_factor, int nlevels) {
+  return predict_scale(max_distance, current_dist, std::log(scale_factor), nlevels);
+}
+
+void orc_predict_scale_ratios(const float* ratio, int n, float scale_factor, int nlevels, int* out) {
+  const float logsf = std::log(scale_factor);
+  // predict_scale(maxd, dist) with maxd / dist == ratio: maxd = ratio, dist = 1
+  for (int i = 0; i < n; ++i) out[i] = predict_scale(ratio[i], 1.0f, logsf, nlevels);
+}
+
+// SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+// (src/ORBmatcher.cc:1328-1470).
+int orc_search_by_projection_last_frame(const orc_kp* kps, const uint8_t* desc, int n, const float* uright,
+                                        float min_x, float max_x, float min_y, float max_y, const float* scale,
+                                        const uint8_t* blocked, const orc_camera* cur, const float* Tlw,
+                                        const orc_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th,
+                                        int bMono, int mbCheckOrientation, int* out, int* out_nmatches) {
+  GridFrame F(kps, desc, n, min_x, max_x, min_y, max_y);
+  std::vector<uint8_t> blk(blocked, blocked + n);  // mvpMapPoints[i2] && Observations() > 0
+  for (int i = 0; i < n; ++i) out[i] = -1;
+  int nmatches = 0;
+  std::vector<int> rotHist[HISTO_LENGTH];
+  const float factor = 1.0f / HISTO_LENGTH;
+  // twc = -Rcw.t()*tcw; tlc = Rlw*twc + tlw  (:1338-1346)
+  float twc[3], tlc[3];
+  PoseMath::neg_rt_t(cur->Tcw, twc);
+  PoseMath::rx_plus_t(Tlw, twc, tlc);
+  const bool bForward = tlc[2] > cur->mb && !bMono;
+  const bool bBackward = -tlc[2] > cur->mb && !bMono;
+  for (int i = 0; i < nmp; i++) {
+    const orc_map_point_world& pMP = mps[i];
+    if (!pMP.valid) continue;  // pMP && !LastFrame.mvbOutlier[i]
+    float x3Dc[3];
+    PoseMath::rx_plus_t(cur->Tcw, pMP.pos, x3Dc);
+    const float xc = x3Dc[0];
+    const float yc = x3Dc[1];
+    const float invzc = 1.0 / x3Dc[2];
+    if (invzc < 0) continue;
+    float u = cur->fx * xc * invzc + cur->cx;
+    float v = cur->fy * yc * invzc + cur->cy;
+    if (u < min_x || u > max_x) continue;
+    if (v < min_y || v > max_y) continue;
+    const int nLastOctave = pMP.octave;
+    const float radius = th * scale[nLastOctave];
+    std::vector<size_t> vIndices2;
+    if (bForward)
+      vIndices2 = F.features_in_area(u, v, radius, nLastOctave, -1);
+    else if (bBackward)
+      vIndices2 = F.features_in_area(u, v, radius, 0, nLastOctave);
+    else
+      vIndices2 = F.features_in_area(u, v, radius, nLastOctave - 1, nLastOctave + 1);
+    if (vIndices2.empty()) continue;
+    const uint8_t* dMP = mpdesc + 32 * (size_t)i;
+    int bestDist = 256, bestIdx2 = -1;
+    for (size_t i2 : vIndices2) {
+      if (blk[i2]) continue;
+      if (uright && uright[i2] > 0) {
+        const float ur = u - cur->mbf * invzc;
+        const float er = fabs(ur - uright[i2]);
+        if (er > radius) continue;
+      }
+      const int dist = descriptor_distance(dMP, desc + 32 * i2);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx2 = (int)i2;
+      }
+    }
+    if (bestDist <= TH_HIGH) {
+      out[bestIdx2] = i;  // CurrentFrame.mvpMapPoints[bestIdx2] = pMP
+      blk[bestIdx2] = pMP.obs_positive;
+      nmatches++;
+      if (mbCheckOrientation) {
+        float rot = pMP.angle - kps[bestIdx2].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = round(rot * factor);
+        if (bin == HISTO_LENGTH) bin = 0;
+        rotHist[bin].push_back(bestIdx2);
+      }
+    }
+  }
+  if (mbCheckOrientation) rotation_filter(rotHist, out, nmatches);
+  *out_nmatches = nmatches;
+  return 0;
+}
+
+// SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, sAlreadyFound, th, ORBdist)
+// (src/ORBmatcher.cc:1472-1599).
+int orc_search_by_projection_keyframe(const orc_kp* kps, const uint8_t* desc, int n, float min_x, float max_x,
+                                      float min_y, float max_y, const float* scale, int nlevels,
+                                      float scale_factor, const uint8_t* has_mp, const orc_camera* cur,
+                                      const orc_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th,
+                                      int ORBdist, int mbCheckOrientation, int* out, int* out_nmatches) {
+  GridFrame F(kps, desc, n, min_x, max_x, min_y, max_y);
+  std::vector<uint8_t> taken(has_mp, has_mp + n);  // CurrentFrame.mvpMapPoints[i2] != NULL
+  for (int i = 0; i < n; ++i) out[i] = -1;
+  const float mfLogScaleFactor = std::log(scale_factor);
+  float Ow[3];
+  PoseMath::neg_rt_t(cur->Tcw, Ow);
+  int nmatches = 0;
+  std::vector<int> rotHist[HISTO_LENGTH];
+  const float factor = 1.0f / HISTO_LENGTH;
+  for (int i = 0; i < nmp; i++) {
+    const orc_map_point_world& pMP = mps[i];
+    if (!pMP.valid) continue;  // pMP && !isBad() && !sAlreadyFound.count(pMP)
+    float x3Dc[3];
+    PoseMath::rx_plus_t(cur->Tcw, pMP.pos, x3Dc);
+    const float xc = x3Dc[0];
+    const float yc = x3Dc[1];
+    const float invzc = 1.0 / x3Dc[2];
+    const float u = cur->fx * xc * invzc + cur->cx;
+    const float v = cur->fy * yc * invzc + cur->cy;
+    if (u < min_x || u > max_x) continue;
+    if (v < min_y || v > max_y) continue;
+    float PO[3];
+    for (int k = 0; k < 3; ++k) PO[k] = pMP.pos[k] - Ow[k];
+    const float dist3D = PoseMath::norm3(PO);
+    const float maxDistance = 1.2f * pMP.max_distance;  // GetMaxDistanceInvariance
+    const float minDistance = 0.8f * pMP.min_distance;  // GetMinDistanceInvariance
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    const int nPredictedLevel = predict_scale(pMP.max_distance, dist3D, mfLogScaleFactor, nlevels);
+    const float radius = th * scale[nPredictedLevel];
+    const std::vector<size_t> vIndices2 =
+        F.features_in_area(u, v, radius, nPredictedLevel - 1, nPredictedLevel + 1);
+    if (vIndices2.empty()) continue;
+    const uint8_t* dMP = mpdesc + 32 * (size_t)i;
+    int bestDist = 256, bestIdx2 = -1;
+    for (size_t i2 : vIndices2) {
+      if (taken[i2]) continue;
+      const int dist = descriptor_distance(dMP, desc + 32 * i2);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx2 = (int)i2;
+      }
+    }
+    if (bestDist <= ORBdist) {
+      out[bestIdx2] = i;
+      taken[bestIdx2] = 1;
+      nmatches++;
+      if (mbCheckOrientation) {
+        float rot = pMP.angle - kps[bestIdx2].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = round(rot * factor);
+        if (bin == HISTO_LENGTH) bin = 0;
+        rotHist[bin].push_back(bestIdx2);
+      }
+    }
+  }
+  if (mbCheckOrientation) rotation_filter(rotHist, out, nmatches);
+  *out_nmatches = nmatches;
+  return 0;
+}
+
+// SearchByProjection(KeyFrame* pKF, cv::Mat Scw, vpPoints, vpMatched, th)
+// (src/ORBmatcher.cc:290-403) with KeyFrame::IsInImage (src/KeyFrame.cc:619-622)
+// and KeyFrame::GetFeaturesInArea (:578-617, no level filter).
+int orc_search_by_projection_sim3(const orc_kp* kps, const uint8_t* desc, int n, float min_x, float max_x,
+                                  float min_y, float max_y, const float* scale, int nlevels, float scale_factor,
+                                  const orc_camera* kf, const orc_map_point_world* mps, const uint8_t* mpdesc,
+                                  int nmp, int th, const int* matched, int* out, int* out_nmatches) {
+  GridFrame F(kps, desc, n, min_x, max_x, min_y, max_y);
+  std::vector<uint8_t> taken(n);
+  for (int i = 0; i < n; ++i) {
+    taken[i] = matched && matched[i] >= 0;  // vpMatched[idx]
+    out[i] = -1;
+  }
+  const float mfLogScaleFactor = std::log(scale_factor);
+  // Decompose Scw (:298-304)
+  const float* S = kf->Tcw;
+  const float scw = std::sqrt(PoseMath::dot3(S, S));  // sRcw.row(0).dot(sRcw.row(0))
+  const float a = (float)(1.0 / (double)scw);         // (Mat / scw): convertTo alpha
+  float T[12];
+  for (int k = 0; k < 12; ++k) T[k] = S[k] * a + 0.0f;  // Rcw = sRcw/scw, tcw = t/scw
+  float Ow[3];
+  PoseMath::neg_rt_t(T, Ow);
+  int nmatches = 0;
+  for (int iMP = 0; iMP < nmp; iMP++) {
+    const orc_map_point_world& pMP = mps[iMP];
+    if (!pMP.valid) continue;  // pMP->isBad() || spAlreadyFound.count(pMP)
+    float p3Dc[3];
+    PoseMath::rx_plus_t(T, pMP.pos, p3Dc);
+    if (p3Dc[2] < 0.0) continue;
+    const float invz = 1 / p3Dc[2];
+    const float x = p3Dc[0] * invz;
+    const float y = p3Dc[1] * invz;
+    const float u = kf->fx * x + kf->cx;
+    const float v = kf->fy * y + kf->cy;
+    if (!(u >= min_x && u < max_x && v >= min_y && v < max_y)) continue;  // pKF->IsInImage
+    const float maxDistance = 1.2f * pMP.max_distance;
+    const float minDistance = 0.8f * pMP.min_distance;
+    float PO[3];
+    for (int k = 0; k < 3; ++k) PO[k] = pMP.pos[k] - Ow[k];
+    const float dist = PoseMath::norm3(PO);
+    if (dist < minDistance || dist > maxDistance) continue;
+    if (PoseMath::dot3(PO, pMP.normal) < 0.5 * dist) continue;  // viewing angle < 60 deg
+    const int nPredictedLevel = predict_scale(pMP.max_distance, dist, mfLogScaleFactor, nlevels);
+    const float radius = th * scale[nPredictedLevel];
+    const std::vector<size_t> vIndices = F.features_in_area(u, v, radius, -1, -1);
+    if (vIndices.empty()) continue;
+    const uint8_t* dMP = mpdesc + 32 * (size_t)iMP;
+    int bestDist = 256, bestIdx = -1;
+    for (size_t idx : vIndices) {
+      if (taken[idx]) continue;
+      const int& kpLevel = kps[idx].octave;
+      if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+      const int dist = descriptor_distance(dMP, desc + 32 * idx);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = (int)idx;
+      }
+    }
+    if (bestDist <= TH_LOW) {
+      out[bestIdx] = iMP;  // vpMatched[bestIdx] = pMP
+      taken[bestIdx] = 1;
+      nmatches++;
+    }
+  }
+  *out_nmatches = nmatches;
+  return 0;
+}
+
 }  // extern "C"

@@ -138,6 +138,64 @@ int orc_search_by_projection(const orc_kp* kps, const uint8_t* desc, int n, cons
                              const orc_map_point_proj* mps, const uint8_t* mpdesc, int nmp, float th,
                              float mfNNratio, int* out, int* out_nmatches);
 
+/* The overloads that project world points with a pose (src/ORBmatcher.cc:290-403,
+ * 1328-1470, 1472-1599). Camera = Frame / KeyFrame fx, fy, cx, cy, mb, mbf and
+ * rows 0..2 of mTcw (row-major 3x4; Scw for the Sim3 overload). */
+typedef struct orc_camera {
+  float fx, fy, cx, cy, mb, mbf;
+  float Tcw[12];
+} orc_camera;
+
+/* A MapPoint as the pose overloads read it: GetWorldPos(), GetNormal(),
+ * mfMinDistance / mfMaxDistance (the *DistanceInvariance getters scale them by
+ * 0.8f / 1.2f), the angle and octave of the keypoint that holds it in the
+ * source frame (LastFrame.mvKeysUn[i] / pKF->mvKeysUn[i]), valid = the point
+ * is searched (LastFrame: pMP && !mvbOutlier[i]; KF: pMP && !isBad() && not
+ * in sAlreadyFound; Sim3: !isBad() && not already found), obs_positive =
+ * Observations() > 0. 48 bytes. */
+typedef struct orc_map_point_world {
+  float pos[3], normal[3];
+  float min_distance, max_distance, angle;
+  int32_t octave;
+  uint8_t valid, obs_positive, pad[6];
+} orc_map_point_world;
+
+/* MapPoint::PredictScale(dist, Frame/KeyFrame*) (src/MapPoint.cc:390-422). */
+int orc_predict_scale(float max_distance, float current_dist, float scale_factor, int nlevels);
+/* The same on ratios = mfMaxDistance/currentDist directly (n of them). */
+void orc_predict_scale_ratios(const float* ratio, int n, float scale_factor, int nlevels, int* out);
+
+/* SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+ * (src/ORBmatcher.cc:1328-1470). Current frame: kps (mvKeysUn), desc, uright
+ * (mvuRight or NULL), grid bounds, scale = mvScaleFactors, blocked[i2] =
+ * mvpMapPoints[i2] && Observations() > 0 on entry. One map point record per
+ * LastFrame keypoint (valid = pMP && !mvbOutlier). out[i2] = index of the
+ * last-frame keypoint whose point this call stored in mvpMapPoints[i2], -1 =
+ * untouched, -2 = stored and then cleared by the rotation check (NULL). */
+int orc_search_by_projection_last_frame(const orc_kp* kps, const uint8_t* desc, int n, const float* uright,
+                                        float min_x, float max_x, float min_y, float max_y, const float* scale,
+                                        const uint8_t* blocked, const orc_camera* cur, const float* Tlw,
+                                        const orc_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th,
+                                        int bMono, int mbCheckOrientation, int* out, int* out_nmatches);
+
+/* SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, sAlreadyFound, th,
+ * ORBdist) (src/ORBmatcher.cc:1472-1599). has_mp[i2] = mvpMapPoints[i2] on
+ * entry; one record per pKF->GetMapPointMatches() entry. out as above. */
+int orc_search_by_projection_keyframe(const orc_kp* kps, const uint8_t* desc, int n, float min_x, float max_x,
+                                      float min_y, float max_y, const float* scale, int nlevels,
+                                      float scale_factor, const uint8_t* has_mp, const orc_camera* cur,
+                                      const orc_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th,
+                                      int ORBdist, int mbCheckOrientation, int* out, int* out_nmatches);
+
+/* SearchByProjection(KeyFrame* pKF, Scw, vpPoints, vpMatched, th)
+ * (src/ORBmatcher.cc:290-403). pKF's keypoints / grid; cam->Tcw = Scw rows
+ * 0..2; matched[idx] >= 0 where vpMatched[idx] is set on entry. out[idx] =
+ * index into vpPoints of the point stored by this call, -1 otherwise. */
+int orc_search_by_projection_sim3(const orc_kp* kps, const uint8_t* desc, int n, float min_x, float max_x,
+                                  float min_y, float max_y, const float* scale, int nlevels, float scale_factor,
+                                  const orc_camera* kf, const orc_map_point_world* mps, const uint8_t* mpdesc,
+                                  int nmp, int th, const int* matched, int* out, int* out_nmatches);
+
 #ifdef __cplusplus
 }
 #endif

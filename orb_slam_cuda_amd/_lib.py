@@ -34,6 +34,26 @@ class GridBounds(C.Structure):
     _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float)]
 
 
+class OrbmCamera(C.Structure):
+    """orbm_camera: fx, fy, cx, cy, mb, mbf and mTcw rows 0..2 (row-major)."""
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("mb", C.c_float), ("mbf", C.c_float), ("Tcw", C.c_float * 12)]
+
+
+class OrbmPose(C.Structure):
+    """orbm_pose (orbm_prepare_pose), 84 bytes."""
+    _fields_ = [("Rt", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("level_mode", C.c_int32)]
+
+
+assert C.sizeof(OrbmPose) == 84
+
+
+def camera(fx, fy, cx, cy, mb, mbf, Tcw) -> OrbmCamera:
+    T = np.asarray(Tcw, np.float32).reshape(-1)[:12]
+    return OrbmCamera(fx, fy, cx, cy, mb, mbf, (C.c_float * 12)(*T.tolist()))
+
+
 class FeatureVectorC(C.Structure):
     _fields_ = [("nodes", C.c_void_p), ("off", C.c_void_p), ("idx", C.c_void_p), ("n_nodes", C.c_int)]
 
@@ -102,6 +122,23 @@ def lib() -> C.CDLL:
         L.orbm_search_by_projection_batch.argtypes = ([C.c_void_p] * 4 + [C.c_int, C.c_void_p, GridBounds,
                                                        C.c_void_p, C.c_int] + [C.c_void_p] * 4
                                                       + [C.c_int, C.c_int, C.c_float, C.c_float] + [C.c_void_p] * 3)
+        PS = [C.c_void_p] * 3 + [C.c_int]  # handle, kps, desc, n
+        L.orbm_prepare_pose.argtypes = [C.c_int, C.POINTER(OrbmCamera), C.c_void_p, C.c_int, C.POINTER(OrbmPose)]
+        L.orbm_predict_scale_thresholds.argtypes = [C.c_float, C.c_int, C.c_void_p]
+        L.orbm_predict_scale.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int]
+        L.orbm_search_by_projection_last_frame.argtypes = (
+            PS + [C.c_void_p, GridBounds, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(OrbmCamera), C.c_void_p,
+                  C.c_void_p, C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_int)])
+        L.orbm_search_by_projection_keyframe.argtypes = (
+            PS + [GridBounds, C.c_void_p, C.c_int, C.c_float, C.c_void_p, C.POINTER(OrbmCamera), C.c_void_p,
+                  C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_int)])
+        L.orbm_search_by_projection_sim3.argtypes = (
+            PS + [GridBounds, C.c_void_p, C.c_int, C.c_float, C.POINTER(OrbmCamera), C.c_void_p, C.c_void_p,
+                  C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int)])
+        L.orbm_search_by_projection_pose_batch.argtypes = (
+            [C.c_void_p, C.c_int] + [C.c_void_p] * 3 + [C.c_int, C.c_void_p, GridBounds, C.c_void_p, C.c_int,
+                                                         C.c_float] + [C.c_void_p] * 5
+            + [C.c_int, C.c_int, C.c_float, C.c_int, C.c_int] + [C.c_void_p] * 3)
         L.orbv_last_error.restype = C.c_char_p
         L.orbv_load_text.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
         L.orbv_create.argtypes = [C.c_int] * 5 + [C.c_void_p] * 4 + [C.c_int, C.POINTER(C.c_void_p)]
@@ -131,6 +168,13 @@ def lib() -> C.CDLL:
         _lib = L
     return _lib
 
+
+# orbm_map_point_world (include/orbx_c.h), 48 bytes
+MAP_POINT_WORLD_DTYPE = np.dtype([("pos", "<f4", (3,)), ("normal", "<f4", (3,)), ("min_distance", "<f4"),
+                                  ("max_distance", "<f4"), ("angle", "<f4"), ("octave", "<i4"), ("valid", "u1"),
+                                  ("obs_positive", "u1"), ("pad", "u1", (6,))])
+assert MAP_POINT_WORLD_DTYPE.itemsize == 48
+ORBM_PROJ_LAST_FRAME, ORBM_PROJ_KEYFRAME, ORBM_PROJ_SIM3 = 1, 2, 3
 
 # orbm_map_point_proj (include/orbx_c.h), 24 bytes
 MAP_POINT_PROJ_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),

@@ -161,6 +161,24 @@ size_t proj_lds_bytes(int kp_pitch);
 int launch_search_proj(const ProjParams& P, const orbx_kp* kps, const uint8_t* desc, const int* n,
                        const float* uright, const uint8_t* blocked, const orbm_map_point_proj* mps,
                        const uint8_t* mpdesc, const int* nmp, int frames, int* out, int* nmatches, void* stream);
+// orbx_project_pose.hip — the pose-projection SearchByProjection overloads, one frame per workgroup
+struct PoseParams {
+  int mode;                                  // ORBM_PROJ_LAST_FRAME / KEYFRAME / SIM3
+  float minX, maxX, minY, maxY, invW, invH;  // grid bounds (image bounds of IsInImage / the u, v tests)
+  float scale[kMaxLevels];                   // mvScaleFactors
+  float pred_thr[kMaxLevels];                // PredictScale thresholds (orbm_predict_scale_thresholds)
+  int L;                                     // mnScaleLevels
+  float th;                                  // window factor
+  int dist_th;                               // TH_HIGH / ORBdist / TH_LOW
+  int check_ori;
+  int kp_pitch, mp_pitch, has_uright;
+  int max_rounds;                            // fixed-point rounds before the sequential pass
+};
+size_t pose_lds_bytes(int kp_pitch);
+int launch_search_pose(const PoseParams& P, const orbx_kp* kps, const uint8_t* desc, const int* n,
+                       const float* uright, const uint8_t* blocked, const orbm_pose* poses,
+                       const orbm_map_point_world* mps, const uint8_t* mpdesc, const int* nmp, int frames, int* picks,
+                       int* out, int* nmatches, void* stream);
 // orbx_host.hip: the pyramid of frames [frame0, frame0 + n) of an extractor's last extraction
 int extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int* w, int* hgt, float* scale,
                       float* inv_scale, int* L);

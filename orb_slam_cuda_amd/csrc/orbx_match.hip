@@ -1070,6 +1070,8 @@ struct orbx_matcher {
   uint32_t* cand = nullptr;
   int* err = nullptr;
   int* stereo_sad = nullptr;  // [max_pairs][max_kps] SAD per left keypoint (-1 = none)
+  int* pose_picks = nullptr;  // pose-projection picks per point (frames x mp_pitch)
+  size_t pose_picks_cap = 0;
   hipStream_t stream = nullptr;
   // staging for the synchronous entry points
   void* stage = nullptr;
@@ -1120,6 +1122,7 @@ int orbm_destroy(orbm_handle m) {
   if (m->cand) (void)hipFree(m->cand);
   if (m->err) (void)hipFree(m->err);
   if (m->stereo_sad) (void)hipFree(m->stereo_sad);
+  if (m->pose_picks) (void)hipFree(m->pose_picks);
   if (m->stage) (void)hipFree(m->stage);
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
@@ -1493,6 +1496,247 @@ int orbm_search_by_projection(orbm_handle m, const orbx_kp* kps, const uint8_t* 
   MHIP(hipStreamSynchronize(st));
   *nmatches = nm;
   return ORBX_OK;
+}
+
+// ---------------------------------------------- pose-projection overloads
+namespace {
+
+// R*x + t via gemm's small-matrix path (float dot, double add of t)
+void host_rx_t(const float* T, const float* x, float* d) {
+  for (int r = 0; r < 3; ++r) {
+    const float t = T[4 * r] * x[0] + T[4 * r + 1] * x[1] + T[4 * r + 2] * x[2];
+    d[r] = (float)((double)t * 1.0 + (double)T[4 * r + 3] * 1.0);
+  }
+}
+// -R.t()*t via the general gemm path (double accumulation)
+void host_neg_rt_t(const float* T, float* d) {
+  for (int r = 0; r < 3; ++r) {
+    double s = 0;
+    for (int k = 0; k < 3; ++k) s += (double)T[4 * k + r] * (double)T[4 * k + 3];
+    d[r] = (float)(s * -1.0);
+  }
+}
+// MapPoint::PredictScale's int level as a predicate of the ratio
+int host_predict_direct(float ratio, float logsf, int L) {
+  const float q = std::ceil(std::log(ratio) / logsf);  // float overloads (logf)
+  int s = (q >= -2147483648.0f && q < 2147483648.0f) ? (int)q : INT_MIN;
+  return s < 0 ? 0 : (s >= L ? L - 1 : s);
+}
+
+}  // namespace
+
+int orbm_prepare_pose(int mode, const orbm_camera* cam, const float* Tlw, int mono, orbm_pose* out) {
+  if (!cam || !out || mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_PROJ_SIM3 ||
+      (mode == ORBM_PROJ_LAST_FRAME && !Tlw))
+    return mfail(ORBX_EINVAL, "bad argument");
+  orbm_pose p{};
+  p.fx = cam->fx;
+  p.fy = cam->fy;
+  p.cx = cam->cx;
+  p.cy = cam->cy;
+  p.mbf = cam->mbf;
+  if (mode == ORBM_PROJ_SIM3) {
+    // scw = sqrt(sRcw.row(0).dot(sRcw.row(0))); Rcw = sRcw/scw; tcw = t/scw
+    // (src/ORBmatcher.cc:298-303): Mat::dot in double, Mat / s = convertTo(1/s)
+    const float* S = cam->Tcw;
+    const double d = (double)S[0] * S[0] + (double)S[1] * S[1] + (double)S[2] * S[2];
+    const float scw = (float)std::sqrt(d);
+    if (!(scw > 0)) return mfail(ORBX_EINVAL, "Scw has a zero scale");
+    const float a = (float)(1.0 / (double)scw);
+    for (int k = 0; k < 12; ++k) p.Rt[k] = S[k] * a + 0.0f;
+  } else {
+    for (int k = 0; k < 12; ++k) p.Rt[k] = cam->Tcw[k];
+  }
+  host_neg_rt_t(p.Rt, p.Ow);  // Ow = -Rcw.t()*tcw
+  p.level_mode = 0;
+  if (mode == ORBM_PROJ_LAST_FRAME) {
+    // twc = -Rcw.t()*tcw; tlc = Rlw*twc + tlw (src/ORBmatcher.cc:1338-1349)
+    float tlc[3];
+    host_rx_t(Tlw, p.Ow, tlc);
+    const bool bForward = tlc[2] > cam->mb && !mono;
+    const bool bBackward = -tlc[2] > cam->mb && !mono;
+    p.level_mode = bForward ? 1 : (bBackward ? 2 : 0);
+  }
+  *out = p;
+  return ORBX_OK;
+}
+
+int orbm_predict_scale_thresholds(float scale_factor, int nlevels, float* thr) {
+  if (!thr || nlevels < 1 || nlevels > kMaxLevels || !(scale_factor > 1.0f))
+    return mfail(ORBX_EINVAL, "bad argument");
+  const float logsf = std::log(scale_factor);  // Frame::mfLogScaleFactor (src/Frame.cc:70)
+  for (int k = 1; k < nlevels; ++k) {
+    // least positive float r with level(r) >= k; level is non-decreasing in r
+    uint32_t lo = 0x00000001u, hi = 0x7f7fffffu;  // level(lo) = 0 < k <= level(FLT_MAX)
+    auto at = [](uint32_t b) {
+      float f;
+      std::memcpy(&f, &b, 4);
+      return f;
+    };
+    if (host_predict_direct(at(hi), logsf, nlevels) < k) return mfail(ORBX_EINVAL, "scale factor too small");
+    while (hi - lo > 1) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (host_predict_direct(at(mid), logsf, nlevels) >= k)
+        hi = mid;
+      else
+        lo = mid;
+    }
+    thr[k - 1] = at(hi);
+  }
+  for (int k = nlevels; k <= kMaxLevels; ++k) thr[k - 1 < kMaxLevels ? k - 1 : 0] = INFINITY;
+  return ORBX_OK;
+}
+
+int orbm_predict_scale(float max_distance, float dist, float scale_factor, int nlevels) {
+  float thr[kMaxLevels];
+  if (orbm_predict_scale_thresholds(scale_factor, nlevels, thr)) return -1;
+  const float ratio = max_distance / dist;
+  if (std::isinf(ratio)) return 0;
+  int l = 0;
+  for (int k = 0; k < nlevels - 1; ++k) l += ratio >= thr[k];
+  return l;
+}
+
+int orbm_search_by_projection_pose_batch(orbm_handle m, int mode, const orbx_kp* d_kps, const uint8_t* d_desc,
+                                         const int* d_n, int kp_pitch, const float* d_uright, orbm_grid_bounds b,
+                                         const float* scale, int nlevels, float scale_factor,
+                                         const uint8_t* d_blocked, const orbm_pose* d_poses,
+                                         const orbm_map_point_world* d_mps, const uint8_t* d_mpdesc,
+                                         const int* d_nmp, int mp_pitch, int frames, float th, int dist_th,
+                                         int check_ori, int* d_out, int* d_nmatches, void* stream) {
+  if (!m || !d_kps || !d_desc || !d_n || !scale || !d_blocked || !d_poses || !d_mps || !d_mpdesc || !d_nmp ||
+      !d_out || !d_nmatches || frames < 1 || kp_pitch < 1 || mp_pitch < 1 || nlevels < 1 ||
+      nlevels > kMaxLevels || mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_PROJ_SIM3)
+    return mfail(ORBX_EINVAL, "bad argument");
+  if (!(b.max_x > b.min_x) || !(b.max_y > b.min_y)) return mfail(ORBX_EINVAL, "empty grid bounds");
+  if (pose_lds_bytes(kp_pitch) > 156 * 1024) return mfail(ORBX_ECAPACITY, "kp_pitch %d too large", kp_pitch);
+  MHIP(hipSetDevice(m->device));
+  PoseParams P{};
+  P.mode = mode;
+  P.minX = b.min_x;
+  P.maxX = b.max_x;
+  P.minY = b.min_y;
+  P.maxY = b.max_y;
+  P.invW = 64.0f / (b.max_x - b.min_x);  // mfGridElementWidthInv (src/Frame.cc:154-155)
+  P.invH = 48.0f / (b.max_y - b.min_y);
+  for (int l = 0; l < kMaxLevels; ++l) P.scale[l] = scale[std::min(l, nlevels - 1)];
+  if (mode != ORBM_PROJ_LAST_FRAME) {
+    int rc = orbm_predict_scale_thresholds(scale_factor, nlevels, P.pred_thr);
+    if (rc) return rc;
+  }
+  P.L = nlevels;
+  P.th = th;
+  P.dist_th = dist_th;
+  P.check_ori = check_ori;
+  P.kp_pitch = kp_pitch;
+  P.mp_pitch = mp_pitch;
+  P.has_uright = d_uright != nullptr && mode == ORBM_PROJ_LAST_FRAME;
+  P.max_rounds = 32;
+  if (const char* e = getenv("ORBX_PROJ_ROUNDS")) P.max_rounds = atoi(e);  // tests: force the sequential pass
+  const size_t need = (size_t)frames * mp_pitch;
+  if (m->pose_picks_cap < need) {
+    if (m->pose_picks) MHIP(hipFree(m->pose_picks));
+    m->pose_picks = nullptr;
+    m->pose_picks_cap = 0;
+    if (hipMalloc(&m->pose_picks, need * 4) != hipSuccess) return mfail(ORBX_ENOMEM, "pose picks workspace");
+    m->pose_picks_cap = need;
+  }
+  if (launch_search_pose(P, d_kps, d_desc, d_n, d_uright, d_blocked, d_poses, d_mps, d_mpdesc, d_nmp, frames,
+                         m->pose_picks, d_out, d_nmatches, stream))
+    return mfail(ORBX_EDEVICE, "search_pose launch: %s", hipGetErrorString(hipGetLastError()));
+  return ORBX_OK;
+}
+
+namespace {
+// One frame through orbm_search_by_projection_pose_batch from host buffers.
+int pose_sync(orbm_handle m, int mode, const orbx_kp* kps, const uint8_t* desc, int n, const float* uright,
+              orbm_grid_bounds b, const float* scale, int nlevels, float scale_factor, const uint8_t* blocked,
+              const orbm_pose& pose, const orbm_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th,
+              int dist_th, int check_ori, int* out, int* nmatches) {
+  if (!m || !nmatches || n < 0 || nmp < 0 || (n && (!kps || !desc || !out)) || (nmp && (!mps || !mpdesc)))
+    return mfail(ORBX_EINVAL, "bad argument");
+  MHIP(hipSetDevice(m->device));
+  const int kp = std::max(n, 1), mp = std::max(nmp, 1);
+  const size_t sz[] = {(size_t)kp * sizeof(orbx_kp), (size_t)kp * 32, (size_t)kp * 4, (size_t)kp,
+                       (size_t)mp * sizeof(orbm_map_point_world), (size_t)mp * 32, (size_t)kp * 4, 16,
+                       sizeof(orbm_pose)};
+  size_t off[9], tot = 0;
+  for (int i = 0; i < 9; ++i) {
+    off[i] = tot;
+    tot += (sz[i] + 255) & ~(size_t)255;
+  }
+  int rc;
+  if ((rc = stage_reserve(m, tot))) return rc;
+  uint8_t* s = (uint8_t*)m->stage;
+  if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+  hipStream_t st = m->stream;
+  int* cnt = (int*)(s + off[7]);  // n, nmp, nmatches
+  const int hn[2] = {n, nmp};
+  std::vector<uint8_t> bl(kp, 0);
+  if (blocked && n) std::memcpy(bl.data(), blocked, n);
+  if (n) {
+    MHIP(hipMemcpyAsync(s + off[0], kps, (size_t)n * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(s + off[1], desc, (size_t)n * 32, hipMemcpyHostToDevice, st));
+    if (uright) MHIP(hipMemcpyAsync(s + off[2], uright, (size_t)n * 4, hipMemcpyHostToDevice, st));
+  }
+  MHIP(hipMemcpyAsync(s + off[3], bl.data(), (size_t)kp, hipMemcpyHostToDevice, st));
+  if (nmp) {
+    MHIP(hipMemcpyAsync(s + off[4], mps, (size_t)nmp * sizeof(orbm_map_point_world), hipMemcpyHostToDevice, st));
+    MHIP(hipMemcpyAsync(s + off[5], mpdesc, (size_t)nmp * 32, hipMemcpyHostToDevice, st));
+  }
+  MHIP(hipMemcpyAsync(cnt, hn, 8, hipMemcpyHostToDevice, st));
+  MHIP(hipMemcpyAsync(s + off[8], &pose, sizeof pose, hipMemcpyHostToDevice, st));
+  rc = orbm_search_by_projection_pose_batch(
+      m, mode, (const orbx_kp*)(s + off[0]), s + off[1], cnt, kp, uright ? (const float*)(s + off[2]) : nullptr, b,
+      scale, nlevels, scale_factor, s + off[3], (const orbm_pose*)(s + off[8]),
+      (const orbm_map_point_world*)(s + off[4]), s + off[5], cnt + 1, mp, 1, th, dist_th, check_ori,
+      (int*)(s + off[6]), cnt + 2, st);
+  if (rc) return rc;
+  int nm = 0;
+  MHIP(hipMemcpyAsync(&nm, cnt + 2, 4, hipMemcpyDeviceToHost, st));
+  if (n) MHIP(hipMemcpyAsync(out, s + off[6], (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  MHIP(hipStreamSynchronize(st));
+  *nmatches = nm;
+  return ORBX_OK;
+}
+}  // namespace
+
+int orbm_search_by_projection_last_frame(orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n,
+                                         const float* uright, orbm_grid_bounds b, const float* scale, int nlevels,
+                                         const uint8_t* blocked, const orbm_camera* cur, const float* Tlw,
+                                         const orbm_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th,
+                                         int mono, int check_ori, int* out, int* nmatches) {
+  orbm_pose pose;
+  int rc = orbm_prepare_pose(ORBM_PROJ_LAST_FRAME, cur, Tlw, mono, &pose);
+  if (rc) return rc;
+  return pose_sync(m, ORBM_PROJ_LAST_FRAME, kps, desc, n, uright, b, scale, nlevels, 1.2f, blocked, pose, mps,
+                   mpdesc, nmp, th, 100 /* TH_HIGH */, check_ori, out, nmatches);
+}
+
+int orbm_search_by_projection_keyframe(orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n,
+                                       orbm_grid_bounds b, const float* scale, int nlevels, float scale_factor,
+                                       const uint8_t* has_mp, const orbm_camera* cur,
+                                       const orbm_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th,
+                                       int orb_dist, int check_ori, int* out, int* nmatches) {
+  orbm_pose pose;
+  int rc = orbm_prepare_pose(ORBM_PROJ_KEYFRAME, cur, nullptr, 0, &pose);
+  if (rc) return rc;
+  return pose_sync(m, ORBM_PROJ_KEYFRAME, kps, desc, n, nullptr, b, scale, nlevels, scale_factor, has_mp, pose,
+                   mps, mpdesc, nmp, th, orb_dist, check_ori, out, nmatches);
+}
+
+int orbm_search_by_projection_sim3(orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n,
+                                   orbm_grid_bounds b, const float* scale, int nlevels, float scale_factor,
+                                   const orbm_camera* kf, const orbm_map_point_world* mps, const uint8_t* mpdesc,
+                                   int nmp, int th, const int* matched, int* out, int* nmatches) {
+  orbm_pose pose;
+  int rc = orbm_prepare_pose(ORBM_PROJ_SIM3, kf, nullptr, 0, &pose);
+  if (rc) return rc;
+  std::vector<uint8_t> bl(std::max(n, 1), 0);
+  if (matched)
+    for (int i = 0; i < n; ++i) bl[i] = matched[i] >= 0;  // vpMatched[idx] set on entry
+  return pose_sync(m, ORBM_PROJ_SIM3, kps, desc, n, nullptr, b, scale, nlevels, scale_factor, bl.data(), pose, mps,
+                   mpdesc, nmp, (float)th, 50 /* TH_LOW */, 0, out, nmatches);
 }
 
 }  // extern "C"

@@ -24,19 +24,15 @@
 //     The system is triangular, so its fixed point is unique and equals the
 //     sequential result; rounds stop when no pick changes (a sequential pass
 //     by one lane resolves it if P.max_rounds is reached).
-#include "orbx_device.cuh"
-#include "orbx_wave.cuh"
+#include "orbx_projgrid.cuh"
 
 namespace orbx {
 
 constexpr int kProjThreads = 1024;
 constexpr int kProjMaxMp = 8 * kProjThreads;  // map points per frame held in registers
-constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS  include/Frame.h:37-38
 constexpr int kProjTHigh = 100;               // ORBmatcher::TH_HIGH
 
-size_t proj_lds_bytes(int kp_pitch) {
-  return (size_t)(kGridCols * kGridRows + 1) * 4 + (size_t)kp_pitch * (16 + 32 + 4 + 4) + 64;
-}
+size_t proj_lds_bytes(int kp_pitch) { return proj_grid_lds_bytes(kp_pitch); }
 
 __global__ __launch_bounds__(kProjThreads) void search_proj_kernel(ProjParams P, const orbx_kp* __restrict__ kps,
                                                                    const uint8_t* __restrict__ desc,
@@ -52,49 +48,19 @@ __global__ __launch_bounds__(kProjThreads) void search_proj_kernel(ProjParams P,
   __shared__ int s_flag;
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int K = P.kp_pitch, n = d_n[f], nmp = min(d_nmp[f], kProjMaxMp);
-  constexpr int NC = kGridCols * kGridRows;
-  int* s_cell = s_dyn;                                      // [NC + 1]
-  uint4* s_kd = (uint4*)(s_cell + ((NC + 1 + 3) & ~3));     // [2K] descriptors by position
-  float4* s_kp = (float4*)(s_kd + 2 * K);                   // [K] x, y, octave (bits), uRight
-  int* s_kid = (int*)(s_kp + K);                            // [K] keypoint index by position
-  int* s_mark = s_kid + K;                                  // [K] by keypoint index: cell / min picker
+  const ProjGridLds g = proj_grid_carve(s_dyn, K);
+  int* s_cell = g.cell;
+  uint4* s_kd = g.kd;
+  float4* s_kp = g.kp;
+  int* s_kid = g.kid;
+  int* s_mark = g.mark;  // by keypoint index: cell / min picker
   const orbx_kp* KP = kps + (size_t)f * K;
   const uint8_t* D = desc + (size_t)f * K * 32;
   const float* UR = P.has_uright ? uright + (size_t)f * K : nullptr;
   const uint8_t* BL = blocked + (size_t)f * K;
 
   // ---- stable grid sort (AssignFeaturesToGrid: cells hold indices ascending)
-  for (int c = tid; c <= NC; c += kProjThreads) s_cell[c] = 0;
-  __syncthreads();
-  for (int i = tid; i < n; i += kProjThreads) {
-    const float x = KP[i].x, y = KP[i].y;
-    const int px = (int)roundf((x - P.minX) * P.invW), py = (int)roundf((y - P.minY) * P.invH);
-    int c = -1;
-    if (!(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows)) {
-      c = px * kGridRows + py;
-      __hip_atomic_fetch_add(&s_cell[c], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    s_mark[i] = c;
-  }
-  __syncthreads();
-  block_scan_excl<kProjThreads>(s_cell, NC + 1, s_tmp);
-  // each cell's keypoints in ascending index: rank within the cell by a count of
-  // smaller indices in the same cell (cells hold a handful of keypoints)
-  for (int i = tid; i < n; i += kProjThreads) {
-    const int c = s_mark[i];
-    if (c < 0) continue;
-    int rank = 0;
-    const int cnt = s_cell[c + 1] - s_cell[c];
-    if (cnt > 1)
-      for (int j = 0; j < i; ++j) rank += s_mark[j] == c;  // O(n) only for shared cells
-    const int q = s_cell[c] + rank;
-    const orbx_kp k = KP[i];
-    s_kp[q] = make_float4(k.x, k.y, __int_as_float(k.octave), UR ? UR[i] : -1.f);
-    s_kid[q] = i;
-    s_kd[2 * q] = ((const uint4*)(D + (size_t)i * 32))[0];
-    s_kd[2 * q + 1] = ((const uint4*)(D + (size_t)i * 32))[1];
-  }
-  __syncthreads();
+  proj_grid_sort<kProjThreads>(g, KP, D, UR, n, P.minX, P.minY, P.invW, P.invH, s_tmp);
 
   long long* prof = P.prof ? P.prof + (size_t)f * 64 : nullptr;  // diagnostics (ORBX_PROJ_PROF)
   if (prof && tid == 0) prof[0] = (long long)__builtin_readcyclecounter();
@@ -116,14 +82,8 @@ __global__ __launch_bounds__(kProjThreads) void search_proj_kernel(ProjParams P,
     if (bFactor) r = r * P.th;
     const float rad = r * P.scale[min(max(lvl, 0), kMaxLevels - 1)];
     const float x = mp.proj_x, y = mp.proj_y;
-    const int cx0 = max(0, (int)floorf((x - P.minX - rad) * P.invW));
-    if (cx0 >= kGridCols) return -1;
-    const int cx1 = min(kGridCols - 1, (int)ceilf((x - P.minX + rad) * P.invW));
-    if (cx1 < 0) return -1;
-    const int cy0 = max(0, (int)floorf((y - P.minY - rad) * P.invH));
-    if (cy0 >= kGridRows) return -1;
-    const int cy1 = min(kGridRows - 1, (int)ceilf((y - P.minY + rad) * P.invH));
-    if (cy1 < 0) return -1;
+    int cx0, cx1, cy0, cy1;
+    if (!proj_window(x, y, rad, P.minX, P.minY, P.invW, P.invH, cx0, cx1, cy0, cy1)) return -1;
     const int minLevel = lvl - 1, maxLevel = lvl;
     const bool check = (minLevel > 0) || (maxLevel >= 0);
     const uint4* md = (const uint4*)(MD + (size_t)j * 32);
@@ -146,8 +106,7 @@ __global__ __launch_bounds__(kProjThreads) void search_proj_kernel(ProjParams P,
           if (er > rad) continue;
         }
         const uint4 a = s_kd[2 * q], b = s_kd[2 * q + 1];
-        const int d = __popc(a.x ^ m0.x) + __popc(a.y ^ m0.y) + __popc(a.z ^ m0.z) + __popc(a.w ^ m0.w) +
-                      __popc(b.x ^ m1.x) + __popc(b.y ^ m1.y) + __popc(b.z ^ m1.z) + __popc(b.w ^ m1.w);
+        const int d = hamming256(a, b, m0, m1);
         if (d < best) {
           best2 = best;
           best = d;

@@ -6,11 +6,16 @@ Mirrors include/ORBmatcher.h:37-102 for the hot-path searches:
     nmatches = m.SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
     nmatches = m.SearchByBoW(pKF, F, vpMapPointMatches)          # KF - Frame
     nmatches = m.SearchByBoW(pKF1, pKF2, vpMatches12)            # KF - KF
+    nmatches = m.SearchByProjection(F, mps, mp_desc, th)         # local map (Frame::isInFrustum records)
+    nmatches = m.SearchByProjection(CurrentFrame, LastFrame, th, bMono)
+    nmatches = m.SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+    nmatches = m.SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
     ORBmatcher.DescriptorDistance(a, b)
 
 `Frame` / `KeyFrame` here are plain containers of the fields these searches
-read (mvKeysUn, mDescriptors, the grid bounds, mFeatVec, MapPoint validity);
-MapPoint pointers are represented by the index of the matched keypoint.
+read (mvKeysUn, mDescriptors, the grid bounds, camera and pose, mFeatVec,
+MapPoint links). MapPoint pointers are row indices into a `MapPoints` table
+(the Map), -1 standing for NULL.
 All searches run in the HIP kernels of liborbx.so.
 """
 from __future__ import annotations
@@ -20,7 +25,61 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import KP_DTYPE, MAP_POINT_PROJ_DTYPE, FeatureVectorC, GridBounds, check, lib, ptr
+from ._lib import (KP_DTYPE, MAP_POINT_PROJ_DTYPE, MAP_POINT_WORLD_DTYPE, ORBM_PROJ_KEYFRAME, ORBM_PROJ_LAST_FRAME,
+                   ORBM_PROJ_SIM3, FeatureVectorC, GridBounds, camera, check, lib, ptr)
+
+
+@dataclass
+class MapPoints:
+    """The MapPoint fields the searches read, one row per MapPoint (a pointer is a row index):
+    GetWorldPos, GetNormal, mfMinDistance / mfMaxDistance, GetDescriptor, Observations(), isBad()."""
+    pos: np.ndarray                        # (M, 3) float32
+    descriptors: np.ndarray                # (M, 32) uint8
+    normal: np.ndarray | None = None       # (M, 3) float32
+    min_distance: np.ndarray | None = None  # (M,) float32
+    max_distance: np.ndarray | None = None  # (M,) float32
+    nobs: np.ndarray | None = None         # (M,) int, default 1
+    bad: np.ndarray | None = None          # (M,) bool, default False
+
+    def __len__(self):
+        return len(self.pos)
+
+    def records(self, idx, angle=None, octave=None, valid=None):
+        """orbm_map_point_world records + descriptors for pointers idx (-1 = NULL -> not valid)."""
+        idx = np.asarray(idx, np.int64)
+        ok = idx >= 0
+        j = np.where(ok, idx, 0)
+        M = len(self)
+        rec = np.zeros(len(idx), MAP_POINT_WORLD_DTYPE)
+        if M == 0:
+            return rec, np.zeros((len(idx), 32), np.uint8)
+        rec["pos"] = np.asarray(self.pos, np.float32)[j]
+        if self.normal is not None:
+            rec["normal"] = np.asarray(self.normal, np.float32)[j]
+        if self.min_distance is not None:
+            rec["min_distance"] = np.asarray(self.min_distance, np.float32)[j]
+        if self.max_distance is not None:
+            rec["max_distance"] = np.asarray(self.max_distance, np.float32)[j]
+        if angle is not None:
+            rec["angle"] = angle
+        if octave is not None:
+            rec["octave"] = octave
+        bad = np.zeros(M, bool) if self.bad is None else np.asarray(self.bad, bool)
+        nobs = np.ones(M, np.int64) if self.nobs is None else np.asarray(self.nobs)
+        rec["valid"] = ok & (True if valid is None else np.asarray(valid, bool))
+        rec["obs_positive"] = ok & (nobs[j] > 0)
+        return rec, np.ascontiguousarray(np.asarray(self.descriptors, np.uint8)[j])
+
+    def bad_of(self, idx):
+        idx = np.asarray(idx, np.int64)
+        if self.bad is None:
+            return np.zeros(len(idx), bool)
+        return np.asarray(self.bad, bool)[np.where(idx >= 0, idx, 0)] & (idx >= 0)
+
+    def obs_of(self, idx):
+        idx = np.asarray(idx, np.int64)
+        nobs = np.ones(len(self), np.int64) if self.nobs is None else np.asarray(self.nobs)
+        return (idx >= 0) & (nobs[np.where(idx >= 0, idx, 0)] > 0)
 
 
 @dataclass
@@ -43,6 +102,15 @@ class Frame:
     mvDepth: np.ndarray | None = None
     mvScaleFactors: np.ndarray | None = None  # (nlevels,) float32 (ORBextractor::GetScaleFactors)
     mvpMapPoints: np.ndarray | None = None    # (N,) int: map point index, -1 = NULL
+    # camera and pose (SearchByProjection overloads that project world points)
+    fx: float = 0.0
+    fy: float = 0.0
+    cx: float = 0.0
+    cy: float = 0.0
+    mTcw: np.ndarray | None = None         # (3, 4) or (4, 4) float32
+    mvbOutlier: np.ndarray | None = None   # (N,) bool
+    mfScaleFactor: float = 1.2
+    mpMap: "MapPoints | None" = None
 
     @property
     def N(self) -> int:
@@ -82,12 +150,33 @@ def ComputeStereoMatches(F: Frame, extractorLeft, extractorRight, matcher: "ORBm
 class KeyFrame:
     mvKeysUn: np.ndarray
     mDescriptors: np.ndarray
-    mvpMapPoints: np.ndarray               # bool/uint8: MapPoint present and !isBad()
+    mvpMapPoints: np.ndarray               # bool/uint8 mask (MapPoint present and !isBad()) or int pointers (-1 = NULL)
     mFeatVec: dict = field(default_factory=dict)
+    mnMinX: float = 0.0
+    mnMaxX: float = 0.0
+    mnMinY: float = 0.0
+    mnMaxY: float = 0.0
+    fx: float = 0.0
+    fy: float = 0.0
+    cx: float = 0.0
+    cy: float = 0.0
+    mvScaleFactors: np.ndarray | None = None
+    mfScaleFactor: float = 1.2
+    mpMap: "MapPoints | None" = None
 
     @property
     def N(self) -> int:
         return len(self.mvKeysUn)
+
+
+def _mp_mask(a) -> np.ndarray:
+    """MapPoint presence from a bool/uint8 mask or an int pointer array (-1 = NULL)."""
+    a = np.asarray(a)
+    return (a != 0) if a.dtype in (np.bool_, np.uint8) else (a >= 0)
+
+
+def _grid(F) -> GridBounds:
+    return GridBounds(F.mnMinX, F.mnMaxX, F.mnMinY, F.mnMaxY)
 
 
 def feature_vector_csr(fv: dict):
@@ -164,8 +253,103 @@ class ORBmatcher:
         self.last_matches12 = m12
         return nm.value
 
-    def SearchByProjection(self, F: Frame, mps: np.ndarray, mp_desc: np.ndarray, th: float = 3.0,
-                           blocked: np.ndarray | None = None) -> int:
+    def SearchByProjection(self, a, b, *args, **kw) -> int:
+        """The four SearchByProjection overloads (include/ORBmatcher.h:48-60), by argument types:
+        (Frame, records, descriptors, th=3)            local map       src/ORBmatcher.cc:45-118
+        (Frame CurrentFrame, Frame LastFrame, th, bMono)  motion model  :1328-1470
+        (Frame CurrentFrame, KeyFrame pKF, sAlreadyFound, th, ORBdist)  relocalization :1472-1599
+        (KeyFrame pKF, Scw, vpPoints, vpMatched, th)  loop closing     :290-403"""
+        if isinstance(a, KeyFrame):
+            return self._search_sim3(a, b, *args, **kw)
+        if isinstance(b, Frame):
+            return self._search_last_frame(a, b, *args, **kw)
+        if isinstance(b, KeyFrame):
+            return self._search_keyframe(a, b, *args, **kw)
+        return self._search_local_map(a, b, *args, **kw)
+
+    def _search_last_frame(self, CurrentFrame: Frame, LastFrame: Frame, th: float, bMono: bool) -> int:
+        """SearchByProjection(Frame&, const Frame&, th, bMono): map points of LastFrame (not outliers)
+        projected with CurrentFrame.mTcw; stores pointers into CurrentFrame.mvpMapPoints."""
+        F, L, mp = CurrentFrame, LastFrame, CurrentFrame.mpMap
+        kps = np.ascontiguousarray(F.mvKeysUn, KP_DTYPE)
+        d = np.ascontiguousarray(F.mDescriptors, np.uint8)
+        n = len(kps)
+        if F.mvpMapPoints is None:
+            F.mvpMapPoints = np.full(n, -1, np.int32)
+        lmp = np.asarray(L.mvpMapPoints, np.int64)
+        outl = np.zeros(L.N, bool) if L.mvbOutlier is None else np.asarray(L.mvbOutlier, bool)
+        rec, md = mp.records(lmp, L.mvKeysUn["angle"], L.mvKeys["octave"], ~outl)
+        bl = np.ascontiguousarray(mp.obs_of(F.mvpMapPoints), np.uint8)
+        ur = None if F.mvuRight is None else np.ascontiguousarray(F.mvuRight, np.float32)
+        sc = np.ascontiguousarray(F.mvScaleFactors, np.float32)
+        cam = camera(F.fx, F.fy, F.cx, F.cy, F.mb, F.mbf, F.mTcw)
+        Tlw = np.ascontiguousarray(np.asarray(L.mTcw, np.float32)[:3], np.float32)
+        out = np.full(max(n, 1), -1, np.int32)
+        nm = C.c_int(0)
+        check(lib().orbm_search_by_projection_last_frame(
+            self._h, ptr(kps), ptr(d), n, ptr(ur), _grid(F), ptr(sc), len(sc), ptr(bl), C.byref(cam), ptr(Tlw),
+            ptr(rec), ptr(md), len(rec), C.c_float(th), int(bool(bMono)), int(self.mbCheckOrientation), ptr(out),
+            C.byref(nm)), matcher=True)
+        o = out[:n]
+        F.mvpMapPoints[o >= 0] = lmp[o[o >= 0]]
+        F.mvpMapPoints[o == -2] = -1
+        self.last_projection = o.copy()
+        return nm.value
+
+    def _search_keyframe(self, CurrentFrame: Frame, pKF: KeyFrame, sAlreadyFound, th: float, ORBdist: int) -> int:
+        """SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)."""
+        F, mp = CurrentFrame, CurrentFrame.mpMap
+        kps = np.ascontiguousarray(F.mvKeysUn, KP_DTYPE)
+        d = np.ascontiguousarray(F.mDescriptors, np.uint8)
+        n = len(kps)
+        if F.mvpMapPoints is None:
+            F.mvpMapPoints = np.full(n, -1, np.int32)
+        kmp = np.asarray(pKF.mvpMapPoints, np.int64)  # pKF->GetMapPointMatches()
+        found = np.isin(kmp, np.fromiter(sAlreadyFound, np.int64)) if len(sAlreadyFound) else np.zeros(len(kmp), bool)
+        rec, md = mp.records(kmp, pKF.mvKeysUn["angle"], None, ~mp.bad_of(kmp) & ~found)
+        hm = np.ascontiguousarray(np.asarray(F.mvpMapPoints) >= 0, np.uint8)
+        sc = np.ascontiguousarray(F.mvScaleFactors, np.float32)
+        cam = camera(F.fx, F.fy, F.cx, F.cy, F.mb, F.mbf, F.mTcw)
+        out = np.full(max(n, 1), -1, np.int32)
+        nm = C.c_int(0)
+        check(lib().orbm_search_by_projection_keyframe(
+            self._h, ptr(kps), ptr(d), n, _grid(F), ptr(sc), len(sc), C.c_float(F.mfScaleFactor), ptr(hm),
+            C.byref(cam), ptr(rec), ptr(md), len(rec), C.c_float(th), int(ORBdist), int(self.mbCheckOrientation),
+            ptr(out), C.byref(nm)), matcher=True)
+        o = out[:n]
+        F.mvpMapPoints[o >= 0] = kmp[o[o >= 0]]
+        F.mvpMapPoints[o == -2] = -1
+        self.last_projection = o.copy()
+        return nm.value
+
+    def _search_sim3(self, pKF: KeyFrame, Scw, vpPoints, vpMatched, th: int) -> int:
+        """SearchByProjection(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&, vector<MapPoint*>&, th):
+        vpMatched (pKF.N pointers, -1 = NULL) is updated in place."""
+        mp = pKF.mpMap
+        kps = np.ascontiguousarray(pKF.mvKeysUn, KP_DTYPE)
+        d = np.ascontiguousarray(pKF.mDescriptors, np.uint8)
+        n = len(kps)
+        pts = np.asarray(vpPoints, np.int64)
+        matched = np.asarray(vpMatched, np.int64)
+        already = np.isin(pts, matched[matched >= 0])
+        rec, md = mp.records(pts, None, None, ~mp.bad_of(pts) & ~already)
+        mt = np.ascontiguousarray(np.where(matched >= 0, 0, -1), np.int32)
+        sc = np.ascontiguousarray(pKF.mvScaleFactors, np.float32)
+        cam = camera(pKF.fx, pKF.fy, pKF.cx, pKF.cy, 0.0, 0.0, Scw)
+        out = np.full(max(n, 1), -1, np.int32)
+        nm = C.c_int(0)
+        check(lib().orbm_search_by_projection_sim3(
+            self._h, ptr(kps), ptr(d), n, _grid(pKF), ptr(sc), len(sc), C.c_float(pKF.mfScaleFactor), C.byref(cam),
+            ptr(rec), ptr(md), len(rec), int(th), ptr(mt), ptr(out), C.byref(nm)), matcher=True)
+        o = out[:n]
+        res = matched.copy()
+        res[o >= 0] = pts[o[o >= 0]]
+        vpMatched[:] = res.tolist() if isinstance(vpMatched, list) else res
+        self.last_projection = o.copy()
+        return nm.value
+
+    def _search_local_map(self, F: Frame, mps: np.ndarray, mp_desc: np.ndarray, th: float = 3.0,
+                          blocked: np.ndarray | None = None) -> int:
         """SearchByProjection(Frame&, const vector<MapPoint*>&, th) (src/ORBmatcher.cc:45-118).
         mps: MAP_POINT_PROJ_DTYPE per map point (Frame::isInFrustum's mTrackProj*, view cos,
         predicted level, in-view and Observations() > 0 flags), mp_desc their descriptors.
@@ -204,8 +388,8 @@ class ORBmatcher:
         dB = np.ascontiguousarray(B.mDescriptors, np.uint8)
         aA = np.ascontiguousarray(A.mvKeysUn["angle"], np.float32)
         aB = np.ascontiguousarray((B.mvKeysUn if kf_vs_kf else B.mvKeys)["angle"], np.float32)
-        mA = np.ascontiguousarray(A.mvpMapPoints, np.uint8)
-        mB = np.ascontiguousarray(B.mvpMapPoints, np.uint8) if kf_vs_kf else None
+        mA = np.ascontiguousarray(_mp_mask(A.mvpMapPoints), np.uint8)
+        mB = np.ascontiguousarray(_mp_mask(B.mvpMapPoints), np.uint8) if kf_vs_kf else None
         res = np.full(len(dA) if kf_vs_kf else len(dB), -1, np.int32)
         nm = C.c_int(0)
         check(lib().orbm_search_by_bow(

@@ -585,3 +585,231 @@ def search_by_projection(kps, desc, uright, bounds, scale, blocked, mps, mpdesc,
                 blk[bi] = bool(mp["obs_positive"])
             nm += 1
     return np.array(out, np.int32), nm
+
+
+# ------------------------------------------- SearchByProjection, pose overloads
+import ctypes as _C  # noqa: E402
+
+_libm = _C.CDLL("libm.so.6")
+_libm.logf.restype = _C.c_float
+_libm.logf.argtypes = [_C.c_float]
+
+
+def _logf(x):
+    return f32(_libm.logf(float(f32(x))))
+
+
+def _mat_rx_t(T, x):
+    """R*x + t: OpenCV gemm small-matrix path (float dot, then double add of t)."""
+    T = np.asarray(T, np.float32).reshape(3, 4)
+    out = []
+    for r in range(3):
+        t = f32(f32(f32(T[r, 0] * f32(x[0])) + f32(T[r, 1] * f32(x[1]))) + f32(T[r, 2] * f32(x[2])))
+        out.append(f32(float(t) + float(T[r, 3])))
+    return out
+
+
+def _mat_neg_rt_t(T):
+    """-R.t()*t: general gemm path with double accumulation."""
+    T = np.asarray(T, np.float32).reshape(3, 4)
+    out = []
+    for r in range(3):
+        s = 0.0
+        for k in range(3):
+            s += float(T[k, r]) * float(T[k, 3])
+        out.append(f32(-s))
+    return out
+
+
+def _norm3(v):
+    s = 0.0
+    for e in v:
+        s += float(e) * float(e)
+    return math.sqrt(s)
+
+
+def _dot3(a, b):
+    s = 0.0
+    for x, y in zip(a, b):
+        s += float(x) * float(y)
+    return s
+
+
+def predict_scale(maxd, dist, sf, L):
+    """MapPoint::PredictScale (src/MapPoint.cc:407-422), float log."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ratio = f32(f32(maxd) / f32(dist))
+        q = f32(_logf(ratio) / _logf(sf))
+    if not np.isfinite(q):
+        return 0  # x86 float->int of a non-finite value: INT_MIN, clamped to 0
+    n = int(math.ceil(float(q)))
+    return 0 if n < 0 else min(n, L - 1)
+
+
+def _rot_filter(hist, out, nm):
+    ind = three_maxima([len(h) for h in hist])
+    for b in range(30):
+        if b not in ind:
+            for i2 in hist[b]:
+                out[i2] = -2
+                nm -= 1
+    return nm
+
+
+def _cam(cam):
+    return (f32(cam.fx), f32(cam.fy), f32(cam.cx), f32(cam.cy), f32(cam.mb), f32(cam.mbf),
+            np.array(list(cam.Tcw), np.float32))
+
+
+def search_by_projection_last_frame(kps, desc, uright, bounds, scale, blocked, cam, Tlw, mps, mpdesc, th, mono,
+                                    check_ori=True):
+    """SearchByProjection(CurrentFrame, LastFrame, th, bMono) (src/ORBmatcher.cc:1328-1470)."""
+    fx, fy, cx, cy, mb, mbf, T = _cam(cam)
+    cells = grid_cells(kps, bounds)
+    minX, maxX, minY, maxY = (f32(b) for b in bounds)
+    twc = _mat_neg_rt_t(T)
+    tlc = _mat_rx_t(np.asarray(Tlw, np.float32), twc)
+    fwd = tlc[2] > mb and not mono
+    bwd = -tlc[2] > mb and not mono
+    blk = [bool(b) for b in blocked]
+    out = [-1] * len(kps)
+    hist = [[] for _ in range(30)]
+    nm = 0
+    th = f32(th)
+    for i in range(len(mps)):
+        mp = mps[i]
+        if not mp["valid"]:
+            continue
+        xc, yc, zc = _mat_rx_t(T, mp["pos"])
+        invzc = f32(1.0 / float(zc)) if zc != 0 else f32(math.copysign(math.inf, float(zc)))
+        if invzc < 0:
+            continue
+        u = f32(f32(f32(fx * xc) * invzc) + cx)
+        v = f32(f32(f32(fy * yc) * invzc) + cy)
+        if u < minX or u > maxX or v < minY or v > maxY:
+            continue
+        lo = int(mp["octave"])
+        rad = f32(th * f32(scale[lo]))
+        if fwd:
+            idxs = features_in_area(kps, cells, bounds, u, v, rad, lo, -1)
+        elif bwd:
+            idxs = features_in_area(kps, cells, bounds, u, v, rad, 0, lo)
+        else:
+            idxs = features_in_area(kps, cells, bounds, u, v, rad, lo - 1, lo + 1)
+        best, bi = 256, -1
+        for i2 in idxs:
+            if blk[i2]:
+                continue
+            if uright is not None and uright[i2] > 0:
+                ur = f32(u - f32(mbf * invzc))
+                if abs(f32(ur - f32(uright[i2]))) > rad:
+                    continue
+            d = hamming(mpdesc[i], desc[i2])
+            if d < best:
+                best, bi = d, i2
+        if best <= 100:
+            out[bi] = i
+            blk[bi] = bool(mp["obs_positive"])
+            nm += 1
+            if check_ori:
+                hist[rot_bin(mp["angle"], kps["angle"][bi])].append(bi)
+    if check_ori:
+        nm = _rot_filter(hist, out, nm)
+    return np.array(out, np.int32), nm
+
+
+def search_by_projection_keyframe(kps, desc, bounds, scale, sf, has_mp, cam, mps, mpdesc, th, orb_dist,
+                                  check_ori=True):
+    """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:1472-1599)."""
+    fx, fy, cx, cy, mb, mbf, T = _cam(cam)
+    cells = grid_cells(kps, bounds)
+    minX, maxX, minY, maxY = (f32(b) for b in bounds)
+    Ow = _mat_neg_rt_t(T)
+    taken = [bool(b) for b in has_mp]
+    out = [-1] * len(kps)
+    hist = [[] for _ in range(30)]
+    nm = 0
+    th = f32(th)
+    L = len(scale)
+    for i in range(len(mps)):
+        mp = mps[i]
+        if not mp["valid"]:
+            continue
+        xc, yc, zc = _mat_rx_t(T, mp["pos"])
+        invzc = f32(1.0 / float(zc)) if zc != 0 else f32(math.copysign(math.inf, float(zc)))
+        u = f32(f32(f32(fx * xc) * invzc) + cx)
+        v = f32(f32(f32(fy * yc) * invzc) + cy)
+        if u < minX or u > maxX or v < minY or v > maxY:
+            continue
+        PO = [f32(f32(mp["pos"][k]) - Ow[k]) for k in range(3)]
+        d3 = f32(_norm3(PO))
+        if d3 < f32(f32(0.8) * f32(mp["min_distance"])) or d3 > f32(f32(1.2) * f32(mp["max_distance"])):
+            continue
+        lvl = predict_scale(mp["max_distance"], d3, sf, L)
+        rad = f32(th * f32(scale[lvl]))
+        best, bi = 256, -1
+        for i2 in features_in_area(kps, cells, bounds, u, v, rad, lvl - 1, lvl + 1):
+            if taken[i2]:
+                continue
+            d = hamming(mpdesc[i], desc[i2])
+            if d < best:
+                best, bi = d, i2
+        if best <= orb_dist:
+            out[bi] = i
+            taken[bi] = True
+            nm += 1
+            if check_ori:
+                hist[rot_bin(mp["angle"], kps["angle"][bi])].append(bi)
+    if check_ori:
+        nm = _rot_filter(hist, out, nm)
+    return np.array(out, np.int32), nm
+
+
+def search_by_projection_sim3(kps, desc, bounds, scale, sf, cam, mps, mpdesc, th, matched=None):
+    """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (src/ORBmatcher.cc:290-403)."""
+    fx, fy, cx, cy, mb, mbf, S = _cam(cam)
+    cells = grid_cells(kps, bounds)
+    minX, maxX, minY, maxY = (f32(b) for b in bounds)
+    scw = f32(math.sqrt(_dot3(S[0:3], S[0:3])))
+    a = f32(1.0 / float(scw))
+    T = np.array([f32(f32(s * a) + f32(0)) for s in S], np.float32)
+    Ow = _mat_neg_rt_t(T)
+    taken = [False] * len(kps) if matched is None else [int(m) >= 0 for m in matched]
+    out = [-1] * len(kps)
+    nm = 0
+    L = len(scale)
+    for i in range(len(mps)):
+        mp = mps[i]
+        if not mp["valid"]:
+            continue
+        X, Y, Z = _mat_rx_t(T, mp["pos"])
+        if Z < 0.0:
+            continue
+        invz = f32(f32(1) / Z)
+        u = f32(f32(fx * f32(X * invz)) + cx)
+        v = f32(f32(fy * f32(Y * invz)) + cy)
+        if not (u >= minX and u < maxX and v >= minY and v < maxY):
+            continue
+        PO = [f32(f32(mp["pos"][k]) - Ow[k]) for k in range(3)]
+        dist = f32(_norm3(PO))
+        if dist < f32(f32(0.8) * f32(mp["min_distance"])) or dist > f32(f32(1.2) * f32(mp["max_distance"])):
+            continue
+        if _dot3(PO, mp["normal"]) < 0.5 * float(dist):
+            continue
+        lvl = predict_scale(mp["max_distance"], dist, sf, L)
+        rad = f32(f32(th) * f32(scale[lvl]))
+        best, bi = 256, -1
+        for idx in features_in_area(kps, cells, bounds, u, v, rad, -1, -1):
+            if taken[idx]:
+                continue
+            o = int(kps["octave"][idx])
+            if o < lvl - 1 or o > lvl:
+                continue
+            d = hamming(mpdesc[i], desc[idx])
+            if d < best:
+                best, bi = d, idx
+        if best <= 50:
+            out[bi] = i
+            taken[bi] = True
+            nm += 1
+    return np.array(out, np.int32), nm

@@ -5,6 +5,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -78,3 +79,50 @@ def test_descriptor_sincosf_matches_host_libm():
     rs, rc = O.sincosf(x)
     assert np.array_equal(s.view(np.uint32), rs.view(np.uint32))
     assert np.array_equal(c.view(np.uint32), rc.view(np.uint32))
+
+
+def test_predict_scale_thresholds_match_logf():
+    """MapPoint::PredictScale (src/MapPoint.cc:407-422) as the pose-projection kernels
+    evaluate it (thresholds on mfMaxDistance/dist found with the host logf) equals the
+    oracle's direct ceil(logf(ratio)/logf(sf)) on every float within 2^15 ulps of each
+    threshold, on a wide random sample and on the special values."""
+    import ctypes as C
+
+    from oracle import oracle as O
+    from orb_slam_cuda_amd import _lib
+    for sf, L in [(1.2, 8), (1.2, 12), (1.5, 5), (2.0, 4)]:
+        thr = np.zeros(16, np.float32)
+        _lib.check(_lib.lib().orbm_predict_scale_thresholds(C.c_float(sf), L, thr.ctypes.data_as(C.c_void_p)))
+        t = thr[:L - 1]
+        assert np.all(np.diff(t) > 0)
+        bits = t.view(np.uint32).astype(np.int64)
+        near = (bits[:, None] + np.arange(-(1 << 15), 1 << 15)[None, :]).reshape(-1).astype(np.uint32).view(np.float32)
+        rng = np.random.default_rng(L)
+        wide = np.exp(rng.uniform(-12, 12, 200000)).astype(np.float32)
+        special = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, 3.4e38, -1.0, 1.0], np.float32)
+        r = np.concatenate([near, wide, special])
+        with np.errstate(invalid="ignore"):
+            lvl = np.where(np.isinf(r), 0, (r[:, None] >= t[None, :]).sum(1))
+        assert np.array_equal(lvl, O.predict_scale_ratios(r, sf, L)), (sf, L)
+
+
+def test_prepare_pose_level_mode():
+    """orbm_prepare_pose: bForward / bBackward of the motion-model search (src/ORBmatcher.cc:1338-1349)
+    and the Sim3 decomposition (:298-304)."""
+    import ctypes as C
+
+    from orb_slam_cuda_amd import _lib
+    T = np.eye(4, dtype=np.float32)[:3]
+    cam = _lib.camera(700, 700, 600, 180, 0.5, 350, T)
+    for dz, mono, want in [(1.0, 0, 1), (-1.0, 0, 2), (0.2, 0, 0), (1.0, 1, 0)]:
+        Tl = T.copy()
+        Tl[2, 3] = dz
+        p = _lib.OrbmPose()
+        _lib.check(_lib.lib().orbm_prepare_pose(_lib.ORBM_PROJ_LAST_FRAME, C.byref(cam),
+                                                Tl.ctypes.data_as(C.c_void_p), mono, C.byref(p)), matcher=True)
+        assert p.level_mode == want
+    S = T.copy() * 2.0
+    p = _lib.OrbmPose()
+    _lib.check(_lib.lib().orbm_prepare_pose(_lib.ORBM_PROJ_SIM3, C.byref(_lib.camera(700, 700, 600, 180, 0.5, 350, S)),
+                                            None, 0, C.byref(p)), matcher=True)
+    assert np.allclose(np.array(p.Rt).reshape(3, 4), T)

@@ -376,3 +376,59 @@ def test_projection_cases_exercise_blocking(O):
     seq = refpy.search_by_projection(kps, desc, ur, bounds, scale, blocked, mps, mpd, 3.0, 0.9)
     ind = refpy.search_by_projection(kps, desc, ur, bounds, scale, blocked, mps, mpd, 3.0, 0.9, independent=True)
     assert seq[1] != ind[1] or not np.array_equal(seq[0], ind[0])
+
+
+# ------------------------------------- SearchByProjection, pose overloads (§8f row 3b)
+@pytest.mark.parametrize("seed,motion,stereo,th", [(1, "none", False, 7.0), (2, "forward", True, 7.0),
+                                                   (3, "backward", True, 15.0), (4, "none", True, 7.0)])
+def test_search_by_projection_last_frame_matches_refpy(O, seed, motion, stereo, th):
+    from posecase import last_frame_case
+    c = last_frame_case(O, seed, 640, 240, 600, 700, stereo=stereo, motion=motion)
+    args = (c["kps"], c["desc"], c["uright"], c["bounds"], c["scale"], c["blocked"], c["cam"], c["Tlw"], c["mps"],
+            c["mpdesc"], th, c["mono"])
+    out, nm = O.search_by_projection_last_frame(*args)
+    eout, enm = refpy.search_by_projection_last_frame(*args)
+    assert nm == enm and np.array_equal(out, eout)
+    assert nm > 100 and (out == -2).any()  # rotation check clears some assignments
+    assert (out[c["blocked"] == 1] == -1).all()
+
+
+def test_search_by_projection_last_frame_no_rotation_check(O):
+    from posecase import last_frame_case
+    c = last_frame_case(O, 5, 640, 240, 600, 700)
+    args = (c["kps"], c["desc"], c["uright"], c["bounds"], c["scale"], c["blocked"], c["cam"], c["Tlw"], c["mps"],
+            c["mpdesc"], 7.0, c["mono"], False)
+    out, nm = O.search_by_projection_last_frame(*args)
+    eout, enm = refpy.search_by_projection_last_frame(*args)
+    assert nm == enm and np.array_equal(out, eout) and not (out == -2).any()
+
+
+@pytest.mark.parametrize("seed,th,orb_dist", [(1, 10.0, 100), (2, 3.0, 64)])
+def test_search_by_projection_keyframe_matches_refpy(O, seed, th, orb_dist):
+    from posecase import keyframe_case
+    c = keyframe_case(O, seed, 640, 240, 600, 700)
+    args = (c["kps"], c["desc"], c["bounds"], c["scale"], 1.2, c["has_mp"], c["cam"], c["mps"], c["mpdesc"], th,
+            orb_dist)
+    out, nm = O.search_by_projection_keyframe(*args)
+    eout, enm = refpy.search_by_projection_keyframe(*args)
+    assert nm == enm and np.array_equal(out, eout)
+    assert nm > 100 and (out[c["has_mp"] == 1] == -1).all()
+
+
+@pytest.mark.parametrize("seed,th,s", [(1, 10, 1.3), (2, 5, 0.7)])
+def test_search_by_projection_sim3_matches_refpy(O, seed, th, s):
+    from posecase import sim3_case
+    c = sim3_case(O, seed, 640, 240, 600, 900, s=s)
+    args = (c["kps"], c["desc"], c["bounds"], c["scale"], 1.2, c["cam"], c["mps"], c["mpdesc"], th, c["matched"])
+    out, nm = O.search_by_projection_sim3(*args)
+    eout, enm = refpy.search_by_projection_sim3(*args)
+    assert nm == enm and np.array_equal(out, eout)
+    assert nm > 100 and (out[c["matched"] >= 0] == -1).all()
+
+
+def test_predict_scale_known_answers(O):
+    """PredictScale: ceil(log(maxd/dist)/log(1.2)) clamped to [0, 7]."""
+    for maxd, dist, want in [(10.0, 10.0, 0), (10.0, 9.0, 1), (10.0, 10 / 1.2 ** 3 * 1.01, 3), (10.0, 0.01, 7),
+                             (10.0, 20.0, 0), (10.0, 0.0, 0)]:
+        assert O.predict_scale(maxd, dist) == want, (maxd, dist)
+        assert refpy.predict_scale(maxd, dist, 1.2, 8) == want
