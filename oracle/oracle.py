@@ -346,3 +346,76 @@ def search_by_projection_sim3(kps, desc, bounds, scale, scale_factor, cam, mps, 
     f(_p(kps), _p(desc), len(kps), *[C.c_float(b) for b in bounds], _p(sc), len(sc), scale_factor,
       C.byref(cam), _p(mps), _p(mpd), len(mps), int(th), None if mt is None else _p(mt), _p(out), C.byref(nm))
     return out[:len(kps)].copy(), nm.value
+
+
+# ------------------------------------- Fuse, SearchBySim3, SearchForTriangulation
+def fuse(kps, desc, uright, bounds, scale, inv_sigma2, scale_factor, cam, mps, mpdesc, th):
+    """Fuse(pKF, vpMapPoints, th), match part: (out[i] = bestIdx or -1, nfused)."""
+    kps, desc, mps, mpd, _, nm = _pose_common(kps, desc, mps, mpdesc)
+    out = np.zeros(max(len(mps), 1), np.int32)
+    ur = None if uright is None else np.ascontiguousarray(uright, np.float32)
+    sc = np.ascontiguousarray(scale, np.float32); isg = np.ascontiguousarray(inv_sigma2, np.float32)
+    f = lib().orc_fuse
+    f.argtypes = ([C.c_void_p] * 2 + [C.c_int, C.c_void_p] + [C.c_float] * 4 + [C.c_void_p] * 2
+                  + [C.c_int, C.c_float] + [C.c_void_p] * 3 + [C.c_int, C.c_float, C.c_void_p, C.c_void_p])
+    f(_p(kps), _p(desc), len(kps), None if ur is None else _p(ur), *[C.c_float(b) for b in bounds], _p(sc),
+      _p(isg), len(sc), scale_factor, C.byref(cam), _p(mps), _p(mpd), len(mps), th, _p(out), C.byref(nm))
+    return out[:len(mps)].copy(), nm.value
+
+
+def fuse_sim3(kps, desc, bounds, scale, scale_factor, cam, mps, mpdesc, th):
+    """Fuse(pKF, Scw, vpPoints, th, vpReplacePoint), match part: (out[i] = bestIdx or -1, nfused)."""
+    kps, desc, mps, mpd, _, nm = _pose_common(kps, desc, mps, mpdesc)
+    out = np.zeros(max(len(mps), 1), np.int32)
+    sc = np.ascontiguousarray(scale, np.float32)
+    f = lib().orc_fuse_sim3
+    f.argtypes = ([C.c_void_p] * 2 + [C.c_int] + [C.c_float] * 4 + [C.c_void_p, C.c_int, C.c_float]
+                  + [C.c_void_p] * 3 + [C.c_int, C.c_float, C.c_void_p, C.c_void_p])
+    f(_p(kps), _p(desc), len(kps), *[C.c_float(b) for b in bounds], _p(sc), len(sc), scale_factor, C.byref(cam),
+      _p(mps), _p(mpd), len(mps), th, _p(out), C.byref(nm))
+    return out[:len(mps)].copy(), nm.value
+
+
+def search_by_sim3(kf1, kf2, cam1, s12, R12, t12, th, scale_factor=1.2):
+    """SearchBySim3. kf1/kf2: dicts with kps, desc, bounds, scale, Tcw (3x4), mps, mpdesc (one record per
+    keypoint). Returns (match1, nfound, vnMatch1, vnMatch2)."""
+    k1 = np.ascontiguousarray(kf1["kps"], KP_DTYPE); k2 = np.ascontiguousarray(kf2["kps"], KP_DTYPE)
+    d1 = np.ascontiguousarray(kf1["desc"], np.uint8); d2 = np.ascontiguousarray(kf2["desc"], np.uint8)
+    b1 = np.asarray(kf1["bounds"], np.float32); b2 = np.asarray(kf2["bounds"], np.float32)
+    s1 = np.ascontiguousarray(kf1["scale"], np.float32); s2 = np.ascontiguousarray(kf2["scale"], np.float32)
+    T1 = np.ascontiguousarray(kf1["Tcw"], np.float32).reshape(-1); T2 = np.ascontiguousarray(kf2["Tcw"], np.float32).reshape(-1)
+    m1 = np.ascontiguousarray(kf1["mps"], MPW_DTYPE); m2 = np.ascontiguousarray(kf2["mps"], MPW_DTYPE)
+    q1 = np.ascontiguousarray(kf1["mpdesc"], np.uint8); q2 = np.ascontiguousarray(kf2["mpdesc"], np.uint8)
+    R = np.ascontiguousarray(R12, np.float32).reshape(-1); t = np.ascontiguousarray(t12, np.float32).reshape(-1)
+    match1 = np.zeros(max(len(k1), 1), np.int32); v1 = np.zeros(max(len(k1), 1), np.int32)
+    v2 = np.zeros(max(len(k2), 1), np.int32); nf = C.c_int(0)
+    f = lib().orc_search_by_sim3
+    f.argtypes = ([C.c_void_p] * 2 + [C.c_int] + [C.c_void_p] * 4 + [C.c_int] + [C.c_void_p] * 2
+                  + [C.c_int, C.c_float] + [C.c_void_p] * 3 + [C.c_float] + [C.c_void_p] * 6 + [C.c_float]
+                  + [C.c_void_p] * 4)
+    f(_p(k1), _p(d1), len(k1), _p(b1), _p(s1), _p(k2), _p(d2), len(k2), _p(b2), _p(s2), len(s1), scale_factor,
+      C.byref(cam1), _p(T1), _p(T2), s12, _p(R), _p(t), _p(m1), _p(q1), _p(m2), _p(q2), th, _p(match1), _p(v1),
+      _p(v2), C.byref(nf))
+    return match1[:len(k1)].copy(), nf.value, v1[:len(k1)].copy(), v2[:len(k2)].copy()
+
+
+def search_for_triangulation(kf1, kf2, cw1, T2w, cam2, sigma2, F12, only_stereo=False, check_ori=True):
+    """SearchForTriangulation. kf: dicts with kps, desc, uright, has_mp and fv = (nodes, off, idx) CSR;
+    kf2 also scale. Returns (matches12, nmatches)."""
+    def arrs(kf):
+        nodes, off, idx = kf["fv"]
+        return (np.ascontiguousarray(kf["kps"], KP_DTYPE), np.ascontiguousarray(kf["desc"], np.uint8),
+                np.ascontiguousarray(kf["uright"], np.float32), np.ascontiguousarray(kf["has_mp"], np.uint8),
+                np.ascontiguousarray(nodes, np.uint32), np.ascontiguousarray(off, np.int32),
+                np.ascontiguousarray(idx, np.int32) if len(idx) else np.zeros(1, np.int32))
+    a1, a2 = arrs(kf1), arrs(kf2)
+    out = np.zeros(max(len(a1[0]), 1), np.int32); nm = C.c_int(0)
+    vec = lambda a: np.ascontiguousarray(a, np.float32).reshape(-1)
+    cw, T, cm, sc2, sg2, F = vec(cw1), vec(T2w), vec(cam2), vec(kf2["scale"]), vec(sigma2), vec(F12)
+    f = lib().orc_search_for_triangulation
+    f.argtypes = ([C.c_void_p] * 4 + [C.c_int] + [C.c_void_p] * 3 + [C.c_int]) * 2 + [C.c_void_p] * 6 + \
+        [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    f(_p(a1[0]), _p(a1[1]), _p(a1[2]), _p(a1[3]), len(a1[0]), _p(a1[4]), _p(a1[5]), _p(a1[6]), len(a1[4]),
+      _p(a2[0]), _p(a2[1]), _p(a2[2]), _p(a2[3]), len(a2[0]), _p(a2[4]), _p(a2[5]), _p(a2[6]), len(a2[4]),
+      _p(cw), _p(T), _p(cm), _p(sc2), _p(sg2), _p(F), int(only_stereo), int(check_ori), _p(out), C.byref(nm))
+    return out[:len(a1[0])].copy(), nm.value

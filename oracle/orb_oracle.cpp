@@ -1564,3 +1564,333 @@ int orc_search_by_projection_sim3(const orc_kp* kps, const uint8_t* desc, int n,
 }
 
 }  // extern "C"
+
+// ===================================== Fuse, SearchBySim3, SearchForTriangulation
+namespace {
+
+// Sim3 decomposition of the loop-closing overloads (src/ORBmatcher.cc:298-304,
+// 986-992): scw = sqrt(row0 . row0) (double dot), Rcw = sRcw/scw, tcw = t/scw.
+void decompose_sim3(const float* S, float* T) {
+  const float scw = std::sqrt(PoseMath::dot3(S, S));
+  const float a = (float)(1.0 / (double)scw);
+  for (int k = 0; k < 12; ++k) T[k] = S[k] * a + 0.0f;
+}
+
+// KeyFrame::IsInImage (src/KeyFrame.cc:619-622)
+inline bool in_image(float u, float v, float min_x, float max_x, float min_y, float max_y) {
+  return u >= min_x && u < max_x && v >= min_y && v < max_y;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Fuse(KeyFrame*, const vector<MapPoint*>&, th) (src/ORBmatcher.cc:825-975), match part.
+int orc_fuse(const orc_kp* kps, const uint8_t* desc, int n, const float* uright, float min_x, float max_x,
+             float min_y, float max_y, const float* scale, const float* inv_sigma2, int nlevels, float scale_factor,
+             const orc_camera* kf, const orc_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th, int* out,
+             int* nfused) {
+  GridFrame F(kps, desc, n, min_x, max_x, min_y, max_y);
+  const float mfLogScaleFactor = std::log(scale_factor);
+  const float* T = kf->Tcw;
+  float Ow[3];
+  PoseMath::neg_rt_t(T, Ow);  // pKF->GetCameraCenter()
+  const float &fx = kf->fx, &fy = kf->fy, &cx = kf->cx, &cy = kf->cy, &bf = kf->mbf;
+  int nFused = 0;
+  for (int i = 0; i < nmp; i++) {
+    out[i] = -1;
+    const orc_map_point_world& pMP = mps[i];
+    if (!pMP.valid) continue;  // !pMP || isBad() || IsInKeyFrame(pKF)
+    float p3Dc[3];
+    PoseMath::rx_plus_t(T, pMP.pos, p3Dc);
+    if (p3Dc[2] < 0.0f) continue;
+    const float invz = 1 / p3Dc[2];
+    const float x = p3Dc[0] * invz;
+    const float y = p3Dc[1] * invz;
+    const float u = fx * x + cx;
+    const float v = fy * y + cy;
+    if (!in_image(u, v, min_x, max_x, min_y, max_y)) continue;
+    const float ur = u - bf * invz;
+    const float maxDistance = 1.2f * pMP.max_distance;
+    const float minDistance = 0.8f * pMP.min_distance;
+    float PO[3];
+    for (int k = 0; k < 3; ++k) PO[k] = pMP.pos[k] - Ow[k];
+    const float dist3D = PoseMath::norm3(PO);
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    if (PoseMath::dot3(PO, pMP.normal) < 0.5 * dist3D) continue;
+    const int nPredictedLevel = predict_scale(pMP.max_distance, dist3D, mfLogScaleFactor, nlevels);
+    const float radius = th * scale[nPredictedLevel];
+    const std::vector<size_t> vIndices = F.features_in_area(u, v, radius, -1, -1);
+    if (vIndices.empty()) continue;
+    const uint8_t* dMP = mpdesc + 32 * (size_t)i;
+    int bestDist = 256, bestIdx = -1;
+    for (size_t idx : vIndices) {
+      const KeyPoint& kp = kps[idx];
+      const int& kpLevel = kp.octave;
+      if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+      if (uright && uright[idx] >= 0) {
+        const float& kpx = kp.x;
+        const float& kpy = kp.y;
+        const float& kpr = uright[idx];
+        const float ex = u - kpx;
+        const float ey = v - kpy;
+        const float er = ur - kpr;
+        const float e2 = ex * ex + ey * ey + er * er;
+        if (e2 * inv_sigma2[kpLevel] > 7.8) continue;
+      } else {
+        const float ex = u - kp.x;
+        const float ey = v - kp.y;
+        const float e2 = ex * ex + ey * ey;
+        if (e2 * inv_sigma2[kpLevel] > 5.99) continue;
+      }
+      const int dist = descriptor_distance(dMP, desc + 32 * idx);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = (int)idx;
+      }
+    }
+    if (bestDist <= TH_LOW) {
+      out[i] = bestIdx;
+      nFused++;
+    }
+  }
+  *nfused = nFused;
+  return 0;
+}
+
+// Fuse(KeyFrame*, cv::Mat Scw, vpPoints, th, vpReplacePoint) (src/ORBmatcher.cc:977-1100), match part.
+int orc_fuse_sim3(const orc_kp* kps, const uint8_t* desc, int n, float min_x, float max_x, float min_y,
+                  float max_y, const float* scale, int nlevels, float scale_factor, const orc_camera* kf,
+                  const orc_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th, int* out, int* nfused) {
+  GridFrame F(kps, desc, n, min_x, max_x, min_y, max_y);
+  const float mfLogScaleFactor = std::log(scale_factor);
+  float T[12], Ow[3];
+  decompose_sim3(kf->Tcw, T);
+  PoseMath::neg_rt_t(T, Ow);
+  int nFused = 0;
+  for (int iMP = 0; iMP < nmp; iMP++) {
+    out[iMP] = -1;
+    const orc_map_point_world& pMP = mps[iMP];
+    if (!pMP.valid) continue;  // isBad() || spAlreadyFound.count(pMP)
+    float p3Dc[3];
+    PoseMath::rx_plus_t(T, pMP.pos, p3Dc);
+    if (p3Dc[2] < 0.0f) continue;
+    const float invz = 1.0 / p3Dc[2];
+    const float x = p3Dc[0] * invz;
+    const float y = p3Dc[1] * invz;
+    const float u = kf->fx * x + kf->cx;
+    const float v = kf->fy * y + kf->cy;
+    if (!in_image(u, v, min_x, max_x, min_y, max_y)) continue;
+    const float maxDistance = 1.2f * pMP.max_distance;
+    const float minDistance = 0.8f * pMP.min_distance;
+    float PO[3];
+    for (int k = 0; k < 3; ++k) PO[k] = pMP.pos[k] - Ow[k];
+    const float dist3D = PoseMath::norm3(PO);
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    if (PoseMath::dot3(PO, pMP.normal) < 0.5 * dist3D) continue;
+    const int nPredictedLevel = predict_scale(pMP.max_distance, dist3D, mfLogScaleFactor, nlevels);
+    const float radius = th * scale[nPredictedLevel];
+    const std::vector<size_t> vIndices = F.features_in_area(u, v, radius, -1, -1);
+    if (vIndices.empty()) continue;
+    const uint8_t* dMP = mpdesc + 32 * (size_t)iMP;
+    int bestDist = INT_MAX, bestIdx = -1;
+    for (size_t idx : vIndices) {
+      const int& kpLevel = kps[idx].octave;
+      if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+      int dist = descriptor_distance(dMP, desc + 32 * idx);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = (int)idx;
+      }
+    }
+    if (bestDist <= TH_LOW) {
+      out[iMP] = bestIdx;
+      nFused++;
+    }
+  }
+  *nfused = nFused;
+  return 0;
+}
+
+// SearchBySim3 (src/ORBmatcher.cc:1102-1326).
+int orc_search_by_sim3(const orc_kp* kps1, const uint8_t* desc1, int n1, const float* bounds1, const float* scale1,
+                       const orc_kp* kps2, const uint8_t* desc2, int n2, const float* bounds2, const float* scale2,
+                       int nlevels, float scale_factor, const orc_camera* cam1, const float* T1w, const float* T2w,
+                       float s12, const float* R12, const float* t12, const orc_map_point_world* mps1,
+                       const uint8_t* mpdesc1, const orc_map_point_world* mps2, const uint8_t* mpdesc2, float th,
+                       int* match1, int* vnMatch1_out, int* vnMatch2_out, int* nfound) {
+  GridFrame F1(kps1, desc1, n1, bounds1[0], bounds1[1], bounds1[2], bounds1[3]);
+  GridFrame F2(kps2, desc2, n2, bounds2[0], bounds2[1], bounds2[2], bounds2[3]);
+  const float mfLogScaleFactor = std::log(scale_factor);
+  const float &fx = cam1->fx, &fy = cam1->fy, &cx = cam1->cx, &cy = cam1->cy;
+  // sR12 = s12*R12; sR21 = (1.0/s12)*R12.t(); t21 = -sR21*t12 (convertTo scaling, small gemm)
+  float S12[12], S21[12];
+  const float a12 = (float)(double)s12, a21 = (float)(1.0 / (double)s12);
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      S12[4 * r + c] = R12[3 * r + c] * a12 + 0.0f;
+      S21[4 * r + c] = R12[3 * c + r] * a21 + 0.0f;
+    }
+  for (int r = 0; r < 3; ++r) {
+    S12[4 * r + 3] = t12[r];
+    const float t = S21[4 * r] * t12[0] + S21[4 * r + 1] * t12[1] + S21[4 * r + 2] * t12[2];
+    S21[4 * r + 3] = (float)((double)t * -1.0 + 0.0 * 0.0);
+  }
+  std::vector<int> vnMatch1(n1, -1), vnMatch2(n2, -1);
+  // one direction: points of A through Taw then S (into B's camera), matched in B
+  auto dir = [&](const orc_map_point_world* mps, const uint8_t* mpdesc, int nA, const float* Taw, const float* S,
+                 const GridFrame& FB, const orc_kp* kpsB, const float* bB, const float* scaleB, std::vector<int>& vm) {
+    for (int i1 = 0; i1 < nA; i1++) {
+      const orc_map_point_world& pMP = mps[i1];
+      if (!pMP.valid) continue;  // !pMP || vbAlreadyMatched || isBad()
+      float p3Dc1[3], p3Dc2[3];
+      PoseMath::rx_plus_t(Taw, pMP.pos, p3Dc1);
+      PoseMath::rx_plus_t(S, p3Dc1, p3Dc2);
+      if (p3Dc2[2] < 0.0) continue;
+      const float invz = 1.0 / p3Dc2[2];
+      const float x = p3Dc2[0] * invz;
+      const float y = p3Dc2[1] * invz;
+      const float u = fx * x + cx;
+      const float v = fy * y + cy;
+      if (!in_image(u, v, bB[0], bB[1], bB[2], bB[3])) continue;
+      const float maxDistance = 1.2f * pMP.max_distance;
+      const float minDistance = 0.8f * pMP.min_distance;
+      const float dist3D = PoseMath::norm3(p3Dc2);
+      if (dist3D < minDistance || dist3D > maxDistance) continue;
+      const int nPredictedLevel = predict_scale(pMP.max_distance, dist3D, mfLogScaleFactor, nlevels);
+      const float radius = th * scaleB[nPredictedLevel];
+      const std::vector<size_t> vIndices = FB.features_in_area(u, v, radius, -1, -1);
+      if (vIndices.empty()) continue;
+      const uint8_t* dMP = mpdesc + 32 * (size_t)i1;
+      int bestDist = INT_MAX, bestIdx = -1;
+      for (size_t idx : vIndices) {
+        const KeyPoint& kp = kpsB[idx];
+        if (kp.octave < nPredictedLevel - 1 || kp.octave > nPredictedLevel) continue;
+        const int dist = descriptor_distance(dMP, FB.desc + 32 * idx);
+        if (dist < bestDist) {
+          bestDist = dist;
+          bestIdx = (int)idx;
+        }
+      }
+      if (bestDist <= TH_HIGH) vm[i1] = bestIdx;
+    }
+  };
+  dir(mps1, mpdesc1, n1, T1w, S21, F2, kps2, bounds2, scale2, vnMatch1);
+  dir(mps2, mpdesc2, n2, T2w, S12, F1, kps1, bounds1, scale1, vnMatch2);
+  int nFound = 0;
+  for (int i1 = 0; i1 < n1; i1++) {
+    match1[i1] = -1;
+    const int idx2 = vnMatch1[i1];
+    if (idx2 >= 0) {
+      const int idx1 = vnMatch2[idx2];
+      if (idx1 == i1) {
+        match1[i1] = idx2;
+        nFound++;
+      }
+    }
+  }
+  if (vnMatch1_out) std::copy(vnMatch1.begin(), vnMatch1.end(), vnMatch1_out);
+  if (vnMatch2_out) std::copy(vnMatch2.begin(), vnMatch2.end(), vnMatch2_out);
+  *nfound = nFound;
+  return 0;
+}
+
+// SearchForTriangulation (src/ORBmatcher.cc:657-823) with CheckDistEpipolarLine (:140-157).
+int orc_search_for_triangulation(const orc_kp* kps1, const uint8_t* desc1, const float* uright1,
+                                 const uint8_t* has_mp1, int n1, const uint32_t* fv1_nodes, const int* fv1_off,
+                                 const int* fv1_idx, int fv1_n, const orc_kp* kps2, const uint8_t* desc2,
+                                 const float* uright2, const uint8_t* has_mp2, int n2, const uint32_t* fv2_nodes,
+                                 const int* fv2_off, const int* fv2_idx, int fv2_n, const float* cw1,
+                                 const float* T2w, const float* cam2, const float* scale2, const float* sigma2,
+                                 const float* F12, int only_stereo, int check_ori, int* matches12, int* nmatches_out) {
+  // Compute epipole in second image
+  float C2[3];
+  PoseMath::rx_plus_t(T2w, cw1, C2);  // C2 = R2w*Cw + t2w
+  const float invz = 1.0f / C2[2];
+  const float ex = cam2[0] * C2[0] * invz + cam2[2];
+  const float ey = cam2[1] * C2[1] * invz + cam2[3];
+  auto check_epipolar = [&](const KeyPoint& kp1, const KeyPoint& kp2) {
+    const float a = kp1.x * F12[0] + kp1.y * F12[3] + F12[6];
+    const float b = kp1.x * F12[1] + kp1.y * F12[4] + F12[7];
+    const float c = kp1.x * F12[2] + kp1.y * F12[5] + F12[8];
+    const float num = a * kp2.x + b * kp2.y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return dsqr < 3.84 * sigma2[kp2.octave];
+  };
+  int nmatches = 0;
+  std::vector<bool> vbMatched2(n2, false);
+  std::vector<int> vMatches12(n1, -1);
+  std::vector<int> rotHist[HISTO_LENGTH];
+  const float factor = 1.0f / HISTO_LENGTH;
+  int f1 = 0, f2 = 0;
+  while (f1 < fv1_n && f2 < fv2_n) {
+    if (fv1_nodes[f1] == fv2_nodes[f2]) {
+      for (int p1 = fv1_off[f1]; p1 < fv1_off[f1 + 1]; p1++) {
+        const size_t idx1 = fv1_idx[p1];
+        if (has_mp1[idx1]) continue;  // already a MapPoint
+        const bool bStereo1 = uright1[idx1] >= 0;
+        if (only_stereo)
+          if (!bStereo1) continue;
+        const KeyPoint& kp1 = kps1[idx1];
+        const uint8_t* d1 = desc1 + 32 * idx1;
+        int bestDist = TH_LOW;
+        int bestIdx2 = -1;
+        for (int p2 = fv2_off[f2]; p2 < fv2_off[f2 + 1]; p2++) {
+          const size_t idx2 = fv2_idx[p2];
+          if (vbMatched2[idx2] || has_mp2[idx2]) continue;
+          const bool bStereo2 = uright2[idx2] >= 0;
+          if (only_stereo)
+            if (!bStereo2) continue;
+          const int dist = descriptor_distance(d1, desc2 + 32 * idx2);
+          if (dist > TH_LOW || dist > bestDist) continue;
+          const KeyPoint& kp2 = kps2[idx2];
+          if (!bStereo1 && !bStereo2) {
+            const float distex = ex - kp2.x;
+            const float distey = ey - kp2.y;
+            if (distex * distex + distey * distey < 100 * scale2[kp2.octave]) continue;
+          }
+          if (check_epipolar(kp1, kp2)) {
+            bestIdx2 = (int)idx2;
+            bestDist = dist;
+          }
+        }
+        if (bestIdx2 >= 0) {
+          const KeyPoint& kp2 = kps2[bestIdx2];
+          vMatches12[idx1] = bestIdx2;
+          nmatches++;
+          if (check_ori) {
+            float rot = kp1.angle - kp2.angle;
+            if (rot < 0.0) rot += 360.0f;
+            int bin = round(rot * factor);
+            if (bin == HISTO_LENGTH) bin = 0;
+            rotHist[bin].push_back((int)idx1);
+          }
+        }
+      }
+      f1++;
+      f2++;
+    } else if (fv1_nodes[f1] < fv2_nodes[f2]) {
+      f1 = (int)(std::lower_bound(fv1_nodes + f1, fv1_nodes + fv1_n, fv2_nodes[f2]) - fv1_nodes);
+    } else {
+      f2 = (int)(std::lower_bound(fv2_nodes + f2, fv2_nodes + fv2_n, fv1_nodes[f1]) - fv2_nodes);
+    }
+  }
+  if (check_ori) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    compute_three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+      if (i == ind1 || i == ind2 || i == ind3) continue;
+      for (size_t j = 0, jend = rotHist[i].size(); j < jend; j++) {
+        vMatches12[rotHist[i][j]] = -1;
+        nmatches--;
+      }
+    }
+  }
+  for (int i = 0; i < n1; ++i) matches12[i] = vMatches12[i];
+  *nmatches_out = nmatches;
+  return 0;
+}
+
+}  // extern "C"

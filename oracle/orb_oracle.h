@@ -196,6 +196,53 @@ int orc_search_by_projection_sim3(const orc_kp* kps, const uint8_t* desc, int n,
                                   const orc_camera* kf, const orc_map_point_world* mps, const uint8_t* mpdesc,
                                   int nmp, int th, const int* matched, int* out, int* out_nmatches);
 
+/* Fuse(pKF, vpMapPoints, th) (src/ORBmatcher.cc:825-975), the match part:
+ * out[i] = bestIdx where point i (valid = pMP && !isBad() &&
+ * !IsInKeyFrame(pKF) at call time) matches with bestDist <= TH_LOW, else -1.
+ * uright = pKF->mvuRight; inv_sigma2 = mvInvLevelSigma2. The side effects
+ * (Replace / AddObservation / AddMapPoint, :935-957) are the caller's.
+ * Returns via *nfused the number of matched points. */
+int orc_fuse(const orc_kp* kps, const uint8_t* desc, int n, const float* uright, float min_x, float max_x,
+             float min_y, float max_y, const float* scale, const float* inv_sigma2, int nlevels, float scale_factor,
+             const orc_camera* kf, const orc_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th, int* out,
+             int* nfused);
+
+/* Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (:977-1100), the match part:
+ * out[i] = bestIdx (bestDist <= TH_LOW) for valid points (!isBad() and not
+ * in pKF->GetMapPoints()), else -1; kf->Tcw = Scw rows 0..2. */
+int orc_fuse_sim3(const orc_kp* kps, const uint8_t* desc, int n, float min_x, float max_x, float min_y,
+                  float max_y, const float* scale, int nlevels, float scale_factor, const orc_camera* kf,
+                  const orc_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th, int* out, int* nfused);
+
+/* SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (:1102-1326).
+ * Per keyframe: keypoints, descriptors, grid bounds, mvScaleFactors, Tcw
+ * rows 0..2, and one map point record per keypoint (valid = pMP &&
+ * !vbAlreadyMatched && !isBad()). cam1 = pKF1's fx, fy, cx, cy (used for
+ * both projections, as the reference does). match1[i1] = idx2 for the
+ * new mutual matches (vpMatches12[i1] = vpMapPoints2[idx2]), else -1;
+ * vnMatch1 / vnMatch2 (optional) receive the one-directional picks. */
+int orc_search_by_sim3(const orc_kp* kps1, const uint8_t* desc1, int n1, const float* bounds1, const float* scale1,
+                       const orc_kp* kps2, const uint8_t* desc2, int n2, const float* bounds2, const float* scale2,
+                       int nlevels, float scale_factor, const orc_camera* cam1, const float* T1w, const float* T2w,
+                       float s12, const float* R12, const float* t12, const orc_map_point_world* mps1,
+                       const uint8_t* mpdesc1, const orc_map_point_world* mps2, const uint8_t* mpdesc2, float th,
+                       int* match1, int* vnMatch1, int* vnMatch2, int* nfound);
+
+/* SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+ * (:657-823, CheckDistEpipolarLine :140-157). Per keyframe: keypoints,
+ * descriptors, mvuRight, has_mp (GetMapPoint(idx) != NULL), FeatureVector as
+ * CSR. cw1 = pKF1->GetCameraCenter(); T2w = pKF2 Tcw rows 0..2; cam2 =
+ * pKF2's fx, fy, cx, cy; scale2 / sigma2 = pKF2->mvScaleFactors /
+ * mvLevelSigma2; F12 row-major 3x3. matches12[idx1] = idx2 or -1
+ * (vMatchedPairs in idx1 order); returns the count via *nmatches. */
+int orc_search_for_triangulation(const orc_kp* kps1, const uint8_t* desc1, const float* uright1,
+                                 const uint8_t* has_mp1, int n1, const uint32_t* fv1_nodes, const int* fv1_off,
+                                 const int* fv1_idx, int fv1_n, const orc_kp* kps2, const uint8_t* desc2,
+                                 const float* uright2, const uint8_t* has_mp2, int n2, const uint32_t* fv2_nodes,
+                                 const int* fv2_off, const int* fv2_idx, int fv2_n, const float* cw1,
+                                 const float* T2w, const float* cam2, const float* scale2, const float* sigma2,
+                                 const float* F12, int only_stereo, int check_ori, int* matches12, int* nmatches);
+
 #ifdef __cplusplus
 }
 #endif

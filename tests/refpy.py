@@ -813,3 +813,235 @@ def search_by_projection_sim3(kps, desc, bounds, scale, sf, cam, mps, mpdesc, th
             taken[bi] = True
             nm += 1
     return np.array(out, np.int32), nm
+
+
+# ------------------------------------ Fuse, SearchBySim3, SearchForTriangulation
+def _in_image(u, v, bounds):
+    minX, maxX, minY, maxY = (f32(b) for b in bounds)
+    return u >= minX and u < maxX and v >= minY and v < maxY
+
+
+def _sim3_T(S):
+    S = np.asarray(S, np.float32).reshape(-1)
+    scw = f32(math.sqrt(_dot3(S[0:3], S[0:3])))
+    a = f32(1.0 / float(scw))
+    return np.array([f32(f32(s * a) + f32(0)) for s in S], np.float32)
+
+
+def _dist_ok(mp, dist):
+    return not (dist < f32(f32(0.8) * f32(mp["min_distance"])) or dist > f32(f32(1.2) * f32(mp["max_distance"])))
+
+
+def _kf_best(kps, desc, cells, bounds, u, v, rad, lvl, dmp, init, extra=None):
+    best, bi = init, -1
+    for idx in features_in_area(kps, cells, bounds, u, v, rad, -1, -1):
+        o = int(kps["octave"][idx])
+        if o < lvl - 1 or o > lvl:
+            continue
+        if extra is not None and not extra(idx):
+            continue
+        d = hamming(dmp, desc[idx])
+        if d < best:
+            best, bi = d, idx
+    return best, bi
+
+
+def fuse(kps, desc, uright, bounds, scale, inv_sigma2, sf, cam, mps, mpdesc, th):
+    """Fuse(pKF, vpMapPoints, th) (src/ORBmatcher.cc:825-930), match part."""
+    fx, fy, cx, cy, mb, bf, T = _cam(cam)
+    cells = grid_cells(kps, bounds)
+    Ow = _mat_neg_rt_t(T)
+    L = len(scale)
+    out = [-1] * len(mps)
+    nf = 0
+    for i in range(len(mps)):
+        mp = mps[i]
+        if not mp["valid"]:
+            continue
+        X, Y, Z = _mat_rx_t(T, mp["pos"])
+        if Z < f32(0):
+            continue
+        invz = f32(f32(1) / Z)
+        u = f32(f32(fx * f32(X * invz)) + cx)
+        v = f32(f32(fy * f32(Y * invz)) + cy)
+        if not _in_image(u, v, bounds):
+            continue
+        ur = f32(u - f32(bf * invz))
+        PO = [f32(f32(mp["pos"][k]) - Ow[k]) for k in range(3)]
+        dist = f32(_norm3(PO))
+        if not _dist_ok(mp, dist) or _dot3(PO, mp["normal"]) < 0.5 * float(dist):
+            continue
+        lvl = predict_scale(mp["max_distance"], dist, sf, L)
+        rad = f32(f32(th) * f32(scale[lvl]))
+
+        def reproj(idx):
+            o = int(kps["octave"][idx])
+            ex = f32(u - f32(kps["x"][idx]))
+            ey = f32(v - f32(kps["y"][idx]))
+            if uright is not None and uright[idx] >= 0:
+                er = f32(ur - f32(uright[idx]))
+                e2 = f32(f32(f32(ex * ex) + f32(ey * ey)) + f32(er * er))
+                return not float(f32(e2 * f32(inv_sigma2[o]))) > 7.8
+            e2 = f32(f32(ex * ex) + f32(ey * ey))
+            return not float(f32(e2 * f32(inv_sigma2[o]))) > 5.99
+        best, bi = _kf_best(kps, desc, cells, bounds, u, v, rad, lvl, mpdesc[i], 256, reproj)
+        if best <= 50:
+            out[i] = bi
+            nf += 1
+    return np.array(out, np.int32), nf
+
+
+def fuse_sim3(kps, desc, bounds, scale, sf, cam, mps, mpdesc, th):
+    """Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (src/ORBmatcher.cc:977-1081), match part."""
+    fx, fy, cx, cy, mb, mbf, S = _cam(cam)
+    T = _sim3_T(S)
+    cells = grid_cells(kps, bounds)
+    Ow = _mat_neg_rt_t(T)
+    L = len(scale)
+    out = [-1] * len(mps)
+    nf = 0
+    for i in range(len(mps)):
+        mp = mps[i]
+        if not mp["valid"]:
+            continue
+        X, Y, Z = _mat_rx_t(T, mp["pos"])
+        if Z < f32(0):
+            continue
+        invz = f32(1.0 / float(Z))
+        u = f32(f32(fx * f32(X * invz)) + cx)
+        v = f32(f32(fy * f32(Y * invz)) + cy)
+        if not _in_image(u, v, bounds):
+            continue
+        PO = [f32(f32(mp["pos"][k]) - Ow[k]) for k in range(3)]
+        dist = f32(_norm3(PO))
+        if not _dist_ok(mp, dist) or _dot3(PO, mp["normal"]) < 0.5 * float(dist):
+            continue
+        lvl = predict_scale(mp["max_distance"], dist, sf, L)
+        rad = f32(f32(th) * f32(scale[lvl]))
+        best, bi = _kf_best(kps, desc, cells, bounds, u, v, rad, lvl, mpdesc[i], 1 << 31)
+        if best <= 50:
+            out[i] = bi
+            nf += 1
+    return np.array(out, np.int32), nf
+
+
+def search_by_sim3(kf1, kf2, cam1, s12, R12, t12, th, sf=1.2):
+    """SearchBySim3 (src/ORBmatcher.cc:1102-1326)."""
+    fx, fy, cx, cy = f32(cam1.fx), f32(cam1.fy), f32(cam1.cx), f32(cam1.cy)
+    R = np.asarray(R12, np.float32).reshape(3, 3)
+    t = np.asarray(t12, np.float32).reshape(3)
+    a12, a21 = f32(s12), f32(1.0 / float(f32(s12)))
+    S12 = np.zeros((3, 4), np.float32)
+    S21 = np.zeros((3, 4), np.float32)
+    for r in range(3):
+        for c in range(3):
+            S12[r, c] = f32(f32(R[r, c] * a12) + f32(0))
+            S21[r, c] = f32(f32(R[c, r] * a21) + f32(0))
+    for r in range(3):
+        S12[r, 3] = t[r]
+        d = f32(f32(f32(S21[r, 0] * t[0]) + f32(S21[r, 1] * t[1])) + f32(S21[r, 2] * t[2]))
+        S21[r, 3] = f32(-float(d))
+
+    def direction(A, B, S):
+        cells = grid_cells(B["kps"], B["bounds"])
+        L = len(B["scale"])
+        vm = [-1] * len(A["kps"])
+        for i in range(len(A["kps"])):
+            mp = A["mps"][i]
+            if not mp["valid"]:
+                continue
+            p1 = _mat_rx_t(np.asarray(A["Tcw"], np.float32), mp["pos"])
+            p2 = _mat_rx_t(S, p1)
+            if p2[2] < 0.0:
+                continue
+            invz = f32(1.0 / float(p2[2]))
+            u = f32(f32(fx * f32(p2[0] * invz)) + cx)
+            v = f32(f32(fy * f32(p2[1] * invz)) + cy)
+            if not _in_image(u, v, B["bounds"]):
+                continue
+            dist = f32(_norm3(p2))
+            if not _dist_ok(mp, dist):
+                continue
+            lvl = predict_scale(mp["max_distance"], dist, sf, L)
+            rad = f32(f32(th) * f32(B["scale"][lvl]))
+            best, bi = _kf_best(B["kps"], B["desc"], cells, B["bounds"], u, v, rad, lvl, A["mpdesc"][i], 1 << 31)
+            if best <= 100:
+                vm[i] = bi
+        return vm
+    v1 = direction(kf1, kf2, S21)
+    v2 = direction(kf2, kf1, S12)
+    m1 = [-1] * len(v1)
+    nf = 0
+    for i1, i2 in enumerate(v1):
+        if i2 >= 0 and v2[i2] == i1:
+            m1[i1] = i2
+            nf += 1
+    return np.array(m1, np.int32), nf
+
+
+def search_for_triangulation(kf1, kf2, cw1, T2w, cam2, sigma2, F12, only_stereo=False, check_ori=True):
+    """SearchForTriangulation (src/ORBmatcher.cc:657-823) + CheckDistEpipolarLine (:140-157)."""
+    C2 = _mat_rx_t(np.asarray(T2w, np.float32), np.asarray(cw1, np.float32))
+    invz = f32(f32(1) / C2[2])
+    cam2 = np.asarray(cam2, np.float32)
+    ex = f32(f32(f32(cam2[0] * C2[0]) * invz) + cam2[2])
+    ey = f32(f32(f32(cam2[1] * C2[1]) * invz) + cam2[3])
+    F = np.asarray(F12, np.float32).reshape(3, 3)
+    k1, k2 = kf1["kps"], kf2["kps"]
+
+    def epi(i1, i2):
+        x1, y1 = f32(k1["x"][i1]), f32(k1["y"][i1])
+        a = f32(f32(f32(x1 * F[0, 0]) + f32(y1 * F[1, 0])) + F[2, 0])
+        b = f32(f32(f32(x1 * F[0, 1]) + f32(y1 * F[1, 1])) + F[2, 1])
+        c = f32(f32(f32(x1 * F[0, 2]) + f32(y1 * F[1, 2])) + F[2, 2])
+        num = f32(f32(f32(a * f32(k2["x"][i2])) + f32(b * f32(k2["y"][i2]))) + c)
+        den = f32(f32(a * a) + f32(b * b))
+        if den == 0:
+            return False
+        dsqr = f32(f32(num * num) / den)
+        return float(dsqr) < 3.84 * float(f32(sigma2[int(k2["octave"][i2])]))
+    n1, (nd1, of1, ix1), (nd2, of2, ix2) = len(k1), kf1["fv"], kf2["fv"]
+    node2 = {int(n): j for j, n in enumerate(nd2)}
+    m12 = [-1] * n1
+    hist = [[] for _ in range(30)]
+    nm = 0
+    for a, node in enumerate(nd1):
+        if int(node) not in node2:
+            continue
+        b = node2[int(node)]
+        for i1 in ix1[of1[a]:of1[a + 1]]:
+            if kf1["has_mp"][i1]:
+                continue
+            st1 = kf1["uright"][i1] >= 0
+            if only_stereo and not st1:
+                continue
+            best, bi = 50, -1
+            for i2 in ix2[of2[b]:of2[b + 1]]:
+                if kf2["has_mp"][i2]:
+                    continue
+                st2 = kf2["uright"][i2] >= 0
+                if only_stereo and not st2:
+                    continue
+                d = hamming(kf1["desc"][i1], kf2["desc"][i2])
+                if d > 50 or d > best:
+                    continue
+                if not st1 and not st2:
+                    dx = f32(ex - f32(k2["x"][i2]))
+                    dy = f32(ey - f32(k2["y"][i2]))
+                    if f32(f32(dx * dx) + f32(dy * dy)) < f32(f32(100) * f32(kf2["scale"][int(k2["octave"][i2])])):
+                        continue
+                if epi(i1, i2):
+                    best, bi = d, i2
+            if bi >= 0:
+                m12[i1] = int(bi)
+                nm += 1
+                if check_ori:
+                    hist[rot_bin(k1["angle"][i1], k2["angle"][bi])].append(i1)
+    if check_ori:
+        ind = three_maxima([len(h) for h in hist])
+        for bn in range(30):
+            if bn not in ind:
+                for i1 in hist[bn]:
+                    m12[i1] = -1
+                    nm -= 1
+    return np.array(m12, np.int32), nm

@@ -432,3 +432,45 @@ def test_predict_scale_known_answers(O):
                              (10.0, 20.0, 0), (10.0, 0.0, 0)]:
         assert O.predict_scale(maxd, dist) == want, (maxd, dist)
         assert refpy.predict_scale(maxd, dist, 1.2, 8) == want
+
+
+# -------------------------- Fuse / SearchBySim3 / SearchForTriangulation (§8f row 4)
+@pytest.mark.parametrize("seed,stereo,th", [(1, True, 3.0), (2, False, 3.0)])
+def test_fuse_matches_refpy(O, seed, stereo, th):
+    from posecase import fuse_case
+    c = fuse_case(O, seed, 640, 240, 600, 800, stereo)
+    args = (c["kps"], c["desc"], c["uright"], c["bounds"], c["scale"], c["inv_sigma2"], 1.2, c["cam"], c["mps"],
+            c["mpdesc"], th)
+    out, nm = O.fuse(*args)
+    eout, enm = refpy.fuse(*args)
+    assert nm == enm and np.array_equal(out, eout) and nm > 100
+
+
+def test_fuse_sim3_matches_refpy(O):
+    from posecase import sim3_case
+    c = sim3_case(O, 3, 640, 240, 600, 800, s=1.4)
+    args = (c["kps"], c["desc"], c["bounds"], c["scale"], 1.2, c["cam"], c["mps"], c["mpdesc"], 4.0)
+    out, nm = O.fuse_sim3(*args)
+    eout, enm = refpy.fuse_sim3(*args)
+    assert nm == enm and np.array_equal(out, eout) and nm > 100
+
+
+@pytest.mark.parametrize("seed,s12", [(1, 1.0), (2, 1.1)])
+def test_search_by_sim3_matches_refpy(O, seed, s12):
+    from posecase import sim3_match_case
+    kf1, kf2, cam1, s, R, t = sim3_match_case(O, seed, 640, 240, 500, s12)
+    m1, nf, _, _ = O.search_by_sim3(kf1, kf2, cam1, s, R, t, 7.5)
+    e1, enf = refpy.search_by_sim3(kf1, kf2, cam1, s, R, t, 7.5)
+    assert nf == enf and np.array_equal(m1, e1)
+    if s12 == 1.0:
+        assert nf > 100
+
+
+@pytest.mark.parametrize("seed,only_stereo,check_ori", [(1, False, True), (2, True, True), (3, False, False)])
+def test_search_for_triangulation_matches_refpy(O, seed, only_stereo, check_ori):
+    from posecase import triangulation_case
+    kf1, kf2, cw1, T2w, cam2, sig2, F12 = triangulation_case(O, seed, 640, 240, 600)
+    m, nm = O.search_for_triangulation(kf1, kf2, cw1, T2w, cam2, sig2, F12, only_stereo, check_ori)
+    e, enm = refpy.search_for_triangulation(kf1, kf2, cw1, T2w, cam2, sig2, F12, only_stereo, check_ori)
+    assert nm == enm and np.array_equal(m, e)
+    assert nm > (20 if only_stereo else 100)
