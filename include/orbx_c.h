@@ -50,7 +50,15 @@
  *                          cv::Mat Scw, const vector<MapPoint*>&,
  *                          vector<MapPoint*>&, th)  include/ORBmatcher.h:60,
  *                          src/ORBmatcher.cc:290-403 (LoopClosing::ComputeSim3)
- *   orbm_search_by_projection_pose_batch  the three above, batched on device
+ *   orbm_fuse / orbm_fuse_sim3  ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>,
+ *                          th) / Fuse(KeyFrame*, Scw, vpPoints, th,
+ *                          vpReplacePoint)  include/ORBmatcher.h:80,83,
+ *                          src/ORBmatcher.cc:825-975, 977-1100 (matching part)
+ *   orbm_search_by_sim3    ORBmatcher::SearchBySim3  include/ORBmatcher.h:77,
+ *                          src/ORBmatcher.cc:1102-1326
+ *   orbm_search_by_projection_pose_batch  all of the above, batched on device
+ *   orbm_search_for_triangulation  ORBmatcher::SearchForTriangulation
+ *                          include/ORBmatcher.h:72, src/ORBmatcher.cc:657-823
  *   orbv_load_text / orbv_create  ORBVocabulary::loadFromTextFile
  *                          (DBoW2 TemplatedVocabulary, include/ORBVocabulary.h:30,
  *                          Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1418)
@@ -287,26 +295,40 @@ typedef struct orbm_map_point_world {
   uint8_t valid, obs_positive, pad[6];
 } orbm_map_point_world;
 
-#define ORBM_PROJ_LAST_FRAME 1 /* src/ORBmatcher.cc:1328-1470 */
-#define ORBM_PROJ_KEYFRAME 2   /* src/ORBmatcher.cc:1472-1599 */
-#define ORBM_PROJ_SIM3 3       /* src/ORBmatcher.cc:290-403   */
+#define ORBM_PROJ_LAST_FRAME 1 /* SearchByProjection  src/ORBmatcher.cc:1328-1470 */
+#define ORBM_PROJ_KEYFRAME 2   /* SearchByProjection  src/ORBmatcher.cc:1472-1599 */
+#define ORBM_PROJ_SIM3 3       /* SearchByProjection  src/ORBmatcher.cc:290-403   */
+#define ORBM_PROJ_FUSE 4       /* Fuse(pKF, vpMapPoints, th)  :825-975            */
+#define ORBM_PROJ_FUSE_SIM3 5  /* Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) :977-1100 */
+#define ORBM_PROJ_SIM3_MATCH 6 /* SearchBySim3, one direction  :1102-1326       */
 
 /* Per-frame projection prepared on the host from a camera (the scalar
  * cv::Mat work each overload does once per call): Rt = the 3x4 transform
  * applied to world points (Sim3: sRcw/scw | tcw/scw), Ow = -R^T t (camera
  * centre), level_mode (last-frame overload: 0 = levels lo-1..lo+1,
- * 1 = bForward: lo.., 2 = bBackward: 0..lo). 84 bytes. */
+ * 1 = bForward: lo.., 2 = bBackward: 0..lo), Rt2 = the second transform of
+ * SearchBySim3 (camera A to camera B: [sR21 | t21] or [sR12 | t12]).
+ * 132 bytes. */
 typedef struct orbm_pose {
   float Rt[12];
   float Ow[3];
   float fx, fy, cx, cy, mbf;
   int32_t level_mode;
+  float Rt2[12];
 } orbm_pose;
 
-/* Fill *out for `mode`. Tlw: LastFrame.mTcw rows 0..2 (ORBM_PROJ_LAST_FRAME
- * only, else NULL); mono = bMono. Host only (no device call). */
+/* Fill *out for `mode` (LAST_FRAME, KEYFRAME, SIM3, FUSE, FUSE_SIM3; for
+ * SIM3 and FUSE_SIM3 cam->Tcw = Scw). Tlw: LastFrame.mTcw rows 0..2
+ * (ORBM_PROJ_LAST_FRAME only, else NULL); mono = bMono. Host only. */
 int orbm_prepare_pose(int mode, const orbm_camera* cam, const float* Tlw, int mono,
                       orbm_pose* out);
+
+/* The two directions of SearchBySim3 (src/ORBmatcher.cc:1114-1124):
+ * out[0] projects pKF1's points into pKF2 (Rt = T1w, Rt2 = [sR21 | t21]),
+ * out[1] pKF2's into pKF1 (Rt = T2w, Rt2 = [sR12 | t12]); both use cam1's
+ * fx, fy, cx, cy as the reference does. R12 row-major 3x3. Host only. */
+int orbm_prepare_sim3_match(const orbm_camera* cam1, const float* T1w, const float* T2w,
+                            float s12, const float* R12, const float* t12, orbm_pose* out);
 
 /* MapPoint::PredictScale(dist, Frame* or KeyFrame*) (src/MapPoint.cc:390-422)
  * as the kernels evaluate it: the level is the number of thresholds
@@ -352,21 +374,65 @@ int orbm_search_by_projection_sim3(
     const orbm_map_point_world* mps, const uint8_t* mpdesc, int nmp, int th,
     const int* matched, int* out, int* nmatches);
 
-/* Batched device-resident variant of the three: frame f's keypoints at
- * d_kps + f*kp_pitch (d_n[f]; descriptors, d_uright (LAST_FRAME, or NULL),
- * d_blocked and d_out likewise), its points at d_mps + f*mp_pitch (d_nmp[f];
- * descriptors likewise), d_poses[f] from orbm_prepare_pose. d_blocked: the
- * blocking state on entry of the mode (LAST_FRAME: a point with
- * observations; KEYFRAME: any point; SIM3: vpMatched set). dist_th: TH_HIGH
- * (100) / ORBdist / TH_LOW (50); th: the window factor (Sim3: its int th).
- * All frames share grid bounds, scale factors and scale_factor. */
+/* Fuse(pKF, vpMapPoints, th), the matching part (src/ORBmatcher.cc:825-930):
+ * pKF's keypoints, descriptors, mvuRight (NULL = all monocular), grid bounds,
+ * mvScaleFactors, mvInvLevelSigma2, mfScaleFactor, camera (fx, fy, cx, cy,
+ * mbf, Tcw); one record per point (valid = pMP && !isBad() &&
+ * !IsInKeyFrame(pKF)). out[i] = keypoint index the point fuses into
+ * (bestDist <= TH_LOW), -1 otherwise; *nfused = their count. The caller
+ * applies the reference's side effects in point order (:932-957: Replace
+ * when the keypoint holds a MapPoint, else AddObservation + AddMapPoint),
+ * re-checking isBad() at each point's turn. */
+int orbm_fuse(orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n, const float* uright,
+              orbm_grid_bounds bounds, const float* scale, const float* inv_sigma2, int nlevels,
+              float scale_factor, const orbm_camera* kf, const orbm_map_point_world* mps,
+              const uint8_t* mpdesc, int nmp, float th, int* out, int* nfused);
+
+/* Fuse(pKF, Scw, vpPoints, th, vpReplacePoint), the matching part
+ * (:977-1081): kf->Tcw = Scw rows 0..2; valid = !isBad() && not in
+ * pKF->GetMapPoints(). out[i] = bestIdx (<= TH_LOW) or -1. The caller's
+ * in-order tail (:1083-1097): GetMapPoint(bestIdx) ? vpReplacePoint[i] =
+ * it (if !isBad()) : AddObservation + AddMapPoint. */
+int orbm_fuse_sim3(orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n,
+                   orbm_grid_bounds bounds, const float* scale, int nlevels, float scale_factor,
+                   const orbm_camera* kf, const orbm_map_point_world* mps, const uint8_t* mpdesc,
+                   int nmp, float th, int* out, int* nfused);
+
+/* SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (:1102-1326).
+ * Per keyframe: keypoints, descriptors, grid bounds, mvScaleFactors, Tcw
+ * rows 0..2 and one record per keypoint for GetMapPointMatches() (valid =
+ * pMP && !vbAlreadyMatched && !isBad()). cam1: pKF1's fx, fy, cx, cy.
+ * match12[i1] = idx2 for every new mutual match (the shim stores
+ * vpMapPoints2[idx2] into vpMatches12[i1]), -1 otherwise; *nfound. */
+int orbm_search_by_sim3(orbm_handle m, const orbx_kp* kps1, const uint8_t* desc1, int n1,
+                        orbm_grid_bounds bounds1, const float* T1w,
+                        const orbm_map_point_world* mps1, const uint8_t* mpdesc1,
+                        const orbx_kp* kps2, const uint8_t* desc2, int n2,
+                        orbm_grid_bounds bounds2, const float* T2w,
+                        const orbm_map_point_world* mps2, const uint8_t* mpdesc2,
+                        const float* scale, int nlevels, float scale_factor,
+                        const orbm_camera* cam1, float s12, const float* R12, const float* t12,
+                        float th, int* match12, int* nfound);
+
+/* Batched device-resident variant of every pose mode: frame f's keypoints
+ * at d_kps + f*kp_pitch (d_n[f]; descriptors, d_uright (LAST_FRAME, FUSE,
+ * or NULL) and d_blocked likewise), its points at d_mps + f*mp_pitch
+ * (d_nmp[f]; descriptors likewise), d_poses[f] from orbm_prepare_pose /
+ * orbm_prepare_sim3_match. d_blocked: the blocking state on entry of the
+ * mode (LAST_FRAME: a point with observations; KEYFRAME: any point; SIM3:
+ * vpMatched set; ignored by FUSE, FUSE_SIM3, SIM3_MATCH). dist_th: TH_HIGH
+ * (100) / ORBdist / TH_LOW (50); th: the window factor. inv_sigma2
+ * (FUSE): mvInvLevelSigma2, nlevels floats (host), else NULL. d_out: per keypoint at
+ * kp_pitch (LAST_FRAME, KEYFRAME, SIM3) or per point at mp_pitch (FUSE,
+ * FUSE_SIM3, SIM3_MATCH: the keypoint each point matched, -1). All frames
+ * share grid bounds, scale factors and scale_factor. */
 int orbm_search_by_projection_pose_batch(
     orbm_handle m, int mode, const orbx_kp* d_kps, const uint8_t* d_desc, const int* d_n,
     int kp_pitch, const float* d_uright, orbm_grid_bounds bounds, const float* scale,
     int nlevels, float scale_factor, const uint8_t* d_blocked, const orbm_pose* d_poses,
     const orbm_map_point_world* d_mps, const uint8_t* d_mpdesc, const int* d_nmp,
-    int mp_pitch, int frames, float th, int dist_th, int check_ori, int* d_out,
-    int* d_nmatches, void* stream);
+    int mp_pitch, int frames, float th, int dist_th, int check_ori,
+    const float* inv_sigma2, int* d_out, int* d_nmatches, void* stream);
 
 /* DBoW2::FeatureVector as CSR: nodes[k] ascending NodeIds; the feature
  * indices of node k are idx[off[k] .. off[k+1]). Each feature index appears
@@ -465,6 +531,53 @@ int orbv_transform_batch(orbv_handle v, const uint8_t* d_desc, size_t desc_pitch
                          uint32_t* d_fv_nodes, int* d_fv_off, int* d_fv_idx,
                          int* d_fv_n, uint32_t* d_word_ids, uint32_t* d_node_ids,
                          double* d_weights, void* stream);
+
+/* ------------------------------------------------ SearchForTriangulation
+ * Per pair: F12 (row-major 3x3, LocalMapping::ComputeF12) and the epipole
+ * (ex, ey) of pKF1's camera centre in pKF2 (src/ORBmatcher.cc:664-670).
+ * 44 bytes. */
+typedef struct orbm_tri_pair {
+  float F12[9];
+  float ex, ey;
+} orbm_tri_pair;
+
+/* Fill *out from pKF1->GetCameraCenter() (cw1, 3 floats), pKF2's Tcw rows
+ * 0..2 (T2w), pKF2's fx, fy, cx, cy (cam2) and F12. Host only. */
+int orbm_prepare_triangulation(const float* cw1, const float* T2w, const float* cam2,
+                               const float* F12, orbm_tri_pair* out);
+
+/* SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+ * (src/ORBmatcher.cc:657-823), host buffers, synchronous. Per keyframe:
+ * mvKeysUn, mDescriptors, mvuRight, has_mp[idx] = GetMapPoint(idx) != NULL,
+ * mFeatVec (CSR). scale2 / sigma2: pKF2's mvScaleFactors / mvLevelSigma2.
+ * matches12[idx1] = idx2 or -1 (vMatchedPairs = the pairs in idx1 order);
+ * *nmatches = their count. */
+int orbm_search_for_triangulation(
+    orbm_handle m, const orbx_kp* kps1, const uint8_t* desc1, const float* uright1,
+    const uint8_t* has_mp1, int n1, orbm_feature_vector fv1, const orbx_kp* kps2,
+    const uint8_t* desc2, const float* uright2, const uint8_t* has_mp2, int n2,
+    orbm_feature_vector fv2, const float* cw1, const float* T2w, const float* cam2,
+    const float* scale2, const float* sigma2, int nlevels, const float* F12, int only_stereo,
+    int check_ori, int* matches12, int* nmatches);
+
+/* Batched device-resident variant: `pairs` keyframe pairs in one launch
+ * (LocalMapping::CreateNewMapPoints: the new keyframe against each
+ * neighbour). Side 1 arrays at kp_pitch1 / node_pitch1 per pair (0 and 0:
+ * one pKF1 shared by every pair), side 2 at kp_pitch2 / node_pitch2.
+ * d_off*: node_pitch + 1 ints per pair; d_nn*: node counts; d_n*: keypoint
+ * counts. d_pairs from orbm_prepare_triangulation. scale2 / sigma2 are
+ * host arrays shared by all pairs. d_matches12: pairs x out_pitch ints
+ * (out_pitch >= n1); d_nmatches: pairs. */
+int orbm_search_for_triangulation_batch(
+    orbm_handle m, const orbx_kp* d_kps1, const uint8_t* d_desc1, const float* d_uright1,
+    const uint8_t* d_has_mp1, const int* d_n1, const uint32_t* d_nodes1, const int* d_off1,
+    const int* d_idx1, const int* d_nn1, int kp_pitch1, int node_pitch1,
+    const orbx_kp* d_kps2, const uint8_t* d_desc2, const float* d_uright2,
+    const uint8_t* d_has_mp2, const int* d_n2, const uint32_t* d_nodes2, const int* d_off2,
+    const int* d_idx2, const int* d_nn2, int kp_pitch2, int node_pitch2,
+    const orbm_tri_pair* d_pairs, const float* scale2, const float* sigma2, int nlevels,
+    int pairs, int only_stereo, int check_ori, int* d_matches12, int out_pitch,
+    int* d_nmatches, void* stream);
 
 /* --------------------------------------------- device plumbing for hosts
  * Thin wrappers so a host without its own HIP binding (ctypes, cgo, JNI)

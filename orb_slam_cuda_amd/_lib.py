@@ -41,12 +41,18 @@ class OrbmCamera(C.Structure):
 
 
 class OrbmPose(C.Structure):
-    """orbm_pose (orbm_prepare_pose), 84 bytes."""
+    """orbm_pose (orbm_prepare_pose / orbm_prepare_sim3_match), 132 bytes."""
     _fields_ = [("Rt", C.c_float * 12), ("Ow", C.c_float * 3), ("fx", C.c_float), ("fy", C.c_float),
-                ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("level_mode", C.c_int32)]
+                ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("level_mode", C.c_int32),
+                ("Rt2", C.c_float * 12)]
 
 
-assert C.sizeof(OrbmPose) == 84
+assert C.sizeof(OrbmPose) == 132
+
+
+class OrbmTriPair(C.Structure):
+    """orbm_tri_pair (orbm_prepare_triangulation), 44 bytes."""
+    _fields_ = [("F12", C.c_float * 9), ("ex", C.c_float), ("ey", C.c_float)]
 
 
 def camera(fx, fy, cx, cy, mb, mbf, Tcw) -> OrbmCamera:
@@ -138,7 +144,26 @@ def lib() -> C.CDLL:
         L.orbm_search_by_projection_pose_batch.argtypes = (
             [C.c_void_p, C.c_int] + [C.c_void_p] * 3 + [C.c_int, C.c_void_p, GridBounds, C.c_void_p, C.c_int,
                                                          C.c_float] + [C.c_void_p] * 5
-            + [C.c_int, C.c_int, C.c_float, C.c_int, C.c_int] + [C.c_void_p] * 3)
+            + [C.c_int, C.c_int, C.c_float, C.c_int, C.c_int] + [C.c_void_p] * 4)
+        L.orbm_prepare_sim3_match.argtypes = [C.POINTER(OrbmCamera), C.c_void_p, C.c_void_p, C.c_float, C.c_void_p,
+                                              C.c_void_p, C.POINTER(OrbmPose)]
+        L.orbm_fuse.argtypes = (PS + [C.c_void_p, GridBounds, C.c_void_p, C.c_void_p, C.c_int, C.c_float,
+                                      C.POINTER(OrbmCamera), C.c_void_p, C.c_void_p, C.c_int, C.c_float, C.c_void_p,
+                                      C.POINTER(C.c_int)])
+        L.orbm_fuse_sim3.argtypes = (PS + [GridBounds, C.c_void_p, C.c_int, C.c_float, C.POINTER(OrbmCamera),
+                                           C.c_void_p, C.c_void_p, C.c_int, C.c_float, C.c_void_p,
+                                           C.POINTER(C.c_int)])
+        L.orbm_search_by_sim3.argtypes = (PS + [GridBounds, C.c_void_p, C.c_void_p, C.c_void_p]
+                                          + [C.c_void_p] * 2 + [C.c_int, GridBounds] + [C.c_void_p] * 4
+                                          + [C.c_int, C.c_float, C.POINTER(OrbmCamera), C.c_float, C.c_void_p,
+                                             C.c_void_p, C.c_float, C.c_void_p, C.POINTER(C.c_int)])
+        L.orbm_prepare_triangulation.argtypes = [C.c_void_p] * 4 + [C.POINTER(OrbmTriPair)]
+        L.orbm_search_for_triangulation.argtypes = (
+            [C.c_void_p] * 5 + [C.c_int, FeatureVectorC] + [C.c_void_p] * 4 + [C.c_int, FeatureVectorC]
+            + [C.c_void_p] * 5 + [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_int)])
+        L.orbm_search_for_triangulation_batch.argtypes = (
+            [C.c_void_p] + ([C.c_void_p] * 9 + [C.c_int, C.c_int]) * 2 + [C.c_void_p] * 3
+            + [C.c_int] * 4 + [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p])
         L.orbv_last_error.restype = C.c_char_p
         L.orbv_load_text.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
         L.orbv_create.argtypes = [C.c_int] * 5 + [C.c_void_p] * 4 + [C.c_int, C.POINTER(C.c_void_p)]
@@ -175,6 +200,7 @@ MAP_POINT_WORLD_DTYPE = np.dtype([("pos", "<f4", (3,)), ("normal", "<f4", (3,)),
                                   ("obs_positive", "u1"), ("pad", "u1", (6,))])
 assert MAP_POINT_WORLD_DTYPE.itemsize == 48
 ORBM_PROJ_LAST_FRAME, ORBM_PROJ_KEYFRAME, ORBM_PROJ_SIM3 = 1, 2, 3
+ORBM_PROJ_FUSE, ORBM_PROJ_FUSE_SIM3, ORBM_PROJ_SIM3_MATCH = 4, 5, 6
 
 # orbm_map_point_proj (include/orbx_c.h), 24 bytes
 MAP_POINT_PROJ_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),

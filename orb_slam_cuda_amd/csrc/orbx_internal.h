@@ -167,6 +167,7 @@ struct PoseParams {
   float minX, maxX, minY, maxY, invW, invH;  // grid bounds (image bounds of IsInImage / the u, v tests)
   float scale[kMaxLevels];                   // mvScaleFactors
   float pred_thr[kMaxLevels];                // PredictScale thresholds (orbm_predict_scale_thresholds)
+  float inv_sigma2[kMaxLevels];              // mvInvLevelSigma2 (FUSE reprojection test)
   int L;                                     // mnScaleLevels
   float th;                                  // window factor
   int dist_th;                               // TH_HIGH / ORBdist / TH_LOW
@@ -179,6 +180,25 @@ int launch_search_pose(const PoseParams& P, const orbx_kp* kps, const uint8_t* d
                        const float* uright, const uint8_t* blocked, const orbm_pose* poses,
                        const orbm_map_point_world* mps, const uint8_t* mpdesc, const int* nmp, int frames, int* picks,
                        int* out, int* nmatches, void* stream);
+// orbx_triangulate.hip — SearchForTriangulation, one keyframe pair per workgroup
+struct TriSide {  // one side of the pairs; pitches of 0 share one keyframe across pairs
+  const orbx_kp* kps;
+  const uint8_t* desc;
+  const float* uright;
+  const uint8_t* has_mp;
+  const int* n;
+  const uint32_t* nodes;
+  const int* off;  // node_pitch + 1 entries per pair
+  const int* idx;
+  const int* nn;
+  int kp_pitch, node_pitch;
+};
+struct TriParams {
+  float scale2[kMaxLevels], sigma2[kMaxLevels];  // pKF2->mvScaleFactors, mvLevelSigma2
+  int only_stereo, check_ori, out_pitch;
+};
+int launch_search_tri(const TriParams& P, const TriSide& A, const TriSide& B, const orbm_tri_pair* pairs, int npairs,
+                      int* matches12, int* nmatches, void* stream);
 // orbx_host.hip: the pyramid of frames [frame0, frame0 + n) of an extractor's last extraction
 int extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int* w, int* hgt, float* scale,
                       float* inv_scale, int* L);

@@ -1526,7 +1526,7 @@ int host_predict_direct(float ratio, float logsf, int L) {
 }  // namespace
 
 int orbm_prepare_pose(int mode, const orbm_camera* cam, const float* Tlw, int mono, orbm_pose* out) {
-  if (!cam || !out || mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_PROJ_SIM3 ||
+  if (!cam || !out || mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_PROJ_FUSE_SIM3 ||
       (mode == ORBM_PROJ_LAST_FRAME && !Tlw))
     return mfail(ORBX_EINVAL, "bad argument");
   orbm_pose p{};
@@ -1535,9 +1535,9 @@ int orbm_prepare_pose(int mode, const orbm_camera* cam, const float* Tlw, int mo
   p.cx = cam->cx;
   p.cy = cam->cy;
   p.mbf = cam->mbf;
-  if (mode == ORBM_PROJ_SIM3) {
+  if (mode == ORBM_PROJ_SIM3 || mode == ORBM_PROJ_FUSE_SIM3) {
     // scw = sqrt(sRcw.row(0).dot(sRcw.row(0))); Rcw = sRcw/scw; tcw = t/scw
-    // (src/ORBmatcher.cc:298-303): Mat::dot in double, Mat / s = convertTo(1/s)
+    // (src/ORBmatcher.cc:298-303, 986-991): Mat::dot in double, Mat / s = convertTo(1/s)
     const float* S = cam->Tcw;
     const double d = (double)S[0] * S[0] + (double)S[1] * S[1] + (double)S[2] * S[2];
     const float scw = (float)std::sqrt(d);
@@ -1558,6 +1558,38 @@ int orbm_prepare_pose(int mode, const orbm_camera* cam, const float* Tlw, int mo
     p.level_mode = bForward ? 1 : (bBackward ? 2 : 0);
   }
   *out = p;
+  return ORBX_OK;
+}
+
+int orbm_prepare_sim3_match(const orbm_camera* cam1, const float* T1w, const float* T2w, float s12, const float* R12,
+                            const float* t12, orbm_pose* out) {
+  if (!cam1 || !T1w || !T2w || !R12 || !t12 || !out || !(s12 != 0.0f)) return mfail(ORBX_EINVAL, "bad argument");
+  // sR12 = s12*R12; sR21 = (1.0/s12)*R12.t(); t21 = -sR21*t12 (src/ORBmatcher.cc:1118-1120):
+  // scalar * Mat = convertTo(alpha) in float, -A*t = gemm small path with alpha -1
+  const float a12 = (float)(double)s12, a21 = (float)(1.0 / (double)s12);
+  float S12[12], S21[12];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      S12[4 * r + c] = R12[3 * r + c] * a12 + 0.0f;
+      S21[4 * r + c] = R12[3 * c + r] * a21 + 0.0f;
+    }
+  for (int r = 0; r < 3; ++r) {
+    S12[4 * r + 3] = t12[r];
+    const float t = S21[4 * r] * t12[0] + S21[4 * r + 1] * t12[1] + S21[4 * r + 2] * t12[2];
+    S21[4 * r + 3] = (float)((double)t * -1.0 + 0.0 * 0.0);
+  }
+  for (int d = 0; d < 2; ++d) {
+    orbm_pose p{};
+    p.fx = cam1->fx;
+    p.fy = cam1->fy;
+    p.cx = cam1->cx;
+    p.cy = cam1->cy;
+    p.mbf = cam1->mbf;
+    std::memcpy(p.Rt, d == 0 ? T1w : T2w, sizeof p.Rt);
+    std::memcpy(p.Rt2, d == 0 ? S21 : S12, sizeof p.Rt2);
+    host_neg_rt_t(p.Rt, p.Ow);
+    out[d] = p;
+  }
   return ORBX_OK;
 }
 
@@ -1603,10 +1635,12 @@ int orbm_search_by_projection_pose_batch(orbm_handle m, int mode, const orbx_kp*
                                          const uint8_t* d_blocked, const orbm_pose* d_poses,
                                          const orbm_map_point_world* d_mps, const uint8_t* d_mpdesc,
                                          const int* d_nmp, int mp_pitch, int frames, float th, int dist_th,
-                                         int check_ori, int* d_out, int* d_nmatches, void* stream) {
+                                         int check_ori, const float* inv_sigma2, int* d_out, int* d_nmatches,
+                                         void* stream) {
   if (!m || !d_kps || !d_desc || !d_n || !scale || !d_blocked || !d_poses || !d_mps || !d_mpdesc || !d_nmp ||
       !d_out || !d_nmatches || frames < 1 || kp_pitch < 1 || mp_pitch < 1 || nlevels < 1 ||
-      nlevels > kMaxLevels || mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_PROJ_SIM3)
+      nlevels > kMaxLevels || mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_PROJ_SIM3_MATCH ||
+      (mode == ORBM_PROJ_FUSE && !inv_sigma2))
     return mfail(ORBX_EINVAL, "bad argument");
   if (!(b.max_x > b.min_x) || !(b.max_y > b.min_y)) return mfail(ORBX_EINVAL, "empty grid bounds");
   if (pose_lds_bytes(kp_pitch) > 156 * 1024) return mfail(ORBX_ECAPACITY, "kp_pitch %d too large", kp_pitch);
@@ -1630,7 +1664,8 @@ int orbm_search_by_projection_pose_batch(orbm_handle m, int mode, const orbx_kp*
   P.check_ori = check_ori;
   P.kp_pitch = kp_pitch;
   P.mp_pitch = mp_pitch;
-  P.has_uright = d_uright != nullptr && mode == ORBM_PROJ_LAST_FRAME;
+  P.has_uright = d_uright != nullptr && (mode == ORBM_PROJ_LAST_FRAME || mode == ORBM_PROJ_FUSE);
+  for (int l = 0; l < kMaxLevels; ++l) P.inv_sigma2[l] = inv_sigma2 ? inv_sigma2[std::min(l, nlevels - 1)] : 0.f;
   P.max_rounds = 32;
   if (const char* e = getenv("ORBX_PROJ_ROUNDS")) P.max_rounds = atoi(e);  // tests: force the sequential pass
   const size_t need = (size_t)frames * mp_pitch;
@@ -1652,13 +1687,15 @@ namespace {
 int pose_sync(orbm_handle m, int mode, const orbx_kp* kps, const uint8_t* desc, int n, const float* uright,
               orbm_grid_bounds b, const float* scale, int nlevels, float scale_factor, const uint8_t* blocked,
               const orbm_pose& pose, const orbm_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th,
-              int dist_th, int check_ori, int* out, int* nmatches) {
-  if (!m || !nmatches || n < 0 || nmp < 0 || (n && (!kps || !desc || !out)) || (nmp && (!mps || !mpdesc)))
+              int dist_th, int check_ori, int* out, int* nmatches, const float* inv_sigma2 = nullptr) {
+  const bool pp = mode == ORBM_PROJ_FUSE || mode == ORBM_PROJ_FUSE_SIM3 || mode == ORBM_PROJ_SIM3_MATCH;
+  if (!m || !nmatches || n < 0 || nmp < 0 || (n && (!kps || !desc)) || (nmp && (!mps || !mpdesc)) ||
+      ((pp ? nmp : n) && !out))
     return mfail(ORBX_EINVAL, "bad argument");
   MHIP(hipSetDevice(m->device));
   const int kp = std::max(n, 1), mp = std::max(nmp, 1);
   const size_t sz[] = {(size_t)kp * sizeof(orbx_kp), (size_t)kp * 32, (size_t)kp * 4, (size_t)kp,
-                       (size_t)mp * sizeof(orbm_map_point_world), (size_t)mp * 32, (size_t)kp * 4, 16,
+                       (size_t)mp * sizeof(orbm_map_point_world), (size_t)mp * 32, (size_t)(pp ? mp : kp) * 4, 16,
                        sizeof(orbm_pose)};
   size_t off[9], tot = 0;
   for (int i = 0; i < 9; ++i) {
@@ -1689,12 +1726,13 @@ int pose_sync(orbm_handle m, int mode, const orbx_kp* kps, const uint8_t* desc, 
   rc = orbm_search_by_projection_pose_batch(
       m, mode, (const orbx_kp*)(s + off[0]), s + off[1], cnt, kp, uright ? (const float*)(s + off[2]) : nullptr, b,
       scale, nlevels, scale_factor, s + off[3], (const orbm_pose*)(s + off[8]),
-      (const orbm_map_point_world*)(s + off[4]), s + off[5], cnt + 1, mp, 1, th, dist_th, check_ori,
+      (const orbm_map_point_world*)(s + off[4]), s + off[5], cnt + 1, mp, 1, th, dist_th, check_ori, inv_sigma2,
       (int*)(s + off[6]), cnt + 2, st);
   if (rc) return rc;
   int nm = 0;
   MHIP(hipMemcpyAsync(&nm, cnt + 2, 4, hipMemcpyDeviceToHost, st));
-  if (n) MHIP(hipMemcpyAsync(out, s + off[6], (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  const int nout = pp ? nmp : n;
+  if (nout) MHIP(hipMemcpyAsync(out, s + off[6], (size_t)nout * 4, hipMemcpyDeviceToHost, st));
   MHIP(hipStreamSynchronize(st));
   *nmatches = nm;
   return ORBX_OK;
@@ -1737,6 +1775,178 @@ int orbm_search_by_projection_sim3(orbm_handle m, const orbx_kp* kps, const uint
     for (int i = 0; i < n; ++i) bl[i] = matched[i] >= 0;  // vpMatched[idx] set on entry
   return pose_sync(m, ORBM_PROJ_SIM3, kps, desc, n, nullptr, b, scale, nlevels, scale_factor, bl.data(), pose, mps,
                    mpdesc, nmp, (float)th, 50 /* TH_LOW */, 0, out, nmatches);
+}
+
+int orbm_fuse(orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n, const float* uright, orbm_grid_bounds b,
+              const float* scale, const float* inv_sigma2, int nlevels, float scale_factor, const orbm_camera* kf,
+              const orbm_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th, int* out, int* nfused) {
+  if (!inv_sigma2) return mfail(ORBX_EINVAL, "bad argument");
+  orbm_pose pose;
+  int rc = orbm_prepare_pose(ORBM_PROJ_FUSE, kf, nullptr, 0, &pose);
+  if (rc) return rc;
+  return pose_sync(m, ORBM_PROJ_FUSE, kps, desc, n, uright, b, scale, nlevels, scale_factor, nullptr, pose, mps,
+                   mpdesc, nmp, th, 50 /* TH_LOW */, 0, out, nfused, inv_sigma2);
+}
+
+int orbm_fuse_sim3(orbm_handle m, const orbx_kp* kps, const uint8_t* desc, int n, orbm_grid_bounds b,
+                   const float* scale, int nlevels, float scale_factor, const orbm_camera* kf,
+                   const orbm_map_point_world* mps, const uint8_t* mpdesc, int nmp, float th, int* out, int* nfused) {
+  orbm_pose pose;
+  int rc = orbm_prepare_pose(ORBM_PROJ_FUSE_SIM3, kf, nullptr, 0, &pose);
+  if (rc) return rc;
+  return pose_sync(m, ORBM_PROJ_FUSE_SIM3, kps, desc, n, nullptr, b, scale, nlevels, scale_factor, nullptr, pose,
+                   mps, mpdesc, nmp, th, 50 /* TH_LOW */, 0, out, nfused);
+}
+
+int orbm_search_by_sim3(orbm_handle m, const orbx_kp* kps1, const uint8_t* desc1, int n1, orbm_grid_bounds b1,
+                        const float* T1w, const orbm_map_point_world* mps1, const uint8_t* mpdesc1,
+                        const orbx_kp* kps2, const uint8_t* desc2, int n2, orbm_grid_bounds b2, const float* T2w,
+                        const orbm_map_point_world* mps2, const uint8_t* mpdesc2, const float* scale, int nlevels,
+                        float scale_factor, const orbm_camera* cam1, float s12, const float* R12, const float* t12,
+                        float th, int* match12, int* nfound) {
+  if (!nfound || n1 < 0 || n2 < 0 || (n1 && !match12)) return mfail(ORBX_EINVAL, "bad argument");
+  orbm_pose pz[2];
+  int rc = orbm_prepare_sim3_match(cam1, T1w, T2w, s12, R12, t12, pz);
+  if (rc) return rc;
+  // direction 1: pKF1's points into pKF2 (vnMatch1); direction 2: pKF2's into pKF1 (vnMatch2)
+  std::vector<int> vn1(std::max(n1, 1), -1), vn2(std::max(n2, 1), -1);
+  int c1 = 0, c2 = 0;
+  if ((rc = pose_sync(m, ORBM_PROJ_SIM3_MATCH, kps2, desc2, n2, nullptr, b2, scale, nlevels, scale_factor, nullptr,
+                      pz[0], mps1, mpdesc1, n1, th, 100 /* TH_HIGH */, 0, vn1.data(), &c1)))
+    return rc;
+  if ((rc = pose_sync(m, ORBM_PROJ_SIM3_MATCH, kps1, desc1, n1, nullptr, b1, scale, nlevels, scale_factor, nullptr,
+                      pz[1], mps2, mpdesc2, n2, th, 100 /* TH_HIGH */, 0, vn2.data(), &c2)))
+    return rc;
+  // Check agreement (:1295-1312)
+  int nFound = 0;
+  for (int i1 = 0; i1 < n1; i1++) {
+    match12[i1] = -1;
+    const int idx2 = vn1[i1];
+    if (idx2 >= 0 && idx2 < n2 && vn2[idx2] == i1) {
+      match12[i1] = idx2;
+      nFound++;
+    }
+  }
+  *nfound = nFound;
+  return ORBX_OK;
+}
+
+int orbm_prepare_triangulation(const float* cw1, const float* T2w, const float* cam2, const float* F12,
+                               orbm_tri_pair* out) {
+  if (!cw1 || !T2w || !cam2 || !F12 || !out) return mfail(ORBX_EINVAL, "bad argument");
+  // C2 = R2w*Cw + t2w; invz = 1.0f/C2.z; ex = fx*C2.x*invz + cx (src/ORBmatcher.cc:664-670)
+  float C2[3];
+  host_rx_t(T2w, cw1, C2);
+  const float invz = 1.0f / C2[2];
+  orbm_tri_pair t{};
+  std::memcpy(t.F12, F12, sizeof t.F12);
+  t.ex = cam2[0] * C2[0] * invz + cam2[2];
+  t.ey = cam2[1] * C2[1] * invz + cam2[3];
+  *out = t;
+  return ORBX_OK;
+}
+
+int orbm_search_for_triangulation_batch(
+    orbm_handle m, const orbx_kp* d_kps1, const uint8_t* d_desc1, const float* d_uright1, const uint8_t* d_has_mp1,
+    const int* d_n1, const uint32_t* d_nodes1, const int* d_off1, const int* d_idx1, const int* d_nn1, int kp_pitch1,
+    int node_pitch1, const orbx_kp* d_kps2, const uint8_t* d_desc2, const float* d_uright2, const uint8_t* d_has_mp2,
+    const int* d_n2, const uint32_t* d_nodes2, const int* d_off2, const int* d_idx2, const int* d_nn2, int kp_pitch2,
+    int node_pitch2, const orbm_tri_pair* d_pairs, const float* scale2, const float* sigma2, int nlevels, int pairs,
+    int only_stereo, int check_ori, int* d_matches12, int out_pitch, int* d_nmatches, void* stream) {
+  if (!m || !d_kps1 || !d_desc1 || !d_uright1 || !d_has_mp1 || !d_n1 || !d_nodes1 || !d_off1 || !d_idx1 || !d_nn1 ||
+      !d_kps2 || !d_desc2 || !d_uright2 || !d_has_mp2 || !d_n2 || !d_nodes2 || !d_off2 || !d_idx2 || !d_nn2 ||
+      !d_pairs || !scale2 || !sigma2 || !d_matches12 || !d_nmatches || pairs < 1 || nlevels < 1 ||
+      nlevels > kMaxLevels || kp_pitch1 < 0 || node_pitch1 < 0 || kp_pitch2 < 1 || node_pitch2 < 1 || out_pitch < 1 ||
+      ((kp_pitch1 == 0) != (node_pitch1 == 0)))
+    return mfail(ORBX_EINVAL, "bad argument");
+  MHIP(hipSetDevice(m->device));
+  TriParams P{};
+  for (int l = 0; l < kMaxLevels; ++l) {
+    P.scale2[l] = scale2[std::min(l, nlevels - 1)];
+    P.sigma2[l] = sigma2[std::min(l, nlevels - 1)];
+  }
+  P.only_stereo = only_stereo;
+  P.check_ori = check_ori;
+  P.out_pitch = out_pitch;
+  const TriSide A{d_kps1, d_desc1, d_uright1, d_has_mp1, d_n1, d_nodes1, d_off1, d_idx1, d_nn1, kp_pitch1,
+                  node_pitch1};
+  const TriSide B{d_kps2, d_desc2, d_uright2, d_has_mp2, d_n2, d_nodes2, d_off2, d_idx2, d_nn2, kp_pitch2,
+                  node_pitch2};
+  if (launch_search_tri(P, A, B, d_pairs, pairs, d_matches12, d_nmatches, stream))
+    return mfail(ORBX_EDEVICE, "search_tri launch: %s", hipGetErrorString(hipGetLastError()));
+  return ORBX_OK;
+}
+
+int orbm_search_for_triangulation(orbm_handle m, const orbx_kp* kps1, const uint8_t* desc1, const float* uright1,
+                                  const uint8_t* has_mp1, int n1, orbm_feature_vector fv1, const orbx_kp* kps2,
+                                  const uint8_t* desc2, const float* uright2, const uint8_t* has_mp2, int n2,
+                                  orbm_feature_vector fv2, const float* cw1, const float* T2w, const float* cam2,
+                                  const float* scale2, const float* sigma2, int nlevels, const float* F12,
+                                  int only_stereo, int check_ori, int* matches12, int* nmatches) {
+  if (!m || !nmatches || n1 < 0 || n2 < 0 || fv1.n_nodes < 0 || fv2.n_nodes < 0 ||
+      (n1 && (!kps1 || !desc1 || !uright1 || !has_mp1 || !matches12)) ||
+      (n2 && (!kps2 || !desc2 || !uright2 || !has_mp2)) || (fv1.n_nodes && (!fv1.nodes || !fv1.off)) ||
+      (fv2.n_nodes && (!fv2.nodes || !fv2.off)))
+    return mfail(ORBX_EINVAL, "bad argument");
+  orbm_tri_pair tp;
+  int rc = orbm_prepare_triangulation(cw1, T2w, cam2, F12, &tp);
+  if (rc) return rc;
+  const int f1 = fv1.n_nodes ? fv1.off[fv1.n_nodes] : 0, f2 = fv2.n_nodes ? fv2.off[fv2.n_nodes] : 0;
+  if (f1 > n1 || f2 > n2) return mfail(ORBX_EINVAL, "feature vector holds more indices than keypoints");
+  for (int i = 0; i < f1; ++i)
+    if (fv1.idx[i] < 0 || fv1.idx[i] >= n1) return mfail(ORBX_EINVAL, "feature index out of range");
+  for (int i = 0; i < f2; ++i)
+    if (fv2.idx[i] < 0 || fv2.idx[i] >= n2) return mfail(ORBX_EINVAL, "feature index out of range");
+  MHIP(hipSetDevice(m->device));
+  const int k1 = std::max(n1, 1), k2 = std::max(n2, 1);
+  const int nn1 = std::max(fv1.n_nodes, 1), nn2 = std::max(fv2.n_nodes, 1);
+  // staging: kps, desc, uright, has_mp, nodes, off, idx per side; counts; pair
+  const size_t sz[] = {(size_t)k1 * sizeof(orbx_kp), (size_t)k1 * 32, (size_t)k1 * 4, (size_t)k1,
+                       (size_t)nn1 * 4, (size_t)(nn1 + 1) * 4, (size_t)k1 * 4,
+                       (size_t)k2 * sizeof(orbx_kp), (size_t)k2 * 32, (size_t)k2 * 4, (size_t)k2,
+                       (size_t)nn2 * 4, (size_t)(nn2 + 1) * 4, (size_t)k2 * 4,
+                       32, sizeof(orbm_tri_pair), (size_t)k1 * 4};
+  constexpr int NS = sizeof(sz) / sizeof(sz[0]);
+  size_t off[NS], tot = 0;
+  for (int i = 0; i < NS; ++i) {
+    off[i] = tot;
+    tot += (sz[i] + 255) & ~(size_t)255;
+  }
+  if ((rc = stage_reserve(m, tot))) return rc;
+  uint8_t* s = (uint8_t*)m->stage;
+  if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+  hipStream_t st = m->stream;
+  auto up = [&](int slot, const void* src, size_t bytes) -> int {
+    if (bytes) MHIP(hipMemcpyAsync(s + off[slot], src, bytes, hipMemcpyHostToDevice, st));
+    return ORBX_OK;
+  };
+  const int zero = 0;
+  const int cnt[6] = {n1, fv1.n_nodes, n2, fv2.n_nodes, 0, 0};
+  if ((rc = up(0, kps1, (size_t)n1 * sizeof(orbx_kp))) || (rc = up(1, desc1, (size_t)n1 * 32)) ||
+      (rc = up(2, uright1, (size_t)n1 * 4)) || (rc = up(3, has_mp1, (size_t)n1)) ||
+      (rc = up(4, fv1.nodes, (size_t)fv1.n_nodes * 4)) ||
+      (rc = up(5, fv1.n_nodes ? fv1.off : &zero, (size_t)(fv1.n_nodes + 1) * 4)) ||
+      (rc = up(6, fv1.idx, (size_t)f1 * 4)) || (rc = up(7, kps2, (size_t)n2 * sizeof(orbx_kp))) ||
+      (rc = up(8, desc2, (size_t)n2 * 32)) || (rc = up(9, uright2, (size_t)n2 * 4)) ||
+      (rc = up(10, has_mp2, (size_t)n2)) || (rc = up(11, fv2.nodes, (size_t)fv2.n_nodes * 4)) ||
+      (rc = up(12, fv2.n_nodes ? fv2.off : &zero, (size_t)(fv2.n_nodes + 1) * 4)) ||
+      (rc = up(13, fv2.idx, (size_t)f2 * 4)) || (rc = up(14, cnt, sizeof cnt)) || (rc = up(15, &tp, sizeof tp)))
+    return rc;
+  int* c = (int*)(s + off[14]);
+  rc = orbm_search_for_triangulation_batch(
+      m, (const orbx_kp*)(s + off[0]), s + off[1], (const float*)(s + off[2]), s + off[3], c,
+      (const uint32_t*)(s + off[4]), (const int*)(s + off[5]), (const int*)(s + off[6]), c + 1, k1, nn1,
+      (const orbx_kp*)(s + off[7]), s + off[8], (const float*)(s + off[9]), s + off[10], c + 2,
+      (const uint32_t*)(s + off[11]), (const int*)(s + off[12]), (const int*)(s + off[13]), c + 3, k2, nn2,
+      (const orbm_tri_pair*)(s + off[15]), scale2, sigma2, nlevels, 1, only_stereo, check_ori,
+      (int*)(s + off[16]), k1, c + 4, st);
+  if (rc) return rc;
+  int nm = 0;
+  MHIP(hipMemcpyAsync(&nm, c + 4, 4, hipMemcpyDeviceToHost, st));
+  if (n1) MHIP(hipMemcpyAsync(matches12, s + off[16], (size_t)n1 * 4, hipMemcpyDeviceToHost, st));
+  MHIP(hipStreamSynchronize(st));
+  *nmatches = nm;
+  return ORBX_OK;
 }
 
 }  // extern "C"

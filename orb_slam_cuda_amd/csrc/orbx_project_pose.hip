@@ -7,6 +7,11 @@
 //               ORBdist)  src/ORBmatcher.cc:1472-1599 (Tracking::Relocalization)
 //   SIM3        SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)
 //               src/ORBmatcher.cc:290-403 (LoopClosing::ComputeSim3)
+//   FUSE        Fuse(KeyFrame*, vpMapPoints, th), matching part  :825-930
+//               (LocalMapping::SearchInNeighbors)
+//   FUSE_SIM3   Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint), matching
+//               part  :977-1081 (LoopClosing::SearchAndFuse)
+//   SIM3_MATCH  SearchBySim3, one direction  :1102-1292 (LoopClosing::ComputeSim3)
 //
 // Per point (in order): project with the pose (R*x + t as OpenCV's 3x3 gemm
 // small-matrix path: float dot, then a double add of t), the image / depth /
@@ -64,28 +69,44 @@ struct PoseQuery {
   bool ok;
 };
 
+// modes whose output is per point (no blocking, no per-keypoint epilogue)
+__host__ __device__ constexpr bool per_point(int mode) {
+  return mode == ORBM_PROJ_FUSE || mode == ORBM_PROJ_FUSE_SIM3 || mode == ORBM_PROJ_SIM3_MATCH;
+}
+
 template <int MODE>
 __device__ inline PoseQuery pose_query(const PoseParams& P, const orbm_pose& C, const orbm_map_point_world& mp) {
   PoseQuery q;
   q.ok = false;
   if (!mp.valid) return q;
   const float X = mp.pos[0], Y = mp.pos[1], Z = mp.pos[2];
-  const float xc = pose_row(C.Rt, 0, X, Y, Z), yc = pose_row(C.Rt, 1, X, Y, Z), zc = pose_row(C.Rt, 2, X, Y, Z);
-  if (MODE == ORBM_PROJ_SIM3) {
+  float xc = pose_row(C.Rt, 0, X, Y, Z), yc = pose_row(C.Rt, 1, X, Y, Z), zc = pose_row(C.Rt, 2, X, Y, Z);
+  if (MODE == ORBM_PROJ_SIM3_MATCH) {  // p3Dc2 = sR21*p3Dc1 + t21 (:1156-1157)
+    const float a = xc, b = yc, c = zc;
+    xc = pose_row(C.Rt2, 0, a, b, c);
+    yc = pose_row(C.Rt2, 1, a, b, c);
+    zc = pose_row(C.Rt2, 2, a, b, c);
+  }
+  float invz;
+  if (MODE == ORBM_PROJ_SIM3 || MODE == ORBM_PROJ_FUSE || MODE == ORBM_PROJ_FUSE_SIM3 ||
+      MODE == ORBM_PROJ_SIM3_MATCH) {
     if (zc < 0.0f) return q;
-    const float invz = __fdiv_rn(1.0f, zc);
+    // float 1/z (:321, :854) or double 1.0/z (:1014, :1164)
+    invz = (MODE == ORBM_PROJ_SIM3 || MODE == ORBM_PROJ_FUSE) ? __fdiv_rn(1.0f, zc)
+                                                                : __double2float_rn(__ddiv_rn(1.0, (double)zc));
     q.u = __fadd_rn(__fmul_rn(C.fx, __fmul_rn(xc, invz)), C.cx);
     q.v = __fadd_rn(__fmul_rn(C.fy, __fmul_rn(yc, invz)), C.cy);
     // KeyFrame::IsInImage (src/KeyFrame.cc:619-622)
     if (!(q.u >= P.minX && q.u < P.maxX && q.v >= P.minY && q.v < P.maxY)) return q;
+    q.ur = __fsub_rn(q.u, __fmul_rn(C.mbf, invz));  // Fuse: ur = u - bf*invz
   } else {
-    const float invzc = __double2float_rn(__ddiv_rn(1.0, (double)zc));
-    if (MODE == ORBM_PROJ_LAST_FRAME && invzc < 0.0f) return q;
-    q.u = __fadd_rn(__fmul_rn(__fmul_rn(C.fx, xc), invzc), C.cx);
-    q.v = __fadd_rn(__fmul_rn(__fmul_rn(C.fy, yc), invzc), C.cy);
+    invz = __double2float_rn(__ddiv_rn(1.0, (double)zc));
+    if (MODE == ORBM_PROJ_LAST_FRAME && invz < 0.0f) return q;
+    q.u = __fadd_rn(__fmul_rn(__fmul_rn(C.fx, xc), invz), C.cx);
+    q.v = __fadd_rn(__fmul_rn(__fmul_rn(C.fy, yc), invz), C.cy);
     if (q.u < P.minX || q.u > P.maxX) return q;
     if (q.v < P.minY || q.v > P.maxY) return q;
-    q.ur = __fsub_rn(q.u, __fmul_rn(C.mbf, invzc));
+    q.ur = __fsub_rn(q.u, __fmul_rn(C.mbf, invz));
   }
   if (MODE == ORBM_PROJ_LAST_FRAME) {
     const int lo = min(max((int)mp.octave, 0), kMaxLevels - 1);
@@ -101,12 +122,20 @@ __device__ inline PoseQuery pose_query(const PoseParams& P, const orbm_pose& C, 
       q.maxL = lo + 1;
     }
   } else {
-    const float PO0 = __fsub_rn(X, C.Ow[0]), PO1 = __fsub_rn(Y, C.Ow[1]), PO2 = __fsub_rn(Z, C.Ow[2]);
-    const float dist = norm3(PO0, PO1, PO2);
+    float dist, PO0, PO1, PO2;
+    if (MODE == ORBM_PROJ_SIM3_MATCH) {  // cv::norm(p3Dc2): camera coordinates
+      dist = norm3(xc, yc, zc);
+      PO0 = PO1 = PO2 = 0.0f;
+    } else {  // PO = p3Dw - Ow
+      PO0 = __fsub_rn(X, C.Ow[0]);
+      PO1 = __fsub_rn(Y, C.Ow[1]);
+      PO2 = __fsub_rn(Z, C.Ow[2]);
+      dist = norm3(PO0, PO1, PO2);
+    }
     const float maxDistance = __fmul_rn(1.2f, mp.max_distance);  // GetMaxDistanceInvariance
     const float minDistance = __fmul_rn(0.8f, mp.min_distance);  // GetMinDistanceInvariance
     if (dist < minDistance || dist > maxDistance) return q;
-    if (MODE == ORBM_PROJ_SIM3) {
+    if (MODE == ORBM_PROJ_SIM3 || MODE == ORBM_PROJ_FUSE || MODE == ORBM_PROJ_FUSE_SIM3) {
       // PO.dot(Pn) < 0.5*dist: viewing angle over 60 degrees (double dot product)
       const double dot = __dadd_rn(__dadd_rn(__dmul_rn((double)PO0, (double)mp.normal[0]),
                                              __dmul_rn((double)PO1, (double)mp.normal[1])),
@@ -118,7 +147,7 @@ __device__ inline PoseQuery pose_query(const PoseParams& P, const orbm_pose& C, 
     if (MODE == ORBM_PROJ_KEYFRAME) {
       q.minL = lvl - 1;
       q.maxL = lvl + 1;
-    } else {  // SIM3: KeyFrame::GetFeaturesInArea has no level band; the matcher keeps lvl-1..lvl
+    } else {  // KeyFrame::GetFeaturesInArea has no level band; the matchers keep lvl-1..lvl
       q.minL = lvl - 1;
       q.maxL = lvl;
     }
@@ -151,6 +180,7 @@ __global__ __launch_bounds__(kPoseThreads) void search_pose_kernel(
 
   proj_grid_sort<kPoseThreads>(g, KP, D, UR, n, P.minX, P.minY, P.invW, P.invH, s_tmp);
   const bool stereo = MODE == ORBM_PROJ_LAST_FRAME && UR != nullptr;
+  const bool has_ur = UR != nullptr;
 
   // point j against the keypoints, given the blocking table g.mark
   auto search = [&](int j) -> int {
@@ -176,6 +206,16 @@ __global__ __launch_bounds__(kPoseThreads) void search_pose_kernel(
           const float er = fabsf(__fsub_rn(q.ur, k.w));
           if (er > q.rad) continue;
         }
+        if (MODE == ORBM_PROJ_FUSE) {  // reprojection error (src/ORBmatcher.cc:900-925)
+          const float ex = __fsub_rn(q.u, k.x), ey = __fsub_rn(q.v, k.y);
+          float e2 = __fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
+          const bool st = has_ur && k.w >= 0.0f;
+          if (st) {
+            const float er = __fsub_rn(q.ur, k.w);
+            e2 = __fadd_rn(e2, __fmul_rn(er, er));
+          }
+          if ((double)__fmul_rn(e2, P.inv_sigma2[min(max(o, 0), kMaxLevels - 1)]) > (st ? 7.8 : 5.99)) continue;
+        }
         const int d = hamming256(g.kd[2 * p], g.kd[2 * p + 1], m0, m1);
         if (d < best) {
           best = d;
@@ -186,6 +226,7 @@ __global__ __launch_bounds__(kPoseThreads) void search_pose_kernel(
     return best <= P.dist_th ? bidx : -1;
   };
   auto blocks = [&](int j) -> bool { return MODE != ORBM_PROJ_LAST_FRAME || MP[j].obs_positive; };
+  constexpr bool kPerPoint = per_point(MODE);
 
   // ---- fixed-point rounds (g.mark[k] = least blocking point that picked k last round)
   bool converged = false;
@@ -211,7 +252,7 @@ __global__ __launch_bounds__(kPoseThreads) void search_pose_kernel(
     __syncthreads();
     const int any = s_flag;
     __syncthreads();
-    if (!any) {
+    if (!any || kPerPoint) {  // per-point modes: no blocking, one round is the result
       converged = true;
       break;
     }
@@ -231,6 +272,22 @@ __global__ __launch_bounds__(kPoseThreads) void search_pose_kernel(
     __syncthreads();
   }
 
+  if (kPerPoint) {  // ---- outputs: per point, the keypoint it matched
+    int* O = out + (size_t)f * P.mp_pitch;
+    int cnt = 0;
+    for (int j = tid; j < nmp; j += kPoseThreads) {
+      const int pk = PK[j];
+      O[j] = pk;
+      cnt += pk >= 0;
+    }
+    cnt = wave_sum_dpp(cnt);
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    if (lane == 0 && cnt) atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (tid == 0) nmatches[f] = s_cnt;
+    return;
+  }
   // ---- outputs: per keypoint the last point that stored itself there
   for (int i = tid; i < n; i += kPoseThreads) {
     g.mark[i] = -1;
@@ -315,10 +372,16 @@ int launch_search_pose(const PoseParams& P, const orbx_kp* kps, const uint8_t* d
                        const orbm_map_point_world* mps, const uint8_t* mpdesc, const int* nmp, int frames, int* picks,
                        int* out, int* nmatches, void* stream) {
   const size_t lds = pose_lds_bytes(P.kp_pitch);
-  const void* fn = P.mode == ORBM_PROJ_LAST_FRAME ? (const void*)search_pose_kernel<ORBM_PROJ_LAST_FRAME>
-                   : P.mode == ORBM_PROJ_KEYFRAME ? (const void*)search_pose_kernel<ORBM_PROJ_KEYFRAME>
-                                                  : (const void*)search_pose_kernel<ORBM_PROJ_SIM3>;
-  static size_t attr[4] = {0, 0, 0, 0};
+  const void* fns[7] = {nullptr,
+                        (const void*)search_pose_kernel<ORBM_PROJ_LAST_FRAME>,
+                        (const void*)search_pose_kernel<ORBM_PROJ_KEYFRAME>,
+                        (const void*)search_pose_kernel<ORBM_PROJ_SIM3>,
+                        (const void*)search_pose_kernel<ORBM_PROJ_FUSE>,
+                        (const void*)search_pose_kernel<ORBM_PROJ_FUSE_SIM3>,
+                        (const void*)search_pose_kernel<ORBM_PROJ_SIM3_MATCH>};
+  if (P.mode < 1 || P.mode > 6) return ORBX_EINVAL;
+  const void* fn = fns[P.mode];
+  static size_t attr[7] = {0, 0, 0, 0, 0, 0, 0};
   if (lds > attr[P.mode]) {
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return ORBX_EDEVICE;
@@ -327,12 +390,14 @@ int launch_search_pose(const PoseParams& P, const orbx_kp* kps, const uint8_t* d
 #define ORBX_POSE_LAUNCH(M)                                                                                       \
   hipLaunchKernelGGL(search_pose_kernel<M>, dim3(frames), dim3(kPoseThreads), lds, (hipStream_t)stream, P, kps, \
                      desc, n, uright, blocked, poses, mps, mpdesc, nmp, picks, out, nmatches)
-  if (P.mode == ORBM_PROJ_LAST_FRAME)
-    ORBX_POSE_LAUNCH(ORBM_PROJ_LAST_FRAME);
-  else if (P.mode == ORBM_PROJ_KEYFRAME)
-    ORBX_POSE_LAUNCH(ORBM_PROJ_KEYFRAME);
-  else
-    ORBX_POSE_LAUNCH(ORBM_PROJ_SIM3);
+  switch (P.mode) {
+    case ORBM_PROJ_LAST_FRAME: ORBX_POSE_LAUNCH(ORBM_PROJ_LAST_FRAME); break;
+    case ORBM_PROJ_KEYFRAME: ORBX_POSE_LAUNCH(ORBM_PROJ_KEYFRAME); break;
+    case ORBM_PROJ_SIM3: ORBX_POSE_LAUNCH(ORBM_PROJ_SIM3); break;
+    case ORBM_PROJ_FUSE: ORBX_POSE_LAUNCH(ORBM_PROJ_FUSE); break;
+    case ORBM_PROJ_FUSE_SIM3: ORBX_POSE_LAUNCH(ORBM_PROJ_FUSE_SIM3); break;
+    default: ORBX_POSE_LAUNCH(ORBM_PROJ_SIM3_MATCH); break;
+  }
 #undef ORBX_POSE_LAUNCH
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }

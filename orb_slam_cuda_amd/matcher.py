@@ -10,6 +10,10 @@ Mirrors include/ORBmatcher.h:37-102 for the hot-path searches:
     nmatches = m.SearchByProjection(CurrentFrame, LastFrame, th, bMono)
     nmatches = m.SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
     nmatches = m.SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
+    nmatches = m.SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+    nfused   = m.Fuse(pKF, vpMapPoints, th)                      # matching part, see Fuse()
+    nfused   = m.Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)
+    nfound   = m.SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
     ORBmatcher.DescriptorDistance(a, b)
 
 `Frame` / `KeyFrame` here are plain containers of the fields these searches
@@ -25,8 +29,8 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import (KP_DTYPE, MAP_POINT_PROJ_DTYPE, MAP_POINT_WORLD_DTYPE, ORBM_PROJ_KEYFRAME, ORBM_PROJ_LAST_FRAME,
-                   ORBM_PROJ_SIM3, FeatureVectorC, GridBounds, camera, check, lib, ptr)
+from ._lib import (KP_DTYPE, MAP_POINT_PROJ_DTYPE, MAP_POINT_WORLD_DTYPE, FeatureVectorC, GridBounds, camera, check,
+                   lib, ptr)
 
 
 @dataclass
@@ -163,6 +167,16 @@ class KeyFrame:
     mvScaleFactors: np.ndarray | None = None
     mfScaleFactor: float = 1.2
     mpMap: "MapPoints | None" = None
+    mTcw: np.ndarray | None = None         # (3, 4) or (4, 4) float32
+    mvuRight: np.ndarray | None = None     # (N,) float32, -1 = monocular
+    mbf: float = 0.0
+    mvLevelSigma2: np.ndarray | None = None
+    mvInvLevelSigma2: np.ndarray | None = None
+
+    def GetCameraCenter(self) -> np.ndarray:
+        """Ow = -Rcw^T tcw (KeyFrame::SetPose, src/KeyFrame.cc:77-92)."""
+        T = np.asarray(self.mTcw, np.float64)
+        return (-T[:3, :3].T @ T[:3, 3]).astype(np.float32)
 
     @property
     def N(self) -> int:
@@ -266,6 +280,126 @@ class ORBmatcher:
         if isinstance(b, KeyFrame):
             return self._search_keyframe(a, b, *args, **kw)
         return self._search_local_map(a, b, *args, **kw)
+
+    def SearchForTriangulation(self, pKF1: KeyFrame, pKF2: KeyFrame, F12, vMatchedPairs: list | None,
+                               bOnlyStereo: bool) -> int:
+        """SearchForTriangulation (src/ORBmatcher.cc:657-823): vMatchedPairs <- [(idx1, idx2)] in idx1 order."""
+        def side(K):
+            return (np.ascontiguousarray(K.mvKeysUn, KP_DTYPE), np.ascontiguousarray(K.mDescriptors, np.uint8),
+                    np.ascontiguousarray(np.full(K.N, -1, np.float32) if K.mvuRight is None else K.mvuRight,
+                                         np.float32),
+                    np.ascontiguousarray(_mp_mask(K.mvpMapPoints), np.uint8), feature_vector_csr(K.mFeatVec))
+        k1, d1, u1, h1, fv1 = side(pKF1)
+        k2, d2, u2, h2, fv2 = side(pKF2)
+        cw1 = np.ascontiguousarray(pKF1.GetCameraCenter(), np.float32)
+        T2 = np.ascontiguousarray(np.asarray(pKF2.mTcw, np.float32)[:3], np.float32)
+        cam2 = np.array([pKF2.fx, pKF2.fy, pKF2.cx, pKF2.cy], np.float32)
+        sc2 = np.ascontiguousarray(pKF2.mvScaleFactors, np.float32)
+        sg2 = np.ascontiguousarray(pKF2.mvLevelSigma2, np.float32)
+        F = np.ascontiguousarray(F12, np.float32).reshape(9)
+        out = np.full(max(len(k1), 1), -1, np.int32)
+        nm = C.c_int(0)
+        check(lib().orbm_search_for_triangulation(
+            self._h, ptr(k1), ptr(d1), ptr(u1), ptr(h1), len(k1), _fvc(fv1), ptr(k2), ptr(d2), ptr(u2), ptr(h2),
+            len(k2), _fvc(fv2), ptr(cw1), ptr(T2), ptr(cam2), ptr(sc2), ptr(sg2), len(sc2), ptr(F),
+            int(bool(bOnlyStereo)), int(self.mbCheckOrientation), ptr(out), C.byref(nm)), matcher=True)
+        m12 = out[:len(k1)]
+        if vMatchedPairs is not None:
+            vMatchedPairs[:] = [(int(i), int(j)) for i, j in enumerate(m12) if j >= 0]
+        self.last_matches = m12.copy()
+        return nm.value
+
+    def Fuse(self, pKF: KeyFrame, *args) -> int:
+        """Fuse(pKF, vpMapPoints, th=3.0) (src/ORBmatcher.cc:825-975) or
+        Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (:977-1100).
+
+        The GPU computes every point's match against pKF; the in-order tail of the reference is
+        applied here on the pointer arrays: a point matched to a keypoint without a MapPoint is
+        added (pKF.mvpMapPoints[idx] = point, so later points see it); otherwise the Scw overload
+        records vpReplacePoint[i] = the keypoint's MapPoint (if not bad) and the first overload
+        records the (point, keypoint MapPoint) pair in self.last_fuse_replace (MapPoint::Replace
+        itself belongs to the Map, outside this matcher). self.last_fuse = per-point keypoints."""
+        mp = pKF.mpMap
+        kps = np.ascontiguousarray(pKF.mvKeysUn, KP_DTYPE)
+        d = np.ascontiguousarray(pKF.mDescriptors, np.uint8)
+        n = len(kps)
+        sc = np.ascontiguousarray(pKF.mvScaleFactors, np.float32)
+        kmp = np.asarray(pKF.mvpMapPoints, np.int64).copy()
+        sim3 = len(args) >= 3
+        if sim3:
+            Scw, vpPoints, th, vpReplacePoint = args[0], args[1], args[2], (args[3] if len(args) > 3 else None)
+            pts = np.asarray(vpPoints, np.int64)
+            found = np.isin(pts, kmp[kmp >= 0])  # spAlreadyFound = pKF->GetMapPoints()
+            rec, md = mp.records(pts, None, None, ~mp.bad_of(pts) & ~found)
+            cam = camera(pKF.fx, pKF.fy, pKF.cx, pKF.cy, 0.0, 0.0, Scw)
+        else:
+            vpMapPoints, th = args[0], (args[1] if len(args) > 1 else 3.0)
+            pts = np.asarray(vpMapPoints, np.int64)
+            inkf = np.isin(pts, kmp[kmp >= 0])  # IsInKeyFrame(pKF)
+            rec, md = mp.records(pts, None, None, ~mp.bad_of(pts) & ~inkf)
+            cam = camera(pKF.fx, pKF.fy, pKF.cx, pKF.cy, 0.0, pKF.mbf, pKF.mTcw)
+        out = np.full(max(len(pts), 1), -1, np.int32)
+        nm = C.c_int(0)
+        if sim3:
+            check(lib().orbm_fuse_sim3(self._h, ptr(kps), ptr(d), n, _grid(pKF), ptr(sc), len(sc),
+                                       C.c_float(pKF.mfScaleFactor), C.byref(cam), ptr(rec), ptr(md), len(rec),
+                                       C.c_float(th), ptr(out), C.byref(nm)), matcher=True)
+        else:
+            ur = None if pKF.mvuRight is None else np.ascontiguousarray(pKF.mvuRight, np.float32)
+            isg = np.ascontiguousarray(pKF.mvInvLevelSigma2, np.float32)
+            check(lib().orbm_fuse(self._h, ptr(kps), ptr(d), n, ptr(ur), _grid(pKF), ptr(sc), ptr(isg), len(sc),
+                                  C.c_float(pKF.mfScaleFactor), C.byref(cam), ptr(rec), ptr(md), len(rec),
+                                  C.c_float(th), ptr(out), C.byref(nm)), matcher=True)
+        o = out[:len(pts)]
+        self.last_fuse = o.copy()
+        replace = []
+        for i in np.nonzero(o >= 0)[0]:  # the reference's in-order tail (:932-957, :1083-1097)
+            idx = int(o[i])
+            cur = int(kmp[idx])
+            if cur >= 0:
+                if not mp.bad_of([cur])[0]:
+                    if sim3 and vpReplacePoint is not None:
+                        vpReplacePoint[i] = cur
+                    replace.append((int(pts[i]), cur))
+            else:
+                kmp[idx] = pts[i]
+        if isinstance(pKF.mvpMapPoints, np.ndarray) and pKF.mvpMapPoints.dtype.kind == "i":
+            pKF.mvpMapPoints[:] = kmp
+        self.last_fuse_replace = replace
+        return nm.value
+
+    def SearchBySim3(self, pKF1: KeyFrame, pKF2: KeyFrame, vpMatches12, s12: float, R12, t12, th: float) -> int:
+        """SearchBySim3 (src/ORBmatcher.cc:1102-1326): vpMatches12 (pKF1.N pointers, -1 = NULL) gains the
+        new mutual matches."""
+        mp = pKF1.mpMap
+        m1 = np.asarray(pKF1.mvpMapPoints, np.int64)
+        m2 = np.asarray(pKF2.mvpMapPoints, np.int64)
+        vm = np.asarray(vpMatches12, np.int64)
+        already1 = vm >= 0
+        already2 = np.isin(m2, vm[vm >= 0]) & (m2 >= 0)  # pMP->GetIndexInKeyFrame(pKF2)
+        r1, q1 = mp.records(m1, None, None, ~already1 & ~mp.bad_of(m1))
+        r2, q2 = mp.records(m2, None, None, ~already2 & ~mp.bad_of(m2))
+        k1 = np.ascontiguousarray(pKF1.mvKeysUn, KP_DTYPE)
+        k2 = np.ascontiguousarray(pKF2.mvKeysUn, KP_DTYPE)
+        d1 = np.ascontiguousarray(pKF1.mDescriptors, np.uint8)
+        d2 = np.ascontiguousarray(pKF2.mDescriptors, np.uint8)
+        T1 = np.ascontiguousarray(np.asarray(pKF1.mTcw, np.float32)[:3], np.float32)
+        T2 = np.ascontiguousarray(np.asarray(pKF2.mTcw, np.float32)[:3], np.float32)
+        sc = np.ascontiguousarray(pKF2.mvScaleFactors, np.float32)
+        cam1 = camera(pKF1.fx, pKF1.fy, pKF1.cx, pKF1.cy, 0.0, 0.0, T1)
+        R = np.ascontiguousarray(R12, np.float32).reshape(9)
+        t = np.ascontiguousarray(t12, np.float32).reshape(3)
+        out = np.full(max(len(k1), 1), -1, np.int32)
+        nf = C.c_int(0)
+        check(lib().orbm_search_by_sim3(
+            self._h, ptr(k1), ptr(d1), len(k1), _grid(pKF1), ptr(T1), ptr(r1), ptr(q1), ptr(k2), ptr(d2), len(k2),
+            _grid(pKF2), ptr(T2), ptr(r2), ptr(q2), ptr(sc), len(sc), C.c_float(pKF2.mfScaleFactor), C.byref(cam1),
+            C.c_float(s12), ptr(R), ptr(t), C.c_float(th), ptr(out), C.byref(nf)), matcher=True)
+        o = out[:len(k1)]
+        for i1 in np.nonzero(o >= 0)[0]:
+            vpMatches12[i1] = int(m2[o[i1]])
+        self.last_matches = o.copy()
+        return nf.value
 
     def _search_last_frame(self, CurrentFrame: Frame, LastFrame: Frame, th: float, bMono: bool) -> int:
         """SearchByProjection(Frame&, const Frame&, th, bMono): map points of LastFrame (not outliers)

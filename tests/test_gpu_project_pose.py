@@ -187,7 +187,7 @@ def test_pose_batch_mixed_frames(pkg, O):
     _lib.check(_lib.lib().orbm_search_by_projection_pose_batch(
         m.handle, _lib.ORBM_PROJ_LAST_FRAME, v(dev["kp"]), v(dev["ds"]), v(dev["n"]), K, v(dev["ur"]),
         _lib.GridBounds(*cases[0]["bounds"]), _v(sc), len(sc), C.c_float(1.2), v(dev["bl"]), v(dev["pz"]),
-        v(dev["mp"]), v(dev["md"]), v(dev["nmp"]), M, B, C.c_float(7.0), 100, 1, v(d_out), v(d_nm), s.s),
+        v(dev["mp"]), v(dev["md"]), v(dev["nmp"]), M, B, C.c_float(7.0), 100, 1, None, v(d_out), v(d_nm), s.s),
         matcher=True)
     s.synchronize()
     out = d_out.download(B * K, np.int32).reshape(B, K)

@@ -65,7 +65,7 @@ def run():
     _lib.check(_lib.lib().orbm_search_by_projection_pose_batch(
         m.handle, MODE, v(dev["kp"]), v(dev["ds"]), v(dev["n"]), K, v(dev["ur"]) if mode == "last" else None,
         _lib.GridBounds(*base[0]["bounds"]), sc.ctypes.data_as(C.c_void_p), len(sc), C.c_float(1.2), v(dev["bl"]),
-        v(dev["pz"]), v(dev["mp"]), v(dev["md"]), v(dev["nmp"]), M, B, C.c_float(th), dist_th, 1, v(d_out),
+        v(dev["pz"]), v(dev["mp"]), v(dev["md"]), v(dev["nmp"]), M, B, C.c_float(th), dist_th, 1, None, v(d_out),
         v(d_nm), s.s), matcher=True)
 
 
