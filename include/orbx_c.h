@@ -197,7 +197,8 @@ int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b);
  * for pair p, A = d_A + p*a_pitch (nA[p] rows of 32 B), B likewise.
  * Outputs per query row (stride a_cap): best index (-1 if none), best
  * distance and second-best distance (256 when absent), with SearchByBoW's
- * sequential semantics (strict '<', first index wins ties). */
+ * sequential semantics (strict '<', first index wins ties). nB[p] <= 65535
+ * (the candidate index shares a 32-bit key with the distance). */
 int orbm_hamming_top2(orbm_handle m, const uint8_t* d_A, size_t a_pitch,
                       const int* d_nA, int a_cap, const uint8_t* d_B,
                       size_t b_pitch, const int* d_nB, int pairs,

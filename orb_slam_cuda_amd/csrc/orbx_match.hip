@@ -62,9 +62,19 @@ __device__ __forceinline__ int med3_i32(int a, int b, int c) {
   return r;
 }
 
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Best / second of (distance, candidate) keys: key = d << 16 | j orders by
+// distance, then by index, so min() keeps the first candidate on ties and
+// med3() the second key (whose distance is the reference's bestDist2, ties
+// included). Per pair 8 v_xor + 8 v_bcnt + v_lshl_or + v_min + v_med3.
 struct Top2Acc {
   uint4 a0, a1;  // query descriptor
-  int b1, b2, bi;
+  uint32_t k1, k2;
   __device__ __forceinline__ void score(const uint4& r0, const uint4& r1, int j) {
     int d = bcnt_acc(a0.x ^ r0.x, 0);
     d = bcnt_acc(a0.y ^ r0.y, d);
@@ -74,20 +84,21 @@ struct Top2Acc {
     d = bcnt_acc(a1.y ^ r1.y, d);
     d = bcnt_acc(a1.z ^ r1.z, d);
     d = bcnt_acc(a1.w ^ r1.w, d);
-    bi = d < b1 ? j : bi;
-    b2 = med3_i32(d, b1, b2);
-    b1 = min(d, b1);
+    const uint32_t key = ((uint32_t)d << 16) | (uint32_t)j;
+    k2 = med3_u32(key, k1, k2);
+    k1 = min(key, k1);
   }
 };
+constexpr uint32_t kTopNone = (256u << 16) | 0xFFFFu;  // distance 256, no candidate
 
 // Two queries per lane against wave-uniform candidate rows. The candidates
 // are split in kTopSplit contiguous ranges, two waves per range (so that 8
 // waves per SIMD are resident); each range stages chunks in LDS (one 16-byte
 // load per thread per chunk) that its lanes read back as broadcast loads, one
-// pair of row reads serving two queries. A pair costs 8 v_xor + 8 v_bcnt + 4
-// top-2 updates: b2 = med3(d, b1, b2) (b1 <= b2 always), b1 = min(d, b1),
-// index by compare. The partial results are merged in range order (earlier
-// range wins ties, as the sequential scan would).
+// pair of row reads serving two queries. A pair costs 8 v_xor + 8 v_bcnt + 3
+// top-2 updates on (distance << 16 | index) keys (Top2Acc). The partial
+// results merge exactly because the keys carry the index (the earlier
+// candidate wins ties, as the sequential scan would).
 __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t* __restrict__ A, long long a_pitch,
                                                                    const int* __restrict__ nA, int a_cap,
                                                                    const uint8_t* __restrict__ B, long long b_pitch,
@@ -95,16 +106,16 @@ __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t
                                                                    int* __restrict__ best_idx, int* __restrict__ best,
                                                                    int* __restrict__ second) {
   __shared__ uint4 sB[kTopSplit][kTopChunk][2];
-  __shared__ int3 part[kTopSplit][kTopQueries];
+  __shared__ uint2 part[kTopSplit][kTopQueries];
   const int p = blockIdx.y, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int k = wv >> 1, h = wv & 1;
   const int qa = h * 64 + lane, qb = 128 + h * 64 + lane;  // this lane's two queries (of 256)
   const int base = blockIdx.x * kTopQueries;
-  const int na = nA[p], nb = nB[p];
+  const int na = nA[p], nb = min(nB[p], 65535);  // candidate indices live in the low 16 key bits
   if (base >= na) return;
   const uint4* Ap = (const uint4*)(A + p * a_pitch);
   const uint4* Bp = (const uint4*)(B + p * b_pitch);
-  Top2Acc x{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 256, 256, -1};
+  Top2Acc x{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), kTopNone, kTopNone};
   Top2Acc y = x;
   if (base + qa < na) {
     x.a0 = Ap[2 * (base + qa)];
@@ -115,7 +126,8 @@ __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t
     y.a1 = Ap[2 * (base + qb) + 1];
   }
   const int per = (nb + kTopSplit - 1) / kTopSplit;
-  const int jb = min(k * per, nb), je = min(jb + per, nb);
+  // wave-uniform range (scalar registers: the key's index operand stays an SGPR)
+  const int jb = __builtin_amdgcn_readfirstlane(min(k * per, nb)), je = __builtin_amdgcn_readfirstlane(min(jb + per, nb));
   // loader role of this thread: range lk, row lr, half lh
   const int lk = tid / (2 * kTopChunk), lr = (tid >> 1) % kTopChunk, lh = tid & 1;
   const int ljb = min(lk * per, nb), lje = min(ljb + per, nb);
@@ -138,24 +150,24 @@ __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t
       y.score(r0, r1, jb + c0 + j);
     }
   }
-  part[k][qa] = make_int3(x.b1, x.bi, x.b2);
-  part[k][qb] = make_int3(y.b1, y.bi, y.b2);
+  part[k][qa] = make_uint2(x.k1, x.k2);
+  part[k][qb] = make_uint2(y.k1, y.k2);
   __syncthreads();
   if (tid >= kTopQueries || base + tid >= na) return;
-  int3 r = part[0][tid];
+  // merge the ranges: keys are globally ordered (distance, index), so the
+  // best / second keys of the union are min / the second smallest
+  uint2 r = part[0][tid];
 #pragma unroll
   for (int s = 1; s < kTopSplit; ++s) {
-    const int3 o = part[s][tid];
-    r.z = min(min(max(r.x, o.x), r.z), o.z);
-    if (o.x < r.x) {
-      r.x = o.x;
-      r.y = o.y;
-    }
+    const uint2 o = part[s][tid];
+    r.y = min(min(max(r.x, o.x), r.y), o.y);
+    r.x = min(r.x, o.x);
   }
   const long long o = (long long)p * a_cap + base + tid;
-  best_idx[o] = r.y;
-  best[o] = r.x;
-  second[o] = r.z;
+  const int d1 = (int)(r.x >> 16);
+  best_idx[o] = d1 < 256 ? (int)(r.x & 0xFFFFu) : -1;
+  best[o] = d1;
+  second[o] = (int)(r.y >> 16);
 }
 
 // ------------------------------------------------------------ wave helpers
