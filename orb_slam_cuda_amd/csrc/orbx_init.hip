@@ -1,0 +1,648 @@
+// orbx_init.hip — ORBmatcher::SearchForInitialization on the GPU
+// (src/ORBmatcher.cc:405-520 + Frame::AssignFeaturesToGrid / GetFeaturesInArea
+// / PosInGrid src/Frame.cc:229-244, 326-391), one workgroup per (F1, F2) pair.
+//
+// The reference visits F1's octave-0 keypoints i1 in order. Each takes the
+// best / second Hamming distance over F2's octave-0 keypoints in its 2r x 2r
+// window (visited cell column by column, index order inside a cell),
+// skipping every i2 whose vMatchedDistance (the distance of the latest
+// earlier query that accepted it) is <= the current distance; accepting
+// steals i2 from its previous owner. Every query's outcome is a function of
+// the earlier outcomes: a triangular system whose unique fixed point is the
+// sequential result.
+//
+// Here one LANE serves one query in every phase (lane-per-query keeps the
+// per-candidate work at a few scalar-like VALU ops and needs no cross-lane
+// reductions):
+//   0. counting sort of F2's octave-0 keypoints by grid cell (stable: index
+//      order inside a cell), positions / indices / descriptors to LDS in
+//      sorted order, so a window column is one contiguous run;
+//   1. per query: candidate count (window test on positions);
+//   2. per query: candidate list (index, distance) in reference order;
+//   3. Jacobi rounds: every query recomputes its top-2 from the previous
+//      round's accepted outcomes, honouring only claims of earlier queries
+//      (per-i2 claim lists); a round without change is the fixed point. Past
+//      kInitMaxRounds one lane runs the sequential greedy instead;
+//   4. the latest acceptor keeps each i2, rotation consistency, outputs.
+#include <climits>
+
+#include "orbx_device.cuh"
+#include "orbx_wave.cuh"
+
+namespace orbx {
+
+constexpr int kInitGridCols = 64, kInitGridRows = 48;  // FRAME_GRID_COLS / ROWS include/Frame.h:37-38
+constexpr int kInitCells = kInitGridCols * kInitGridRows;
+constexpr int kInitHisto = 30;  // HISTO_LENGTH
+constexpr int kInitThLow = 50;  // TH_LOW
+constexpr int kInitMaxRounds = 48;
+constexpr int kD0Stride = 9;  // words per staged F2 descriptor: odd, so random rows spread over the LDS banks
+
+#define LDSP __attribute__((address_space(3)))
+
+size_t init_lds_fixed_bytes(int kp_pitch) {
+  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  const size_t K = (size_t)kp_pitch;
+  return r16(4 * (kInitCells + 1)) + r16(4 * K) /* cof / head / md */ + r16(8 * K) /* pos / nxt */ +
+         r16(4 * K) /* idx / m21 */ + r16(4 * (K + 1)) /* coff */ + r16(4 * K) /* qlist / res */ +
+         r16(4 * K) /* src */ + r16(4 * K) /* queue */ + 3 * r16(128);
+}
+
+// Frame::PosInGrid: round() of a float, half away from zero
+__device__ __forceinline__ bool init_pos_in_grid(float x, float y, const InitParams& P, int* c) {
+  const int px = (int)roundf(__fmul_rn(__fsub_rn(x, P.minX), P.invW));
+  const int py = (int)roundf(__fmul_rn(__fsub_rn(y, P.minY), P.invH));
+  *c = px * kInitGridRows + py;
+  return !(px < 0 || px >= kInitGridCols || py < 0 || py >= kInitGridRows);
+}
+
+// GetFeaturesInArea's cell window (src/Frame.cc:330-346); false when empty
+__device__ __forceinline__ bool init_window(float x, float y, const InitParams& P, int& cx0, int& cx1, int& cy0,
+                                           int& cy1) {
+  const float r = P.r;
+  cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, P.minX), r), P.invW)));
+  if (cx0 >= kInitGridCols) return false;
+  cx1 = min(kInitGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, P.minX), r), P.invW)));
+  if (cx1 < 0) return false;
+  cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, P.minY), r), P.invH)));
+  if (cy0 >= kInitGridRows) return false;
+  cy1 = min(kInitGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, P.minY), r), P.invH)));
+  if (cy1 < 0) return false;
+  return true;
+}
+
+__device__ __forceinline__ int init_hamming(uint4 a0, uint4 a1, uint4 b0, uint4 b1) {
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// 16-lane row (one query) helpers on DPP; all 16 lanes of the row must be active
+__device__ __forceinline__ int row_incl_scan(int v) {
+  v += dpp_i<kDppShr1>(0, v);
+  v += dpp_i<kDppShr2>(0, v);
+  v += dpp_i<kDppShr4>(0, v);
+  v += dpp_i<kDppShr8>(0, v);
+  return v;
+}
+__device__ __forceinline__ int row_sum(int v) {
+  v += dpp_i<kDppQuad1032>(0, v);
+  v += dpp_i<kDppQuad2301>(0, v);
+  v += dpp_i<kDppHalfMirror>(0, v);
+  v += dpp_i<kDppMirror>(0, v);
+  return v;
+}
+// (k1, k2) = the two smallest keys of the row
+template <int CTRL>
+__device__ __forceinline__ void row_top2_step(uint32_t& k1, uint32_t& k2) {
+  const uint32_t o1 = (uint32_t)dpp_i<CTRL>(0, (int)k1), o2 = (uint32_t)dpp_i<CTRL>(0, (int)k2);
+  k2 = min(min(max(k1, o1), k2), o2);
+  k1 = min(k1, o1);
+}
+__device__ __forceinline__ void row_top2(uint32_t& k1, uint32_t& k2) {
+  row_top2_step<kDppQuad1032>(k1, k2);
+  row_top2_step<kDppQuad2301>(k1, k2);
+  row_top2_step<kDppHalfMirror>(k1, k2);
+  row_top2_step<kDppMirror>(k1, k2);
+}
+
+struct InitShared {
+  LDSP int* cell;     // [kInitCells + 1] first sorted position of each cell
+  LDSP int* cof;      // [K] cell of each F2 keypoint (sort), then head[i2] (rounds), md[i2] (fallback)
+  LDSP float* pos;    // [2K] sorted positions x, y (phases 1-2), then nxt[i1] (rounds)
+  LDSP int* idx;      // [K] sorted position -> i2 (phases 0-2), then m21[i2] (fallback)
+  LDSP int* coff;     // [K + 1] candidate offsets per i1
+  LDSP int* qlist;    // [K] octave-0 queries (phases 1-2), then res[i1] / vnMatches12
+  LDSP int* src;      // [K] i2 accepted by i1 (rotHist entries), -1
+  LDSP int* queue;    // [K] queries with candidates
+  LDSP float* src_f;    // src viewed as query window x (phases 1-2)
+  LDSP float* queue_f;  // queue viewed as query window y (phases 1-2)
+  LDSP int* var;      // [32]
+  LDSP int* hist;     // [32]
+  LDSP int* tmp;      // [32]
+  LDSP uint32_t* d0;  // [kD0Stride n0] sorted descriptors (when they fit)
+  LDSP uint32_t* cand;  // candidate entries in LDS
+};
+
+__device__ __forceinline__ int lds_atomic_add(LDSP int* p, int v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Exclusive scan of a[0..n) in LDS (NT threads); returns the total.
+template <int NT>
+__device__ int init_scan(LDSP int* a, int n, LDSP int* s_tmp) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int per = (n + NT - 1) / NT;
+  const int b = min(tid * per, n), e = min(b + per, n);
+  int sum = 0;
+  for (int i = b; i < e; ++i) sum += a[i];
+  const int x = wave_incl_scan_dpp(sum);
+  if (lane == 63) s_tmp[w] = x;
+  __syncthreads();
+  int wpre = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    const int v = s_tmp[i];
+    if (i < w) wpre += v;
+    total += v;
+  }
+  int run = wpre + x - sum;
+  for (int i = b; i < e; ++i) {
+    const int v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+// Phases 2-4 with the candidate list in one memory space (LDS or global), so
+// each instantiation addresses a single known space.
+__device__ __forceinline__ void init_stamp(const InitParams& P, int k) {
+  if (P.prof && threadIdx.x == 0) P.prof[blockIdx.x * 16 + k] = (long long)__builtin_amdgcn_s_memtime();
+}
+
+template <typename CandPtr, bool DESC_LDS>
+__device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr cand, const orbx_kp* __restrict__ kp1,
+                           const uint8_t* __restrict__ desc1, const uint8_t* __restrict__ desc2,
+                           const float* __restrict__ prev, int n1, int n2, int nq0, int total) {
+  const int tid = threadIdx.x;
+  // ---- phase 2a: candidate lists in reference order: a 16-lane row per
+  // query, a lane per window column; column c's entries follow the entries of
+  // columns < c (row prefix sum), each (query slot << 12 | sorted position)
+  for (int g = tid >> 4; g < nq0; g += kInitThreads / 16) {
+    const int l16 = tid & 15;
+    const int i1 = S.qlist[g];
+    const int off = S.coff[i1];
+    if (off == S.coff[i1 + 1]) continue;  // row-uniform
+    const float x = S.src_f[g], y = S.queue_f[g];
+    int cx0, cx1, cy0, cy1;
+    init_window(x, y, P, cx0, cx1, cy0, cy1);
+    const int ncol = cx1 - cx0 + 1;
+    int base = off;
+    for (int c0 = 0; c0 < ncol; c0 += 16) {
+      const int ci = c0 + l16;
+      int pb = 0, pe = 0, own = 0;
+      if (ci < ncol) {
+        const int ix = cx0 + ci;
+        pb = S.cell[ix * kInitGridRows + cy0];
+        pe = S.cell[ix * kInitGridRows + cy1 + 1];
+        for (int p = pb; p < pe; ++p) {
+          const float qx = S.pos[2 * p], qy = S.pos[2 * p + 1];
+          own += (fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r) ? 1 : 0;
+        }
+      }
+      int o = base + row_incl_scan(own) - own;
+      for (int p = pb; p < pe; ++p) {
+        const float qx = S.pos[2 * p], qy = S.pos[2 * p + 1];
+        if (fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r)
+          cand[o++] = ((uint32_t)g << 12) | (uint32_t)p;
+      }
+      base += row_sum(own);
+    }
+  }
+  __syncthreads();
+  init_stamp(P, 4);
+  // the queries' descriptors to LDS (in the position array, free from here on)
+  const bool qd_lds = nq0 * 8 <= 2 * P.kp_pitch;
+  LDSP uint32_t* qd = (LDSP uint32_t*)S.pos;
+  if (qd_lds) {
+    for (int t = tid; t < 2 * nq0; t += kInitThreads) {
+      const uint4 v = ((const uint4*)(desc1 + (size_t)S.qlist[t >> 1] * 32))[t & 1];
+      LDSP uint32_t* w = qd + 4 * t;
+      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    }
+    __syncthreads();
+  }
+  // ---- phase 2b: every candidate's Hamming distance, candidate-parallel;
+  // the entry becomes (i2 | distance << 23)
+  for (int c = tid; c < total; c += kInitThreads) {
+    const uint32_t e = cand[c];
+    const int g = (int)(e >> 12), p = (int)(e & 0xFFF);
+    uint4 a0, a1;
+    if (qd_lds) {
+      const LDSP uint32_t* w = qd + 8 * g;
+      a0 = make_uint4(w[0], w[1], w[2], w[3]);
+      a1 = make_uint4(w[4], w[5], w[6], w[7]);
+    } else {
+      const uint4* dq = (const uint4*)(desc1 + (size_t)S.qlist[g] * 32);
+      a0 = dq[0];
+      a1 = dq[1];
+    }
+    const int i2 = S.idx[p];
+    uint4 b0, b1;
+    if (DESC_LDS) {
+      const LDSP uint32_t* w = S.d0 + kD0Stride * p;
+      b0 = make_uint4(w[0], w[1], w[2], w[3]);
+      b1 = make_uint4(w[4], w[5], w[6], w[7]);
+    } else {
+      const uint4* d2 = (const uint4*)(desc2 + (size_t)i2 * 32);
+      b0 = d2[0];
+      b1 = d2[1];
+    }
+    cand[c] = (uint32_t)i2 | ((uint32_t)init_hamming(a0, a1, b0, b1) << 23);
+  }
+  __syncthreads();
+  init_stamp(P, 5);
+  if (P.stop == 3) return;
+
+  // ---- phase 3: Jacobi rounds over the queue of queries with candidates
+  LDSP int* res = S.qlist;          // per i1: -1, or bestIdx2 << 9 | bestDist
+  LDSP int* head = S.cof;           // per i2: latest claiming i1 of the snapshot, or -1
+  LDSP int* nxt = (LDSP int*)S.pos;  // per i1: (next claimer + 1) << 9 | its distance
+  for (int i = tid; i < n1; i += kInitThreads) res[i] = -1;
+  for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
+  if (tid == 0) {
+    S.var[0] = 0;  // nmatches
+    S.var[6] = 1;  // changed
+    S.var[7] = 0;  // queue length
+  }
+  __syncthreads();
+  for (int i = tid; i < n1; i += kInitThreads)
+    if (S.coff[i + 1] > S.coff[i]) S.queue[lds_atomic_add(&S.var[7], 1)] = i;
+  __syncthreads();
+  const int nq = S.var[7];
+  bool converged = false;
+  for (int round = 0; round < kInitMaxRounds; ++round) {
+    if (S.var[6] == 0) {
+      converged = true;
+      if (P.prof && tid == 0) P.prof[blockIdx.x * 16 + 11] = round;
+      break;
+    }
+    __syncthreads();
+    if (tid == 0) S.var[6] = 0;
+    __syncthreads();
+    int changed = 0;
+    // a 16-lane row per query: lane l scans candidates c0 + l, c0 + l + 16, ...
+    // keeping the two smallest (distance << 22 | position) keys; the row merge
+    // gives the sequential scan's best (earliest on equal distances) and second
+    for (int g = tid >> 4; g < nq; g += kInitThreads / 16) {
+      const int l16 = tid & 15;
+      const int i1 = S.queue[g];
+      const int c0 = S.coff[i1], c1 = S.coff[i1 + 1];
+      uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
+      for (int c = c0 + l16; c < c1; c += 16) {
+        const uint32_t e = cand[c];
+        const int i2 = (int)(e & 0x7FFFFF), dist = (int)(e >> 23);
+        int md = INT_MAX;  // vMatchedDistance[i2] at i1's turn
+        for (int hd = head[i2]; hd >= 0;) {
+          const int x = nxt[hd];
+          if (hd < i1) md = min(md, x & 511);
+          hd = (x >> 9) - 1;
+        }
+        if (md <= dist) continue;  // (:444-445)
+        const uint32_t key = ((uint32_t)dist << 22) | (uint32_t)(c - c0);
+        k2 = min(k2, max(k1, key));
+        k1 = min(k1, key);
+      }
+      row_top2(k1, k2);
+      const int best = k1 == 0xFFFFFFFFu ? INT_MAX : (int)(k1 >> 22);
+      const int best2 = k2 == 0xFFFFFFFFu ? INT_MAX : (int)(k2 >> 22);
+      const bool ok = best <= kInitThLow && (float)best < __fmul_rn((float)best2, P.nnratio);
+      if (l16 == 0) {
+        const int r = ok ? ((int)(cand[c0 + (k1 & 0x3FFFFF)] & 0x7FFFFF) << 9 | best) : -1;
+        if (res[i1] != r) {
+          res[i1] = r;
+          changed = 1;
+        }
+      }
+    }
+    if (changed) S.var[6] = 1;
+    __syncthreads();
+    // snapshot of this round's outcomes as per-i2 claim lists
+    for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
+    __syncthreads();
+    for (int qq = tid; qq < nq; qq += kInitThreads) {
+      const int i1 = S.queue[qq];
+      const int r = res[i1];
+      if (r >= 0)
+        nxt[i1] = ((__hip_atomic_exchange(&head[r >> 9], i1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1)
+                   << 9) |
+                  (r & 511);
+    }
+    __syncthreads();
+  }
+  init_stamp(P, 6);
+  if (P.prof && tid == 0) P.prof[blockIdx.x * 16 + 12] = converged ? 1 : 0;
+  if (converged) {
+    // the latest accepting query keeps each i2 (earlier ones were stolen
+    // from, :463-467); every accepted query entered rotHist (:469-470)
+    for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
+    __syncthreads();
+    for (int qq = tid; qq < nq; qq += kInitThreads) {
+      const int i1 = S.queue[qq];
+      const int r = res[i1];
+      if (r >= 0) __hip_atomic_fetch_max(&head[r >> 9], i1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    int kept = 0;
+    for (int i = tid; i < n1; i += kInitThreads) {
+      const int r = res[i];
+      const int b = r >= 0 ? (r >> 9) : -1;
+      const bool keep = r >= 0 && head[b] == i;
+      S.src[i] = b;
+      res[i] = keep ? b : -1;  // res becomes vnMatches12
+      kept += keep ? 1 : 0;
+    }
+    kept = wave_sum_dpp(kept);
+    if ((tid & 63) == 0 && kept) lds_atomic_add(&S.var[0], kept);
+    __syncthreads();
+    return;
+  }
+  // ---- sequential greedy in i1 order (one lane; pathological chains only)
+  LDSP int* md = S.cof;
+  LDSP int* m21 = S.idx;
+  LDSP int* m12 = res;
+  for (int i = tid; i < n2; i += kInitThreads) {
+    md[i] = INT_MAX;
+    m21[i] = -1;
+  }
+  for (int i = tid; i < n1; i += kInitThreads) {
+    m12[i] = -1;
+    S.src[i] = -1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int nm = 0;
+    for (int i1 = 0; i1 < n1; ++i1) {
+      const int c1 = S.coff[i1 + 1];
+      int best = INT_MAX, best2 = INT_MAX, bidx = -1;
+      for (int c = S.coff[i1]; c < c1; ++c) {
+        const uint32_t e = cand[c];
+        const int i2 = (int)(e & 0x7FFFFF), dist = (int)(e >> 23);
+        if (md[i2] <= dist) continue;
+        if (dist < best) {
+          best2 = best;
+          best = dist;
+          bidx = i2;
+        } else if (dist < best2) {
+          best2 = dist;
+        }
+      }
+      if (best <= kInitThLow && (float)best < __fmul_rn((float)best2, P.nnratio)) {
+        if (m21[bidx] >= 0) {  // steal (:463-467)
+          m12[m21[bidx]] = -1;
+          nm--;
+        }
+        m12[i1] = bidx;
+        m21[bidx] = i1;
+        md[bidx] = best;
+        nm++;
+        S.src[i1] = bidx;
+      }
+    }
+    S.var[0] = nm;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kInitThreads) void search_init_kernel(
+    InitParams P, const orbx_kp* __restrict__ kp1_all, const uint8_t* __restrict__ desc1_all,
+    const int* __restrict__ n1_all, const orbx_kp* __restrict__ kp2_all, const uint8_t* __restrict__ desc2_all,
+    const int* __restrict__ n2_all, float* __restrict__ prev_all, uint32_t* __restrict__ cand_all,
+    int* __restrict__ matches_all, int* __restrict__ nmatches, int* err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int pr = blockIdx.x, tid = threadIdx.x;
+  const int n1 = n1_all[pr], n2 = n2_all[pr], K = P.kp_pitch;
+  const orbx_kp* kp1 = kp1_all + (size_t)pr * K;
+  const orbx_kp* kp2 = kp2_all + (size_t)pr * K;
+  const uint8_t* desc1 = desc1_all + (size_t)pr * K * 32;
+  const uint8_t* desc2 = desc2_all + (size_t)pr * K * 32;
+  // prev_all == nullptr: windows centred on F1's own keypoints (the initial
+  // mvbPrevMatched of Tracking::MonocularInitialization, src/Tracking.cc:645-647)
+  float* prev = prev_all ? prev_all + (size_t)pr * K * 2 : nullptr;
+  int* m12_out = matches_all + (size_t)pr * K;
+
+  LDSP unsigned char* sp = (LDSP unsigned char*)smem;
+  auto take = [&](size_t bytes) {
+    LDSP unsigned char* r = sp;
+    sp += (bytes + 15) & ~(size_t)15;
+    return r;
+  };
+  InitShared S;
+  S.cell = (LDSP int*)take(4ull * (kInitCells + 1));
+  S.cof = (LDSP int*)take(4ull * K);
+  S.pos = (LDSP float*)take(8ull * K);
+  S.idx = (LDSP int*)take(4ull * K);
+  S.coff = (LDSP int*)take(4ull * (K + 1));
+  S.qlist = (LDSP int*)take(4ull * K);
+  S.src = (LDSP int*)take(4ull * K);
+  S.queue = (LDSP int*)take(4ull * K);
+  S.src_f = (LDSP float*)S.src;
+  S.queue_f = (LDSP float*)S.queue;
+  S.var = (LDSP int*)take(128);
+  S.hist = (LDSP int*)take(128);
+  S.tmp = (LDSP int*)take(128);
+  LDSP uint32_t* tail = (LDSP uint32_t*)sp;  // P.cand_lds entries: descriptors, then candidates
+
+  init_stamp(P, 0);
+  // ---- phase 0: counting sort of F2's octave-0 keypoints by cell (the only
+  // ones GetFeaturesInArea(.., 0, 0) returns), stable in index order
+  for (int c = tid; c <= kInitCells; c += kInitThreads) S.cell[c] = 0;
+  if (tid < 32) {
+    S.hist[tid] = 0;
+    S.var[tid] = 0;
+  }
+  __syncthreads();
+  LDSP int* slot = S.src;     // arrival slot of each F2 keypoint in its cell (free until phase 3)
+  LDSP int* members = S.queue;  // cell members in arrival order (free until phase 3)
+  for (int i = tid; i < n2; i += kInitThreads) {
+    const orbx_kp k = kp2[i];
+    int c = -1;
+    if (!(k.octave == 0 && init_pos_in_grid(k.x, k.y, P, &c))) c = -1;
+    S.cof[i] = c;
+    if (c >= 0) slot[i] = lds_atomic_add(&S.cell[c], 1);
+  }
+  __syncthreads();
+  const int n0 = init_scan<kInitThreads>(S.cell, kInitCells + 1, S.tmp);
+  const bool d0_lds = kD0Stride * n0 <= P.cand_lds / 2;
+  S.d0 = tail;
+  S.cand = tail + (d0_lds ? kD0Stride * n0 : 0);
+  const int cand_lds = P.cand_lds - (d0_lds ? kD0Stride * n0 : 0);
+  for (int i = tid; i < n2; i += kInitThreads) {
+    const int c = S.cof[i];
+    if (c >= 0) members[S.cell[c] + slot[i]] = i;
+  }
+  __syncthreads();
+  // stable placement: rank inside the cell = members with a smaller index
+  // (cells hold a handful of octave-0 keypoints)
+  for (int i = tid; i < n2; i += kInitThreads) {
+    const int c = S.cof[i];
+    if (c < 0) continue;
+    const int b = S.cell[c], e = S.cell[c + 1];
+    int p = b;
+    for (int q = b; q < e; ++q) p += members[q] < i ? 1 : 0;
+    const orbx_kp k = kp2[i];
+    S.pos[2 * p] = k.x;
+    S.pos[2 * p + 1] = k.y;
+    S.idx[p] = i;
+    if (d0_lds) {
+      const uint4* d = (const uint4*)(desc2 + (size_t)i * 32);
+      const uint4 u = d[0], v = d[1];
+      LDSP uint32_t* w = S.d0 + kD0Stride * p;
+      w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+      w[4] = v.x; w[5] = v.y; w[6] = v.z; w[7] = v.w;
+    }
+  }
+  // F1's octave-0 queries, compacted in index order
+  for (int i = tid; i <= n1; i += kInitThreads) S.coff[i] = 0;
+  __syncthreads();
+  init_stamp(P, 1);
+  if (P.stop == 1) return;
+  {
+    const int lane = tid & 63;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int i0 = (tid >> 6) * 64; i0 < n1; i0 += kInitThreads) {
+      const int i = i0 + lane;
+      const bool z = i < n1 && kp1[i].octave == 0;
+      const uint64_t mz = __ballot(z);
+      int base = 0;
+      if (lane == 0 && mz) base = lds_atomic_add(&S.var[5], __popcll(mz));
+      base = __builtin_amdgcn_readlane(base, 0);
+      if (z) S.qlist[base + __popcll(mz & lt)] = i;
+    }
+  }
+  __syncthreads();
+  const int nq0 = S.var[5];
+  // window centres of the queries (vbPrevMatched, or the keypoints) to LDS
+  LDSP float* qx = (LDSP float*)S.src;    // free until phase 3
+  LDSP float* qy = (LDSP float*)S.queue;  // free until phase 3
+  for (int g = tid; g < nq0; g += kInitThreads) {
+    const int i1 = S.qlist[g];
+    qx[g] = prev ? prev[2 * i1] : kp1[i1].x;
+    qy[g] = prev ? prev[2 * i1 + 1] : kp1[i1].y;
+  }
+  __syncthreads();
+  init_stamp(P, 2);
+  // ---- phase 1: candidate counts (Frame::GetFeaturesInArea(x, y, r, 0, 0));
+  // one 16-lane row per query, a lane per window column
+  for (int g = tid >> 4; g < nq0; g += kInitThreads / 16) {
+    const int l16 = tid & 15;
+    const int i1 = S.qlist[g];
+    const float x = qx[g], y = qy[g];
+    int cx0, cx1, cy0, cy1, cnt = 0;
+    const int ncol = init_window(x, y, P, cx0, cx1, cy0, cy1) ? cx1 - cx0 + 1 : 0;
+    for (int ci = l16; ci < ncol; ci += 16) {
+      const int ix = cx0 + ci;
+      const int pe = S.cell[ix * kInitGridRows + cy1 + 1];
+      for (int p = S.cell[ix * kInitGridRows + cy0]; p < pe; ++p) {
+        const float qx = S.pos[2 * p], qy = S.pos[2 * p + 1];
+        cnt += (fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r) ? 1 : 0;
+      }
+    }
+    cnt = row_sum(cnt);
+    if (l16 == 0) S.coff[i1] = cnt;
+  }
+  __syncthreads();
+  const int total = init_scan<kInitThreads>(S.coff, n1 + 1, S.tmp);
+  init_stamp(P, 3);
+  if (P.prof && tid == 0) P.prof[blockIdx.x * 16 + 13] = total;
+  if (P.stop == 2) return;
+  if (total > cand_lds && total > P.cand_cap) {
+    if (tid == 0) atomicOr(err, 8);
+    return;
+  }
+  if (total <= cand_lds) {
+    if (d0_lds)
+      init_solve<LDSP uint32_t*, true>(P, S, S.cand, kp1, desc1, desc2, prev, n1, n2, nq0, total);
+    else
+      init_solve<LDSP uint32_t*, false>(P, S, S.cand, kp1, desc1, desc2, prev, n1, n2, nq0, total);
+  } else {
+    uint32_t* c = cand_all + (size_t)pr * P.cand_cap;
+    if (d0_lds)
+      init_solve<uint32_t*, true>(P, S, c, kp1, desc1, desc2, prev, n1, n2, nq0, total);
+    else
+      init_solve<uint32_t*, false>(P, S, c, kp1, desc1, desc2, prev, n1, n2, nq0, total);
+  }
+  if (P.stop == 3) return;
+  LDSP int* m12 = S.qlist;  // vnMatches12
+  // rotation consistency (src/ORBmatcher.cc:473-512, ComputeThreeMaxima :1601-1642)
+  const float factor = 1.0f / kInitHisto;
+  if (P.check_ori) {
+    for (int i = tid; i < n1; i += kInitThreads) {
+      const int j = S.src[i];
+      int bin = -1;
+      if (j >= 0) {
+        float rot = __fsub_rn(kp1[i].angle, kp2[j].angle);
+        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+        bin = (int)roundf(__fmul_rn(rot, factor));
+        if (bin == kInitHisto) bin = 0;
+        lds_atomic_add(&S.hist[bin], 1);
+      }
+      S.src[i] = bin;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+      for (int i = 0; i < kInitHisto; i++) {
+        const int s = S.hist[i];
+        if (s > max1) {
+          max3 = max2; max2 = max1; max1 = s;
+          ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+          max3 = max2; max2 = s;
+          ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+          max3 = s;
+          ind3 = i;
+        }
+      }
+      if (max2 < __fmul_rn(0.1f, (float)max1)) {
+        ind2 = -1;
+        ind3 = -1;
+      } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
+        ind3 = -1;
+      }
+      S.var[1] = ind1;
+      S.var[2] = ind2;
+      S.var[3] = ind3;
+    }
+    __syncthreads();
+    const int ind1 = S.var[1], ind2 = S.var[2], ind3 = S.var[3];
+    int rej = 0;
+    for (int i = tid; i < n1; i += kInitThreads) {
+      const int b = S.src[i];
+      if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
+      if (m12[i] >= 0) {
+        m12[i] = -1;
+        ++rej;
+      }
+    }
+    rej = wave_sum_dpp(rej);
+    if ((tid & 63) == 0 && rej) lds_atomic_add(&S.var[0], -rej);
+    __syncthreads();
+  }
+  // outputs: vnMatches12 and the vbPrevMatched update (:515-517)
+  for (int i = tid; i < n1; i += kInitThreads) {
+    const int j = m12[i];
+    m12_out[i] = j;
+    if (prev && j >= 0) {
+      prev[2 * i] = kp2[j].x;
+      prev[2 * i + 1] = kp2[j].y;
+    }
+  }
+  if (tid == 0) nmatches[pr] = S.var[0];
+  init_stamp(P, 7);
+}
+
+int launch_search_init(const InitParams& P0, const orbx_kp* kp1, const uint8_t* desc1, const int* n1,
+                       const orbx_kp* kp2, const uint8_t* desc2, const int* n2, float* prev, uint32_t* cand,
+                       int* matches12, int* nmatches, int* err, int pairs, void* stream) {
+  InitParams P = P0;
+  const size_t fixed = init_lds_fixed_bytes(P.kp_pitch);
+  // sorted positions are 12-bit fields of the phase-2 entries
+  if (P.kp_pitch > 4096 || fixed + 4096 > kInitLdsBudget) return ORBX_ECAPACITY;
+  P.cand_lds = (int)((kInitLdsBudget - fixed) / 4) & ~15;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)search_init_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kInitLdsBudget) != hipSuccess)
+      return ORBX_EDEVICE;
+    attr = true;
+  }
+  const size_t lds = fixed + (size_t)P.cand_lds * 4;
+  hipLaunchKernelGGL(search_init_kernel, dim3(pairs), dim3(kInitThreads), lds, (hipStream_t)stream, P, kp1, desc1, n1,
+                     kp2, desc2, n2, prev, cand, matches12, nmatches, err);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+}  // namespace orbx

@@ -148,6 +148,23 @@ size_t stereo_lds_bytes(int nrows, int kp_pitch, int jobs_cap);
 int launch_stereo(const StereoParams& P, const orbx_kp* kpL, const uint8_t* descL, const int* nL,
                   const orbx_kp* kpR, const uint8_t* descR, const int* nR, int pairs, float* uRight,
                   float* depth, int* sad, int* nkept, void* stream);
+// orbx_init.hip — SearchForInitialization, one (F1, F2) pair per workgroup
+struct InitParams {
+  float minX, maxX, minY, maxY, invW, invH;  // F2 grid bounds
+  float r;                                   // windowSize
+  float nnratio;
+  int check_ori;
+  int kp_pitch;
+  int cand_lds;        // candidate entries that fit in LDS (set by the launcher)
+  long long cand_cap;  // global candidate entries per pair (fallback)
+  int stop;            // diagnostics: 0 = full kernel, k = return after phase k
+  long long* prof;     // diagnostics (ORBX_INIT_PROF): phase clocks per pair, or null
+};
+constexpr int kInitThreads = 1024;
+constexpr size_t kInitLdsBudget = 160 * 1024 - 512;
+int launch_search_init(const InitParams& P, const orbx_kp* kp1, const uint8_t* desc1, const int* n1,
+                       const orbx_kp* kp2, const uint8_t* desc2, const int* n2, float* prev, uint32_t* cand,
+                       int* matches12, int* nmatches, int* err, int pairs, void* stream);
 // orbx_project.hip — SearchByProjection(Frame&, vector<MapPoint*>, th), one frame per workgroup
 struct ProjParams {
   float minX, maxX, minY, maxY, invW, invH;  // Frame grid bounds, FRAME_GRID_COLS/ROWS over their extent

@@ -3,9 +3,7 @@
 //   hamming_top2_kernel   dense best/second search (the inner loop shared by
 //                         every ORBmatcher search), lane-per-query, candidate
 //                         rows broadcast from LDS, 8 x v_bcnt per pair
-//   search_init_kernel    SearchForInitialization   src/ORBmatcher.cc:405-520
-//                         + Frame::AssignFeaturesToGrid / GetFeaturesInArea
-//                         src/Frame.cc:229-244, 326-391
+//   (SearchForInitialization: orbx_init.hip)
 //   search_bow_kernel     SearchByBoW (KF-F :159-288, KF-KF :522-655)
 //
 // The reference resolves matches greedily in a fixed order (a later query can
@@ -203,700 +201,6 @@ __device__ __forceinline__ Top2 wave_top2(bool valid, int dist, int pos) {
   return r;
 }
 
-// ------------------------------------------------------------ SearchForInitialization
-struct InitParams {
-  float minX, maxX, minY, maxY, invW, invH;
-  float r;  // windowSize
-  float nnratio;
-  int check_ori;
-  int kp_pitch;
-  int sortn;        // pow2 >= kp_pitch (LDS sort capacity)
-  int cand_lds;     // candidate entries kept in LDS
-  long long cand_cap;  // global candidate entries per pair (fallback)
-  int stop;            // diagnostics: 0 = full kernel, k = return before pass k
-};
-
-constexpr int kInitThreads = 1024;
-constexpr int kInitMaxRounds = 48;
-
-// Frame::PosInGrid (src/Frame.cc:381-391): round() of a float (half away from zero)
-__device__ __forceinline__ bool pos_in_grid(float x, float y, const InitParams& P, int* gx, int* gy) {
-  const int px = (int)roundf(__fmul_rn(__fsub_rn(x, P.minX), P.invW));
-  const int py = (int)roundf(__fmul_rn(__fsub_rn(y, P.minY), P.invH));
-  *gx = px;
-  *gy = py;
-  return !(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows);
-}
-
-template <int NT>
-__device__ int block_scan_excl(int* a, int n, int* s_tmp) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int per = (n + NT - 1) / NT;
-  const int b = min(tid * per, n), e = min(b + per, n);
-  int sum = 0;
-  for (int i = b; i < e; ++i) sum += a[i];
-  int x = sum;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) s_tmp[w] = x;
-  __syncthreads();
-  int wpre = 0, total = 0;
-#pragma unroll
-  for (int i = 0; i < NT / 64; ++i) {
-    const int v = s_tmp[i];
-    if (i < w) wpre += v;
-    total += v;
-  }
-  int run = wpre + x - sum;
-  for (int i = b; i < e; ++i) {
-    const int v = a[i];
-    a[i] = run;
-    run += v;
-  }
-  __syncthreads();
-  return total;
-}
-
-// The candidate window of one query, flattened: per grid column ix in
-// [cx0, cx1] the sorted-grid range of cells [cy0, cy1] is contiguous, so a
-// candidate is (column, offset). Lanes 0..ncol-1 hold one column each.
-struct Window {
-  bool ok;
-  float x, y;
-  int cx0, ncol, total;
-  int col_start;  // per lane: first sorted position of its column
-  int col_pre;    // per lane: inclusive prefix of column lengths
-};
-
-template <typename CellPtr>
-__device__ __forceinline__ Window make_window(float x, float y, const InitParams& P, CellPtr s_cell) {
-  Window w;
-  w.ok = false;
-  w.x = x;
-  w.y = y;
-  w.total = 0;
-  const float r = P.r;
-  const int lane = threadIdx.x & 63;
-  const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, P.minX), r), P.invW)));
-  const int nMaxCellX = min(kGridCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, P.minX), r), P.invW)));
-  const int nMinCellY = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, P.minY), r), P.invH)));
-  const int nMaxCellY = min(kGridRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, P.minY), r), P.invH)));
-  if (nMinCellX >= kGridCols || nMaxCellX < 0 || nMinCellY >= kGridRows || nMaxCellY < 0) return w;
-  w.ok = true;
-  w.cx0 = nMinCellX;
-  w.ncol = max(0, nMaxCellX - nMinCellX + 1);
-  int len = 0;
-  w.col_start = 0;
-  if (lane < w.ncol) {
-    const int ix = nMinCellX + lane;
-    w.col_start = s_cell[ix * kGridRows + nMinCellY];
-    len = max(0, s_cell[ix * kGridRows + nMaxCellY + 1] - w.col_start);
-  }
-  const int x2 = wave_incl_scan_dpp(len);
-  w.col_pre = x2;
-  w.total = __builtin_amdgcn_readlane(x2, 63);
-  return w;
-}
-
-// sorted-grid position of flat candidate f (0 <= f < total): a scan over the
-// window's few columns with wave-uniform readlanes (no LDS round trips)
-__device__ __forceinline__ int window_pos(const Window& w, int f) {
-  int s = 0, prev = 0;
-  for (int c = 0; c < w.ncol; ++c) {
-    const int pre = __builtin_amdgcn_readlane(w.col_pre, c);
-    const int st = __builtin_amdgcn_readlane(w.col_start, c);
-    if (f >= prev && f < pre) s = st + (f - prev);
-    prev = pre;
-  }
-  return s;
-}
-
-// Passes 2 and 3 of search_init_kernel, instantiated once with the candidate
-// list in LDS and once in global memory, so that each copy addresses a single
-// known memory space (a run-time choice between the two would make the
-// compiler emit flat_* accesses, which wait on both memory counters).
-#define LDS __attribute__((address_space(3)))
-
-// workgroup-scope LDS atomics (the atomicAdd family takes generic pointers)
-__device__ __forceinline__ int lds_add(LDS int* p, int v) {
-  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ int lds_exch(LDS int* p, int v) {
-  return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ int lds_max(LDS int* p, int v) {
-  return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ int lds_add_g(int* p, int v) { return lds_add((LDS int*)p, v); }
-__device__ __forceinline__ uint64_t lanemask_lt_w(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
-
-struct InitCtx {
-  InitParams P;
-  const orbx_kp* kp1;
-  const orbx_kp* kp2;
-  const uint8_t* desc1;
-  const uint8_t* desc2;
-  const float* prev;
-  uint32_t* s_sort;
-  float2* s_xy;
-  float2* s_pos;
-  uint4* s_d0;
-  int2* s_queue;
-  int* s_m12;
-  int* s_cell;
-  int* s_md;
-  int* s_m21;
-  int* s_src;
-  int* s_coff;
-  int* s_var;
-  int n1, n2, total;
-  int qb, qe;  // this wave's range of the octave-0 query list
-  int* err;
-};
-
-template <typename CandPtr, bool DESC_LDS>
-__device__ __forceinline__ void init_pass23(const InitCtx& C, CandPtr cand) {
-  const InitParams& P = C.P;
-  const orbx_kp* kp1 = C.kp1;
-  const orbx_kp* kp2 = C.kp2;
-  const uint8_t* desc1 = C.desc1;
-  const uint8_t* desc2 = C.desc2;
-  const float* prev = C.prev;
-  const LDS uint32_t* s_sort = (const LDS uint32_t*)C.s_sort;
-  const LDS float* s_pos = (const LDS float*)C.s_pos;  // (x, y) by sorted position (passes 1-2)
-  const LDS uint32_t* s_d0 = (const LDS uint32_t*)C.s_d0;  // descriptors by sorted position (DESC_LDS)
-  LDS int* s_queue = (LDS int*)C.s_queue;             // {i1, first candidate} pairs
-  LDS int* s_m12 = (LDS int*)C.s_m12;
-  const LDS int* s_cell = (const LDS int*)C.s_cell;
-  LDS int* s_md = (LDS int*)C.s_md;
-  LDS int* s_m21 = (LDS int*)C.s_m21;
-  LDS int* s_src = (LDS int*)C.s_src;
-  const LDS int* s_coff = (const LDS int*)C.s_coff;
-  LDS int* s_var = (LDS int*)C.s_var;
-  const int n1 = C.n1, total = C.total;
-  int* err = C.err;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  (void)kp2;
-  (void)err;
-  if (P.stop == 2) return;
-  // ---- pass 2: fill candidates (reference order) with their Hamming distances
-  const LDS int* s_qlist = (const LDS int*)C.s_src;  // octave-0 queries (pass 1)
-  for (int q0 = C.qb; q0 < C.qe; q0 += 64) {
-    const int e = q0 + lane;
-    const int qi = e < C.qe ? s_qlist[e] : 0;
-    float cxl = 0.f, cyl = 0.f;
-    bool has = false;
-    uint4 dl0 = make_uint4(0, 0, 0, 0), dl1 = dl0;
-    if (e < C.qe) {
-      has = s_coff[qi + 1] > s_coff[qi];
-      if (has) {
-        const orbx_kp k = kp1[qi];
-        cxl = prev ? prev[2 * qi] : k.x;
-        cyl = prev ? prev[2 * qi + 1] : k.y;
-        const uint4* d1 = (const uint4*)(desc1 + (long long)qi * 32);
-        dl0 = d1[0];
-        dl1 = d1[1];
-      }
-    }
-    uint64_t todo = __ballot(has);
-    while (todo) {
-      const int j = __ffsll((long long)todo) - 1;
-      todo &= todo - 1;
-      const float x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxl), j));
-      const float y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cyl), j));
-      const uint4 a0 = make_uint4(__builtin_amdgcn_readlane(dl0.x, j), __builtin_amdgcn_readlane(dl0.y, j),
-                                  __builtin_amdgcn_readlane(dl0.z, j), __builtin_amdgcn_readlane(dl0.w, j));
-      const uint4 a1 = make_uint4(__builtin_amdgcn_readlane(dl1.x, j), __builtin_amdgcn_readlane(dl1.y, j),
-                                  __builtin_amdgcn_readlane(dl1.z, j), __builtin_amdgcn_readlane(dl1.w, j));
-      const Window w = make_window(x, y, P, s_cell);
-      int base = s_coff[__builtin_amdgcn_readlane(qi, j)];
-      const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-      for (int f0 = 0; f0 < w.total; f0 += 64) {
-        const int f = f0 + lane;
-        const int s = window_pos(w, f);
-        bool ok = false;
-        if (f < w.total)
-          ok = fabsf(__fsub_rn(s_pos[2 * s], x)) < P.r && fabsf(__fsub_rn(s_pos[2 * s + 1], y)) < P.r;
-        const uint64_t m = __ballot(ok);
-        if (ok) {
-          const int i2 = (int)(s_sort[s] & 0xFFFF);
-          uint4 b0, b1;
-          if (DESC_LDS) {
-            const LDS uint32_t* w = s_d0 + 8 * s;
-            b0 = make_uint4(w[0], w[1], w[2], w[3]);
-            b1 = make_uint4(w[4], w[5], w[6], w[7]);
-          } else {
-            const uint4* d2 = (const uint4*)(desc2 + (long long)i2 * 32);
-            b0 = d2[0];
-            b1 = d2[1];
-          }
-          const int d = hamming256(a0, a1, b0, b1);
-          cand[base + __popcll(m & lt)] = (uint32_t)i2 | ((uint32_t)d << 23);
-        }
-        base += __popcll(m);
-      }
-    }
-  }
-  __syncthreads();
-  if (P.stop == 3) return;
-  // ---- pass 3: greedy resolution (src/ORBmatcher.cc:436-470)
-  // The reference resolves the queries one after another in i1 order: query
-  // i1 skips every candidate i2 whose vMatchedDistance[i2] (the distance of
-  // the latest earlier query that accepted i2) is <= its own distance. Each
-  // query's outcome is therefore a function of the outcomes of the queries
-  // before it -- a triangular system. It is solved here by Jacobi rounds:
-  // every query recomputes its top-2 from a snapshot of all accepted
-  // outcomes, keeping only claims by earlier queries; a round that changes no
-  // outcome is a fixed point, and the triangular system has exactly one --
-  // the sequential result. Rounds needed = length of the longest chain of
-  // outcome dependencies (a handful in practice); past kInitMaxRounds the
-  // sequential wavefront below finishes the job instead.
-  LDS int* res = s_m12;                  // per i1: -1, or bestIdx2 << 9 | bestDist
-  LDS int* head = (LDS int*)C.s_xy;      // per i2: latest claiming i1 of the snapshot, or -1
-  LDS int* nxt = head + P.kp_pitch;      // per i1: (next claimer + 1) << 9 | its distance
-  LDS int* queue = s_md;                 // queries that have candidates (unordered)
-  const int n2 = C.n2;
-  for (int i = tid; i < n1; i += kInitThreads) res[i] = -1;
-  for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
-  if (tid == 0) {
-    s_var[0] = 0;
-    s_var[6] = 1;
-    s_var[7] = 0;
-  }
-  __syncthreads();
-  for (int i = tid; i < n1; i += kInitThreads)
-    if (s_coff[i + 1] > s_coff[i]) queue[lds_add(&s_var[7], 1)] = i;
-  __syncthreads();
-  const int nq = s_var[7];
-  int rounds = 0;
-  bool converged = false;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  (void)lt;
-  while (rounds < kInitMaxRounds) {
-    // s_var[6] = "an outcome changed" of the previous round; read, then reset
-    if (s_var[6] == 0) {
-      converged = true;
-      break;
-    }
-    __syncthreads();
-    if (tid == 0) s_var[6] = 0;
-    ++rounds;
-    for (int qq = wv; qq < nq; qq += kInitThreads / 64) {
-      const int i1 = queue[qq];
-      const int c0 = s_coff[i1], c1 = s_coff[i1 + 1];
-      Top2 acc{INT_MAX, -1, INT_MAX};
-      for (int cb = c0; cb < c1; cb += 64) {
-        const int c = cb + lane;
-        bool valid = false;
-        int dist = 0, i2 = -1;
-        if (c < c1) {
-          const uint32_t e = cand[c];
-          i2 = (int)(e & 0x7FFFFF);
-          dist = (int)(e >> 23);
-          int md = INT_MAX;
-          for (int h = head[i2]; h >= 0;) {
-            const int x = nxt[h];
-            if (h < i1) md = min(md, x & 511);
-            h = (x >> 9) - 1;
-          }
-          valid = !(md <= dist);  // vMatchedDistance[i2] <= dist -> skip (:444-445)
-        }
-        const Top2 t = wave_top2(valid, dist, i2);
-        const int npos = (acc.best <= t.best) ? acc.pos : t.pos;
-        acc.second = min(min(max(acc.best, t.best), acc.second), t.second);
-        acc.best = min(acc.best, t.best);
-        acc.pos = npos;
-      }
-      const bool ok = acc.best <= kThLow && (float)acc.best < __fmul_rn((float)acc.second, P.nnratio);
-      const int r = ok ? (acc.pos << 9 | acc.best) : -1;
-      if (lane == 0 && res[i1] != r) {
-        res[i1] = r;
-        s_var[6] = 1;
-      }
-    }
-    __syncthreads();
-    // snapshot of this round's outcomes as per-i2 claim lists
-    for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
-    __syncthreads();
-    for (int qq = tid; qq < nq; qq += kInitThreads) {
-      const int i1 = queue[qq];
-      const int r = res[i1];
-      if (r >= 0) nxt[i1] = ((lds_exch(&head[r >> 9], i1) + 1) << 9) | (r & 511);
-    }
-    __syncthreads();
-  }
-  if (converged) {
-    // the latest accepting query keeps each i2 (earlier ones were stolen
-    // from, :463-467); every accepted query entered rotHist (:469-470)
-    for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
-    __syncthreads();
-    for (int qq = tid; qq < nq; qq += kInitThreads) {
-      const int i1 = queue[qq];
-      const int r = res[i1];
-      if (r >= 0) lds_max(&head[r >> 9], i1);
-    }
-    __syncthreads();
-    int kept = 0;
-    for (int i = tid; i < n1; i += kInitThreads) {
-      const int r = res[i];
-      const int best = r >= 0 ? (r >> 9) : -1;
-      const bool keep = r >= 0 && head[best] == i;
-      s_src[i] = best;
-      res[i] = keep ? best : -1;  // res aliases vnMatches12
-      kept += keep ? 1 : 0;
-    }
-    kept = wave_sum_dpp(kept);
-    if (lane == 0 && kept) lds_add(&s_var[0], kept);
-  } else {
-    // sequential fallback state: vMatchedDistance, vnMatches21, rotHist entries (queue is dead)
-    for (int i = tid; i < n2; i += kInitThreads) {
-      s_md[i] = INT_MAX;
-      s_m21[i] = -1;
-    }
-    for (int i = tid; i < n1; i += kInitThreads) s_src[i] = -1;
-  }
-  if (P.stop == 9 && tid == 0) {  // diagnostics: rounds, queue length, candidates
-    atomicMax(err + 1, rounds + (converged ? 0 : 1000));
-    atomicMax(err + 2, nq);
-    atomicMax(err + 3, total * 2 + (total <= P.cand_lds ? 1 : 0));
-  }
-  __syncthreads();
-  // sequential greedy in i1 order (one wavefront, LDS state only)
-  if (!converged && wv == 0) {
-    volatile LDS int* md = s_md;
-    volatile LDS int* m21 = s_m21;
-    volatile LDS int* m12 = s_m12;
-    // ordered queue of the queries that have candidates: {i1, first candidate};
-    // candidates of entry q end where entry q+1's begin (empty queries between
-    // them own no candidates)
-    int nq = 0;  // shadows the unordered queue count
-    for (int q0 = 0; q0 < n1; q0 += 64) {
-      const int qi = q0 + lane;
-      const bool act = qi < n1 && s_coff[qi + 1] > s_coff[qi];
-      const uint64_t m = __ballot(act);
-      if (qi < n1) m12[qi] = -1;
-      if (act) {
-        const int q = nq + __popcll(m & lt);
-        s_queue[2 * q] = qi;
-        s_queue[2 * q + 1] = s_coff[qi];
-      }
-      nq += __popcll(m);
-    }
-    if (lane == 0) {
-      s_queue[2 * nq] = n1;
-      s_queue[2 * nq + 1] = total;
-    }
-    __builtin_amdgcn_wave_barrier();
-    int nm = 0;
-    // two-deep prefetch of the greedy-independent data: queue entries q+1, q+2
-    // and the first candidate chunk of query q+1
-    auto qload = [&](int q) { return make_int2(s_queue[2 * q], s_queue[2 * q + 1]); };
-    int2 qa = nq > 0 ? qload(0) : make_int2(0, 0);
-    int2 qb = nq > 0 ? qload(1) : make_int2(0, 0);
-    uint32_t ea = (nq > 0 && qa.y + lane < qb.y) ? cand[qa.y + lane] : 0u;
-    for (int qi = 0; qi < nq; ++qi) {
-      const int i1 = qa.x, c0 = qa.y, c1 = qb.y;
-      const uint32_t e0 = ea;
-      int2 qc = make_int2(0, total);
-      if (qi + 2 <= nq) qc = qload(qi + 2);
-      ea = (qi + 1 < nq && qb.y + lane < qc.y) ? cand[qb.y + lane] : 0u;
-      qa = qb;
-      qb = qc;
-      Top2 acc{INT_MAX, -1, INT_MAX};
-      int owner = -1;  // vnMatches21 of this lane's candidate, read with its distance
-      for (int cb = c0; cb < c1; cb += 64) {
-        const int c = cb + lane;
-        bool valid = false;
-        int dist = 0, i2 = -1, o = -1;
-        if (c < c1) {
-          const uint32_t e = (cb == c0) ? e0 : cand[c];
-          i2 = (int)(e & 0x7FFFFF);
-          dist = (int)(e >> 23);
-          valid = !(md[i2] <= dist);  // vMatchedDistance[i2] <= dist -> skip (:444-445)
-          o = m21[i2];
-        }
-        const Top2 t = wave_top2(valid, dist, i2);
-        const int nb = min(acc.best, t.best);
-        const int npos = (acc.best <= t.best) ? acc.pos : t.pos;
-        const int nsec = min(min(max(acc.best, t.best), acc.second), t.second);
-        if (t.best < acc.best) {
-          const uint64_t eq = __ballot(valid && dist == t.best);
-          owner = __builtin_amdgcn_readlane(o, __ffsll((long long)eq) - 1);
-        }
-        acc.best = nb;
-        acc.pos = npos;
-        acc.second = nsec;
-      }
-      const int bestDist = acc.best, bestDist2 = acc.second, bestIdx2 = acc.pos;
-      if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)bestDist2, P.nnratio)) {
-        if (lane == 0) {
-          if (owner >= 0) {  // steal: the earlier query loses its match (:463-467)
-            m12[owner] = -1;
-            nm--;
-          }
-          m12[i1] = bestIdx2;
-          m21[bestIdx2] = i1;
-          md[bestIdx2] = bestDist;
-          nm++;
-          s_src[i1] = bestIdx2;  // rotHist[bin].push_back(i1), bin from this pair
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    if (lane == 0) s_var[0] = nm;
-  }
-}
-
-__global__ __launch_bounds__(kInitThreads) void search_init_kernel(
-    InitParams P, const orbx_kp* __restrict__ kp1_all, const uint8_t* __restrict__ desc1_all,
-    const int* __restrict__ n1_all, const orbx_kp* __restrict__ kp2_all, const uint8_t* __restrict__ desc2_all,
-    const int* __restrict__ n2_all, float* __restrict__ prev_all, uint32_t* __restrict__ cand_all,
-    int* __restrict__ matches_all, int* __restrict__ nmatches, int* err) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int n1 = n1_all[pr], n2 = n2_all[pr];
-  const orbx_kp* kp1 = kp1_all + (long long)pr * P.kp_pitch;
-  const orbx_kp* kp2 = kp2_all + (long long)pr * P.kp_pitch;
-  const uint8_t* desc1 = desc1_all + (long long)pr * P.kp_pitch * 32;
-  const uint8_t* desc2 = desc2_all + (long long)pr * P.kp_pitch * 32;
-  // prev_all == nullptr: windows centred on F1's own keypoints, the initial
-  // mvbPrevMatched of Tracking::MonocularInitialization (src/Tracking.cc:645-647)
-  float* prev = prev_all ? prev_all + (long long)pr * P.kp_pitch * 2 : nullptr;
-  int* m12_out = matches_all + (long long)pr * P.kp_pitch;
-
-  unsigned char* sp = smem;
-  auto take = [&](size_t bytes) { unsigned char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
-  uint32_t* s_sort = (uint32_t*)take(4ull * P.sortn);   // (cell << 16 | index), sorted
-  float2* s_xy = (float2*)take(8ull * (P.kp_pitch + 1));  // F2 positions (passes 1-2)
-  int2* s_queue = (int2*)s_xy;                          // pass 3: {query, first candidate}
-  int* s_m12 = (int*)s_sort;                            // pass 3: vnMatches12 (sort keys are dead)
-  int* s_cell = (int*)take(4ull * (kGridCols * kGridRows + 1));
-  int* s_md = (int*)take(4ull * P.kp_pitch);            // vMatchedDistance
-  int* s_m21 = (int*)take(4ull * P.kp_pitch);           // vnMatches21
-  int* s_src = (int*)take(4ull * P.kp_pitch);           // i2 an i1 matched when it entered rotHist, or -1
-  int* s_coff = (int*)take(4ull * (P.kp_pitch + 1));    // candidate offsets per i1
-  int* s_tmp = (int*)take(64);
-  int* s_var = (int*)take(64);
-  int* s_hist = (int*)take(4 * 32);
-  uint32_t* s_cand = (uint32_t*)take(4ull * P.cand_lds);
-
-  // ---- octave-0 keypoints of F2 with a valid grid cell (the only ones
-  // GetFeaturesInArea(.., 0, 0) can return); slot order is irrelevant because
-  // the keys (cell << 16 | index) are sorted next.
-  if (tid == 0) s_var[5] = 0;
-  if (tid < 32) s_hist[tid] = 0;
-  __syncthreads();
-  for (int i = tid; i < n2; i += kInitThreads) {
-    const orbx_kp k = kp2[i];
-    int gx, gy;
-    if (k.octave == 0 && pos_in_grid(k.x, k.y, P, &gx, &gy)) {
-      s_xy[i] = make_float2(k.x, k.y);
-      s_sort[atomicAdd(&s_var[5], 1)] = ((uint32_t)(gx * kGridRows + gy) << 16) | (uint32_t)i;
-    }
-  }
-  __syncthreads();
-  const int n0 = s_var[5];
-  int sortn = 1;
-  while (sortn < n0) sortn <<= 1;
-  for (int i = n0 + tid; i < sortn; i += kInitThreads) s_sort[i] = 0xFFFFFFFFu;
-  __syncthreads();
-  for (int kk = 2; kk <= sortn; kk <<= 1) {  // bitonic sort: grid cell-major, then index
-    for (int j = kk >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < sortn; i += kInitThreads) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint32_t a = s_sort[i], b = s_sort[ixj];
-          const bool up = (i & kk) == 0;
-          if (up ? (a > b) : (a < b)) {
-            s_sort[i] = b;
-            s_sort[ixj] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int c = tid; c <= kGridCols * kGridRows; c += kInitThreads) {  // first sorted position of each cell
-    int lo = 0, hi = n0;
-    const uint32_t key = (uint32_t)c << 16;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (s_sort[mid] < key) lo = mid + 1;
-      else hi = mid;
-    }
-    s_cell[c] = lo;
-  }
-  __syncthreads();
-  if (P.stop == 1) return;
-
-  // F2's level-0 positions, and its descriptors when they fit beside the
-  // candidate list, copied in sorted-grid order: a window's candidates are
-  // then contiguous LDS entries
-  float2* s_pos = (float2*)s_md;  // s_md / s_m21 (adjacent) are free until pass 3
-  const bool d0_lds = 8 * n0 <= P.cand_lds / 2;
-  uint4* s_d0 = (uint4*)s_cand;
-  for (int s = tid; s < n0; s += kInitThreads) {
-    const int i2 = (int)(s_sort[s] & 0xFFFF);
-    s_pos[s] = s_xy[i2];
-    if (d0_lds) {
-      const uint4* d = (const uint4*)(desc2 + (long long)i2 * 32);
-      s_d0[2 * s] = d[0];
-      s_d0[2 * s + 1] = d[1];
-    }
-  }
-  const int cand_off = d0_lds ? 8 * n0 : 0;  // uint32 entries of s_cand taken by s_d0
-  const int cand_lds = P.cand_lds - cand_off;
-  // the octave-0 queries, compacted so that every wave gets an equal share
-  // (keypoints are level-major: they are all at the front); order is
-  // irrelevant, results are indexed by query
-  int* s_qlist = s_src;  // s_src is written in pass 3
-  if (tid == 0) s_var[6] = 0;
-  for (int i = tid; i <= n1; i += kInitThreads) s_coff[i] = 0;
-  __syncthreads();
-  {
-    const uint64_t lt = lanemask_lt_w(lane);
-    for (int i0 = wv * 64; i0 < n1; i0 += kInitThreads) {
-      const int i = i0 + lane;
-      const bool z = i < n1 && kp1[i].octave == 0;
-      const uint64_t mz = __ballot(z);
-      int base = 0;
-      if (lane == 0 && mz) base = lds_add_g(s_var + 6, __popcll(mz));
-      base = __builtin_amdgcn_readlane(base, 0);
-      if (z) s_qlist[base + __popcll(mz & lt)] = i;
-    }
-  }
-  __syncthreads();
-  const int nq0 = s_var[6];
-  const int qper = (nq0 + kInitThreads / 64 - 1) / (kInitThreads / 64);
-  const int qb = min(wv * qper, nq0), qe = min(qb + qper, nq0);
-
-  // Passes 1 and 2 walk the queries 64 at a time per wave: lane j prefetches
-  // query q0+j's octave, window centre and descriptor words with coalesced
-  // loads, and readlane broadcasts them when query q0+j is processed.
-  // ---- pass 1: candidate counts per query (Frame::GetFeaturesInArea, octave 0)
-  for (int q0 = qb; q0 < qe; q0 += 64) {
-    const int e = q0 + lane;
-    float cxl = 0.f, cyl = 0.f;
-    int qi = 0;
-    if (e < qe) {
-      qi = s_qlist[e];
-      const orbx_kp k = kp1[qi];
-      cxl = prev ? prev[2 * qi] : k.x;
-      cyl = prev ? prev[2 * qi + 1] : k.y;
-    }
-    uint64_t todo = __ballot(e < qe);
-    while (todo) {
-      const int j = __ffsll((long long)todo) - 1;
-      todo &= todo - 1;
-      const int qj = __builtin_amdgcn_readlane(qi, j);
-      const float x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxl), j));
-      const float y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cyl), j));
-      const Window w = make_window(x, y, P, s_cell);
-      int cnt = 0;
-      if (w.ok) {
-        for (int f0 = 0; f0 < w.total; f0 += 64) {
-          const int f = f0 + lane;
-          const int s = window_pos(w, f);
-          if (f < w.total) {
-            const float2 q = s_pos[s];
-            cnt += (fabsf(__fsub_rn(q.x, x)) < P.r && fabsf(__fsub_rn(q.y, y)) < P.r) ? 1 : 0;
-          }
-        }
-      }
-      cnt = wave_sum_i(cnt);
-      if (lane == 0) s_coff[qj] = cnt;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) s_coff[n1] = 0;
-  __syncthreads();
-  const int total = block_scan_excl<kInitThreads>(s_coff, n1 + 1, s_tmp);
-  if (total > cand_lds && total > P.cand_cap) {
-    if (tid == 0) atomicOr(err, 8);
-    return;
-  }
-  InitCtx ctx{P, kp1, kp2, desc1, desc2, prev, s_sort, s_xy, s_pos, s_d0, s_queue, s_m12, s_cell, s_md, s_m21, s_src,
-              s_coff, s_var, n1, n2, total, qb, qe, err};
-  if (total <= cand_lds) {
-    LDS uint32_t* c = (LDS uint32_t*)s_cand + cand_off;
-    if (d0_lds) init_pass23<LDS uint32_t*, true>(ctx, c);
-    else init_pass23<LDS uint32_t*, false>(ctx, c);
-  } else {
-    uint32_t* c = cand_all + (long long)pr * P.cand_cap;
-    if (d0_lds) init_pass23<uint32_t*, true>(ctx, c);
-    else init_pass23<uint32_t*, false>(ctx, c);
-  }
-  if (P.stop == 2 || P.stop == 3) return;  // diagnostics: the passes were cut short
-  __syncthreads();
-  // rotation consistency (src/ORBmatcher.cc:473-512, ComputeThreeMaxima :1601-1642)
-  const float factor = 1.0f / kHistoLength;
-  if (P.check_ori) {
-    for (int i = tid; i < n1; i += kInitThreads) {
-      const int j = s_src[i];
-      int bin = -1;
-      if (j >= 0) {
-        float rot = __fsub_rn(kp1[i].angle, kp2[j].angle);
-        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-        bin = (int)roundf(__fmul_rn(rot, factor));
-        if (bin == kHistoLength) bin = 0;
-        atomicAdd(&s_hist[bin], 1);
-      }
-      s_src[i] = bin;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-      for (int i = 0; i < kHistoLength; i++) {
-        const int s = s_hist[i];
-        if (s > max1) {
-          max3 = max2; max2 = max1; max1 = s;
-          ind3 = ind2; ind2 = ind1; ind1 = i;
-        } else if (s > max2) {
-          max3 = max2; max2 = s;
-          ind3 = ind2; ind2 = i;
-        } else if (s > max3) {
-          max3 = s;
-          ind3 = i;
-        }
-      }
-      if (max2 < __fmul_rn(0.1f, (float)max1)) {
-        ind2 = -1;
-        ind3 = -1;
-      } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
-        ind3 = -1;
-      }
-      s_var[1] = ind1;
-      s_var[2] = ind2;
-      s_var[3] = ind3;
-    }
-    __syncthreads();
-    const int ind1 = s_var[1], ind2 = s_var[2], ind3 = s_var[3];
-    for (int i = tid; i < n1; i += kInitThreads) {
-      const int b = s_src[i];
-      if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
-      if (s_m12[i] >= 0) {
-        s_m12[i] = -1;
-        atomicSub(&s_var[0], 1);
-      }
-    }
-    __syncthreads();
-  }
-  // outputs: vnMatches12 and the vbPrevMatched update (:515-517)
-  for (int i = tid; i < n1; i += kInitThreads) {
-    const int j = s_m12[i];
-    m12_out[i] = j;
-    if (prev && j >= 0) {
-      prev[2 * i] = kp2[j].x;
-      prev[2 * i + 1] = kp2[j].y;
-    }
-  }
-  if (tid == 0) nmatches[pr] = s_var[0];
-}
-
 // ------------------------------------------------------------ SearchByBoW
 // One block; shared vocabulary nodes are independent (DBoW2 puts every
 // feature in exactly one node), so each wave takes whole nodes and runs the
@@ -1041,13 +345,6 @@ int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_c
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
-constexpr size_t kInitLdsBudget = 160 * 1024 - 512;
-static size_t init_lds_bytes(const InitParams& P) {
-  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-  return r16(4ull * P.sortn) + r16(8ull * (P.kp_pitch + 1)) + r16(4ull * (kGridCols * kGridRows + 1)) +
-         3 * r16(4ull * P.kp_pitch) + r16(4ull * (P.kp_pitch + 1)) + 2 * r16(64) + r16(128) +
-         r16(4ull * P.cand_lds);
-}
 
 }  // namespace orbx
 
@@ -1121,8 +418,6 @@ int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out) {
     return mfail(ORBX_ENOMEM, "matcher workspace allocation failed");
   }
   (void)hipMemset(m->err, 0, 16);
-  (void)hipFuncSetAttribute((const void*)search_init_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kInitLdsBudget);
   *out = m;
   return ORBX_OK;
 }
@@ -1166,41 +461,52 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
   if (!m || pairs < 1 || pairs > m->max_pairs || kp_pitch < 1 || kp_pitch > m->max_kps)
     return mfail(ORBX_EINVAL, "pairs/kp_pitch exceed the matcher workspace");
   MHIP(hipSetDevice(m->device));
-  InitParams P;
+  InitParams P{};
   P.minX = b.min_x;
   P.maxX = b.max_x;
   P.minY = b.min_y;
   P.maxY = b.max_y;
+  // mfGridElementWidthInv / HeightInv (src/Frame.cc:154-155)
   P.invW = static_cast<float>(kGridCols) / static_cast<float>(b.max_x - b.min_x);
   P.invH = static_cast<float>(kGridRows) / static_cast<float>(b.max_y - b.min_y);
   P.r = (float)window;
   P.nnratio = nnratio;
   P.check_ori = check_ori;
   P.kp_pitch = kp_pitch;
-  P.sortn = 1;
-  while (P.sortn < kp_pitch) P.sortn <<= 1;
   P.cand_cap = m->cand_cap;
   {
     const char* st = getenv("ORBX_INIT_STOP");  // diagnostics only
     P.stop = st ? atoi(st) : 0;
   }
-  P.cand_lds = 0;
-  if (init_lds_bytes(P) > kInitLdsBudget)
-    return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization's LDS grid (max ~5000)",
-                 kp_pitch);
-  P.cand_lds = (int)((kInitLdsBudget - init_lds_bytes(P)) / 4) & ~15;
-  hipLaunchKernelGGL(search_init_kernel, dim3(pairs), dim3(kInitThreads), init_lds_bytes(P),
-                     (hipStream_t)stream, P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2,
-                     d_prev_xy, m->cand, d_matches12, d_nmatches, m->err);
-  MHIP(hipGetLastError());
-  if (P.stop == 9) {  // diagnostics only
-    int e[4] = {0, 0, 0, 0};
-    MHIP(hipStreamSynchronize((hipStream_t)stream));
-    MHIP(hipMemcpy(e, m->err, 16, hipMemcpyDeviceToHost));
-    fprintf(stderr, "search_init pass3: max cycles %d, max queue %d, max candidates %d (lds %d, cand_lds %d)\n", e[1],
-            e[2], e[3] / 2, e[3] & 1, P.cand_lds);
-    MHIP(hipMemset(m->err, 0, 16));
+  static long long* prof = nullptr;  // ORBX_INIT_PROF: phase clocks of every pair, averaged after the call
+  const bool do_prof = getenv("ORBX_INIT_PROF") != nullptr;
+  if (do_prof) {
+    if (!prof) MHIP(hipMalloc(&prof, (size_t)4096 * 16 * 8));
+    MHIP(hipMemset(prof, 0, (size_t)pairs * 16 * 8));
+    P.prof = prof;
   }
+  const int rc = launch_search_init(P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, d_prev_xy, m->cand, d_matches12,
+                                    d_nmatches, m->err, pairs, stream);
+  if (do_prof && !rc) {
+    std::vector<long long> h((size_t)pairs * 16);
+    MHIP(hipStreamSynchronize((hipStream_t)stream));
+    MHIP(hipMemcpy(h.data(), prof, h.size() * 8, hipMemcpyDeviceToHost));
+    double ph[8] = {0}, rounds = 0, conv = 0, tot = 0;
+    for (int q = 0; q < pairs; ++q) {
+      for (int k = 1; k < 8; ++k)
+        if (h[q * 16 + k]) ph[k] += (double)(h[q * 16 + k] - h[q * 16]);
+      rounds += h[q * 16 + 11];
+      conv += h[q * 16 + 12];
+      tot += h[q * 16 + 13];
+    }
+    fprintf(stderr, "search_init phases (avg clocks from start): sort %.0f qlist %.0f count %.0f walk %.0f dist %.0f "
+            "rounds %.0f end %.0f | rounds %.1f converged %.2f candidates %.0f\n", ph[1] / pairs, ph[2] / pairs,
+            ph[3] / pairs, ph[4] / pairs, ph[5] / pairs, ph[6] / pairs, ph[7] / pairs, rounds / pairs, conv / pairs,
+            tot / pairs);
+  }
+  if (rc == ORBX_ECAPACITY)
+    return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization's LDS grid", kp_pitch);
+  if (rc) return mfail(ORBX_EDEVICE, "search_init launch: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
 }
 
