@@ -41,6 +41,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "frames/s ORB extract+match, 1241×376 mono nFeatures=2000; achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+# VALU lane-op peak: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (the 157.3 TFLOPS FP32-vector spec / 2);
+# the v_xor_b32 + v_bcnt_u32_b32 mix issues at about half of it (tools/valu_microbench.hip: 0.58 T
+# wave-instructions/s = 37 T lane-ops/s)
+VALU_PEAK_TOPS = 78.6
+VALU_MIX_TOPS = 37.1
 STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_top2", "search_init"]
 KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
@@ -295,6 +300,19 @@ def main():
             "algorithmic_bytes_per_launch": int(hbm_stages[rk] * BS),
             "avg_launch_ms": round(st[rk], 4)}
 
+    # the dense matcher is bound by VALU issue, not HBM (SURVEY.md §8(d) "Roofline (match)"):
+    # algorithmic work = 16 lane-ops per (query, candidate) pair (8 x 32-bit XOR + 8 popcounts)
+    match_roof = None
+    if not args.no_match and st["hamming_top2"] > 0:
+        cnt = d_counts[(total_steps - 1) % NS].download(B + 1, np.int32).astype(np.int64)
+        pairs = int((cnt[1:] * cnt[:-1]).sum())
+        ops = 16.0 * pairs / (st["hamming_top2"] * 1e-3) / 1e12
+        match_roof = {"kernel": KERNELS["hamming_top2"], "bound": "valu", "unit": "Tops/s",
+                      "achieved": round(ops, 2), "peak": VALU_PEAK_TOPS, "frac": round(ops / VALU_PEAK_TOPS, 4),
+                      "peak_xor_bcnt_mix": VALU_MIX_TOPS, "frac_of_mix": round(ops / VALU_MIX_TOPS, 4),
+                      "pairs_per_launch": pairs, "pairs_per_s": round(pairs / (st["hamming_top2"] * 1e-3), 1),
+                      "avg_launch_ms": round(st["hamming_top2"], 4)}
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         sample = frames if args.cpu_sample <= len(frames) else seq_cpu(rank, W, H, args.cpu_sample)
@@ -312,6 +330,7 @@ def main():
                        "frames_per_step_per_gpu": B, "parallelism": f"frame-sharded x{world}, no collectives",
                        "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS},
             "roofline": roof,
+            "match_roofline": match_roof,
             "cpu_baseline": cpu,
             "pyr_fast_pass_hbm_gbs": round(pf_gbs, 1),
             "dominant_kernel": KERNELS[dominant],
