@@ -92,6 +92,7 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   int* ord = (int*)take(4ull * MN);    // processing rank -> node
   int* coff = (int*)take(4ull * (P.max_cells_level + 1));
   int* s_soff = (int*)take(4ull * (P.max_cells_level + 1));  // cell slot offsets
+  int2* s_mid = (int2*)take(8ull * MN);  // halves() of every node of this round
   int* s_tmp = (int*)take(64);
   int* s_var = (int*)take(64);
   uint32_t* lkeys = (uint32_t*)take(4ull * P.kcap_lds);
@@ -115,14 +116,47 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     for (int c = tid; c < g.ncells; c += kQtThreads) s_soff[c] = cells[g.cell0 + c].slot_off;
     if (tid == 0) coff[g.ncells] = K;
     __syncthreads();
-    for (int k = tid; k < K; k += kQtThreads) {
-      int lo = 0, hi = g.ncells - 1;  // last c with coff[c] <= k
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (coff[mid] <= k) lo = mid;
-        else hi = mid - 1;
+    // four keys per thread per batch: their searches interleave and their
+    // global loads are in flight together (one memory latency per batch)
+    for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
+      int lo[4], hi[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        lo[u] = 0;
+        hi[u] = g.ncells - 1;
       }
-      keys[k] = fslots[s_soff[lo] + k - coff[lo]];
+      const int last = g.ncells - 1;
+      for (int span = last; span > 0; span >>= 1) {  // ceil(log2) rounds of the interleaved searches
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = k0 + u * kQtThreads;
+          if (lo[u] < hi[u]) {
+            const int mid = (lo[u] + hi[u] + 1) >> 1;
+            if (coff[mid] <= k) lo[u] = mid;
+            else hi[u] = mid - 1;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // finish searches the rounds above left open (rare)
+        const int k = k0 + u * kQtThreads;
+        while (lo[u] < hi[u]) {
+          const int mid = (lo[u] + hi[u] + 1) >> 1;
+          if (coff[mid] <= k) lo[u] = mid;
+          else hi[u] = mid - 1;
+        }
+      }
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * kQtThreads;
+        v[u] = k < K ? fslots[s_soff[lo[u]] + k - coff[lo[u]]] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * kQtThreads;
+        if (k < K) keys[k] = v[u];
+      }
     }
   }
   // ---- root nodes: nIni columns of width hX (src/ORBextractor.cc:894-936)
@@ -167,13 +201,19 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     const bool sorted_phase = s_var[1] != 0;
     ph(-1);
     // child key counts of every splittable node
-    for (int n = tid; n < size; n += kQtThreads) cc[n] = make_int4(0, 0, 0, 0);
+    for (int n = tid; n < size; n += kQtThreads) {
+      cc[n] = make_int4(0, 0, 0, 0);
+      int mx, my;
+      halves(nodeA[n], &mx, &my);
+      s_mid[n] = make_int2(mx, my);
+    }
     __syncthreads();
     for (int k = tid; k < K; k += kQtThreads) {
       const int n = knode[k];
       if (nkA[n] > 1) {
         const uint32_t kk = keys[k];
-        atomicAdd(((int*)&cc[n]) + quadrant(nodeA[n], key_x(kk), key_y(kk)), 1);
+        const int2 m = s_mid[n];
+        atomicAdd(((int*)&cc[n]) + (key_x(kk) >= m.x ? 1 : 0) + (key_y(kk) >= m.y ? 2 : 0), 1);
       }
     }
     __syncthreads();
@@ -293,7 +333,8 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
         knode[k] = (uint16_t)(T + tB[n]);
       } else {
         const uint32_t kk = keys[k];
-        knode[k] = (uint16_t)((const int*)&cc[n])[quadrant(nodeA[n], key_x(kk), key_y(kk))];
+        const int2 m = s_mid[n];
+        knode[k] = (uint16_t)((const int*)&cc[n])[(key_x(kk) >= m.x ? 1 : 0) + (key_y(kk) >= m.y ? 2 : 0)];
       }
     }
     __syncthreads();
@@ -352,8 +393,8 @@ size_t quadtree_lds_bytes(const ExtractParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t MN = P.maxnodes, SN = P.sortn;
   return r16(8 * SN) + 2 * r16(sizeof(QNode) * MN) + 4 * r16(4 * MN) + r16(16 * MN) + 2 * r16(4 * (MN + 1)) +
-         2 * r16(4 * MN) + 2 * r16(4 * (P.max_cells_level + 1)) + 2 * r16(64) + r16(4ull * P.kcap_lds) +
-         r16(2ull * P.kcap_lds);
+         2 * r16(4 * MN) + 2 * r16(4 * (P.max_cells_level + 1)) + r16(8 * MN) + 2 * r16(64) +
+         r16(4ull * P.kcap_lds) + r16(2ull * P.kcap_lds);
 }
 
 const void* quadtree_kernel_ptr() { return (const void*)quadtree_kernel; }
