@@ -103,6 +103,7 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   for (int c = tid; c < g.ncells; c += kQtThreads) coff[c] = cntp[c];
   __syncthreads();
   const int K = block_scan_excl<kQtThreads>(coff, g.ncells, s_tmp);
+  const unsigned long long t_scan = __builtin_amdgcn_s_memtime();
   uint32_t* keys = lkeys;
   uint16_t* knode = lnode;
   if (K > P.kcap_lds) {  // too many for LDS: same algorithm on an L2-resident scratch copy
@@ -111,54 +112,27 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   }
   const uint32_t* fslots = slots + (long long)f * P.slots_per_frame;
   {
-    // gather the K keys with independent loads: key k lives in cell c with
-    // coff[c] <= k < coff[c+1] (binary search in LDS), at slot_off(c) + k - coff[c]
+    // gather the K keys: cell c's keys (slot_off(c) .. + count) go to coff[c] ..
     for (int c = tid; c < g.ncells; c += kQtThreads) s_soff[c] = cells[g.cell0 + c].slot_off;
     if (tid == 0) coff[g.ncells] = K;
     __syncthreads();
-    // four keys per thread per batch: their searches interleave and their
-    // global loads are in flight together (one memory latency per batch)
-    for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
-      int lo[4], hi[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        lo[u] = 0;
-        hi[u] = g.ncells - 1;
+    // per cell: its keys are one contiguous slot run; loads in groups of
+    // four so that a thread's memory latencies overlap
+    for (int c = tid; c < g.ncells; c += kQtThreads) {
+      const int b = coff[c], n = coff[c + 1] - b;
+      const uint32_t* src = fslots + s_soff[c];
+      int i = 0;
+      for (; i + 4 <= n; i += 4) {
+        const uint32_t v0 = src[i], v1 = src[i + 1], v2 = src[i + 2], v3 = src[i + 3];
+        keys[b + i] = v0;
+        keys[b + i + 1] = v1;
+        keys[b + i + 2] = v2;
+        keys[b + i + 3] = v3;
       }
-      const int last = g.ncells - 1;
-      for (int span = last; span > 0; span >>= 1) {  // ceil(log2) rounds of the interleaved searches
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int k = k0 + u * kQtThreads;
-          if (lo[u] < hi[u]) {
-            const int mid = (lo[u] + hi[u] + 1) >> 1;
-            if (coff[mid] <= k) lo[u] = mid;
-            else hi[u] = mid - 1;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {  // finish searches the rounds above left open (rare)
-        const int k = k0 + u * kQtThreads;
-        while (lo[u] < hi[u]) {
-          const int mid = (lo[u] + hi[u] + 1) >> 1;
-          if (coff[mid] <= k) lo[u] = mid;
-          else hi[u] = mid - 1;
-        }
-      }
-      uint32_t v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + u * kQtThreads;
-        v[u] = k < K ? fslots[s_soff[lo[u]] + k - coff[lo[u]]] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + u * kQtThreads;
-        if (k < K) keys[k] = v[u];
-      }
+      for (; i < n; ++i) keys[b + i] = src[i];
     }
   }
+  const unsigned long long t_gather = __builtin_amdgcn_s_memtime();
   // ---- root nodes: nIni columns of width hX (src/ORBextractor.cc:894-936)
   const int nIni = g.nIni;
   int* rootCnt = tA;  // nIni <= MN
@@ -208,13 +182,25 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
       s_mid[n] = make_int2(mx, my);
     }
     __syncthreads();
-    for (int k = tid; k < K; k += kQtThreads) {
-      const int n = knode[k];
-      if (nkA[n] > 1) {
-        const uint32_t kk = keys[k];
-        const int2 m = s_mid[n];
-        atomicAdd(((int*)&cc[n]) + (key_x(kk) >= m.x ? 1 : 0) + (key_y(kk) >= m.y ? 2 : 0), 1);
+    for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {  // four keys in flight per thread
+      int n[4], q[4];
+      uint32_t kk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * kQtThreads;
+        n[u] = k < K ? knode[k] : 0;
+        kk[u] = k < K ? keys[k] : 0u;
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int2 m = s_mid[n[u]];
+        q[u] = (k0 + u * kQtThreads < K && nkA[n[u]] > 1)
+                   ? (key_x(kk[u]) >= m.x ? 1 : 0) + (key_y(kk[u]) >= m.y ? 2 : 0)
+                   : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (q[u] >= 0) atomicAdd(((int*)&cc[n[u]]) + q[u], 1);
     }
     __syncthreads();
     ph(0);
@@ -255,8 +241,15 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
       for (int i = tid; i < size; i += kQtThreads) {
         const unsigned long long ki = s_key[i];
         if (ki) {
-          int r = 0;
-          for (int j = 0; j < size; ++j) r += s_key[j] > ki ? 1 : 0;
+          int r = 0, j = 0;
+          for (; j + 8 <= size; j += 8) {  // eight broadcast reads in flight
+            unsigned long long v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = s_key[j + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) r += v[u] > ki ? 1 : 0;
+          }
+          for (; j < size; ++j) r += s_key[j] > ki ? 1 : 0;
           s_sort[r] = ki;
         }
       }
@@ -326,15 +319,30 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     __syncthreads();
     ph(2);
     // re-home the keys
-    for (int k = tid; k < K; k += kQtThreads) {
-      const int n = knode[k];
-      const int j = rank[n];
-      if (j < 0) {
-        knode[k] = (uint16_t)(T + tB[n]);
-      } else {
-        const uint32_t kk = keys[k];
-        const int2 m = s_mid[n];
-        knode[k] = (uint16_t)((const int*)&cc[n])[(key_x(kk) >= m.x ? 1 : 0) + (key_y(kk) >= m.y ? 2 : 0)];
+    for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {  // four keys in flight per thread
+      int n[4], j[4], nn[4];
+      uint32_t kk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * kQtThreads;
+        n[u] = k < K ? knode[k] : 0;
+        kk[u] = k < K ? keys[k] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) j[u] = rank[n[u]];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (j[u] < 0) {
+          nn[u] = T + tB[n[u]];
+        } else {
+          const int2 m = s_mid[n[u]];
+          nn[u] = ((const int*)&cc[n[u]])[(key_x(kk[u]) >= m.x ? 1 : 0) + (key_y(kk[u]) >= m.y ? 2 : 0)];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * kQtThreads;
+        if (k < K) knode[k] = (uint16_t)nn[u];
       }
     }
     __syncthreads();
@@ -385,6 +393,8 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     d[3] = dbg_sorted;
     d[4] = K;
     d[5] = size;
+    d[6] = (int)(t_scan - t_begin);
+    d[7] = (int)(t_gather - t_begin);
     for (int k = 0; k < 5; ++k) dbg[gridDim.x * gridDim.y * 8 + (blockIdx.y * gridDim.x + blockIdx.x) * 8 + k] = (int)dbg_ph[k];
   }
 }
@@ -422,10 +432,15 @@ int launch_quadtree(const ExtractParams& P, const ExtractBuffers& X, int batch, 
       double q[5] = {0};
       for (int f = 0; f < batch; ++f)
         for (int k = 0; k < 5; ++k) q[k] += h[(size_t)nwg * 8 + (f * P.L + l) * 8 + k];
+      double sc = 0, ga = 0;
+      for (int f = 0; f < batch; ++f) {
+        sc += h[(f * P.L + l) * 8 + 6];
+        ga += h[(f * P.L + l) * 8 + 7];
+      }
       fprintf(stderr, "quadtree L%d: avg cycles rounds %.0f total %.0f (max %d) rounds %.1f sorted %.1f K %.0f out %.0f"
-              " | count %.0f order %.0f sortorder %.0f table %.0f rehome %.0f\n",
+              " | scan %.0f gather %.0f | count %.0f order %.0f sortorder %.0f table %.0f rehome %.0f\n",
               l, a[0] / batch, a[1] / batch, mx, a[2] / batch, a[3] / batch, a[4] / batch, a[5] / batch,
-              q[0] / batch, q[1] / batch, q[4] / batch, q[2] / batch, q[3] / batch);
+              sc / batch, ga / batch, q[0] / batch, q[1] / batch, q[4] / batch, q[2] / batch, q[3] / batch);
     }
   }
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
