@@ -212,10 +212,14 @@ static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
   const int HL = P.lv[L - 1].h;
   // prefer bands small enough for two workgroups per CU (the kernel is
   // latency-bound: more resident waves beat less halo recompute)
+  // Several band heights R are planned (R0 = HL/18 and up to five taller);
+  // launch_pyramid picks the one whose workgroup count best fits the chip for
+  // the launch's batch (576 workgroups on 512 slots cost two full rounds).
   const size_t budgets[2] = {78 * 1024, 160 * 1024 - 1024};
   const int R0 = std::max(1, (HL + 17) / 18);
-  for (int pass = 0; pass < 2; ++pass)
-  for (int R = R0; R >= std::max(1, R0 / 3); --R) {
+  P.pyr_nplans = 0;
+  for (int pass = 0; pass < 2 && P.pyr_nplans == 0; ++pass)
+  for (int R = pass == 0 ? R0 + 5 : R0; R >= std::max(1, R0 / 3) && P.pyr_nplans < 6; --R) {
     const size_t budget = budgets[pass];
     const int nb = (HL + R - 1) / R;
     std::vector<int> lo((size_t)nb * L), chi((size_t)nb * L), ohi((size_t)nb * L);
@@ -246,19 +250,35 @@ static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
       ybytes = std::max(ybytes, s);
     }
     if (need[0] + need[1] + ybytes + 16 > budget) continue;
-    P.pyr_fused = 1;
-    P.pyr_nbands = nb;
-    P.pyr_lds_a = (int)need[0];
-    P.pyr_lds_b = (int)need[1];
-    P.pyr_lds_y = (int)ybytes;
-    P.pyr_bands = (int)rtab.size();
+    if (P.pyr_nplans > 0 && P.pyr_plan[P.pyr_nplans - 1].nbands == nb) continue;  // same band count as a taller R
+    long long cost = 0;
+    for (int b = 0; b < nb; ++b) {
+      long long c = 0;
+      for (int l = 0; l < L; ++l) c += (long long)(chi[b * L + l] - lo[b * L + l] + 1) * P.lv[l].w;
+      cost = std::max(cost, c);
+    }
+    ExtractParams::PyrPlan& q = P.pyr_plan[P.pyr_nplans++];
+    q.nbands = nb;
+    q.lds_a = (int)need[0];
+    q.lds_b = (int)need[1];
+    q.lds_y = (int)ybytes;
+    q.bands = (int)rtab.size();
+    q.cost = (int)cost;
     for (int b = 0; b < nb; ++b)
       for (int l = 0; l < L; ++l) {
         rtab.push_back(make_int2(lo[b * L + l], chi[b * L + l]));
         rtab.push_back(make_int2(lo[b * L + l], ohi[b * L + l]));
       }
-    return;
+    if (pass == 1) break;  // the large-LDS fallback: one workgroup per CU, one plan
   }
+  if (P.pyr_nplans == 0) return;
+  // default plan (R0's or the nearest): the LDS attribute covers the largest
+  P.pyr_fused = 1;
+  int def = 0;
+  for (int i = 0; i < P.pyr_nplans; ++i)
+    if (std::abs(P.pyr_plan[i].nbands - (HL + R0 - 1) / R0) < std::abs(P.pyr_plan[def].nbands - (HL + R0 - 1) / R0))
+      def = i;
+  select_pyr_plan(P, def);
 }
 
 static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
@@ -423,9 +443,19 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   HIP_OK(hipMemcpy(pl.cells_d.p, pl.cells.data(), pl.cells.size() * sizeof(CellGeom), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(pl.umax_d.p, h->umax, 16 * sizeof(int), hipMemcpyHostToDevice));
   HIP_OK(hipMemset(pl.err.p, 0, 16));
-  if (P.pyr_fused)
-    HIP_OK(hipFuncSetAttribute(pyr_band_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)pyr_band_lds_bytes(P)));
+  if (P.pyr_fused && getenv("ORBX_PYR_PROF") && getenv("ORBX_PYR_PROF")[0] == '1')
+    for (int i = 0; i < P.pyr_nplans; ++i)
+      fprintf(stderr, "pyr plan %d: %d bands, lds %d + %d + %d, cost %d\n", i, P.pyr_plan[i].nbands,
+              P.pyr_plan[i].lds_a, P.pyr_plan[i].lds_b, P.pyr_plan[i].lds_y, P.pyr_plan[i].cost);
+  if (P.pyr_fused) {
+    size_t mx = 0;
+    for (int i = 0; i < P.pyr_nplans; ++i) {
+      ExtractParams Q = P;
+      select_pyr_plan(Q, i);
+      mx = std::max(mx, pyr_band_lds_bytes(Q));
+    }
+    HIP_OK(hipFuncSetAttribute(pyr_band_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx));
+  }
   HIP_OK(hipFuncSetAttribute(quadtree_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)quadtree_lds_bytes(P)));
   return ORBX_OK;

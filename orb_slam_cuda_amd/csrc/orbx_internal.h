@@ -70,9 +70,41 @@ struct ExtractParams {
   int pyr_bands;               // int2 offset in the resize table: per (band, level) {comp_lo, comp_hi}, {own_lo, own_hi}
   int pyr_lds_a, pyr_lds_b;    // LDS bytes of the even-level and odd-level row buffers
   int pyr_lds_y;               // LDS bytes of the band's staged row coefficients
+  // alternative band heights, one picked per launch (launch_pyramid): the
+  // workgroup count nbands x batch against two resident workgroups per CU
+  struct PyrPlan {
+    int nbands, bands, lds_a, lds_b, lds_y;
+    int cost;  // largest per-band pixel count over the levels (level 0 staged + computed rows)
+  } pyr_plan[6];
+  int pyr_nplans;
   int gauss[7];                // 7-tap Gaussian fixed-point kernel (sum 257)
   LevelGeom lv[kMaxLevels];
 };
+
+inline void select_pyr_plan(ExtractParams& P, int i) {
+  const ExtractParams::PyrPlan& q = P.pyr_plan[i];
+  P.pyr_nbands = q.nbands;
+  P.pyr_bands = q.bands;
+  P.pyr_lds_a = q.lds_a;
+  P.pyr_lds_b = q.lds_b;
+  P.pyr_lds_y = q.lds_y;
+}
+
+// The band plan for a launch of `batch` frames: fewest (rounds of `slots`
+// resident workgroups) x (the tallest band's pixel count).
+inline int pick_pyr_plan(const ExtractParams& P, int batch, int slots) {
+  int best = 0;
+  long long best_t = -1;
+  for (int i = 0; i < P.pyr_nplans; ++i) {
+    const long long wgs = (long long)P.pyr_plan[i].nbands * batch;
+    const long long t = ((wgs + slots - 1) / slots) * (long long)P.pyr_plan[i].cost;
+    if (best_t < 0 || t < best_t) {
+      best = i;
+      best_t = t;
+    }
+  }
+  return best;
+}
 
 // Pointers to level data for one launch. Level 0 is the caller's frames.
 struct LevelPtrs {

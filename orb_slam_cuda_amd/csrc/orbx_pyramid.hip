@@ -291,31 +291,50 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams
 size_t pyr_band_lds_bytes(const ExtractParams& P) { return (size_t)P.pyr_lds_a + P.pyr_lds_b + P.pyr_lds_y + 16; }
 const void* pyr_band_kernel_ptr() { return (const void*)pyr_band_kernel; }
 
+static int launch_band(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab, int batch, hipStream_t s) {
+  static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_PYR_PROF=1)
+  static int dbg_cap = 0;
+  static const bool prof = getenv("ORBX_PYR_PROF") && getenv("ORBX_PYR_PROF")[0] == '1';
+  const int nwg = P.pyr_nbands * batch;
+  if (prof && nwg > dbg_cap) {
+    if (dbg) (void)hipFree(dbg);
+    (void)hipMalloc(&dbg, (size_t)nwg * 16 * 4);
+    dbg_cap = nwg;
+  }
+  hipLaunchKernelGGL(pyr_band_kernel, dim3(nwg), dim3(kPyrBandThreads), pyr_band_lds_bytes(P), s, P, lp, rtab,
+                     prof ? dbg : nullptr);
+  if (prof) {
+    std::vector<int> h((size_t)nwg * 16);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), dbg, h.size() * 4, hipMemcpyDeviceToHost);
+    double avg[16] = {0};
+    int mx[16] = {0};
+    for (int w = 0; w < nwg; ++w)
+      for (int k = 0; k < P.L; ++k) {
+        avg[k] += h[w * 16 + k];
+        mx[k] = std::max(mx[k], h[w * 16 + k]);
+      }
+    fprintf(stderr, "pyr_band: %d WGs (%d bands); phase cycles avg/max:", nwg, P.pyr_nbands);
+    for (int k = 0; k < P.L; ++k) fprintf(stderr, " [%d] %.0f/%d", k, avg[k] / nwg, mx[k]);
+    fprintf(stderr, "\n");
+  }
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
 int launch_pyramid(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab, int batch, hipStream_t s) {
   if (P.L < 2) return ORBX_OK;
   if (P.pyr_fused) {
-    static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_PYR_PROF=1)
-    static const bool prof = getenv("ORBX_PYR_PROF") && getenv("ORBX_PYR_PROF")[0] == '1';
-    const int nwg = P.pyr_nbands * batch;
-    if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)nwg * 16 * 4);
-    hipLaunchKernelGGL(pyr_band_kernel, dim3(nwg), dim3(kPyrBandThreads), pyr_band_lds_bytes(P), s, P, lp, rtab,
-                       prof ? dbg : nullptr);
-    if (prof) {
-      std::vector<int> h((size_t)nwg * 16);
-      (void)hipStreamSynchronize(s);
-      (void)hipMemcpy(h.data(), dbg, h.size() * 4, hipMemcpyDeviceToHost);
-      double avg[16] = {0};
-      int mx[16] = {0};
-      for (int w = 0; w < nwg; ++w)
-        for (int k = 0; k < P.L; ++k) {
-          avg[k] += h[w * 16 + k];
-          mx[k] = std::max(mx[k], h[w * 16 + k]);
-        }
-      fprintf(stderr, "pyr_band: %d WGs; phase cycles avg/max:", nwg);
-      for (int k = 0; k < P.L; ++k) fprintf(stderr, " [%d] %.0f/%d", k, avg[k] / nwg, mx[k]);
-      fprintf(stderr, "\n");
-    }
-    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+    // two resident 512-thread workgroups per CU (every plan's LDS <= 78 KB),
+    // unless the plan is the one-per-CU fallback
+    static const int cus = [] {
+      int dev = 0, n = 256;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return n;
+    }();
+    ExtractParams Q = P;
+    select_pyr_plan(Q, pick_pyr_plan(P, batch, pyr_band_lds_bytes(P) > 80 * 1024 ? cus : 2 * cus));
+    return launch_band(Q, lp, rtab, batch, s);
   }
   for (int l = 1; l < P.L; ++l) {
     const LevelGeom& sg = P.lv[l - 1];
