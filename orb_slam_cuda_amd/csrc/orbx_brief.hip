@@ -63,56 +63,92 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   const int bx = wg % gridDim.x, f = wg / gridDim.x, tid = threadIdx.x;
   const int lane = tid & 31, hk = tid >> 5;  // keypoint of this half-wave within the workgroup
   const int slot = bx * kObKps + hk;
+
+  // ---- the loads that depend on nothing are issued together: the key, the
+  // frame's level counts (uniform; the buffer is padded to kMaxLevels), the
+  // test table and the IC coefficient table (written to LDS after the patch
+  // loads are in flight)
+  const uint32_t key_raw = slot < P.kp_per_frame ? qkeys[(long long)f * P.kp_per_frame + slot] : 0u;
   const int* cnt = qcounts + f * P.L;
-  if (bx == 0 && tid == 0) {
-    int tot = 0;
-    for (int i = 0; i < P.L; ++i) tot += cnt[i];
-    out_counts[f] = tot;
+  int c[kMaxLevels];
+#pragma unroll
+  for (int i = 0; i < kMaxLevels; ++i) c[i] = cnt[i];
+  const int test_v = c_brief_tests[P.pattern_upstream ? 1 : 0][tid];
+  const uint32_t ic0 = c_ic_coef[tid], ic1 = c_ic_coef[min(tid + kObThreads, 16 * 24 - 1)];
+
+  // level of this half-wave's slot (kbase is uniform: scalar compares)
+  int l = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxLevels; ++i)
+    if (i < P.L && slot >= P.lv[i].kbase) l = i;
+  // the level fields of both half-waves by uniform index, selected per half
+  const int lA = __builtin_amdgcn_readlane(l, 0), lB = __builtin_amdgcn_readlane(l, 32);
+  const bool hiHalf = (tid & 32) != 0;
+  const LevelGeom& gA = P.lv[lA];
+  const LevelGeom& gB = P.lv[lB];
+#define OB_PICK(a, b) (hiHalf ? (b) : (a))
+  const int g_kbase = OB_PICK(gA.kbase, gB.kbase), g_minBX = OB_PICK(gA.minBX, gB.minBX),
+            g_minBY = OB_PICK(gA.minBY, gB.minBY), g_w = OB_PICK(gA.w, gB.w), g_h = OB_PICK(gA.h, gB.h),
+            g_pitch = OB_PICK(gA.pitch, gB.pitch);
+  const long long g_off = OB_PICK(gA.off, gB.off), g_plane = OB_PICK(gA.plane, gB.plane);
+  const float g_scale = OB_PICK(gA.scale, gB.scale), g_size = OB_PICK(gA.size, gB.size);
+  const int lpitch = OB_PICK(lp.pitch[lA], lp.pitch[lB]);
+  const uint8_t* lbase = OB_PICK(lp.base[lA], lp.base[lB]);
+  const long long lfstride = OB_PICK(lp.fstride[lA], lp.fstride[lB]);
+#undef OB_PICK
+  int cnt_l = 0, before = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kMaxLevels; ++i) {
+    const int ci = i < P.L ? c[i] : 0;
+    if (i == l) cnt_l = ci;
+    if (i < l) before += ci;
+    tot += ci;
   }
-  s_tests[tid] = c_brief_tests[P.pattern_upstream ? 1 : 0][tid];
-  for (int i = tid; i < 16 * 24; i += kObThreads) s_ictab[i] = c_ic_coef[i];
+  if (bx == 0 && tid == 0) out_counts[f] = tot;
 
   // ---- the keypoint of this half-wave
-  int l = 0;
-  while (l + 1 < P.L && slot >= P.lv[l + 1].kbase) ++l;
-  const LevelGeom& g = P.lv[l];
-  const int idx = slot - g.kbase;
-  const bool valid = slot < P.kp_per_frame && idx < cnt[l];
-  uint32_t key = 0;
-  if (valid) key = qkeys[(long long)f * P.kp_per_frame + slot];
+  const int idx = slot - g_kbase;
+  const bool valid = slot < P.kp_per_frame && idx < cnt_l;
+  const uint32_t key = valid ? key_raw : 0u;
   // an empty slot works on a dummy keypoint at the level centre (never stored)
-  const int x = valid ? key_x(key) + g.minBX : g.w / 2, y = valid ? key_y(key) + g.minBY : g.h / 2;
+  const int x = valid ? key_x(key) + g_minBX : g_w / 2, y = valid ? key_y(key) + g_minBY : g_h / 2;
 
-  // ---- one burst of loads: blurred patch -> LDS (16-byte chunks), IC rows ->
-  // registers (lane v - 15 = patch row: the row's 31 pixels as 9 dwords)
+  // ---- one burst of loads: blurred patch (16-byte chunks, five per lane) and
+  // IC rows (lane v - 15 = patch row: the row's 31 pixels within 9 dwords from
+  // the dword boundary below x - 15; they reach at most byte x + 20 <= w of a
+  // row <= h - 5, so they stay inside the level). Every load is unconditional
+  // (lanes without a chunk, or of an empty slot, read the buffer start) so
+  // that no branch join waits for them; only the LDS stores are predicated.
   const int c0 = (x - kObRadius) & ~15;
-  const int pitch = lp.pitch[l];
-  const uint8_t* lrow = lp.base[l] + f * lp.fstride[l] + (long long)(y - kHalfPatch) * pitch + (x - kHalfPatch);
-  uint32_t w[9] = {};
-  int sh = 0;
-  if (valid) {
-    const uint8_t* brow = blur + g.off + f * g.plane + (long long)(y - kObRadius) * g.pitch + c0;
+  const int pitch = lpitch;
+  constexpr int kChunks = kObRows * 4, kPerLane = (kChunks + 31) / 32;
+  uint4 pv[kPerLane];
+  const uint8_t* brow = blur + g_off + f * g_plane + (long long)(y - kObRadius) * g_pitch + c0;
+#pragma unroll
+  for (int k = 0; k < kPerLane; ++k) {
+    const int i = min(lane + 32 * k, kChunks - 1), r = i >> 2, ch = i & 3;
+    // chunks past the row end (c0 and the pitch are multiples of 16) are never sampled
+    const bool ok = valid && c0 + ch * 16 + 16 <= g_pitch;
+    pv[k] = *(const uint4*)(ok ? brow + (long long)r * g_pitch + ch * 16 : blur);
+  }
+  const uint8_t* rp = lbase + f * lfstride + (long long)(y - kHalfPatch + min(lane, kPatchSize - 1)) * pitch +
+                      (x - kHalfPatch);
+  const uint32_t* q = valid ? (const uint32_t*)((uintptr_t)rp & ~(uintptr_t)3) : (const uint32_t*)lbase;
+  const int sh = (int)((uintptr_t)rp & 3);
+  uint32_t w[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) w[k] = q[k];
+  s_tests[tid] = test_v;
+  s_ictab[tid] = ic0;
+  if (tid + kObThreads < 16 * 24) s_ictab[tid + kObThreads] = ic1;
+  // unpredicated stores (an empty slot writes its own unused patch, lanes past
+  // the last chunk rewrite it with the same bytes), so no load waits in a branch
+  {
     uint8_t* dst = s_patch[hk];
-    for (int i = lane; i < kObRows * 4; i += 32) {
-      const int r = i >> 2, ch = i & 3;
-      if (c0 + ch * 16 + 16 <= g.pitch)
-        *(uint4*)(dst + r * kObStride + ch * 16) = *(const uint4*)(brow + (long long)r * g.pitch + ch * 16);
-    }
-    if (lane < kPatchSize) {
-      const uint8_t* rp = lrow + (long long)lane * pitch;
-      if (lp.aligned16[l]) {
-        // dword loads covering [x - 15, x + 16], at most byte x + 18 (< w: the
-        // keypoints keep EDGE_THRESHOLD = 19 from the border)
-        const uint32_t* q = (const uint32_t*)((uintptr_t)rp & ~(uintptr_t)3);
-        sh = (int)((uintptr_t)rp & 3);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) w[k] = q[k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          w[k] = (uint32_t)rp[4 * k] | ((uint32_t)rp[4 * k + 1] << 8) | ((uint32_t)rp[4 * k + 2] << 16) |
-                 ((uint32_t)rp[4 * k + 3] << 24);
-      }
+    for (int k = 0; k < kPerLane; ++k) {
+      const int i = min(lane + 32 * k, kChunks - 1), r = i >> 2, ch = i & 3;
+      *(uint4*)(dst + r * kObStride + ch * 16) = pv[k];
     }
   }
   __syncthreads();  // staged patch, test table, IC coefficient table
@@ -161,9 +197,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   }
 
   if (!valid) return;
-  int outpos = idx;
-  for (int i = 0; i < l; ++i) outpos += cnt[i];
-  const long long o = (long long)f * P.kp_per_frame + outpos;
+  const long long o = (long long)f * P.kp_per_frame + before + idx;
   if (lane < 2) {
     uint4* d = (uint4*)(out_desc + o * 32) + lane;
     *d = lane ? make_uint4(dword[4], dword[5], dword[6], dword[7])
@@ -172,12 +206,12 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
     orbx_kp kp;
     float fxp = (float)x, fyp = (float)y;
     if (l != 0) {
-      fxp = __fmul_rn(fxp, g.scale);
-      fyp = __fmul_rn(fyp, g.scale);
+      fxp = __fmul_rn(fxp, g_scale);
+      fyp = __fmul_rn(fyp, g_scale);
     }
     kp.x = fxp;
     kp.y = fyp;
-    kp.size = g.size;
+    kp.size = g_size;
     kp.angle = angle;
     kp.response = (float)key_score(key);
     kp.octave = l;

@@ -435,7 +435,7 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   if ((rc = pl.slots.alloc((size_t)B * slot * 4 + 4))) return rc;
   if ((rc = pl.cell_counts.alloc((size_t)B * P.ncells_total * 4))) return rc;
   if ((rc = pl.qkeys.alloc((size_t)B * P.kp_per_frame * 4))) return rc;
-  if ((rc = pl.qcounts.alloc((size_t)B * L * 4))) return rc;
+  if ((rc = pl.qcounts.alloc((size_t)B * L * 4 + 4 * kMaxLevels))) return rc;  // orient_brief reads kMaxLevels counts per frame
   if ((rc = pl.qscratch.alloc((size_t)B * slot * 4 + 4))) return rc;
   if ((rc = pl.qnscratch.alloc((size_t)B * slot * 2 + 4))) return rc;
   if ((rc = pl.err.alloc(16))) return rc;

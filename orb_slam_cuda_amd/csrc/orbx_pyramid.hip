@@ -332,8 +332,11 @@ int launch_pyramid(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
       return n;
     }();
+    static const int forced = getenv("ORBX_PYR_PLAN") ? atoi(getenv("ORBX_PYR_PLAN")) : -1;  // experiments only
     ExtractParams Q = P;
-    select_pyr_plan(Q, pick_pyr_plan(P, batch, pyr_band_lds_bytes(P) > 80 * 1024 ? cus : 2 * cus));
+    select_pyr_plan(Q, forced >= 0 && forced < P.pyr_nplans
+                           ? forced
+                           : pick_pyr_plan(P, batch, pyr_band_lds_bytes(P) > 80 * 1024 ? cus : 2 * cus));
     return launch_band(Q, lp, rtab, batch, s);
   }
   for (int l = 1; l < P.L; ++l) {
