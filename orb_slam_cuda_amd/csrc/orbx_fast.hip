@@ -112,7 +112,19 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
   };
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
   const int cell = wg % P.ncells_total, f = wg / P.ncells_total, lane = threadIdx.x;
-  const CellGeom cg = cells[cell];
+  // the whole 16-byte cell record in one scalar load (int16 fields unpacked
+  // from it, so no 16-bit vector load sits on the critical path)
+  CellGeom cg;
+  {
+    const int4 raw = ((const int4*)cells)[cell];
+    cg.c0 = (int16_t)(raw.x & 0xFFFF);
+    cg.r0 = (int16_t)(raw.x >> 16);
+    cg.c1 = (int16_t)(raw.y & 0xFFFF);
+    cg.r1 = (int16_t)(raw.y >> 16);
+    cg.slot_off = raw.z;
+    cg.cap = (int16_t)(raw.w & 0xFFFF);
+    cg.level = (int16_t)(raw.w >> 16);
+  }
   int* cnt = cell_counts + (long long)f * P.ncells_total + cell;
   const int rw = cg.c1 - cg.c0, rh = cg.r1 - cg.r0;
   const int bw = rw - 6, bh = rh - 6;
@@ -134,24 +146,23 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
   const int a0 = cg.c0 & ~15, ox = cg.c0 - a0;
   if (lp.aligned16[l]) {
     // the ROI's 16-byte chunks in flight at once (4 per lane; tall cells loop for the rest)
+    // unpredicated: lanes past the last chunk load and store it again (same
+    // bytes), so the four loads stay in registers and in flight together
     const int nch = (cg.c1 - a0 + 15) >> 4, total = rh * nch;
-    uint4 v[4];
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 here ends up in scratch)
+    u32x4 v[4];
+    int ro[4], lo[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int i = lane + 64 * k;
-      if (i < total) {
-        const int r = i / nch, ch = i - r * nch;
-        v[k] = *(const uint4*)(rows + (long long)r * pitch + a0 + ch * 16);
-      }
+      const int i = min(lane + 64 * k, total - 1);
+      const int r = i / nch, ch = i - r * nch;
+      ro[k] = r * kRoiStride + ch * 16;
+      lo[k] = r * pitch + ch * 16;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = lane + 64 * k;
-      if (i < total) {
-        const int r = i / nch, ch = i - r * nch;
-        *(uint4*)(roi + r * kRoiStride + ch * 16) = v[k];
-      }
-    }
+    for (int k = 0; k < 4; ++k) v[k] = *(const u32x4*)(rows + a0 + lo[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) *(u32x4*)(roi + ro[k]) = v[k];
     for (int i = lane + 256; i < total; i += 64) {
       const int r = i / nch, ch = i - r * nch;
       *(uint4*)(roi + r * kRoiStride + ch * 16) = *(const uint4*)(rows + (long long)r * pitch + a0 + ch * 16);
