@@ -47,25 +47,42 @@ __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp
   const uint8_t* S = lp.base[l] + f * lp.fstride[l];
   const int pitch = lp.pitch[l];
   // stage rows y0-3 .. y0+TH+2, columns x0-16 .. x0+TW+15
-  constexpr int kChunks = kBlurInW / 16;
-  for (int i = tid; i < (kBlurTH + 6) * kChunks; i += 256) {
-    const int r = i / kChunks, ch = i - r * kChunks;
-    const int gy = reflect101(min(max(y0 + r - 3, -(H - 1)), 2 * H - 2), H);
-    const int gx = x0 - 16 + ch * 16;
-    const uint8_t* src = S + (long long)gy * pitch;
-    uint4 v;
-    if (gx >= 0 && gx + 16 <= W && (((uintptr_t)(src + gx)) & 15) == 0) {
-      v = *(const uint4*)(src + gx);
-    } else {
-      uint8_t b[16];
+  // every thread's chunks are loaded at once (unpredicated: a chunk that
+  // leaves the image loads the level start and is rewritten from byte loads
+  // with reflection after the aligned chunks are stored)
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int kChunks = kBlurInW / 16, kItems = (kBlurTH + 6) * kChunks, kPer = (kItems + 255) / 256;
+  u32x4 v[kPer];
+  bool direct[kPer];
+  int gys[kPer];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int xx = min(max(gx + k, -(W - 1)), 2 * W - 2);
-        b[k] = src[reflect101(xx, W)];
-      }
-      v = *(const uint4*)b;
+  for (int q = 0; q < kPer; ++q) {
+    const int i = min(tid + 256 * q, kItems - 1);
+    const int r = i / kChunks, ch = i - r * kChunks;
+    gys[q] = reflect101(min(max(y0 + r - 3, -(H - 1)), 2 * H - 2), H);
+    const int gx = x0 - 16 + ch * 16;
+    const uint8_t* src = S + (long long)gys[q] * pitch + gx;
+    direct[q] = gx >= 0 && gx + 16 <= W && (((uintptr_t)src) & 15) == 0;
+    v[q] = *(const u32x4*)(direct[q] ? src : S);
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int i = min(tid + 256 * q, kItems - 1);
+    const int r = i / kChunks, ch = i - r * kChunks;
+    *(u32x4*)&in[r][ch * 16] = v[q];
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    if (direct[q]) continue;
+    const int i = min(tid + 256 * q, kItems - 1);
+    const int r = i / kChunks, ch = i - r * kChunks;
+    const int gx = x0 - 16 + ch * 16;
+    const uint8_t* src = S + (long long)gys[q] * pitch;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int xx = min(max(gx + k, -(W - 1)), 2 * W - 2);
+      in[r][ch * 16 + k] = src[reflect101(xx, W)];
     }
-    *(uint4*)&in[r][ch * 16] = v;
   }
   __syncthreads();
   const int* k = P.gauss;

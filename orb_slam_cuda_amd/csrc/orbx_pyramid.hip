@@ -201,15 +201,38 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams
   // the band's row coefficients of every level, staged once: a global load
   // per output row would put one memory latency on every row iteration
   int2* const s_yt = (int2*)(smem + P.pyr_lds_a + P.pyr_lds_b);
-  for (int l = 1, off = 0; l < L; ++l) {
-    const LevelGeom& g = P.lv[l];
-    const int2 cd = bt[2 * l];
-    const int n = cd.y - cd.x + 1;
-    for (int i = tid; i < n; i += kPyrBandThreads) {
-      const int r = cd.x + i;
-      s_yt[off + i] = g.area2x ? make_int2((2 * r) | ((2 * r + 1) << 16), 0) : rtab[g.ytab + r];
+  // one staged row coefficient per thread (rows of levels 1..L-1 flattened;
+  // bands hold far fewer than kPyrBandThreads rows, larger ones loop), its
+  // load issued before the level-0 loads so that both are in flight together
+  // (no early exit and constant level indices: the band table and level
+  // fields are scalar loads issued together)
+  int yrow = 0, ytot = 0, yarea = 1, ytab = 0;
+#pragma unroll
+  for (int l = 1; l < kMaxLevels; ++l) {
+    const int2 cd = bt[2 * min(l, L - 1)];
+    const int n = l < L ? cd.y - cd.x + 1 : 0;
+    if (tid >= ytot && tid < ytot + n) {
+      yrow = cd.x + tid - ytot;
+      yarea = P.lv[l].area2x;
+      ytab = P.lv[l].ytab;
     }
-    off += n;
+    ytot += n;
+  }
+  int2 yval = make_int2(0, 0);
+  if (tid < ytot) yval = yarea ? make_int2((2 * yrow) | ((2 * yrow + 1) << 16), 0) : rtab[ytab + yrow];
+  for (int i = tid + kPyrBandThreads; i < ytot; i += kPyrBandThreads) {  // very tall bands only
+    int rem = i;
+    for (int l = 1; l < L; ++l) {
+      const int2 cd = bt[2 * l];
+      const int n = cd.y - cd.x + 1;
+      if (rem < n) {
+        const LevelGeom& g = P.lv[l];
+        const int r = cd.x + rem;
+        s_yt[i] = g.area2x ? make_int2((2 * r) | ((2 * r + 1) << 16), 0) : rtab[g.ytab + r];
+        break;
+      }
+      rem -= n;
+    }
   }
 
   // ---- stage level-0 rows [comp_lo, comp_hi], full width, 4 loads in flight per thread
@@ -218,26 +241,28 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams
     const int rows = c0.y - c0.x + 1, W0 = P.lv[0].w, lp0 = P.lv[0].lpitch, pitch = lp.pitch[0];
     const uint8_t* S = lp.base[0] + f * lp.fstride[0] + (long long)c0.x * pitch;
     if (lp.aligned16[0]) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
       const int nch = (W0 + 15) >> 4, total = rows * nch;
-      auto ld = [&](int i) -> uint4 {
-        if (i >= total) return make_uint4(0, 0, 0, 0);
-        const int r = i / nch, ch = i - r * nch;
-        return *(const uint4*)(S + (long long)r * pitch + ch * 16);
-      };
-      auto st = [&](int i, const uint4& v) {
-        if (i >= total) return;
-        const int r = i / nch, ch = i - r * nch;
-        *(uint4*)(bufA + r * lp0 + ch * 16) = v;
-      };
+      // unpredicated (indices past the end repeat the last chunk)
       for (int i0 = tid; i0 < total; i0 += 4 * kPyrBandThreads) {
-        const uint4 v0 = ld(i0), v1 = ld(i0 + kPyrBandThreads), v2 = ld(i0 + 2 * kPyrBandThreads),
-                    v3 = ld(i0 + 3 * kPyrBandThreads);
-        st(i0, v0);
-        st(i0 + kPyrBandThreads, v1);
-        st(i0 + 2 * kPyrBandThreads, v2);
-        st(i0 + 3 * kPyrBandThreads, v3);
+        u32x4 v[4];
+        int so[4], lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = min(i0 + q * kPyrBandThreads, total - 1);
+          const int r = i / nch, ch = i - r * nch;
+          lo[q] = r * pitch + ch * 16;
+          so[q] = r * lp0 + ch * 16;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = *(const u32x4*)(S + lo[q]);
+        if (i0 == tid && tid < ytot) s_yt[tid] = yval;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *(u32x4*)(bufA + so[q]) = v[q];
       }
+      if (tid >= total && tid < ytot) s_yt[tid] = yval;
     } else {
+      if (tid < ytot) s_yt[tid] = yval;
       for (int r = 0; r < rows; ++r)
         for (int c = tid; c < W0; c += kPyrBandThreads) bufA[r * lp0 + c] = S[(long long)r * pitch + c];
     }
