@@ -12,7 +12,11 @@ import re
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# ORBX_LIB_VARIANT=<name> loads variants/liborbx_<name>.so (tools/variant.sh
+# builds them: a kernel compiled with other tuning constants, for A/B timing)
 LIB_PATH = os.path.join(HERE, "liborbx.so")
+if os.environ.get("ORBX_LIB_VARIANT"):
+    LIB_PATH = os.path.join(HERE, "variants", "liborbx_%s.so" % os.environ["ORBX_LIB_VARIANT"])
 HEADER = os.path.join(os.path.dirname(HERE), "include", "orbx_c.h")
 
 ORBX_OK, ORBX_EINVAL, ORBX_EDEVICE, ORBX_ECAPACITY, ORBX_ENOMEM = 0, -1, -2, -3, -4

@@ -8,7 +8,7 @@
 namespace orbx {
 
 // Separable 7-tap fixed-point Gaussian, BORDER_REFLECT_101 at the level edges.
-// Tile = 128 x 32 outputs per 256-thread block. The input tile (+3 halo, 16-B
+// Tile = 128 x 64 outputs per 256-thread block (64 rows: 1.1x halo rows instead of 1.2x; measured best of 16..80). The input tile (+3 halo, 16-B
 // aligned: columns [x0-16, x0+144)) is staged with 16-byte loads (byte loads
 // with reflection only where a chunk leaves the image).
 //   row pass:    v_dot4_u32_u8 of a pixel dword with a tap dword: 10 dot4 per
@@ -16,7 +16,13 @@ namespace orbx {
 //                vertically adjacent rows are packed into one dword,
 //   column pass: v_dot2_u32_u16 of such a row pair with a tap pair: 4 dot2
 //                per output, then (acc + 2^15) >> 16.
-constexpr int kBlurTW = 128, kBlurTH = 32, kBlurInW = kBlurTW + 32;
+#ifndef ORBX_BLUR_TH
+#define ORBX_BLUR_TH 64
+#endif
+#ifndef ORBX_BLUR_TW
+#define ORBX_BLUR_TW 128
+#endif
+constexpr int kBlurTW = ORBX_BLUR_TW, kBlurTH = ORBX_BLUR_TH, kBlurInW = kBlurTW + 32;
 constexpr int kBlurPairs = (kBlurTH + 6 + 1) / 2;  // 19 staged row pairs
 
 typedef unsigned short us2_t __attribute__((ext_vector_type(2)));

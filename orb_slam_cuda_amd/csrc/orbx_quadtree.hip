@@ -67,10 +67,16 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
   int dbg_rounds = 0, dbg_sorted = 0;
-  unsigned long long dbg_ph[5] = {0, 0, 0, 0, 0}, dbg_t = 0;
+  // phase clocks (ORBX_QT_PROF): scalars, not an array, so nothing lands in scratch
+  unsigned long long dbg_p0 = 0, dbg_p1 = 0, dbg_p2 = 0, dbg_p3 = 0, dbg_p4 = 0, dbg_t = 0;
   auto ph = [&](int k) {
-    const unsigned long long t = __builtin_amdgcn_s_memtime();
-    if (k >= 0) dbg_ph[k] += t - dbg_t;
+    if (!dbg) return;
+    const unsigned long long t = __builtin_amdgcn_s_memtime(), d = t - dbg_t;
+    if (k == 0) dbg_p0 += d;
+    else if (k == 1) dbg_p1 += d;
+    else if (k == 2) dbg_p2 += d;
+    else if (k == 3) dbg_p3 += d;
+    else if (k == 4) dbg_p4 += d;
     dbg_t = t;
   };
   const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
@@ -395,7 +401,12 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     d[5] = size;
     d[6] = (int)(t_scan - t_begin);
     d[7] = (int)(t_gather - t_begin);
-    for (int k = 0; k < 5; ++k) dbg[gridDim.x * gridDim.y * 8 + (blockIdx.y * gridDim.x + blockIdx.x) * 8 + k] = (int)dbg_ph[k];
+    int* dp = dbg + gridDim.x * gridDim.y * 8 + (blockIdx.y * gridDim.x + blockIdx.x) * 8;
+    dp[0] = (int)dbg_p0;
+    dp[1] = (int)dbg_p1;
+    dp[2] = (int)dbg_p2;
+    dp[3] = (int)dbg_p3;
+    dp[4] = (int)dbg_p4;
   }
 }
 
