@@ -197,7 +197,9 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
       // >= 2 brighter than v + t  <=>  their 2nd largest is
       const int s1 = min(n0, n4), l1 = max(n0, n4), s2 = min(n8, n12), l2 = max(n8, n12);
       const int a = max(s1, s2), b = min(l1, l2);
-      fl[q] = by < bh && lc < bw && (min(a, b) < v - t || max(a, b) > v + t);
+      // bitwise, not short-circuit: the reads are clamped, so all four row
+      // groups' loads can be in flight before the first use
+      fl[q] = (int)(by < bh) & (int)(lc < bw) & ((int)(min(a, b) < v - t) | (int)(max(a, b) > v + t));
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
