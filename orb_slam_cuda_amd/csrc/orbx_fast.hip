@@ -30,7 +30,15 @@
 
 namespace orbx {
 
-constexpr int kRoiStride = 80;  // >= 65-px ROI + 15 bytes of 16-B alignment slack
+// ROI row stride in LDS: 44 when every cell ROI fits 3 + rw <= 44 bytes (cells
+// of <= 35 px, KITTI and EuRoC: staged with dword loads from the dword below
+// the ROI), else 80 (>= 65-px ROI + 15 bytes of 16-B alignment slack, 16-byte
+// staging). The tight stride cuts a wave's LDS from ~8.0 KB to ~6.3 KB.
+#ifndef ORBX_FAST_TIGHT_E
+#define ORBX_FAST_TIGHT_E 4   // staging element of the tight stride: 4 -> stride 44, 8 -> stride 48
+#endif
+constexpr int kTightE = ORBX_FAST_TIGHT_E;
+constexpr int kRoiTight = kTightE == 4 ? 44 : 48, kRoiWide = 80;
 
 // popcount of the bits of m below this lane
 __device__ __forceinline__ int mbcnt64(uint64_t m) {
@@ -82,17 +90,19 @@ __device__ __forceinline__ bool has_arc9(uint32_t m) {
 }
 
 // Bresenham ring of radius 3, k = 0..15 (cv::makeOffsets, pattern 16)
+template <int kRoiStride>
 __device__ __forceinline__ int ring_off(int k) {
   constexpr int rx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
   constexpr int ry[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
   return ry[k] * kRoiStride + rx[k];
 }
 
+template <int kRoiStride>
 __device__ __forceinline__ void ring_masks(const uint8_t* c, int lo, int hi, uint32_t* dark, uint32_t* bright) {
   uint32_t dk = 0, br = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int x = c[ring_off(k)];
+    const int x = c[ring_off<kRoiStride>(k)];
     dk |= (uint32_t)(x < lo) << k;
     br |= (uint32_t)(x > hi) << k;
   }
@@ -100,7 +110,11 @@ __device__ __forceinline__ void ring_masks(const uint8_t* c, int lo, int hi, uin
   *bright = br;
 }
 
-__global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPtrs lp,
+#ifndef ORBX_FAST_WAVES
+#define ORBX_FAST_WAVES 6  // VGPR budget: 6 waves per SIMD (<= 80 VGPRs)
+#endif
+template <int kRoiStride>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WAVES))) void fast_cells_kernel(ExtractParams P, LevelPtrs lp,
                                                         const CellGeom* __restrict__ cells,
                                                         uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_counts, int* dbg) {
@@ -135,7 +149,9 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
   unsigned char* sp = smem;
   auto take = [&](size_t bytes) { unsigned char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
   uint8_t* roi = (uint8_t*)take((size_t)P.fast_rh_max * kRoiStride);
-  uint8_t* sc = (uint8_t*)take((size_t)(P.fast_bw_max + 2) * (P.fast_bh_max + 2));
+  // score map with a zero ring, row stride bw + 1: the right border of a row
+  // is the left border of the next, which no score is ever written to
+  uint8_t* sc = (uint8_t*)take((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1);
   uint16_t* list = (uint16_t*)take(2ull * P.fast_bw_max * P.fast_bh_max);
   uint64_t* ball = (uint64_t*)take(16ull * ((P.fast_bw_max * P.fast_bh_max + 63) / 64));
 
@@ -143,11 +159,35 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
   const LevelGeom& g = P.lv[l];
   const int pitch = lp.pitch[l];
   const uint8_t* rows = lp.base[l] + f * lp.fstride[l] + (long long)cg.r0 * pitch;
-  const int a0 = cg.c0 & ~15, ox = cg.c0 - a0;
-  if (lp.aligned16[l]) {
-    // the ROI's 16-byte chunks in flight at once (4 per lane; tall cells loop for the rest)
-    // unpredicated: lanes past the last chunk load and store it again (same
-    // bytes), so the four loads stay in registers and in flight together
+  constexpr bool kTight = kRoiStride == kRoiTight;
+  const int a0 = kTight ? (cg.c0 & ~(kTightE - 1)) : (cg.c0 & ~15), ox = cg.c0 - a0;
+  // unpredicated staging: lanes past the last piece load and store it again
+  // (same bytes), so all of a lane's loads stay in registers and in flight
+  if (lp.aligned16[l] && kTight) {
+    // kTightE-byte pieces from the piece at or below c0 (<= 11 dwords or 6
+    // qwords per row), kK per lane in flight
+    typedef unsigned int piece_t __attribute__((ext_vector_type(kTightE / 4)));
+    constexpr int kK = kTightE == 4 ? 8 : 5;
+    const int nd = (cg.c1 - a0 + kTightE - 1) / kTightE, total = rh * nd;
+    piece_t v[kK];
+    int ro[kK], lo[kK];
+#pragma unroll
+    for (int k = 0; k < kK; ++k) {
+      const int i = min(lane + 64 * k, total - 1);
+      const int r = i / nd, d = i - r * nd;
+      ro[k] = r * kRoiStride + kTightE * d;
+      lo[k] = r * pitch + kTightE * d;
+    }
+#pragma unroll
+    for (int k = 0; k < kK; ++k) v[k] = *(const piece_t*)(rows + a0 + lo[k]);
+#pragma unroll
+    for (int k = 0; k < kK; ++k) *(piece_t*)(roi + ro[k]) = v[k];
+    for (int i = lane + 64 * kK; i < total; i += 64) {
+      const int r = i / nd, d = i - r * nd;
+      *(piece_t*)(roi + r * kRoiStride + kTightE * d) = *(const piece_t*)(rows + (long long)r * pitch + a0 + kTightE * d);
+    }
+  } else if (lp.aligned16[l]) {
+    // the ROI's 16-byte chunks, 4 per lane (tall cells loop for the rest)
     const int nch = (cg.c1 - a0 + 15) >> 4, total = rh * nch;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 here ends up in scratch)
     u32x4 v[4];
@@ -171,8 +211,8 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
     for (int r = 0; r < rh; ++r)
       for (int c = lane; c < rw; c += 64) roi[r * kRoiStride + ox + c] = rows[(long long)r * pitch + cg.c0 + c];
   }
-  const int sw = bw + 2;  // score map with a zero ring
-  for (int i = lane; i < (sw * (bh + 2) + 3) >> 2; i += 64) ((uint32_t*)sc)[i] = 0;
+  const int sw = bw + 1;
+  for (int i = lane; i < (sw * (bh + 2) + 1 + 3) >> 2; i += 64) ((uint32_t*)sc)[i] = 0;
   __syncthreads();
   stamp(0);
 
@@ -220,7 +260,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
       const uint8_t* c = band + (e >> 8) * kRoiStride + (e & 255);
       const int v = c[0];
       uint32_t dk, br;
-      ring_masks(c, v - t, v + t, &dk, &br);
+      ring_masks<kRoiStride>(c, v - t, v + t, &dk, &br);
       det = has_arc9(dk) || has_arc9(br);
     }
     const uint64_t m = __ballot(det);
@@ -235,7 +275,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
     const int v = c[0];
     int d[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) d[k] = v - c[ring_off(k)];
+    for (int k = 0; k < 16; ++k) d[k] = v - c[ring_off<kRoiStride>(k)];
     sc[((e >> 8) + 1) * sw + (e & 255) + 1] = (uint8_t)corner_score16(d, t);
   }
   __syncthreads();
@@ -292,10 +332,13 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(ExtractParams P, LevelPt
   }
 }
 
+static bool fast_tight(const ExtractParams& P) { return P.fast_bw_max + 6 + kTightE - 1 <= kRoiTight; }
+
 size_t fast_lds_bytes(const ExtractParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t band = (size_t)P.fast_bw_max * P.fast_bh_max;
-  return r16((size_t)P.fast_rh_max * kRoiStride) + r16((size_t)(P.fast_bw_max + 2) * (P.fast_bh_max + 2)) +
+  const int stride = fast_tight(P) ? kRoiTight : kRoiWide;
+  return r16((size_t)P.fast_rh_max * stride) + r16((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1) +
          r16(2 * band) + r16(16 * ((band + 63) / 64));
 }
 
@@ -306,8 +349,12 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
   const int nwg = P.ncells_total * batch;
   if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)nwg * 32);
   if (prof) (void)hipMemsetAsync(dbg, 0, (size_t)nwg * 32, s);
-  hipLaunchKernelGGL(fast_cells_kernel, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P, lp, cells,
-                     slots, cell_counts, prof ? dbg : nullptr);
+  if (fast_tight(P))
+    hipLaunchKernelGGL(fast_cells_kernel<kRoiTight>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
+                       lp, cells, slots, cell_counts, prof ? dbg : nullptr);
+  else
+    hipLaunchKernelGGL(fast_cells_kernel<kRoiWide>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
+                       lp, cells, slots, cell_counts, prof ? dbg : nullptr);
   if (prof) {
     std::vector<int> h((size_t)nwg * 8);
     (void)hipStreamSynchronize(s);
