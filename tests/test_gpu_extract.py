@@ -97,6 +97,7 @@ def test_golden_vectors(pkg, name):
     dict(nf=2000, ini=30, mn=10),
     dict(nf=2000, ini=5, mn=12),                    # iniTh < minTh
     dict(nf=0),                                     # no features requested
+    dict(nf=600, W=369, H=300),                     # 37-px cells at level 4: FAST's 80-byte ROI stride path
 ])
 def test_config_parity(pkg, O, kw):
     from orb_slam_cuda_amd.synth import synth_frame
