@@ -176,6 +176,13 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   __syncthreads();
 
   const int N = g.N;
+  // node tables ping-pong between rounds (A = this round's list, B = the next)
+  QNode* nA = nodeA;
+  QNode* nB = nodeB;
+  int* kA = nkA;
+  int* kB = nkB;
+  int* qA = seqA;
+  int* qB = seqB;
   for (int round = 0; round < 64; ++round) {
     const int size = s_var[0];
     const bool sorted_phase = s_var[1] != 0;
@@ -184,8 +191,13 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     for (int n = tid; n < size; n += kQtThreads) {
       cc[n] = make_int4(0, 0, 0, 0);
       int mx, my;
-      halves(nodeA[n], &mx, &my);
+      halves(nA[n], &mx, &my);
       s_mid[n] = make_int2(mx, my);
+    }
+    if (tid == 0) {
+      s_var[2] = 0;  // nodes split this round
+      s_var[4] = 0;  // split children that hold > 1 key
+      s_var[5] = 0;  // T: list positions taken by the children block
     }
     __syncthreads();
     for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {  // four keys in flight per thread
@@ -200,7 +212,7 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int2 m = s_mid[n[u]];
-        q[u] = (k0 + u * kQtThreads < K && nkA[n[u]] > 1)
+        q[u] = (k0 + u * kQtThreads < K && kA[n[u]] > 1)
                    ? (key_x(kk[u]) >= m.x ? 1 : 0) + (key_y(kk[u]) >= m.y ? 2 : 0)
                    : -1;
       }
@@ -210,34 +222,71 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     }
     __syncthreads();
     ph(0);
-    // processing order and cut-off: split while the list size is < N
+    // After the order step every node has rank[n] (processing rank of a split
+    // node, -1 if kept); the table step writes the next list and leaves in
+    // tB[n] the new position of a kept node and in cc[n] those of a split
+    // node's children. Children block: rank j lands at T - (E_j + C_j), E_j =
+    // children of the ranks before j (last split first).
     if (!sorted_phase) {
-      for (int n = tid; n < size; n += kQtThreads) {
-        const bool cand = nkA[n] > 1;
-        tA[n] = cand ? nonempty(cc[n]) - 1 : 0;
-        tB[n] = cand ? 1 : 0;
-      }
+      // breadth round: candidates = nodes with > 1 key in list order; one
+      // packed scan gives per node C = candidates before it (low half) and
+      // E' = sum of (children - 1) over them (high half). The split nodes are
+      // the candidates with size + E' < N, a prefix of them, so for split node
+      // n: rank = C, E_rank = E' + C; for a kept node: position T + n - min(C, m).
+      for (int n = tid; n < size; n += kQtThreads)
+        tA[n] = kA[n] > 1 ? ((nonempty(cc[n]) - 1) << 16) | 1 : 0;
       __syncthreads();
       block_scan_excl<kQtThreads>(tA, size, s_tmp);
-      block_scan_excl<kQtThreads>(tB, size, s_tmp);
-      if (tid == 0) s_var[2] = 0;
-      __syncthreads();
       for (int n = tid; n < size; n += kQtThreads) {
-        if (nkA[n] > 1 && size + tA[n] < N) {
-          rank[n] = tB[n];
-          ord[tB[n]] = n;
+        const int v = tA[n], E = v >> 16, C = v & 0xFFFF;
+        if (kA[n] > 1 && size + E < N) {
+          rank[n] = C;
           atomicAdd(&s_var[2], 1);
+          atomicMax(&s_var[5], E + C + nonempty(cc[n]));
         } else {
           rank[n] = -1;
+        }
+      }
+      __syncthreads();
+      ph(1);
+      const int m = s_var[2], T = s_var[5];
+      for (int n = tid; n < size; n += kQtThreads) {
+        const int j = rank[n], v = tA[n];
+        if (j < 0) {
+          const int pos = T + n - min(v & 0xFFFF, m);
+          nB[pos] = nA[n];
+          kB[pos] = kA[n];
+          qB[pos] = qA[n];
+          tB[n] = pos;
+        } else {
+          const int4 c = cc[n];
+          const int cnts[4] = {c.x, c.y, c.z, c.w};
+          const int base = T - ((v >> 16) + (v & 0xFFFF) + nonempty(c));
+          int pos4[4];
+          int after = 0, expand = 0;
+#pragma unroll
+          for (int q = 3; q >= 0; --q) {
+            if (cnts[q] > 0) {
+              pos4[q] = base + after++;
+              nB[pos4[q]] = child_box(nA[n], q);
+              kB[pos4[q]] = cnts[q];
+              qB[pos4[q]] = j * 4 + q;  // creation order: split rank, then n1..n4
+              expand += cnts[q] > 1;
+            } else {
+              pos4[q] = -1;
+            }
+          }
+          cc[n] = make_int4(pos4[0], pos4[1], pos4[2], pos4[3]);
+          if (expand) atomicAdd(&s_var[4], expand);
         }
       }
     } else {
       // descending order of the candidates by (size, creation): each candidate
       // counts the larger keys (keys are distinct), no sorting network
-      unsigned long long* s_key = (unsigned long long*)nodeB;  // free until the table phase
+      unsigned long long* s_key = (unsigned long long*)nB;  // free until the table step
       for (int i = tid; i < size; i += kQtThreads) {
-        s_key[i] = nkA[i] > 1
-                       ? ((unsigned long long)nkA[i] << 40) | ((unsigned long long)seqA[i] << 16) | (unsigned long long)i
+        s_key[i] = kA[i] > 1
+                       ? ((unsigned long long)kA[i] << 40) | ((unsigned long long)qA[i] << 16) | (unsigned long long)i
                        : 0ull;
         s_sort[i] = 0;
         rank[i] = -1;
@@ -268,8 +317,6 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
       __syncthreads();
       const int ncand = s_var[3];
       block_scan_excl<kQtThreads>(tA, ncand, s_tmp);
-      if (tid == 0) s_var[2] = 0;
-      __syncthreads();
       for (int j = tid; j < ncand; j += kQtThreads) {
         if (size + tA[j] < N) {
           const int n = (int)(s_sort[j] & 0xFFFF);
@@ -278,52 +325,51 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
           atomicAdd(&s_var[2], 1);
         }
       }
-    }
-    __syncthreads();
-    ph(sorted_phase ? 4 : 1);
-    const int m = s_var[2];  // nodes split this round
-    // children block: processing rank j lands at T - (E_j + C_j) (last split first)
-    for (int j = tid; j < m; j += kQtThreads) tA[j] = nonempty(cc[ord[j]]);
-    __syncthreads();
-    const int T = block_scan_excl<kQtThreads>(tA, m, s_tmp);
-    for (int n = tid; n < size; n += kQtThreads) tB[n] = rank[n] < 0 ? 1 : 0;
-    __syncthreads();
-    const int nKept = block_scan_excl<kQtThreads>(tB, size, s_tmp);
-    const int newSize = T + nKept;
-    if (tid == 0) s_var[4] = 0;
-    __syncthreads();
-    // new node table; cc[n] becomes the list positions of split node n's children
-    for (int n = tid; n < size; n += kQtThreads) {
-      const int j = rank[n];
-      if (j < 0) {
-        const int pos = T + tB[n];
-        nodeB[pos] = nodeA[n];
-        nkB[pos] = nkA[n];
-        seqB[pos] = seqA[n];
-      } else {
-        const int4 c = cc[n];
-        const int cnts[4] = {c.x, c.y, c.z, c.w};
-        const int base = T - (tA[j] + nonempty(c));
-        int pos4[4];
-        int after = 0, expand = 0;
+      __syncthreads();
+      ph(4);
+      const int m = s_var[2];
+      for (int j = tid; j < m; j += kQtThreads) tA[j] = nonempty(cc[ord[j]]);
+      __syncthreads();
+      const int T = block_scan_excl<kQtThreads>(tA, m, s_tmp);
+      for (int n = tid; n < size; n += kQtThreads) tB[n] = rank[n] < 0 ? 1 : 0;
+      __syncthreads();
+      block_scan_excl<kQtThreads>(tB, size, s_tmp);
+      if (tid == 0) s_var[5] = T;
+      for (int n = tid; n < size; n += kQtThreads) {
+        const int j = rank[n];
+        if (j < 0) {
+          const int pos = T + tB[n];
+          nB[pos] = nA[n];
+          kB[pos] = kA[n];
+          qB[pos] = qA[n];
+          tB[n] = pos;
+        } else {
+          const int4 c = cc[n];
+          const int cnts[4] = {c.x, c.y, c.z, c.w};
+          const int base = T - (tA[j] + nonempty(c));
+          int pos4[4];
+          int after = 0, expand = 0;
 #pragma unroll
-        for (int q = 3; q >= 0; --q) {
-          if (cnts[q] > 0) {
-            pos4[q] = base + after++;
-            nodeB[pos4[q]] = child_box(nodeA[n], q);
-            nkB[pos4[q]] = cnts[q];
-            seqB[pos4[q]] = j * 4 + q;  // creation order: split rank, then n1..n4
-            expand += cnts[q] > 1;
-          } else {
-            pos4[q] = -1;
+          for (int q = 3; q >= 0; --q) {
+            if (cnts[q] > 0) {
+              pos4[q] = base + after++;
+              nB[pos4[q]] = child_box(nA[n], q);
+              kB[pos4[q]] = cnts[q];
+              qB[pos4[q]] = j * 4 + q;
+              expand += cnts[q] > 1;
+            } else {
+              pos4[q] = -1;
+            }
           }
+          cc[n] = make_int4(pos4[0], pos4[1], pos4[2], pos4[3]);
+          if (expand) atomicAdd(&s_var[4], expand);
         }
-        cc[n] = make_int4(pos4[0], pos4[1], pos4[2], pos4[3]);
-        if (expand) atomicAdd(&s_var[4], expand);
       }
     }
     __syncthreads();
     ph(2);
+    const int m = s_var[2], T = s_var[5];
+    const int newSize = T + (size - m);
     // re-home the keys
     for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {  // four keys in flight per thread
       int n[4], j[4], nn[4];
@@ -339,10 +385,10 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (j[u] < 0) {
-          nn[u] = T + tB[n[u]];
+          nn[u] = tB[n[u]];
         } else {
-          const int2 m = s_mid[n[u]];
-          nn[u] = ((const int*)&cc[n[u]])[(key_x(kk[u]) >= m.x ? 1 : 0) + (key_y(kk[u]) >= m.y ? 2 : 0)];
+          const int2 mm = s_mid[n[u]];
+          nn[u] = ((const int*)&cc[n[u]])[(key_x(kk[u]) >= mm.x ? 1 : 0) + (key_y(kk[u]) >= mm.y ? 2 : 0)];
         }
       }
 #pragma unroll
@@ -350,12 +396,6 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
         const int k = k0 + u * kQtThreads;
         if (k < K) knode[k] = (uint16_t)nn[u];
       }
-    }
-    __syncthreads();
-    for (int n = tid; n < newSize; n += kQtThreads) {
-      nodeA[n] = nodeB[n];
-      nkA[n] = nkB[n];
-      seqA[n] = seqB[n];
     }
     // finish when the list reached N or a round changed nothing (src/ORBextractor.cc:1011, 1093);
     // the breadth phase ends once one more full round would overshoot N (:1015)
@@ -365,6 +405,11 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     if (tid == 0) {
       if (!finish && !sorted_phase && newSize + 3 * nExp > N) s_var[1] = 1;
       s_var[0] = newSize;
+    }
+    {  // the next list becomes this one
+      QNode* t0 = nA; nA = nB; nB = t0;
+      int* t1 = kA; kA = kB; kB = t1;
+      int* t2 = qA; qA = qB; qB = t2;
     }
     __syncthreads();
     ph(3);
