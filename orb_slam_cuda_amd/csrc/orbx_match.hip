@@ -44,8 +44,11 @@ __device__ __forceinline__ int hamming256(const uint4& a0, const uint4& a1, cons
 
 // ------------------------------------------------------------ dense top-2
 constexpr int kTopQueries = 256;  // queries per workgroup, two per lane
-constexpr int kTopSplit = 8;      // candidate ranges per query (two waves each)
-constexpr int kTopThreads = 1024;
+#ifndef ORBX_TOP_SPLIT
+#define ORBX_TOP_SPLIT 8
+#endif
+constexpr int kTopSplit = ORBX_TOP_SPLIT;  // candidate ranges per query (two waves each)
+constexpr int kTopThreads = 128 * kTopSplit;
 constexpr int kTopChunk = kTopThreads / (2 * kTopSplit);  // candidates per range per staged chunk (64)
 // popcount(x) + acc as ONE v_bcnt_u32_b32 (the compiler otherwise splits the
 // chain into bcnt(x, 0) and v_add3)
