@@ -171,6 +171,177 @@ __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t
   second[o] = (int)(r.y >> 16);
 }
 
+// ------------------------------------------------ dense top-2 on the matrix cores
+// The all-pairs distance matrix is a GEMM: with bits mapped to +-1, the dot
+// product of two descriptors is 256 - 2 * Hamming. The kernel runs it on the
+// block-scaled FP4 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 operands:
+// 0x2 = +1.0, 0xA = -1.0; 4x the BF16 rate), K = 256 bits in four MFMAs.
+//   candidates (A, rows):  bit set -> -1, clear -> +1, block scale 2^14
+//   queries    (B, cols):  bit set -> +1, clear -> -1, block scale 2^0
+// so A.B = 2^14 * (2h - 256), and with the accumulator seeded with
+// 2^22 + (candidate index within a 32768 block) every result IS the sort key
+// 32768 * h + index, an integer below 2^24, exact in f32 whatever the
+// accumulation order. Per (candidate, query) value the lane then does one
+// v_min_f32 + one v_med3_f32 (the best / second update of Top2Acc). The bit
+// order inside K is free as long as A and B use the same one (dot products
+// are order-independent): word w of a descriptor goes to the 16-byte
+// fragment of MFMA step w >> 1, lane half w & 1, bit 4n + m to nibble n of
+// dword m.
+// C/D layout (gfx950, 32x32): lane l holds column l & 31 (the query) and
+// rows (r & 3) + 8 (r >> 2) + 4 (l >> 5), r = 0..15 (the candidates).
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+constexpr int kMqTiles = 2;                  // 32-query tiles per wave
+constexpr int kMWaves = 4;                   // query waves per candidate half
+constexpr int kMHalves = 2;                  // candidate halves per workgroup
+constexpr int kMQueries = 32 * kMqTiles * kMWaves;  // 256 queries per workgroup
+constexpr int kMChunk = 128;                 // candidates per staged chunk per half (4 tiles, 16 KB)
+constexpr int kMThreads = 64 * kMWaves * kMHalves;
+constexpr int kMBlock = 32768;               // candidate indices per float-key block
+constexpr float kMNone = 3.0e38f;            // float key of "no candidate"
+
+// 32 descriptor bits -> 32 e2m1 nibbles (bit 4n + m -> nibble n of dword m)
+__device__ __forceinline__ i32x4_t fp4_expand(uint32_t w) {
+  i32x4_t o;
+  o[0] = (int)(((w << 3) & 0x88888888u) | 0x22222222u);
+  o[1] = (int)(((w << 2) & 0x88888888u) | 0x22222222u);
+  o[2] = (int)(((w << 1) & 0x88888888u) | 0x22222222u);
+  o[3] = (int)((w & 0x88888888u) | 0x22222222u);
+  return o;
+}
+__device__ __forceinline__ uint32_t top2_ukey(float k, int base) {
+  if (!(k < 1.0e30f)) return kTopNone;
+  const int v = (int)k;
+  return ((uint32_t)(v >> 15) << 16) | (uint32_t)((v & (kMBlock - 1)) + base);
+}
+__device__ __forceinline__ void top2_merge(uint32_t& u1, uint32_t& u2, uint32_t x1, uint32_t x2) {
+  u2 = min(min(max(u1, x1), u2), x2);
+  u1 = min(u1, x1);
+}
+
+__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(4))) void hamming_top2_mfma_kernel(
+    const uint8_t* __restrict__ A, long long a_pitch, const int* __restrict__ nA, int a_cap,
+    const uint8_t* __restrict__ B, long long b_pitch, const int* __restrict__ nB, int* __restrict__ best_idx,
+    int* __restrict__ best, int* __restrict__ second) {
+  __shared__ __attribute__((aligned(16))) i32x4_t sC[kMHalves][kMChunk / 32][4][64];  // [half][tile][step][lane]
+  __shared__ uint2 part[kMQueries];
+  const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int hf = tid / (64 * kMWaves), wv = (tid >> 6) % kMWaves, ht = tid % (64 * kMWaves);
+  const int base = blockIdx.x * kMQueries;
+  const int na = nA[p], nb = min(nB[p], 65535);  // final keys hold the index in 16 bits
+  if (base >= na) return;
+  // queries (the B operand), this wave's kMqTiles tiles, held for the whole kernel
+  const uint4* Ap = (const uint4*)(A + p * a_pitch);
+  const uint4* Bp = (const uint4*)(B + p * b_pitch);
+  const int hl = lane >> 5;
+  i32x4_t qf[kMqTiles][4];
+#pragma unroll
+  for (int q = 0; q < kMqTiles; ++q) {
+    const int qi = min(base + wv * 32 * kMqTiles + q * 32 + (lane & 31), na - 1);
+    const uint4 d0 = Ap[2 * qi], d1 = Ap[2 * qi + 1];
+    const uint32_t w[4] = {hl ? d0.y : d0.x, hl ? d0.w : d0.z, hl ? d1.y : d1.x, hl ? d1.w : d1.z};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[q][s] = fp4_expand(~w[s]);
+  }
+  // candidate rows of this lane in a tile, as float key offsets
+  float rk0[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) rk0[r] = 4194304.0f + (float)((r & 3) + 8 * (r >> 2) + 4 * hl);
+  float k1[kMqTiles], k2[kMqTiles];
+  uint32_t u1[kMqTiles], u2[kMqTiles];
+#pragma unroll
+  for (int q = 0; q < kMqTiles; ++q) {
+    k1[q] = k2[q] = kMNone;
+    u1[q] = u2[q] = kTopNone;
+  }
+  const int per = (nb + kMHalves - 1) / kMHalves;
+  const int jb = min(hf * per, nb), je = min(jb + per, nb);  // this half's candidates
+  const int nchunks = (per + kMChunk - 1) / kMChunk;         // the same for both halves (barriers)
+  int blk = jb;                                              // first index of the current key block
+  const int sr = ht >> 1, spart = ht & 1;                    // staging role: row, 16-byte half
+  for (int c = 0; c < nchunks; ++c) {
+    const int c0 = jb + c * kMChunk;
+    __syncthreads();
+    if (c0 < je) {
+      const uint4 d = Bp[2 * min(c0 + sr, je - 1) + spart];
+      const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int wi = 4 * spart + i;
+        sC[hf][sr >> 5][wi >> 1][(sr & 31) + 32 * (wi & 1)] = fp4_expand(w[i]);
+      }
+    }
+    __syncthreads();
+    if (c0 >= je) continue;
+    if (c0 - blk >= kMBlock) {  // key block full: fold the float keys into the index keys
+#pragma unroll
+      for (int q = 0; q < kMqTiles; ++q) {
+        top2_merge(u1[q], u2[q], top2_ukey(k1[q], blk), top2_ukey(k2[q], blk));
+        k1[q] = k2[q] = kMNone;
+      }
+      blk = c0;
+    }
+    const int nval = min(kMChunk, je - c0);
+    for (int t = 0; t * 32 < nval; ++t) {
+      i32x8_t af[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const i32x4_t v = sC[hf][t][s][lane];
+        af[s] = (i32x8_t){v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+      }
+      const float rel = (float)(c0 + 32 * t - blk);
+      const int nrow = nval - 32 * t;  // valid rows of this tile
+      f32x16_t rk;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * hl;
+        rk[r] = row < nrow ? rk0[r] + rel : kMNone;
+      }
+#pragma unroll
+      for (int q = 0; q < kMqTiles; ++q) {
+        f32x16_t acc = rk;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const i32x8_t bf = (i32x8_t){qf[q][s][0], qf[q][s][1], qf[q][s][2], qf[q][s][3], 0, 0, 0, 0};
+          acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[s], bf, acc, 4, 4, 0, 141, 0, 127);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          k2[q] = __builtin_amdgcn_fmed3f(acc[r], k1[q], k2[q]);
+          k1[q] = fminf(acc[r], k1[q]);
+        }
+      }
+    }
+  }
+  // fold the last block, then merge the two lane halves (rows 0-3 / 4-7 of each 8)
+#pragma unroll
+  for (int q = 0; q < kMqTiles; ++q) {
+    top2_merge(u1[q], u2[q], top2_ukey(k1[q], blk), top2_ukey(k2[q], blk));
+    const uint32_t o1 = __shfl_xor(u1[q], 32), o2 = __shfl_xor(u2[q], 32);
+    top2_merge(u1[q], u2[q], o1, o2);
+  }
+  const int qloc = wv * 32 * kMqTiles + (lane & 31);
+  if (hf == 1 && lane < 32) {
+#pragma unroll
+    for (int q = 0; q < kMqTiles; ++q) part[qloc + 32 * q] = make_uint2(u1[q], u2[q]);
+  }
+  __syncthreads();
+  if (hf != 0 || lane >= 32) return;
+#pragma unroll
+  for (int q = 0; q < kMqTiles; ++q) {
+    const int qi = base + qloc + 32 * q;
+    if (qi >= na) continue;
+    const uint2 o = part[qloc + 32 * q];
+    top2_merge(u1[q], u2[q], o.x, o.y);
+    const long long oi = (long long)p * a_cap + qi;
+    const int d1 = (int)(u1[q] >> 16);
+    best_idx[oi] = d1 < 256 ? (int)(u1[q] & 0xFFFFu) : -1;
+    best[oi] = d1;
+    second[oi] = (int)(u2[q] >> 16);
+  }
+}
+
 // ------------------------------------------------------------ wave helpers
 __device__ __forceinline__ int wave_min(int v) { return wave_min_dpp(v); }
 __device__ __forceinline__ int wave_sum_i(int v) { return wave_sum_dpp(v); }
@@ -342,6 +513,14 @@ __global__ __launch_bounds__(256) void search_bow_kernel(
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap, const uint8_t* B,
                         size_t b_pitch, const int* nB, int pairs, int* best_idx, int* best, int* second,
                         void* stream) {
+  // ORBX_TOP2_VALU=1 selects the VALU kernel (A/B timing and cross-checks only)
+  static const bool valu = getenv("ORBX_TOP2_VALU") && getenv("ORBX_TOP2_VALU")[0] == '1';
+  if (!valu) {
+    dim3 grid((a_cap + kMQueries - 1) / kMQueries, pairs);
+    hipLaunchKernelGGL(hamming_top2_mfma_kernel, grid, dim3(kMThreads), 0, (hipStream_t)stream, A, (long long)a_pitch,
+                       nA, a_cap, B, (long long)b_pitch, nB, best_idx, best, second);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+  }
   dim3 grid((a_cap + kTopQueries - 1) / kTopQueries, pairs);
   hipLaunchKernelGGL(hamming_top2_kernel, grid, dim3(kTopThreads), 0, (hipStream_t)stream, A, (long long)a_pitch, nA, a_cap,
                      B, (long long)b_pitch, nB, best_idx, best, second);

@@ -146,6 +146,45 @@ def test_hamming_top2_parity(pkg, O):
         assert np.array_equal(sd[p, :len(a)], rs)
 
 
+@pytest.mark.parametrize("na,nb,dups", [(300, 40000, 0), (517, 3001, 1), (64, 33, 1), (2, 32769, 1)])
+def test_hamming_top2_blocks_and_ties(pkg, O, na, nb, dups):
+    """Candidate counts past one 32768-index key block of the MFMA kernel, ragged
+    tiles, and exact ties (duplicated candidate rows: the earlier index must win
+    and the second distance equals the best); also distance-256 complements."""
+    import ctypes as C
+
+    from orb_slam_cuda_amd import _lib
+    rng = np.random.default_rng(na * 7 + nb)
+    A = rng.integers(0, 256, (na, 32), dtype=np.uint8)
+    B = rng.integers(0, 256, (nb, 32), dtype=np.uint8)
+    if dups:
+        # near copies of the queries, each twice at scattered positions, plus exact complements
+        for i in range(min(na, nb // 4)):
+            a = A[i].copy()
+            a[i % 32] ^= np.uint8(1 << (i % 8)) if i % 3 else np.uint8(0)
+            B[rng.integers(0, nb)] = a
+            B[rng.integers(0, nb)] = a
+            B[rng.integers(0, nb)] = ~A[i]
+    cap_a, cap_b = na, nb
+    dA, dB = _lib.DeviceArray(A.nbytes), _lib.DeviceArray(B.nbytes)
+    dA.upload(A)
+    dB.upload(B)
+    dnA, dnB = _lib.DeviceArray(4), _lib.DeviceArray(4)
+    dnA.upload(np.array([na], np.int32))
+    dnB.upload(np.array([nb], np.int32))
+    outs = [_lib.DeviceArray(cap_a * 4) for _ in range(3)]
+    m = pkg.ORBmatcher(0.9, True, max_pairs=1, max_kps=max(cap_a, cap_b))
+    L = _lib.lib()
+    _lib.check(L.orbm_hamming_top2(m.handle, C.c_void_p(dA.ptr), cap_a * 32, C.c_void_p(dnA.ptr), cap_a,
+                                   C.c_void_p(dB.ptr), cap_b * 32, C.c_void_p(dnB.ptr), 1,
+                                   *(C.c_void_p(o.ptr) for o in outs), None), matcher=True)
+    L.orbx_stream_synchronize(None)
+    bi, bd, sd = (o.download(cap_a, np.int32) for o in outs)
+    ri, rd, rs = O.hamming_top2(A, B)
+    assert np.array_equal(bd, rd) and np.array_equal(sd, rs)
+    assert np.array_equal(bi, ri)
+
+
 def _featvec(rng, n, nodes):
     node = rng.integers(0, nodes, size=n)
     ids = sorted(set(int(v) * 13 + 1 for v in node))
