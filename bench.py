@@ -41,15 +41,16 @@ sys.path.insert(0, ROOT)
 
 METRIC = "frames/s ORB extract+match, 1241×376 mono nFeatures=2000; achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
-# VALU lane-op peak: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (the 157.3 TFLOPS FP32-vector spec / 2);
-# the v_xor_b32 + v_bcnt_u32_b32 mix issues at about half of it (tools/valu_microbench.hip: 0.58 T
-# wave-instructions/s = 37 T lane-ops/s)
+# Dense FP4 MFMA peak (the Hamming top-2 runs on v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1
+# operands): 65536 MACs per 32 cycles per SIMD x 1024 SIMDs x 2.4 GHz = 10.07 PFLOP/s
+# (MI355X_MICROARCH.md: FP4 = 4x the BF16 rate, dense, no sparsity)
+MFMA_FP4_PEAK_TFLOPS = 10066.3
+# VALU lane-op peak: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (the top-2 update costs 2 lane-ops per pair)
 VALU_PEAK_TOPS = 78.6
-VALU_MIX_TOPS = 37.1
 STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_top2", "search_init"]
 KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
-           "hamming_top2": "hamming_top2_kernel", "search_init": "search_init_kernel"}
+           "hamming_top2": "hamming_top2_mfma_kernel", "search_init": "search_init_kernel"}
 
 CONFIGS = {
     "kitti": dict(W=1241, H=376, nfeatures=2000,
@@ -302,17 +303,19 @@ def main():
             "algorithmic_bytes_per_launch": int(hbm_stages[rk] * BS),
             "avg_launch_ms": round(st[rk], 4)}
 
-    # the dense matcher is bound by VALU issue, not HBM (SURVEY.md §8(d) "Roofline (match)"):
-    # algorithmic work = 16 lane-ops per (query, candidate) pair (8 x 32-bit XOR + 8 popcounts)
+    # the dense matcher runs on the matrix cores: algorithmic work = one 256-element +-1 dot
+    # product per (query, candidate) pair = 512 FLOP, against the dense FP4 MFMA peak; the
+    # per-pair top-2 update (v_min + v_med3) is reported against the VALU lane-op peak
     match_roof = None
     if not args.no_match and st["hamming_top2"] > 0:
         cnt = d_counts[(total_steps - 1) % NS].download(B + 1, np.int32).astype(np.int64)
         pairs = int((cnt[1:] * cnt[:-1]).sum())
-        ops = 16.0 * pairs / (st["hamming_top2"] * 1e-3) / 1e12
-        match_roof = {"kernel": KERNELS["hamming_top2"], "bound": "valu", "unit": "Tops/s",
-                      "achieved": round(ops, 2), "peak": VALU_PEAK_TOPS, "frac": round(ops / VALU_PEAK_TOPS, 4),
-                      "peak_xor_bcnt_mix": VALU_MIX_TOPS, "frac_of_mix": round(ops / VALU_MIX_TOPS, 4),
-                      "pairs_per_launch": pairs, "pairs_per_s": round(pairs / (st["hamming_top2"] * 1e-3), 1),
+        sec = st["hamming_top2"] * 1e-3
+        tf = 512.0 * pairs / sec / 1e12
+        match_roof = {"kernel": KERNELS["hamming_top2"], "bound": "mfma", "unit": "TFLOP/s",
+                      "achieved": round(tf, 1), "peak": MFMA_FP4_PEAK_TFLOPS, "frac": round(tf / MFMA_FP4_PEAK_TFLOPS, 4),
+                      "dtype": "fp4 e2m1 (+-1 bits, exact)", "top2_valu_frac": round(2.0 * pairs / sec / 1e12 / VALU_PEAK_TOPS, 4),
+                      "pairs_per_launch": pairs, "pairs_per_s": round(pairs / sec, 1),
                       "avg_launch_ms": round(st["hamming_top2"], 4)}
 
     cpu = cpu1 = None

@@ -179,8 +179,8 @@ __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t
 //   candidates (A, rows):  bit set -> -1, clear -> +1, block scale 2^14
 //   queries    (B, cols):  bit set -> +1, clear -> -1, block scale 2^0
 // so A.B = 2^14 * (2h - 256), and with the accumulator seeded with
-// 2^22 + (candidate index within a 32768 block) every result IS the sort key
-// 32768 * h + index, an integer below 2^24, exact in f32 whatever the
+// 2^22 + 1 + (candidate index within a 32768 block) every result IS the sort
+// key 32768 * h + index + 1, an integer in [1, 2^24), exact in f32 whatever the
 // accumulation order. Per (candidate, query) value the lane then does one
 // v_min_f32 + one v_med3_f32 (the best / second update of Top2Acc). The bit
 // order inside K is free as long as A and B use the same one (dot products
@@ -192,11 +192,28 @@ __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
-constexpr int kMqTiles = 2;                  // 32-query tiles per wave
-constexpr int kMWaves = 4;                   // query waves per candidate half
-constexpr int kMHalves = 2;                  // candidate halves per workgroup
+#ifndef ORBX_M_QT
+#define ORBX_M_QT 4
+#endif
+#ifndef ORBX_M_WPE
+#define ORBX_M_WPE 2
+#endif
+#ifndef ORBX_M_CHUNK
+#define ORBX_M_CHUNK 128
+#endif
+constexpr int kMqTiles = ORBX_M_QT;          // 32-query tiles per wave
+#ifndef ORBX_M_WAVES
+#define ORBX_M_WAVES 2
+#endif
+#ifndef ORBX_M_HALVES
+#define ORBX_M_HALVES 2
+#endif
+constexpr int kMWaves = ORBX_M_WAVES;        // query waves per candidate range
+constexpr int kMHalves = ORBX_M_HALVES;      // candidate ranges per workgroup
 constexpr int kMQueries = 32 * kMqTiles * kMWaves;  // 256 queries per workgroup
-constexpr int kMChunk = 128;                 // candidates per staged chunk per half (4 tiles, 16 KB)
+constexpr int kMChunk = ORBX_M_CHUNK;        // candidates per staged chunk per half (a multiple of 128)
+constexpr int kMRowsPerPass = 32 * kMWaves;  // staged rows per pass (two threads per row)
+static_assert(kMChunk % kMRowsPerPass == 0, "a chunk is whole staging passes");
 constexpr int kMThreads = 64 * kMWaves * kMHalves;
 constexpr int kMBlock = 32768;               // candidate indices per float-key block
 constexpr float kMNone = 3.0e38f;            // float key of "no candidate"
@@ -210,9 +227,10 @@ __device__ __forceinline__ i32x4_t fp4_expand(uint32_t w) {
   o[3] = (int)((w & 0x88888888u) | 0x22222222u);
   return o;
 }
-__device__ __forceinline__ uint32_t top2_ukey(float k, int base) {
+__device__ __forceinline__ uint32_t top2_ukey(uint32_t kb, int base) {
+  const float k = __builtin_bit_cast(float, kb);
   if (!(k < 1.0e30f)) return kTopNone;
-  const int v = (int)k;
+  const int v = (int)k - 1;
   return ((uint32_t)(v >> 15) << 16) | (uint32_t)((v & (kMBlock - 1)) + base);
 }
 __device__ __forceinline__ void top2_merge(uint32_t& u1, uint32_t& u2, uint32_t x1, uint32_t x2) {
@@ -220,12 +238,12 @@ __device__ __forceinline__ void top2_merge(uint32_t& u1, uint32_t& u2, uint32_t 
   u1 = min(u1, x1);
 }
 
-__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(4))) void hamming_top2_mfma_kernel(
+__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(ORBX_M_WPE))) void hamming_top2_mfma_kernel(
     const uint8_t* __restrict__ A, long long a_pitch, const int* __restrict__ nA, int a_cap,
     const uint8_t* __restrict__ B, long long b_pitch, const int* __restrict__ nB, int* __restrict__ best_idx,
     int* __restrict__ best, int* __restrict__ second) {
-  __shared__ __attribute__((aligned(16))) i32x4_t sC[kMHalves][kMChunk / 32][4][64];  // [half][tile][step][lane]
-  __shared__ uint2 part[kMQueries];
+  __shared__ __attribute__((aligned(16))) i32x4_t sC[2][kMHalves][kMChunk / 32][4][64];  // [buffer][half][tile][step][lane]
+  __shared__ uint2 part[kMHalves > 1 ? kMHalves - 1 : 1][kMQueries];
   const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int hf = tid / (64 * kMWaves), wv = (tid >> 6) % kMWaves, ht = tid % (64 * kMWaves);
   const int base = blockIdx.x * kMQueries;
@@ -244,15 +262,21 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[q][s] = fp4_expand(~w[s]);
   }
-  // candidate rows of this lane in a tile, as float key offsets
-  float rk0[16];
+  // running row keys: 2^22 + 1 + (index of this lane's row r in the next tile - blk);
+  // the + 1 keeps every key >= 1, so no result is a signed zero (whose bit
+  // pattern would order last)
+  f32x16_t rk;
+  auto rk_reset = [&]() {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) rk0[r] = 4194304.0f + (float)((r & 3) + 8 * (r >> 2) + 4 * hl);
-  float k1[kMqTiles], k2[kMqTiles];
+    for (int r = 0; r < 16; ++r) rk[r] = 4194305.0f + (float)((r & 3) + 8 * (r >> 2) + 4 * hl);
+  };
+  rk_reset();
+  uint32_t k1[kMqTiles], k2[kMqTiles];  // float keys as bit patterns
   uint32_t u1[kMqTiles], u2[kMqTiles];
+  const uint32_t kNoneBits = __builtin_bit_cast(uint32_t, kMNone);
 #pragma unroll
   for (int q = 0; q < kMqTiles; ++q) {
-    k1[q] = k2[q] = kMNone;
+    k1[q] = k2[q] = kNoneBits;
     u1[q] = u2[q] = kTopNone;
   }
   const int per = (nb + kMHalves - 1) / kMHalves;
@@ -260,16 +284,61 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   const int nchunks = (per + kMChunk - 1) / kMChunk;         // the same for both halves (barriers)
   int blk = jb;                                              // first index of the current key block
   const int sr = ht >> 1, spart = ht & 1;                    // staging role: row, 16-byte half
-  for (int c = 0; c < nchunks; ++c) {
-    const int c0 = jb + c * kMChunk;
-    __syncthreads();
-    if (c0 < je) {
-      const uint4 d = Bp[2 * min(c0 + sr, je - 1) + spart];
-      const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+  // double-buffered staging: chunk c+1's global load is in flight while chunk
+  // c is computed; one barrier per chunk (a wave writing buffer c & 1 has
+  // passed the barrier every wave reaches only after computing chunk c - 2)
+  constexpr int kRep = kMChunk / kMRowsPerPass;  // staged rows per thread per chunk
+  uint4 pre[kRep];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int wi = 4 * spart + i;
-        sC[hf][sr >> 5][wi >> 1][(sr & 31) + 32 * (wi & 1)] = fp4_expand(w[i]);
+  for (int i = 0; i < kRep; ++i) pre[i] = jb < je ? Bp[2 * min(jb + sr + kMRowsPerPass * i, je - 1) + spart] : make_uint4(0, 0, 0, 0);
+  auto top2_tile = [&](const i32x8_t (&af)[4], const f32x16_t& rkt) {
+#pragma unroll
+    for (int q = 0; q < kMqTiles; ++q) {
+      f32x16_t acc = rkt;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const i32x8_t bf = (i32x8_t){qf[q][s][0], qf[q][s][1], qf[q][s][2], qf[q][s][3], 0, 0, 0, 0};
+#if defined(ORBX_M_NOMFMA)  // timing experiment only: the top-2 update without MFMA
+        acc[s] += __builtin_bit_cast(float, af[s][0] ^ bf[0]);
+#else
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[s], bf, acc, 4, 4, 0, 141, 0, 127);
+#endif
+      }
+#if defined(ORBX_M_NOTOP2)  // timing experiment only: MFMA without the top-2 update
+      const float x0 = acc[0];
+      k1[q] = min(__float_as_uint(x0), k1[q]);
+#else
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        // positive floats order as their bit patterns: the best key is an
+        // integer v_min_u32 and the second a v_med3_f32 (the target builtin);
+        // fminf would first canonicalise every MFMA result with a v_max_f32.
+        // (__float_as_uint of a float copy: ROCm 7.2 clang lowers
+        // __builtin_bit_cast(uint32_t, acc[r]) of an ext_vector element to a
+        // read of element 0)
+        const float xf = acc[r];
+        k2[q] = __float_as_uint(__builtin_amdgcn_fmed3f(xf, __uint_as_float(k1[q]), __uint_as_float(k2[q])));
+        k1[q] = min(__float_as_uint(xf), k1[q]);
+      }
+#endif
+    }
+  };
+  for (int c = 0; c < nchunks; ++c) {
+    const int c0 = jb + c * kMChunk, buf = c & 1;
+    if (c0 < je) {
+#pragma unroll
+      for (int k = 0; k < kRep; ++k) {
+        const int row = sr + kMRowsPerPass * k;
+        const uint32_t w[4] = {pre[k].x, pre[k].y, pre[k].z, pre[k].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int wi = 4 * spart + i;
+          sC[buf][hf][row >> 5][wi >> 1][(row & 31) + 32 * (wi & 1)] = fp4_expand(w[i]);
+        }
+      }
+      if (c0 + kMChunk < je) {
+#pragma unroll
+        for (int k = 0; k < kRep; ++k) pre[k] = Bp[2 * min(c0 + kMChunk + sr + kMRowsPerPass * k, je - 1) + spart];
       }
     }
     __syncthreads();
@@ -278,40 +347,29 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
       for (int q = 0; q < kMqTiles; ++q) {
         top2_merge(u1[q], u2[q], top2_ukey(k1[q], blk), top2_ukey(k2[q], blk));
-        k1[q] = k2[q] = kMNone;
+        k1[q] = k2[q] = kNoneBits;
       }
       blk = c0;
+      rk_reset();
     }
     const int nval = min(kMChunk, je - c0);
     for (int t = 0; t * 32 < nval; ++t) {
       i32x8_t af[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const i32x4_t v = sC[hf][t][s][lane];
+        const i32x4_t v = sC[buf][hf][t][s][lane];
         af[s] = (i32x8_t){v[0], v[1], v[2], v[3], 0, 0, 0, 0};
       }
-      const float rel = (float)(c0 + 32 * t - blk);
       const int nrow = nval - 32 * t;  // valid rows of this tile
-      f32x16_t rk;
+      if (nrow >= 32) {
+        top2_tile(af, rk);
+      } else {  // ragged last tile: rows past the end never win
+        f32x16_t rkt;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * hl;
-        rk[r] = row < nrow ? rk0[r] + rel : kMNone;
+        for (int r = 0; r < 16; ++r) rkt[r] = (r & 3) + 8 * (r >> 2) + 4 * hl < nrow ? rk[r] : kMNone;
+        top2_tile(af, rkt);
       }
-#pragma unroll
-      for (int q = 0; q < kMqTiles; ++q) {
-        f32x16_t acc = rk;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const i32x8_t bf = (i32x8_t){qf[q][s][0], qf[q][s][1], qf[q][s][2], qf[q][s][3], 0, 0, 0, 0};
-          acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[s], bf, acc, 4, 4, 0, 141, 0, 127);
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          k2[q] = __builtin_amdgcn_fmed3f(acc[r], k1[q], k2[q]);
-          k1[q] = fminf(acc[r], k1[q]);
-        }
-      }
+      rk += 32.0f;
     }
   }
   // fold the last block, then merge the two lane halves (rows 0-3 / 4-7 of each 8)
@@ -322,18 +380,20 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     top2_merge(u1[q], u2[q], o1, o2);
   }
   const int qloc = wv * 32 * kMqTiles + (lane & 31);
-  if (hf == 1 && lane < 32) {
+  if (hf >= 1 && lane < 32) {
 #pragma unroll
-    for (int q = 0; q < kMqTiles; ++q) part[qloc + 32 * q] = make_uint2(u1[q], u2[q]);
+    for (int q = 0; q < kMqTiles; ++q) part[hf - 1][qloc + 32 * q] = make_uint2(u1[q], u2[q]);
   }
-  __syncthreads();
+  if (kMHalves > 1) __syncthreads();
   if (hf != 0 || lane >= 32) return;
 #pragma unroll
   for (int q = 0; q < kMqTiles; ++q) {
     const int qi = base + qloc + 32 * q;
     if (qi >= na) continue;
-    const uint2 o = part[qloc + 32 * q];
-    top2_merge(u1[q], u2[q], o.x, o.y);
+    for (int h = 0; h + 1 < kMHalves; ++h) {  // ranges in index order: keys merge exactly in any order
+      const uint2 o = part[h][qloc + 32 * q];
+      top2_merge(u1[q], u2[q], o.x, o.y);
+    }
     const long long oi = (long long)p * a_cap + qi;
     const int d1 = (int)(u1[q] >> 16);
     best_idx[oi] = d1 < 256 ? (int)(u1[q] & 0xFFFFu) : -1;
