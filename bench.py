@@ -254,6 +254,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.warmup, total_steps):
         step(k, evsets[k], ev_ext, ev_done)
+    t_issue = time.perf_counter()  # host time to enqueue the timed steps (launch-bound if close to wall)
     sync_all()
     t1 = time.perf_counter()
     if dist is not None:
@@ -344,7 +345,7 @@ def main():
             "dominant_kernel": KERNELS[dominant],
             "stage_ms_per_step": {s: round(v, 4) for s, v in st.items()},
             "extract_only_frames_per_s": round(BS / (extract_ms * 1e-3), 1),
-            "event_ms_per_step": round(ev_ms / args.steps, 4),
+            "host_issue_ms_per_step": round((t_issue - t0) / args.steps * 1e3, 4), "event_ms_per_step": round(ev_ms / args.steps, 4),
             "keypoints_per_frame": round(nkp_mean, 1),
             "init_matches_per_pair": round(float(nm[1:].mean()), 1),
         }
