@@ -27,6 +27,7 @@
 #include <string>
 #include <vector>
 
+#include "orbx_device.cuh"
 #include "orbx_internal.h"
 #include "orbx_wave.cuh"
 
@@ -244,9 +245,12 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(ORBX_
     int* __restrict__ best, int* __restrict__ second) {
   __shared__ __attribute__((aligned(16))) i32x4_t sC[2][kMHalves][kMChunk / 32][4][64];  // [buffer][half][tile][step][lane]
   __shared__ uint2 part[kMHalves > 1 ? kMHalves - 1 : 1][kMQueries];
-  const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  // XCD-aware order: a pair's query blocks are consecutive logical ids, which
+  // xcd_remap keeps on one XCD, so its candidates are fetched into one L2
+  const int lg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+  const int p = lg / gridDim.x, tid = threadIdx.x, lane = tid & 63;
   const int hf = tid / (64 * kMWaves), wv = (tid >> 6) % kMWaves, ht = tid % (64 * kMWaves);
-  const int base = blockIdx.x * kMQueries;
+  const int base = (lg % gridDim.x) * kMQueries;
   const int na = nA[p], nb = min(nB[p], 65535);  // final keys hold the index in 16 bits
   if (base >= na) return;
   // queries (the B operand), this wave's kMqTiles tiles, held for the whole kernel
