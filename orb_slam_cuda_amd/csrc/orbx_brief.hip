@@ -24,8 +24,10 @@
 
 namespace orbx {
 
-// packed test t: {x0, y0, x1, y1} as signed bytes (fork and upstream tables)
-__constant__ int c_brief_tests[2][256];
+// test t: {x0, y0, x1, y1} as floats (fork and upstream tables), converted once
+// on the host so a test costs one 16-byte LDS read instead of 4 byte
+// extracts + 4 int->float conversions per lane
+__constant__ float4 c_brief_tests[2][256];
 
 constexpr int kObThreads = 256;              // 4 waves, 8 keypoints
 constexpr int kObKps = kObThreads / 32;
@@ -57,7 +59,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
                                                                   uint8_t* __restrict__ out_desc,
                                                                   int* __restrict__ out_counts) {
   __shared__ __attribute__((aligned(16))) uint8_t s_patch[kObKps][kObRows * kObStride];
-  __shared__ int s_tests[256];
+  __shared__ float4 s_tests[256];
   __shared__ uint32_t s_ictab[16 * 24];
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
   const int bx = wg % gridDim.x, f = wg / gridDim.x, tid = threadIdx.x;
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   int c[kMaxLevels];
 #pragma unroll
   for (int i = 0; i < kMaxLevels; ++i) c[i] = cnt[i];
-  const int test_v = c_brief_tests[P.pattern_upstream ? 1 : 0][tid];
+  const float4 test_v = c_brief_tests[P.pattern_upstream ? 1 : 0][tid];
   const uint32_t ic0 = c_ic_coef[tid], ic1 = c_ic_coef[min(tid + kObThreads, 16 * 24 - 1)];
 
   // level of this half-wave's slot (kbase is uniform: scalar compares)
@@ -185,9 +187,8 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   uint32_t dword[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int t = s_tests[lane + 32 * k];
-    const float px0 = (float)(signed char)(t & 0xFF), py0 = (float)(signed char)((t >> 8) & 0xFF);
-    const float px1 = (float)(signed char)((t >> 16) & 0xFF), py1 = (float)(t >> 24);
+    const float4 t = s_tests[lane + 32 * k];
+    const float px0 = t.x, py0 = t.y, px1 = t.z, py1 = t.w;
     const int ry0 = __float2int_rn(__fadd_rn(__fmul_rn(px0, b), __fmul_rn(py0, a)));
     const int rx0 = __float2int_rn(__fsub_rn(__fmul_rn(px0, a), __fmul_rn(py0, b)));
     const int ry1 = __float2int_rn(__fadd_rn(__fmul_rn(px1, b), __fmul_rn(py1, a)));
@@ -225,13 +226,13 @@ static bool g_pattern_uploaded = false;
 int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const ExtractBuffers& X, orbx_kp* kps,
                         uint8_t* desc, int* counts, int batch, hipStream_t s) {
   if (!g_pattern_uploaded) {
-    int t[2][256];
+    float4 t[2][256];
     for (int m = 0; m < 2; ++m)
       for (int i = 0; i < 256; ++i) {
         int x0 = kBriefPointX[2 * i];
         if (m == 1 && 2 * i == kBriefForkPoint) x0 = kBriefUpstreamX;
         const int y0 = kBriefPointY[2 * i], x1 = kBriefPointX[2 * i + 1], y1 = kBriefPointY[2 * i + 1];
-        t[m][i] = (x0 & 0xFF) | ((y0 & 0xFF) << 8) | ((x1 & 0xFF) << 16) | ((y1 & 0xFF) << 24);
+        t[m][i] = make_float4((float)x0, (float)y0, (float)x1, (float)y1);
       }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_tests), t, sizeof(t)) != hipSuccess) return ORBX_EDEVICE;
     // umax of the r = 15 circle (ORBextractor ctor :540-555; PATCH_SIZE is fixed at 31)
