@@ -577,8 +577,10 @@ __global__ __launch_bounds__(256) void search_bow_kernel(
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap, const uint8_t* B,
                         size_t b_pitch, const int* nB, int pairs, int* best_idx, int* best, int* second,
                         void* stream) {
-  // ORBX_TOP2_VALU=1 selects the VALU kernel (A/B timing and cross-checks only)
-  static const bool valu = getenv("ORBX_TOP2_VALU") && getenv("ORBX_TOP2_VALU")[0] == '1';
+  // ORBX_TOP2_VALU=1 selects the VALU kernel (A/B timing and the cross-check
+  // in tests/test_gpu_match.py; read per call so a test can switch it)
+  const char* ev = getenv("ORBX_TOP2_VALU");
+  const bool valu = ev && ev[0] == '1';
   if (!valu) {
     dim3 grid((a_cap + kMQueries - 1) / kMQueries, pairs);
     hipLaunchKernelGGL(hamming_top2_mfma_kernel, grid, dim3(kMThreads), 0, (hipStream_t)stream, A, (long long)a_pitch,

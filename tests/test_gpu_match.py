@@ -146,12 +146,18 @@ def test_hamming_top2_parity(pkg, O):
         assert np.array_equal(sd[p, :len(a)], rs)
 
 
+@pytest.mark.parametrize("kernel", ["mfma", "valu"])
 @pytest.mark.parametrize("na,nb,dups", [(300, 40000, 0), (517, 3001, 1), (64, 33, 1), (2, 32769, 1)])
-def test_hamming_top2_blocks_and_ties(pkg, O, na, nb, dups):
+def test_hamming_top2_blocks_and_ties(pkg, O, na, nb, dups, kernel, monkeypatch):
     """Candidate counts past one 32768-index key block of the MFMA kernel, ragged
     tiles, and exact ties (duplicated candidate rows: the earlier index must win
-    and the second distance equals the best); also distance-256 complements."""
+    and the second distance equals the best); also distance-256 complements.
+    Both kernels: the FP4 MFMA one (default) and the VALU one (ORBX_TOP2_VALU=1)."""
     import ctypes as C
+    if kernel == "valu":
+        monkeypatch.setenv("ORBX_TOP2_VALU", "1")
+    else:
+        monkeypatch.delenv("ORBX_TOP2_VALU", raising=False)
 
     from orb_slam_cuda_amd import _lib
     rng = np.random.default_rng(na * 7 + nb)
