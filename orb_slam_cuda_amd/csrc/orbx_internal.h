@@ -24,7 +24,10 @@ constexpr int kHalfPatch = 15;          // HALF_PATCH_SIZE src/ORBextractor.cc:9
 constexpr int kGridW = 30;              // W               src/ORBextractor.cc:1126
 constexpr int kMaxRoi = 66;             // largest FAST cell ROI side (+6 halo)
 constexpr int kMaxLevelDim = 4096;      // packed key coordinates are 12 bits
-constexpr int kQtThreads = 256;
+#ifndef ORBX_QT_THREADS
+#define ORBX_QT_THREADS 512
+#endif
+constexpr int kQtThreads = ORBX_QT_THREADS;  // quadtree workgroup size
 
 struct LevelGeom {
   int w, h, pitch;
