@@ -29,7 +29,10 @@ namespace orbx {
 // extracts + 4 int->float conversions per lane
 __constant__ float4 c_brief_tests[2][256];
 
-constexpr int kObThreads = 256;              // 4 waves, 8 keypoints
+#ifndef ORBX_OB_THREADS
+#define ORBX_OB_THREADS 256
+#endif
+constexpr int kObThreads = ORBX_OB_THREADS;  // 256: 4 waves, 8 keypoints
 constexpr int kObKps = kObThreads / 32;
 constexpr int kObRadius = 19;                // |rotated pattern offset| <= 18.4, rounded
 constexpr int kObRows = 2 * kObRadius + 1;   // 39
@@ -75,8 +78,13 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   int c[kMaxLevels];
 #pragma unroll
   for (int i = 0; i < kMaxLevels; ++i) c[i] = cnt[i];
-  const float4 test_v = c_brief_tests[P.pattern_upstream ? 1 : 0][tid];
-  const uint32_t ic0 = c_ic_coef[tid], ic1 = c_ic_coef[min(tid + kObThreads, 16 * 24 - 1)];
+  constexpr int kTestsPer = (256 + kObThreads - 1) / kObThreads, kIcPer = (16 * 24 + kObThreads - 1) / kObThreads;
+  float4 test_v[kTestsPer];
+  uint32_t ic_v[kIcPer];
+#pragma unroll
+  for (int k = 0; k < kTestsPer; ++k) test_v[k] = c_brief_tests[P.pattern_upstream ? 1 : 0][min(tid + k * kObThreads, 255)];
+#pragma unroll
+  for (int k = 0; k < kIcPer; ++k) ic_v[k] = c_ic_coef[min(tid + k * kObThreads, 16 * 24 - 1)];
 
   // level of this half-wave's slot (kbase is uniform: scalar compares)
   int l = 0;
@@ -140,9 +148,12 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   uint32_t w[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) w[k] = q[k];
-  s_tests[tid] = test_v;
-  s_ictab[tid] = ic0;
-  if (tid + kObThreads < 16 * 24) s_ictab[tid + kObThreads] = ic1;
+#pragma unroll
+  for (int k = 0; k < kTestsPer; ++k)
+    if (tid + k * kObThreads < 256) s_tests[tid + k * kObThreads] = test_v[k];
+#pragma unroll
+  for (int k = 0; k < kIcPer; ++k)
+    if (tid + k * kObThreads < 16 * 24) s_ictab[tid + k * kObThreads] = ic_v[k];
   // unpredicated stores (an empty slot writes its own unused patch, lanes past
   // the last chunk rewrite it with the same bytes), so no load waits in a branch
   {
