@@ -291,13 +291,17 @@ def main():
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
                   "orient_brief": ab["orient_brief"]}
     rk = dominant if dominant in hbm_stages else max(hbm_stages, key=lambda s: st[s])
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
+    def pmc_bytes(kernel):
+        """HBM-side bytes per launch of `kernel` from the committed PMC passes (profiles/)."""
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         try:
-            traffic = json.load(open(pmc_path)).get(KERNELS[rk].split(" ")[0], {}).get("bytes_per_launch")
+            pmc = json.load(open(pmc_path))
         except Exception:
-            traffic = None
+            return None
+        want = kernel.split(" ")[0]  # profile keys carry template arguments ("fast_cells_kernel<44>")
+        return next((v.get("bytes_per_launch") for k, v in pmc.items() if k.split("<")[0] == want), None)
+
+    traffic = pmc_bytes(KERNELS[rk])
     ach = hbm_stages[rk] * BS / (st[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -316,6 +320,7 @@ def main():
         match_roof = {"kernel": KERNELS["hamming_top2"], "bound": "mfma", "unit": "TFLOP/s",
                       "achieved": round(tf, 1), "peak": MFMA_FP4_PEAK_TFLOPS, "frac": round(tf / MFMA_FP4_PEAK_TFLOPS, 4),
                       "dtype": "fp4 e2m1 (+-1 bits, exact)", "top2_valu_frac": round(2.0 * pairs / sec / 1e12 / VALU_PEAK_TOPS, 4),
+                      "traffic": pmc_bytes(KERNELS["hamming_top2"]),
                       "pairs_per_launch": pairs, "pairs_per_s": round(pairs / sec, 1),
                       "avg_launch_ms": round(st["hamming_top2"], 4)}
 
