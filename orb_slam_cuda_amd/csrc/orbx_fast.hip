@@ -110,6 +110,9 @@ __device__ __forceinline__ void ring_masks(const uint8_t* c, int lo, int hi, uin
   *bright = br;
 }
 
+#ifndef ORBX_FAST_PK
+#define ORBX_FAST_PK 1  // packed-u16 compass pre-test (0: the scalar form, for A/B)
+#endif
 #ifndef ORBX_FAST_WAVES
 #define ORBX_FAST_WAVES 6  // VGPR budget: 6 waves per SIMD (<= 80 VGPRs)
 #endif
@@ -227,6 +230,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   int n1 = 0;
   for (int by0 = 0; by0 < bh; by0 += 4 * rstep) {
     bool fl[4];
+#if ORBX_FAST_PK
+    // two row groups per packed u16x2 register: the min/max network, the
+    // thresholds (saturating subtract) and the tests run as v_pk_* ops
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+      const int byA = by0 + q * rstep + lr, byB = byA + rstep;
+      const uint8_t* cA = band + min(byA, bh - 1) * kRoiStride + min(lc, bw - 1);
+      const uint8_t* cB = band + min(byB, bh - 1) * kRoiStride + min(lc, bw - 1);
+      auto pk = [](int lo, int hi) { return (u16x2){(unsigned short)lo, (unsigned short)hi}; };
+      const u16x2 v = pk(cA[0], cB[0]);
+      const u16x2 n0 = pk(cA[3 * kRoiStride], cB[3 * kRoiStride]), n4 = pk(cA[3], cB[3]);
+      const u16x2 n8 = pk(cA[-3 * kRoiStride], cB[-3 * kRoiStride]), n12 = pk(cA[-3], cB[-3]);
+      const u16x2 s1 = __builtin_elementwise_min(n0, n4), l1 = __builtin_elementwise_max(n0, n4);
+      const u16x2 s2 = __builtin_elementwise_min(n8, n12), l2 = __builtin_elementwise_max(n8, n12);
+      const u16x2 a = __builtin_elementwise_max(s1, s2), b = __builtin_elementwise_min(l1, l2);
+      const u16x2 tt = {(unsigned short)t, (unsigned short)t};
+      // min(a,b) < v - t  <=>  sat(sat(v - t) - min(a,b)) != 0;  max(a,b) > v + t  <=>  sat(max(a,b) - (v + t)) != 0
+      const u16x2 dk = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), __builtin_elementwise_min(a, b));
+      const u16x2 br = __builtin_elementwise_sub_sat(__builtin_elementwise_max(a, b), v + tt);
+      const u16x2 any = dk | br;
+      fl[q] = (int)(byA < bh) & (int)(lc < bw) & (int)(any.x != 0);
+      fl[q + 1] = (int)(byB < bh) & (int)(lc < bw) & (int)(any.y != 0);
+    }
+#else
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int by = by0 + q * rstep + lr;
@@ -241,6 +269,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
       // groups' loads can be in flight before the first use
       fl[q] = (int)(by < bh) & (int)(lc < bw) & ((int)(min(a, b) < v - t) | (int)(max(a, b) > v + t));
     }
+#endif
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int by = by0 + q * rstep + lr;
