@@ -136,7 +136,10 @@ __global__ __launch_bounds__(256) void pyr_resize_kernel(
 // every level's rows; the few source rows two bands share are recomputed by
 // both instead of exchanged). Row ranges per (band, level) come from the host
 // (orbx_host.hip build_plan): comp = rows computed, own = rows written.
-constexpr int kPyrBandThreads = 512;
+#ifndef ORBX_PYR_THREADS
+#define ORBX_PYR_THREADS 512
+#endif
+constexpr int kPyrBandThreads = ORBX_PYR_THREADS;
 
 // Rows of one level for one thread: all 32 source bytes of a row pair are
 // read before any is used, so one LDS wait covers them.
