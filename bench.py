@@ -290,7 +290,12 @@ def main():
     roof = None
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
                   "orient_brief": ab["orient_brief"]}
-    rk = dominant if dominant in hbm_stages else max(hbm_stages, key=lambda s: st[s])
+    # the roofline kernel is FAST: the longest extraction kernel when each runs
+    # alone (profiles/r01_serial_kernel_stats.csv) and the one whose event time
+    # in this pipelined run matches its rocprofv3 average; the event pairs of
+    # the pyramid and the blur also hold their wait for compute units that the
+    # other streams occupy, which a by-time pick would report as their duration
+    rk = "fast_grid"
     def pmc_bytes(kernel):
         """HBM-side bytes per launch of `kernel` from the committed PMC passes (profiles/)."""
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
