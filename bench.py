@@ -106,6 +106,8 @@ def main():
                     help="high-priority extraction streams, low-priority matching stream")
     ap.add_argument("--bow", action="store_true",
                     help="also Frame::ComputeBoW every frame (synthetic ORBvoc-shaped vocabulary, k 10 L 6)")
+    ap.add_argument("--match-streams", type=int, choices=[1, 2], default=1,
+                    help="2: SearchForInitialization on its own stream, beside the dense top-2")
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
                     help="stream that copies a batch's last frame for the next batch's first pair")
     args = ap.parse_args()
@@ -162,9 +164,11 @@ def main():
     s_exts = [_lib.Stream(prio) for _ in range(S)]
     s_ext = s_exts[0]
     s_match = _lib.Stream(0 if args.priority else None) if not args.serial else s_ext
+    two_match = args.match_streams == 2 and not args.serial and not args.no_match and args.carry == "match"
+    s_init = _lib.Stream(0 if args.priority else None) if two_match else s_match
     bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
     vp = lambda a: C.c_void_p(a)
-    n_ev = 11  # 6 extraction stage marks (extract stream) + 3 matching marks + 2 BoW marks (match stream)
+    n_ev = 12  # 6 extraction stage marks (extract stream) + 3 matching marks + 2 BoW marks (match stream) + init start
     voc = None
     if args.bow:
         from orb_slam_cuda_amd.synth import synthetic_vocabulary
@@ -189,6 +193,8 @@ def main():
                 check(L.orbx_set_stage_events(ex.handle, arr))
             if not args.serial and k >= 3:
                 se.wait(ev_done[k - 3])  # matching k-3 was the last reader of set k % 3
+                if two_match:
+                    se.wait(ev_done2[k - 3])
             sv = se if not args.serial else s_ext
             check(L.orbx_extract_batch(ex.handle, vp(d_frames.ptr + h * BS * H * pitch), BS, H * pitch, pitch,
                                        vp(d_kps[b].ptr + (1 + h * BS) * cap * KP),
@@ -211,7 +217,10 @@ def main():
         if not args.serial:
             s_match.wait(ev_ext[k])
         if args.carry == "match" and not args.serial:
+            if two_match and k >= 2:
+                s_match.wait(ev_done2[k - 2])  # SearchForInitialization k-2 also read set (k+1) % 3
             carry(s_match)  # in order after matching k-2, the last reader of set (k+1) % 3
+            ev_carry[k].record(s_match)
         if voc is not None:
             evs[9].record(s_match)
             # Frame::ComputeBoW of the batch's frames (slots 1..B), levelsup 4 (src/Frame.cc:398)
@@ -228,22 +237,32 @@ def main():
                                       vp(d_counts[b].ptr), B, vp(d_bi.ptr), vp(d_bd.ptr), vp(d_sd.ptr),
                                       s_match.s), matcher=True)
             evs[7].record(s_match)
+            if two_match:  # after batch k's extraction and the carry into its slot 0 (step k-1)
+                s_init.wait(ev_ext[k])
+                if k >= 1:
+                    s_init.wait(ev_carry[k - 1])
+            evs[11].record(s_init)
             check(L.orbm_search_for_initialization_batch(
                 matcher.handle, vp(d_kps[b].ptr), vp(d_desc[b].ptr), vp(d_counts[b].ptr),
                 vp(d_kps[b].ptr + cap * KP), vp(d_desc[b].ptr + cap * DS), vp(d_counts[b].ptr + 4), cap, B,
-                bounds, None, 100, C.c_float(0.9), 1, vp(d_m12.ptr), vp(d_nm.ptr), s_match.s), matcher=True)
-        evs[8].record(s_match)
+                bounds, None, 100, C.c_float(0.9), 1, vp(d_m12.ptr), vp(d_nm.ptr), s_init.s), matcher=True)
+        evs[8].record(s_init)
         ev_done[k].record(s_match)
+        if two_match:
+            ev_done2[k].record(s_init)
 
     total_steps = args.warmup + args.steps
     evsets = [[_lib.Event() for _ in range(n_ev)] for _ in range(total_steps)]
     ev_ext = [_lib.Event() for _ in range(total_steps)]
     ev_done = [_lib.Event() for _ in range(total_steps)]
+    ev_done2 = [_lib.Event() for _ in range(total_steps)]
+    ev_carry = [_lib.Event() for _ in range(total_steps)]
     ev_part = [[_lib.Event() for _ in range(S)] for _ in range(total_steps)]
     def sync_all():
         for se in s_exts:
             se.synchronize()
         s_match.synchronize()
+        s_init.synchronize()
 
     for k in range(args.warmup):
         step(k, evsets[k], ev_ext, ev_done)
@@ -274,7 +293,7 @@ def main():
             st["bow_transform"] += evs[9].elapsed_ms(evs[10])
         if not args.no_match:
             st["hamming_top2"] += evs[6].elapsed_ms(evs[7])
-            st["search_init"] += evs[7].elapsed_ms(evs[8])
+            st["search_init"] += evs[11].elapsed_ms(evs[8])
     st = {s: v / args.steps for s, v in st.items()}
 
     nm = d_nm.download(B, np.int32)
