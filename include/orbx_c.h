@@ -160,6 +160,26 @@ int orbx_get_level(orbx_handle h, int frame, int level, int blurred,
  * box, response = FAST score). */
 int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out,
                              int cap, int* n);
+/* Quadtree tie-rule exposure of frames [frame0, frame0 +
+ * nframes) of the last extraction: per (frame, level) three ints {events,
+ * group nodes, kept keypoints}. DistributeOctTree's sorted rounds split nodes
+ * in (size, heap-pointer) order (src/ORBextractor.cc:1041-1042) and stop at N;
+ * an event is a cut-off inside a group of equal-size nodes, where the
+ * reference's choice depends on its allocator and this library's on node
+ * creation order (the oracle's rule). `kept keypoints` counts the outputs
+ * that come from that group. Synchronous (waits for the device). */
+int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out);
+/* Device status word of the handle's kernels since the last call (0 = ok;
+ * bit 1: quadtree round limit, bit 2: quadtree output over capacity).
+ * Waits for the device; `reset` != 0 clears it. orbx_extract checks and clears
+ * it itself; batch callers (orbx_extract_batch) poll it here. */
+int orbx_get_status(orbx_handle h, int reset, int* status);
+/* The rBRIEF test table the kernels use (bit_pattern_31_,
+ * src/ORBextractor.cc:236-494): 1024 ints in the reference's flat order
+ * (test i = entries 4i..4i+3 = x0, y0, x1, y1), for pattern_mode
+ * ORBX_PATTERN_FORK (entry 96 = VX_FAILURE-2 = -3, :261-262) or
+ * ORBX_PATTERN_UPSTREAM (-2). Host only, no device needed. */
+int orbx_get_pattern(int pattern_mode, int* out1024);
 /* Per-stage device time (ms) of the last extraction, stage names as the
  * reference's GetTime labels (src/ORBextractor.cc:1131,1331,1737,1753,1841).
  * Filled only when the handle was created with timing enabled
@@ -189,6 +209,21 @@ const char* orbm_last_error(void);
  * max_kps keypoints per frame. */
 int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out);
 int orbm_destroy(orbm_handle m);
+
+/* Device status word of the matcher's batched kernels since the last call
+ * (0 = ok; bit 8: SearchForInitialization candidate overflow, that pair got
+ * no matches; bit 16: orbm_hamming_top2 input over its limits, nA[p] > a_cap
+ * or nB[p] > 65535, the excess rows / candidates were not searched). Waits
+ * for the device; `reset` != 0 clears it. The synchronous entry points check
+ * and clear it themselves.
+ *
+ * Device workspaces (candidate lists, stereo SAD, pose picks) belong to the
+ * handle: batched calls on different streams are ordered by the library
+ * (each waits for the previous user of the workspace), so they never
+ * overlap on it. The same holds for an extractor handle's plan buffers, and
+ * orbm_compute_stereo_matches_batch orders itself after and before the two
+ * extractors whose pyramids it reads. */
+int orbm_get_status(orbm_handle m, int reset, int* status);
 
 /* Hamming distance of two 32-byte descriptors (host, exact). */
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b);

@@ -127,6 +127,31 @@ def distribute(keys: np.ndarray, minX: int, maxX: int, minY: int, maxY: int, N: 
     return out[:n.value].copy()
 
 
+def tie_stats(cfg: OrcConfig, img: np.ndarray) -> dict:
+    """Per-level tie-straddle exposure of the quadtree's creation-order tie rule
+    (orb_oracle.h orc_extract_tie_stats): events, group nodes, kept keypoints."""
+    img = np.ascontiguousarray(img, np.uint8)
+    L = cfg.nlevels
+    ev, nd, kp = (np.zeros(L, np.int32) for _ in range(3))
+    lib().orc_extract_tie_stats(C.byref(cfg), _p(img), img.shape[1], img.shape[0], C.c_size_t(img.strides[0]),
+                                _p(ev), _p(nd), _p(kp))
+    return dict(events=ev, nodes=nd, kps=kp)
+
+
+def distribute_ties(keys: np.ndarray, minX: int, maxX: int, minY: int, maxY: int, N: int):
+    keys = np.ascontiguousarray(keys, KP_DTYPE)
+    ev, nd, kp = C.c_int(0), C.c_int(0), C.c_int(0)
+    lib().orc_distribute_ties(_p(keys), len(keys), minX, maxX, minY, maxY, N, C.byref(ev), C.byref(nd), C.byref(kp))
+    return ev.value, nd.value, kp.value
+
+
+def pattern(pattern_mode: int = 0) -> np.ndarray:
+    """The oracle's rBRIEF table, 1024 int8 entries in the reference's flat order."""
+    out = np.zeros(1024, np.int8)
+    lib().orc_pattern(pattern_mode, _p(out))
+    return out
+
+
 def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
     a = np.ascontiguousarray(a, np.uint8); b = np.ascontiguousarray(b, np.uint8)
     return lib().orc_descriptor_distance(_p(a), _p(b))

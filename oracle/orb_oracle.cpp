@@ -330,6 +330,18 @@ const int PATCH_SIZE = 31;
 const int HALF_PATCH_SIZE = 15;
 const int EDGE_THRESHOLD = 19;
 
+// Exposure of the creation-order stand-in for the reference's heap-pointer
+// tie-break: the sorted rounds split nodes in descending
+// (size, pointer) order and stop as soon as the list reaches N (:1041-1088).
+// When that cut-off falls inside a group of equal-size nodes, WHICH of them
+// were split was decided by the tie rule. `events` counts such cut-offs (0 or
+// 1 per call), `nodes` the nodes of the straddled group, `kps` the kept
+// keypoints that come from them (the children of its split nodes plus one per
+// unsplit node): the outputs another tie order could change.
+struct TieStats {
+  int events = 0, nodes = 0, kps = 0;
+};
+
 struct Extractor {
   orc_config cfg;
   std::vector<float> mvScaleFactor, mvInvScaleFactor, mvLevelSigma2, mvInvLevelSigma2;
@@ -453,7 +465,8 @@ struct Extractor {
     }
   }
 
-  void extract(const Mat8& image, std::vector<KeyPoint>& out, std::vector<uint8_t>& desc);
+  void extract(const Mat8& image, std::vector<KeyPoint>& out, std::vector<uint8_t>& desc,
+               std::vector<TieStats>* ties = nullptr);
 };
 
 // --------------------------------------------------------------- quadtree
@@ -518,7 +531,8 @@ struct SizeSeqNode {
 };
 
 std::vector<KeyPoint> distribute_oct_tree(const std::vector<KeyPoint>& vToDistributeKeys,
-                                          int minX, int maxX, int minY, int maxY, int N) {
+                                          int minX, int maxX, int minY, int maxY, int N,
+                                          TieStats* ties = nullptr) {
   const int nIni = round(static_cast<float>(maxX - minX) / (maxY - minY));
   const float hX = static_cast<float>(maxX - minX) / nIni;
   long seq = 0;
@@ -596,15 +610,30 @@ std::vector<KeyPoint> distribute_oct_tree(const std::vector<KeyPoint>& vToDistri
         std::vector<SizeSeqNode> vPrevSizeAndPointerToNode = vSizeAndPointerToNode;
         vSizeAndPointerToNode.clear();
         std::sort(vPrevSizeAndPointerToNode.begin(), vPrevSizeAndPointerToNode.end());
+        std::vector<int> children(vPrevSizeAndPointerToNode.size(), 0);
         for (int j = vPrevSizeAndPointerToNode.size() - 1; j >= 0; j--) {
           ExtractorNode n1, n2, n3, n4;
           vPrevSizeAndPointerToNode[j].node->DivideNode(n1, n2, n3, n4);
+          children[j] = (n1.vKeys.size() > 0) + (n2.vKeys.size() > 0) + (n3.vKeys.size() > 0) +
+                        (n4.vKeys.size() > 0);
           push_child(n1, vSizeAndPointerToNode, nullptr);
           push_child(n2, vSizeAndPointerToNode, nullptr);
           push_child(n3, vSizeAndPointerToNode, nullptr);
           push_child(n4, vSizeAndPointerToNode, nullptr);
           lNodes.erase(vPrevSizeAndPointerToNode[j].node->lit);
-          if ((int)lNodes.size() >= N) break;
+          if ((int)lNodes.size() >= N) {
+            // cut-off after node j: a straddle if the next (unsplit) node has j's size
+            const int s = vPrevSizeAndPointerToNode[j].size;
+            if (ties && j > 0 && vPrevSizeAndPointerToNode[j - 1].size == s) {
+              ties->events++;
+              for (int i = 0; i < (int)vPrevSizeAndPointerToNode.size(); ++i) {
+                if (vPrevSizeAndPointerToNode[i].size != s) continue;
+                ties->nodes++;
+                ties->kps += i >= j ? children[i] : 1;
+              }
+            }
+            break;
+          }
         }
         if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) bFinish = true;
       }
@@ -669,10 +698,12 @@ void orb_descriptor(const KeyPoint& kpt, const Mat8& img, const signed char test
 }
 
 // operator() CPU branch (src/ORBextractor.cc:1701-1809) + ComputeKeyPointsOctTree.
-void Extractor::extract(const Mat8& image, std::vector<KeyPoint>& out, std::vector<uint8_t>& desc) {
+void Extractor::extract(const Mat8& image, std::vector<KeyPoint>& out, std::vector<uint8_t>& desc,
+                        std::vector<TieStats>* ties) {
   out.clear();
   desc.clear();
   if (image.w == 0 || image.h == 0) return;
+  if (ties) ties->assign(cfg.nlevels, TieStats{});
   compute_pyramid(image);
   std::vector<std::vector<KeyPoint>> allKeypoints(cfg.nlevels);
   std::vector<KeyPoint> cand;
@@ -680,7 +711,8 @@ void Extractor::extract(const Mat8& image, std::vector<KeyPoint>& out, std::vect
     int bx[4];
     fast_level(level, cand, bx);
     std::vector<KeyPoint>& keypoints = allKeypoints[level];
-    keypoints = distribute_oct_tree(cand, bx[0], bx[1], bx[2], bx[3], mnFeaturesPerLevel[level]);
+    keypoints = distribute_oct_tree(cand, bx[0], bx[1], bx[2], bx[3], mnFeaturesPerLevel[level],
+                                    ties ? &(*ties)[level] : nullptr);
     const int scaledPatchSize = PATCH_SIZE * mvScaleFactor[level];
     for (auto& kp : keypoints) {
       kp.x += bx[0];
@@ -894,6 +926,40 @@ int orc_distribute(const orc_kp* keys, int nkeys, int minX, int maxX, int minY, 
 }
 
 int orc_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
+
+int orc_extract_tie_stats(const orc_config* cfg, const uint8_t* img, int w, int h, size_t stride, int* events,
+                          int* nodes, int* kps) {
+  Extractor ex(*cfg);
+  std::vector<KeyPoint> out;
+  std::vector<uint8_t> d;
+  std::vector<TieStats> t;
+  ex.extract(wrap_image(img, w, h, stride), out, d, &t);
+  for (int l = 0; l < cfg->nlevels; ++l) {
+    const TieStats z = l < (int)t.size() ? t[l] : TieStats{};
+    if (events) events[l] = z.events;
+    if (nodes) nodes[l] = z.nodes;
+    if (kps) kps[l] = z.kps;
+  }
+  return 0;
+}
+
+int orc_distribute_ties(const orc_kp* keys, int nkeys, int minX, int maxX, int minY, int maxY, int N, int* events,
+                        int* nodes, int* kps) {
+  std::vector<KeyPoint> in(keys, keys + nkeys);
+  TieStats t;
+  distribute_oct_tree(in, minX, maxX, minY, maxY, N, &t);
+  *events = t.events;
+  *nodes = t.nodes;
+  *kps = t.kps;
+  return 0;
+}
+
+void orc_pattern(int pattern_mode, signed char* out1024) {
+  signed char t[256][4];
+  std::memcpy(t, kOracleBriefTests, sizeof(t));
+  if (pattern_mode == 1) t[kOracleForkIndex / 4][kOracleForkIndex % 4] = kOracleUpstreamValue;
+  std::memcpy(out1024, t, sizeof(t));
+}
 
 
 int orc_compute_stereo_matches(const orc_kp* kpL, const uint8_t* descL, int nL, const orc_kp* kpR,

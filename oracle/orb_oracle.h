@@ -64,6 +64,18 @@ int orc_fast_level(const orc_config* cfg, const uint8_t* img, int w, int h,
 int orc_distribute(const orc_kp* keys, int nkeys, int minX, int maxX,
                    int minY, int maxY, int N, orc_kp* out, int cap, int* n);
 
+/* Tie-straddle exposure of the quadtree's creation-order tie rule (SURVEY.md
+ * §8c): per level, the cut-offs at N that fell inside a group of equal-size
+ * nodes (src/ORBextractor.cc:1041-1088), the nodes of that group and the kept
+ * keypoints that came from them. */
+int orc_extract_tie_stats(const orc_config* cfg, const uint8_t* img, int w, int h,
+                          size_t stride, int* events, int* nodes, int* kps);
+int orc_distribute_ties(const orc_kp* keys, int nkeys, int minX, int maxX, int minY,
+                        int maxY, int N, int* events, int* nodes, int* kps);
+/* The rBRIEF test table (bit_pattern_31_, src/ORBextractor.cc:236-494) the
+ * oracle uses: 1024 entries, fork (0) or upstream (1) variant. */
+void orc_pattern(int pattern_mode, signed char* out1024);
+
 /* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1647-1663). */
 int orc_descriptor_distance(const uint8_t* a, const uint8_t* b);
 

@@ -102,6 +102,10 @@ def lib() -> C.CDLL:
                                                C.POINTER(C.c_int)]
         L.orbx_get_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
         L.orbx_set_stage_events.argtypes = [C.c_void_p, C.c_void_p]
+        L.orbx_get_tie_stats.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        L.orbx_get_status.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+        L.orbx_get_pattern.argtypes = [C.c_int, C.c_void_p]
+        L.orbm_get_status.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
         L.orbm_create.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
         L.orbm_destroy.argtypes = [C.c_void_p]
         L.orbm_descriptor_distance.argtypes = [C.c_void_p, C.c_void_p]

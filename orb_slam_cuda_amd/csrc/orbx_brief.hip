@@ -232,18 +232,29 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   }
 }
 
-static bool g_pattern_uploaded = false;
+// Test i of pattern mode m (0 fork, 1 upstream) as {x0, y0, x1, y1}: points
+// 2i and 2i+1 of the 512-point table (ORBextractor ctor :534-536).
+static void brief_test(int m, int i, int t[4]) {
+  t[0] = kBriefPointX[2 * i];
+  if (m == 1 && 2 * i == kBriefForkPoint) t[0] = kBriefUpstreamX;
+  t[1] = kBriefPointY[2 * i];
+  t[2] = kBriefPointX[2 * i + 1];
+  t[3] = kBriefPointY[2 * i + 1];
+}
+
+static bool g_pattern_uploaded[64] = {};  // per device: constant memory is per device
 
 int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const ExtractBuffers& X, orbx_kp* kps,
                         uint8_t* desc, int* counts, int batch, hipStream_t s) {
-  if (!g_pattern_uploaded) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return ORBX_EDEVICE;
+  if (!g_pattern_uploaded[dev]) {
     float4 t[2][256];
     for (int m = 0; m < 2; ++m)
       for (int i = 0; i < 256; ++i) {
-        int x0 = kBriefPointX[2 * i];
-        if (m == 1 && 2 * i == kBriefForkPoint) x0 = kBriefUpstreamX;
-        const int y0 = kBriefPointY[2 * i], x1 = kBriefPointX[2 * i + 1], y1 = kBriefPointY[2 * i + 1];
-        t[m][i] = make_float4((float)x0, (float)y0, (float)x1, (float)y1);
+        int q[4];
+        brief_test(m, i, q);
+        t[m][i] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
       }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_tests), t, sizeof(t)) != hipSuccess) return ORBX_EDEVICE;
     // umax of the r = 15 circle (ORBextractor ctor :540-555; PATCH_SIZE is fixed at 31)
@@ -259,7 +270,7 @@ int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const Extra
         coef[av * 24 + 16 + k] |= 1u << sh;
       }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_ic_coef), coef, sizeof(coef)) != hipSuccess) return ORBX_EDEVICE;
-    g_pattern_uploaded = true;
+    g_pattern_uploaded[dev] = true;
   }
   dim3 grid((P.kp_per_frame + kObKps - 1) / kObKps, batch);
   hipLaunchKernelGGL(orient_brief_kernel, grid, dim3(kObThreads), 0, s, P, lp, X.blur, X.qkeys, X.qcounts, X.umax,
@@ -268,3 +279,9 @@ int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const Extra
 }
 
 }  // namespace orbx
+
+extern "C" int orbx_get_pattern(int pattern_mode, int* out1024) {
+  if (!out1024 || (pattern_mode != ORBX_PATTERN_FORK && pattern_mode != ORBX_PATTERN_UPSTREAM)) return ORBX_EINVAL;
+  for (int i = 0; i < 256; ++i) orbx::brief_test(pattern_mode, i, out1024 + 4 * i);
+  return ORBX_OK;
+}

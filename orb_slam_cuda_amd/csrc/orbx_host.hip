@@ -74,7 +74,7 @@ struct Plan {
   ExtractParams P{};
   std::vector<CellGeom> cells;
   std::vector<int2> rtab;
-  DeviceBuf pyr, blur, rtab_d, cells_d, umax_d, slots, cell_counts, qkeys, qcounts, qscratch, qnscratch, err;
+  DeviceBuf pyr, blur, rtab_d, cells_d, umax_d, slots, cell_counts, qkeys, qcounts, qties, qscratch, qnscratch, err;
 };
 
 }  // namespace
@@ -95,8 +95,11 @@ struct orbx_extractor {
   hipEvent_t ev[6] = {};
   void* user_ev[ORBX_STAGE_EVENTS] = {};
   bool has_user_ev = false;
+  WsOrder ws;  // stream order of the plan buffers (pyramid, blur, slots, quadtree)
   std::mutex mu;
 };
+
+WsOrder* orbx::extractor_ws(orbx_handle h) { return h ? &h->ws : nullptr; }
 
 // ORBextractor::ORBextractor scalar tables (src/ORBextractor.cc:500-532) and
 // umax (:540-555); the fork's scale override (:674-680) in mode F.
@@ -436,6 +439,7 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   if ((rc = pl.cell_counts.alloc((size_t)B * P.ncells_total * 4))) return rc;
   if ((rc = pl.qkeys.alloc((size_t)B * P.kp_per_frame * 4))) return rc;
   if ((rc = pl.qcounts.alloc((size_t)B * L * 4 + 4 * kMaxLevels))) return rc;  // orient_brief reads kMaxLevels counts per frame
+  if ((rc = pl.qties.alloc((size_t)B * L * 16))) return rc;
   if ((rc = pl.qscratch.alloc((size_t)B * slot * 4 + 4))) return rc;
   if ((rc = pl.qnscratch.alloc((size_t)B * slot * 2 + 4))) return rc;
   if ((rc = pl.err.alloc(16))) return rc;
@@ -454,10 +458,11 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
       select_pyr_plan(Q, i);
       mx = std::max(mx, pyr_band_lds_bytes(Q));
     }
-    HIP_OK(hipFuncSetAttribute(pyr_band_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx));
+    if (raise_lds_limit(pyr_band_kernel_ptr(), mx))
+      return fail(ORBX_EDEVICE, "LDS limit of pyr_band_kernel: %s", hipGetErrorString(hipGetLastError()));
   }
-  HIP_OK(hipFuncSetAttribute(quadtree_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)quadtree_lds_bytes(P)));
+  if (raise_lds_limit(quadtree_kernel_ptr(), quadtree_lds_bytes(P)))
+    return fail(ORBX_EDEVICE, "LDS limit of quadtree_kernel: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
 }
 
@@ -472,6 +477,7 @@ static ExtractBuffers buffers_of(const Plan& pl) {
   X.cell_counts = pl.cell_counts.as<int>();
   X.qkeys = pl.qkeys.as<uint32_t>();
   X.qcounts = pl.qcounts.as<int>();
+  X.qties = pl.qties.as<int>();
   X.qscratch = pl.qscratch.as<uint32_t>();
   X.qnode_scratch = pl.qnscratch.as<uint16_t>();
   X.qscratch_per_fl = 0;
@@ -507,6 +513,29 @@ int orbx::extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int
     scale[l] = h->scale[l];
     inv_scale[l] = h->inv_scale[l];
   }
+  return ORBX_OK;
+}
+
+// Dynamic-LDS limits are per kernel and device, shared by every handle of the
+// process: only ever raise them (a handle with a smaller plan must not lower
+// the limit a larger one launches with).
+int orbx::raise_lds_limit(const void* fn, size_t bytes) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<const void*, int>, size_t>> set;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return ORBX_EDEVICE;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& e : set)
+    if (e.first.first == fn && e.first.second == dev) {
+      if (bytes <= e.second) return ORBX_OK;
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+        return ORBX_EDEVICE;
+      e.second = bytes;
+      return ORBX_OK;
+    }
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+    return ORBX_EDEVICE;
+  set.push_back({{fn, dev}, bytes});
   return ORBX_OK;
 }
 
@@ -558,6 +587,8 @@ int orbx_destroy(orbx_handle h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
+  if (h->ws.ev) (void)hipEventSynchronize(h->ws.ev);
+  h->ws.release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return ORBX_OK;
@@ -573,8 +604,10 @@ int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch, size_t
   HIP_OK(hipSetDevice(h->cfg.device));
   void** ev = h->has_user_ev ? h->user_ev : (h->timing ? (void**)h->ev : nullptr);
   h->has_user_ev = false;
+  if (h->ws.before((hipStream_t)stream)) return fail(ORBX_EDEVICE, "stream wait on the handle's last use failed");
   const int rc = launch_extract(h->plan.P, buffers_of(h->plan), d_frames, batch, frame_pitch, row_stride, d_kps,
                                 d_desc, d_counts, stream, ev);
+  if (!rc && h->ws.after((hipStream_t)stream)) return fail(ORBX_EDEVICE, "event record failed");
   h->last_batch = batch;
   h->last_frames = d_frames;
   h->last_fpitch = frame_pitch;
@@ -592,8 +625,9 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   if (!img || w < 0 || hh < 0 || stride < (size_t)w) return fail(ORBX_EINVAL, "bad image");
   HIP_OK(hipSetDevice(h->cfg.device));
   if (w != h->plan.W || hh != h->plan.H) {
-    // the reference accepts any image size per call: re-plan for it
-    (void)hipStreamSynchronize(h->stream);
+    // the reference accepts any image size per call: re-plan for it (after
+    // every launch that uses the current plan's buffers)
+    if (h->ws.ev) (void)hipEventSynchronize(h->ws.ev);
     const int rc = build_plan(h, w, hh, h->plan.B);
     if (rc) return rc;
     h->d_in.alloc(0);
@@ -615,7 +649,10 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   HIP_OK(hipMemcpyAsync(&cnt, h->d_counts.p, 4, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipMemcpyAsync(&err, h->plan.err.p, 4, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipStreamSynchronize(h->stream));
-  if (err) return fail(ORBX_ECAPACITY, "device error word 0x%x", err);
+  if (err) {
+    HIP_OK(hipMemset(h->plan.err.p, 0, 16));  // reported once, not on every later call
+    return fail(ORBX_ECAPACITY, "device error word 0x%x", err);
+  }
   *n = cnt;
   if (cnt > cap) return fail(ORBX_ECAPACITY, "%d keypoints do not fit cap %d", cnt, cap);
   if (kps) HIP_OK(hipMemcpy(kps, h->d_kps.p, (size_t)cnt * sizeof(orbx_kp), hipMemcpyDeviceToHost));
@@ -698,6 +735,33 @@ int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out, 
   }
   *n = k;
   return k > cap ? fail(ORBX_ECAPACITY, "cap too small") : ORBX_OK;
+}
+
+int orbx_get_status(orbx_handle h, int reset, int* status) {
+  if (!h || !status) return fail(ORBX_EINVAL, "null argument");
+  HIP_OK(hipSetDevice(h->cfg.device));
+  if (h->ws.ev) HIP_OK(hipEventSynchronize(h->ws.ev));
+  int e = 0;
+  HIP_OK(hipMemcpy(&e, h->plan.err.p, 4, hipMemcpyDeviceToHost));
+  if (reset && e) HIP_OK(hipMemset(h->plan.err.p, 0, 16));
+  *status = e;
+  return ORBX_OK;
+}
+
+int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out) {
+  if (!h || !out) return fail(ORBX_EINVAL, "null argument");
+  const Plan& pl = h->plan;
+  if (frame0 < 0 || nframes < 1 || frame0 + nframes > h->last_batch)
+    return fail(ORBX_EINVAL, "frames [%d, %d) not in the last extraction (%d frames)", frame0, frame0 + nframes,
+                h->last_batch);
+  HIP_OK(hipSetDevice(h->cfg.device));
+  HIP_OK(hipDeviceSynchronize());  // the last extraction may have run on a caller stream
+  const int L = pl.P.L;
+  std::vector<int> t((size_t)nframes * L * 4);
+  HIP_OK(hipMemcpy(t.data(), pl.qties.as<int>() + (size_t)frame0 * L * 4, t.size() * 4, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < (size_t)nframes * L; ++i)
+    for (int k = 0; k < 3; ++k) out[i * 3 + k] = t[i * 4 + k];
+  return ORBX_OK;
 }
 
 int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap, int* n) {

@@ -538,7 +538,13 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   if (P.prof && tid == 0) P.prof[blockIdx.x * 16 + 13] = total;
   if (P.stop == 2) return;
   if (total > cand_lds && total > P.cand_cap) {
-    if (tid == 0) atomicOr(err, 8);
+    // overflow is reported (status bit 8), never truncated: the pair gets no
+    // matches rather than stale outputs of an earlier call
+    for (int i = tid; i < min(n1, K); i += kInitThreads) m12_out[i] = -1;
+    if (tid == 0) {
+      atomicOr(err, 8);
+      nmatches[pr] = 0;
+    }
     return;
   }
   if (total <= cand_lds) {
@@ -632,13 +638,7 @@ int launch_search_init(const InitParams& P0, const orbx_kp* kp1, const uint8_t* 
   // sorted positions are 12-bit fields of the phase-2 entries
   if (P.kp_pitch > 4096 || fixed + 4096 > kInitLdsBudget) return ORBX_ECAPACITY;
   P.cand_lds = (int)((kInitLdsBudget - fixed) / 4) & ~15;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)search_init_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kInitLdsBudget) != hipSuccess)
-      return ORBX_EDEVICE;
-    attr = true;
-  }
+  if (raise_lds_limit((const void*)search_init_kernel, kInitLdsBudget)) return ORBX_EDEVICE;
   const size_t lds = fixed + (size_t)P.cand_lds * 4;
   hipLaunchKernelGGL(search_init_kernel, dim3(pairs), dim3(kInitThreads), lds, (hipStream_t)stream, P, kp1, desc1, n1,
                      kp2, desc2, n2, prev, cand, matches12, nmatches, err);

@@ -11,6 +11,7 @@
 //   quadtree counts  : [B][L]                i32
 //   outputs          : caller's [B][cap] orbx_kp + [B][cap][32] u8 + [B] i32
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/orbx_c.h"
@@ -136,6 +137,7 @@ struct ExtractBuffers {
   int* cell_counts;
   uint32_t* qkeys;
   int* qcounts;
+  int* qties;          // [B][L][4] tie-straddle events, group nodes, kept keys (quadtree)
   uint32_t* qscratch;  // global fallback for quadtree keys (K > kcap_lds)
   uint16_t* qnode_scratch;
   long long qscratch_per_fl;  // entries per (frame, level)
@@ -155,7 +157,7 @@ struct MatchBuffers {
 };
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap,
                         const uint8_t* B, size_t b_pitch, const int* nB, int pairs, int* best_idx,
-                        int* best, int* second, void* stream);
+                        int* best, int* second, int* err, void* stream);
 int launch_search_init(const MatchBuffers& M, const orbx_kp* kp1, const uint8_t* desc1,
                        const int* n1, const orbx_kp* kp2, const uint8_t* desc2, const int* n2,
                        int kp_pitch, int pairs, orbm_grid_bounds b, float* prev_xy, int window,
@@ -251,6 +253,33 @@ struct TriParams {
 };
 int launch_search_tri(const TriParams& P, const TriSide& A, const TriSide& B, const orbm_tri_pair* pairs, int npairs,
                       int* matches12, int* nmatches, void* stream);
+// Stream order of a handle's device workspace: a launch that uses it first
+// waits for the last launch that used it (on whatever stream that was), so
+// calls of one handle on different streams never overlap on its scratch.
+struct WsOrder {
+  hipEvent_t ev = nullptr;
+  bool used = false;
+  int before(hipStream_t s) {
+    return used && hipStreamWaitEvent(s, ev, 0) != hipSuccess ? ORBX_EDEVICE : ORBX_OK;
+  }
+  int after(hipStream_t s) {
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return ORBX_EDEVICE;
+    if (hipEventRecord(ev, s) != hipSuccess) return ORBX_EDEVICE;
+    used = true;
+    return ORBX_OK;
+  }
+  void release() {
+    if (ev) (void)hipEventDestroy(ev);
+    ev = nullptr;
+    used = false;
+  }
+};
+// orbx_host.hip: the workspace order of an extractor (its pyramid is read by
+// the stereo matcher)
+WsOrder* extractor_ws(orbx_handle h);
+// orbx_host.hip: raise a kernel's dynamic-LDS limit on the current device to at
+// least `bytes` (never lowers it; process-wide, thread-safe)
+int raise_lds_limit(const void* fn, size_t bytes);
 // orbx_host.hip: the pyramid of frames [frame0, frame0 + n) of an extractor's last extraction
 int extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int* w, int* hgt, float* scale,
                       float* inv_scale, int* L);

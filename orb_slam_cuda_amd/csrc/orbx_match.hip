@@ -106,14 +106,16 @@ __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t
                                                                    const uint8_t* __restrict__ B, long long b_pitch,
                                                                    const int* __restrict__ nB,
                                                                    int* __restrict__ best_idx, int* __restrict__ best,
-                                                                   int* __restrict__ second) {
+                                                                   int* __restrict__ second, int* err) {
   __shared__ uint4 sB[kTopSplit][kTopChunk][2];
   __shared__ uint2 part[kTopSplit][kTopQueries];
   const int p = blockIdx.y, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int k = wv >> 1, h = wv & 1;
   const int qa = h * 64 + lane, qb = 128 + h * 64 + lane;  // this lane's two queries (of 256)
   const int base = blockIdx.x * kTopQueries;
-  const int na = nA[p], nb = min(nB[p], 65535);  // candidate indices live in the low 16 key bits
+  // candidate indices live in the low 16 key bits; rows past a_cap have no output slot
+  const int na = min(nA[p], a_cap), nb = min(nB[p], 65535);
+  if (tid == 0 && blockIdx.x == 0 && (nB[p] > 65535 || nA[p] > a_cap)) atomicOr(err, 16);
   if (base >= na) return;
   const uint4* Ap = (const uint4*)(A + p * a_pitch);
   const uint4* Bp = (const uint4*)(B + p * b_pitch);
@@ -165,6 +167,7 @@ __global__ __launch_bounds__(kTopThreads) void hamming_top2_kernel(const uint8_t
     r.y = min(min(max(r.x, o.x), r.y), o.y);
     r.x = min(r.x, o.x);
   }
+  if (base + tid >= na) return;
   const long long o = (long long)p * a_cap + base + tid;
   const int d1 = (int)(r.x >> 16);
   best_idx[o] = d1 < 256 ? (int)(r.x & 0xFFFFu) : -1;
@@ -242,7 +245,7 @@ __device__ __forceinline__ void top2_merge(uint32_t& u1, uint32_t& u2, uint32_t 
 __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(ORBX_M_WPE))) void hamming_top2_mfma_kernel(
     const uint8_t* __restrict__ A, long long a_pitch, const int* __restrict__ nA, int a_cap,
     const uint8_t* __restrict__ B, long long b_pitch, const int* __restrict__ nB, int* __restrict__ best_idx,
-    int* __restrict__ best, int* __restrict__ second) {
+    int* __restrict__ best, int* __restrict__ second, int* err) {
   __shared__ __attribute__((aligned(16))) i32x4_t sC[2][kMHalves][kMChunk / 32][4][64];  // [buffer][half][tile][step][lane]
   __shared__ uint2 part[kMHalves > 1 ? kMHalves - 1 : 1][kMQueries];
   // XCD-aware order: a pair's query blocks are consecutive logical ids, which
@@ -251,7 +254,9 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(ORBX_
   const int p = lg / gridDim.x, tid = threadIdx.x, lane = tid & 63;
   const int hf = tid / (64 * kMWaves), wv = (tid >> 6) % kMWaves, ht = tid % (64 * kMWaves);
   const int base = (lg % gridDim.x) * kMQueries;
-  const int na = nA[p], nb = min(nB[p], 65535);  // final keys hold the index in 16 bits
+  // final keys hold the index in 16 bits; rows past a_cap have no output slot
+  const int na = min(nA[p], a_cap), nb = min(nB[p], 65535);
+  if (tid == 0 && (lg % gridDim.x) == 0 && (nB[p] > 65535 || nA[p] > a_cap)) atomicOr(err, 16);
   if (base >= na) return;
   // queries (the B operand), this wave's kMqTiles tiles, held for the whole kernel
   const uint4* Ap = (const uint4*)(A + p * a_pitch);
@@ -576,7 +581,7 @@ __global__ __launch_bounds__(256) void search_bow_kernel(
 // ------------------------------------------------------------ launchers
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap, const uint8_t* B,
                         size_t b_pitch, const int* nB, int pairs, int* best_idx, int* best, int* second,
-                        void* stream) {
+                        int* err, void* stream) {
   // ORBX_TOP2_VALU=1 selects the VALU kernel (A/B timing and the cross-check
   // in tests/test_gpu_match.py; read per call so a test can switch it)
   const char* ev = getenv("ORBX_TOP2_VALU");
@@ -584,12 +589,12 @@ int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_c
   if (!valu) {
     dim3 grid((a_cap + kMQueries - 1) / kMQueries, pairs);
     hipLaunchKernelGGL(hamming_top2_mfma_kernel, grid, dim3(kMThreads), 0, (hipStream_t)stream, A, (long long)a_pitch,
-                       nA, a_cap, B, (long long)b_pitch, nB, best_idx, best, second);
+                       nA, a_cap, B, (long long)b_pitch, nB, best_idx, best, second, err);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
   }
   dim3 grid((a_cap + kTopQueries - 1) / kTopQueries, pairs);
   hipLaunchKernelGGL(hamming_top2_kernel, grid, dim3(kTopThreads), 0, (hipStream_t)stream, A, (long long)a_pitch, nA, a_cap,
-                     B, (long long)b_pitch, nB, best_idx, best, second);
+                     B, (long long)b_pitch, nB, best_idx, best, second, err);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
@@ -630,6 +635,7 @@ struct orbx_matcher {
   int* pose_picks = nullptr;  // pose-projection picks per point (frames x mp_pitch)
   size_t pose_picks_cap = 0;
   hipStream_t stream = nullptr;
+  WsOrder ws;  // stream order of cand / stereo_sad / pose_picks across caller streams
   // staging for the synchronous entry points
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -674,6 +680,8 @@ int orbm_destroy(orbm_handle m) {
   if (!m) return ORBX_OK;
   (void)hipSetDevice(m->device);
   if (m->stream) (void)hipStreamSynchronize(m->stream);
+  if (m->ws.ev) (void)hipEventSynchronize(m->ws.ev);
+  m->ws.release();
   if (m->cand) (void)hipFree(m->cand);
   if (m->err) (void)hipFree(m->err);
   if (m->stereo_sad) (void)hipFree(m->stereo_sad);
@@ -681,6 +689,17 @@ int orbm_destroy(orbm_handle m) {
   if (m->stage) (void)hipFree(m->stage);
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
+  return ORBX_OK;
+}
+
+int orbm_get_status(orbm_handle m, int reset, int* status) {
+  if (!m || !status) return mfail(ORBX_EINVAL, "null argument");
+  MHIP(hipSetDevice(m->device));
+  MHIP(hipDeviceSynchronize());  // the matcher's kernels run on caller streams
+  int e = 0;
+  MHIP(hipMemcpy(&e, m->err, 4, hipMemcpyDeviceToHost));
+  if (reset && e) MHIP(hipMemset(m->err, 0, 16));
+  *status = e;
   return ORBX_OK;
 }
 
@@ -697,7 +716,7 @@ int orbm_hamming_top2(orbm_handle m, const uint8_t* d_A, size_t a_pitch, const i
   if ((a_pitch | b_pitch) & 15) return mfail(ORBX_EINVAL, "pitches must be multiples of 16 bytes");
   MHIP(hipSetDevice(m->device));
   const int rc = launch_hamming_top2(d_A, a_pitch, d_nA, a_cap, d_B, b_pitch, d_nB, pairs, d_best_idx, d_best,
-                                     d_second, stream);
+                                     d_second, m->err, stream);
   return rc ? mfail(rc, "launch failed") : ORBX_OK;
 }
 
@@ -733,8 +752,10 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
     MHIP(hipMemset(prof, 0, (size_t)pairs * 16 * 8));
     P.prof = prof;
   }
+  if (m->ws.before((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
   const int rc = launch_search_init(P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, d_prev_xy, m->cand, d_matches12,
                                     d_nmatches, m->err, pairs, stream);
+  if (!rc && m->ws.after((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "event record failed");
   if (do_prof && !rc) {
     std::vector<long long> h((size_t)pairs * 16);
     MHIP(hipStreamSynchronize((hipStream_t)stream));
@@ -914,10 +935,18 @@ int orbm_compute_stereo_matches_batch(orbm_handle m, orbx_handle left, int left_
   P.jobs_cap = (kp_pitch + P.groups - 1) / P.groups;
   if (stereo_lds_bytes(P.nrows, kp_pitch, P.jobs_cap) > 156 * 1024)
     return mfail(ORBX_ECAPACITY, "stereo row table does not fit in LDS (rows %d, kp_pitch %d)", P.nrows, kp_pitch);
-  return launch_stereo(P, d_kpL, d_descL, d_nL, d_kpR, d_descR, d_nR, pairs, d_uRight, d_depth, m->stereo_sad,
-                       d_nkept, stream) == ORBX_OK
-             ? ORBX_OK
-             : mfail(ORBX_EDEVICE, "stereo launch: %s", hipGetErrorString(hipGetLastError()));
+  // the SAD scratch is the matcher's, the pyramids the extractors': order
+  // this launch after their last users and make their next users wait for it
+  hipStream_t s = (hipStream_t)stream;
+  WsOrder* wl = extractor_ws(left);
+  WsOrder* wr2 = extractor_ws(right);
+  if (m->ws.before(s) || wl->before(s) || wr2->before(s))
+    return mfail(ORBX_EDEVICE, "stream wait on the workspaces failed");
+  if (launch_stereo(P, d_kpL, d_descL, d_nL, d_kpR, d_descR, d_nR, pairs, d_uRight, d_depth, m->stereo_sad, d_nkept,
+                    stream) != ORBX_OK)
+    return mfail(ORBX_EDEVICE, "stereo launch: %s", hipGetErrorString(hipGetLastError()));
+  if (m->ws.after(s) || wl->after(s) || wr2->after(s)) return mfail(ORBX_EDEVICE, "event record failed");
+  return ORBX_OK;
 }
 
 int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle right, const orbx_kp* kpL,
@@ -1235,7 +1264,9 @@ int orbm_search_by_projection_pose_batch(orbm_handle m, int mode, const orbx_kp*
   P.max_rounds = 32;
   if (const char* e = getenv("ORBX_PROJ_ROUNDS")) P.max_rounds = atoi(e);  // tests: force the sequential pass
   const size_t need = (size_t)frames * mp_pitch;
+  if (m->ws.before((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
   if (m->pose_picks_cap < need) {
+    if (m->ws.ev) MHIP(hipEventSynchronize(m->ws.ev));
     if (m->pose_picks) MHIP(hipFree(m->pose_picks));
     m->pose_picks = nullptr;
     m->pose_picks_cap = 0;
@@ -1245,6 +1276,7 @@ int orbm_search_by_projection_pose_batch(orbm_handle m, int mode, const orbx_kp*
   if (launch_search_pose(P, d_kps, d_desc, d_n, d_uright, d_blocked, d_poses, d_mps, d_mpdesc, d_nmp, frames,
                          m->pose_picks, d_out, d_nmatches, stream))
     return mfail(ORBX_EDEVICE, "search_pose launch: %s", hipGetErrorString(hipGetLastError()));
+  if (m->ws.after((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "event record failed");
   return ORBX_OK;
 }
 

@@ -206,13 +206,7 @@ int launch_search_proj(const ProjParams& P, const orbx_kp* kps, const uint8_t* d
                        const float* uright, const uint8_t* blocked, const orbm_map_point_proj* mps,
                        const uint8_t* mpdesc, const int* nmp, int frames, int* out, int* nmatches, void* stream) {
   const size_t lds = proj_lds_bytes(P.kp_pitch);
-  static size_t attr = 0;
-  if (lds > attr) {
-    if (hipFuncSetAttribute((const void*)search_proj_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-        hipSuccess)
-      return ORBX_EDEVICE;
-    attr = lds;
-  }
+  if (raise_lds_limit((const void*)search_proj_kernel, lds)) return ORBX_EDEVICE;
   hipLaunchKernelGGL(search_proj_kernel, dim3(frames), dim3(kProjThreads), lds, (hipStream_t)stream, P, kps, desc, n,
                      uright, blocked, mps, mpdesc, nmp, out, nmatches);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;

@@ -381,12 +381,7 @@ int launch_search_pose(const PoseParams& P, const orbx_kp* kps, const uint8_t* d
                         (const void*)search_pose_kernel<ORBM_PROJ_SIM3_MATCH>};
   if (P.mode < 1 || P.mode > 6) return ORBX_EINVAL;
   const void* fn = fns[P.mode];
-  static size_t attr[7] = {0, 0, 0, 0, 0, 0, 0};
-  if (lds > attr[P.mode]) {
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return ORBX_EDEVICE;
-    attr[P.mode] = lds;
-  }
+  if (raise_lds_limit(fn, lds)) return ORBX_EDEVICE;
 #define ORBX_POSE_LAUNCH(M)                                                                                       \
   hipLaunchKernelGGL(search_pose_kernel<M>, dim3(frames), dim3(kPoseThreads), lds, (hipStream_t)stream, P, kps, \
                      desc, n, uright, blocked, poses, mps, mpdesc, nmp, picks, out, nmatches)

@@ -63,7 +63,8 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
                                                               uint32_t* __restrict__ qscratch,
                                                               uint16_t* __restrict__ qnscratch,
                                                               uint32_t* __restrict__ qkeys,
-                                                              int* __restrict__ qcounts, int* err, int* dbg) {
+                                                              int* __restrict__ qcounts, int* __restrict__ qties,
+                                                              int* err, int* dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
   int dbg_rounds = 0, dbg_sorted = 0;
@@ -170,6 +171,7 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     }
     s_var[0] = n;  // list size
     s_var[1] = 0;  // sorted-phase flag
+    s_var[6] = s_var[7] = s_var[8] = 0;  // tie-straddle events / group nodes / kept keys
   }
   __syncthreads();
   for (int k = tid; k < K; k += kQtThreads) knode[k] = (uint16_t)rootCnt[knode[k]];
@@ -328,6 +330,21 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
       __syncthreads();
       ph(4);
       const int m = s_var[2];
+      // tie-straddle exposure: the cut-off at N fell inside a
+      // group of equal-size candidates, so the creation-order stand-in for
+      // the reference's heap-pointer order (src/ORBextractor.cc:1041) picked
+      // which of them were split; count the group and the kept keys it yields
+      if (m > 0 && m < ncand && (s_sort[m - 1] >> 40) == (s_sort[m] >> 40)) {
+        const unsigned long long sz = s_sort[m - 1] >> 40;
+        for (int j = tid; j < ncand; j += kQtThreads) {
+          const unsigned long long key = s_sort[j];
+          if ((key >> 40) == sz) {
+            atomicAdd(&s_var[7], 1);
+            atomicAdd(&s_var[8], j < m ? nonempty(cc[(int)(key & 0xFFFF)]) : 1);
+          }
+        }
+        if (tid == 0) s_var[6] += 1;
+      }
       for (int j = tid; j < m; j += kQtThreads) tA[j] = nonempty(cc[ord[j]]);
       __syncthreads();
       const int T = block_scan_excl<kQtThreads>(tA, m, s_tmp);
@@ -434,6 +451,11 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     out[n] = keys[0xFFFFFFFFu - (uint32_t)(s_sort[n] & 0xFFFFFFFFull)];
   if (tid == 0) {
     qcounts[f * P.L + l] = min(size, g.kcap);
+    int* qt = qties + ((long long)f * P.L + l) * 4;
+    qt[0] = s_var[6];
+    qt[1] = s_var[7];
+    qt[2] = s_var[8];
+    qt[3] = 0;
     if (size > g.kcap) atomicOr(err, 4);
   }
   if (dbg && tid == 0) {  // diagnostics only (ORBX_QT_PROF=1)
@@ -471,7 +493,7 @@ int launch_quadtree(const ExtractParams& P, const ExtractBuffers& X, int batch, 
   const int nwg = P.L * batch;
   if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)nwg * 64);
   hipLaunchKernelGGL(quadtree_kernel, dim3(P.L, batch), dim3(kQtThreads), quadtree_lds_bytes(P), s, P,
-                     X.cell_counts, X.slots, X.cells, X.qscratch, X.qnode_scratch, X.qkeys, X.qcounts, X.err,
+                     X.cell_counts, X.slots, X.cells, X.qscratch, X.qnode_scratch, X.qkeys, X.qcounts, X.qties, X.err,
                      prof ? dbg : nullptr);
   if (prof) {
     std::vector<int> h((size_t)nwg * 16);

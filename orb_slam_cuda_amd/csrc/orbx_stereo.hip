@@ -426,13 +426,7 @@ int launch_stereo(const StereoParams& P, const orbx_kp* kpL, const uint8_t* desc
                   float* depth, int* sad, int* nkept, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = stereo_lds_bytes(P.nrows, P.kp_pitch, P.jobs_cap);
-  static size_t attr_lds = 0;  // dynamic LDS the kernel is currently allowed
-  if (lds > attr_lds) {
-    if (hipFuncSetAttribute((const void*)stereo_match_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
-      return ORBX_EDEVICE;
-    attr_lds = lds;
-  }
+  if (raise_lds_limit((const void*)stereo_match_kernel, lds)) return ORBX_EDEVICE;
   dim3 grid(P.groups, pairs);
   hipLaunchKernelGGL(stereo_match_kernel, grid, dim3(kStThreads), lds, s, P, kpL, descL, nL, kpR, descR, nR,
                      uRight, depth, sad);

@@ -278,7 +278,6 @@ struct orbv_vocabulary {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   hipStream_t stream = nullptr;
-  size_t attr_lds = 0;
 };
 
 static int ws_reserve(orbv_vocabulary* v, size_t bytes) {
@@ -483,10 +482,8 @@ int orbv_transform_batch(orbv_handle v, const uint8_t* d_desc, size_t desc_pitch
   int S = 1;
   while (S < cap) S <<= 1;
   const size_t lds = (size_t)S * 12;
-  if (lds > v->attr_lds) {
-    VHIP(hipFuncSetAttribute((const void*)voc_assemble_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    v->attr_lds = lds;
-  }
+  if (raise_lds_limit((const void*)voc_assemble_kernel, lds))
+    return vfail(ORBX_EDEVICE, "hipFuncSetAttribute(voc_assemble_kernel): %s", hipGetErrorString(hipGetLastError()));
   int l1 = v->scoring != 1;
   const int must = v->scoring != 5;
   const int tf = v->weighting == 0 || v->weighting == 1;

@@ -149,3 +149,24 @@ class ORBextractor:
         n = C.c_int(0)
         check(lib().orbx_get_stage_times(self._h, ptr(ms), names, 8, C.byref(n)))
         return {names[i].decode(): float(ms[i]) for i in range(n.value)}
+
+    def tie_stats(self, frame0: int = 0, nframes: int = 1) -> np.ndarray:
+        """Quadtree tie-rule exposure of the last extraction (orbx_get_tie_stats):
+        int array (nframes, nlevels, 3) of {events, group nodes, kept keypoints}."""
+        out = np.zeros((nframes, self.nlevels, 3), np.int32)
+        check(lib().orbx_get_tie_stats(self._h, frame0, nframes, ptr(out)))
+        return out
+
+    def status(self, reset: bool = True) -> int:
+        """Device status word of the handle's kernels (orbx_get_status); 0 = ok."""
+        st = C.c_int(0)
+        check(lib().orbx_get_status(self._h, int(reset), C.byref(st)))
+        return st.value
+
+
+def brief_pattern(pattern: str = "fork") -> np.ndarray:
+    """The rBRIEF test table the kernels use (orbx_get_pattern), 1024 ints in the
+    reference's bit_pattern_31_ order (src/ORBextractor.cc:236-494). Host only."""
+    out = np.zeros(1024, np.int32)
+    check(lib().orbx_get_pattern(PATTERNS[pattern], ptr(out)))
+    return out

@@ -238,6 +238,12 @@ class ORBmatcher:
     def handle(self):
         return self._h
 
+    def status(self, reset: bool = True) -> int:
+        """Device status word of the matcher's batched kernels (orbm_get_status); 0 = ok."""
+        st = C.c_int(0)
+        check(lib().orbm_get_status(self._h, int(reset), C.byref(st)), matcher=True)
+        return st.value
+
     @staticmethod
     def DescriptorDistance(a: np.ndarray, b: np.ndarray) -> int:
         a = np.ascontiguousarray(a, np.uint8).reshape(32)

@@ -1,0 +1,101 @@
+"""Pins of the oracle (and the product's tables) to bytes the reference holds,
+and the quadtree tie-rule exposure counter.
+
+* bit_pattern_31_: tests/golden/bit_pattern.npy is parsed from the reference
+  source text (tests/golden/make_pattern.py, src/ORBextractor.cc:236-494, the
+  fork's `VX_FAILURE-2` element at :261-262). Both the oracle's table and the
+  table liborbx.so uploads to the device must equal it; every descriptor bit
+  depends on it.
+* tie straddles: DistributeOctTree splits equal-size nodes in heap-pointer
+  order (src/ORBextractor.cc:1041-1042); the oracle and the kernels use node
+  creation order instead. The counter reports where that choice decided
+  which keypoints were kept.
+"""
+import os
+
+import numpy as np
+
+from conftest import GOLDEN
+
+
+def golden_pattern():
+    return np.load(os.path.join(GOLDEN, "bit_pattern.npy"))
+
+
+def test_pattern_golden_shape_and_fork_entry():
+    t = golden_pattern()
+    assert t.dtype == np.int8 and t.shape == (1024,)
+    assert int(t[96]) == -3            # VX_FAILURE - 2 (src/ORBextractor.cc:261-262)
+    assert t.min() >= -13 and t.max() <= 12  # 31x31 patch, as the descriptor assumes
+
+
+def test_oracle_pattern_equals_reference_table(O):
+    t = golden_pattern()
+    assert np.array_equal(O.pattern(0), t)
+    up = O.pattern(1)
+    diff = np.nonzero(up != t)[0]
+    assert diff.tolist() == [96] and int(up[96]) == -2  # upstream ORB-SLAM2
+
+
+def test_product_pattern_equals_reference_table():
+    from orb_slam_cuda_amd.extractor import brief_pattern
+    t = golden_pattern().astype(np.int32)
+    assert np.array_equal(brief_pattern("fork"), t)
+    up = brief_pattern("upstream")
+    assert np.nonzero(up != t)[0].tolist() == [96] and int(up[96]) == -2
+
+
+def test_pattern_script_parses_reference_if_present():
+    src = "/root/reference/src/ORBextractor.cc"
+    if not os.path.exists(src):
+        return  # the GPU box has no reference tree; the committed .npy is the pin
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_pattern", os.path.join(GOLDEN, "make_pattern.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    with open(src, encoding="utf-8", errors="replace") as f:
+        assert np.array_equal(m.parse(f.read()), golden_pattern())
+
+
+def _kps(xy):
+    from oracle.oracle import KP_DTYPE
+    k = np.zeros(len(xy), KP_DTYPE)
+    k["x"] = [p[0] for p in xy]
+    k["y"] = [p[1] for p in xy]
+    k["response"] = 10
+    k["octave"] = 0
+    k["class_id"] = -1
+    return k
+
+
+def test_tie_straddle_known_case(O):
+    # one 40x40 root, two keys in each quadrant (different sub-quadrants):
+    # round 1 splits the root into four size-2 nodes (4 < N = 5); 4 + 4*3 > 5
+    # starts the sorted phase over four EQUAL sizes; splitting the first one
+    # reaches 5 nodes, so the tie rule alone chose which quadrant was split
+    pts = [(5, 5), (15, 15), (25, 5), (35, 15), (5, 25), (15, 35), (25, 25), (35, 35)]
+    kept = O.distribute(_kps(pts), 0, 40, 0, 40, 5)
+    assert len(kept) == 5
+    assert O.distribute_ties(_kps(pts), 0, 40, 0, 40, 5) == (1, 4, 5)  # event, 4 nodes, 2 + 3 kept keys
+
+
+def test_no_tie_straddle_when_sizes_differ(O):
+    # the same, but one quadrant holds 3 keys: it is split first, alone in its size group
+    pts = [(5, 5), (15, 15), (12, 3), (25, 5), (35, 15), (5, 25), (15, 35), (25, 25), (35, 35)]
+    assert O.distribute_ties(_kps(pts), 0, 40, 0, 40, 5) == (0, 0, 0)
+
+
+def test_tie_stats_invariants_on_synthetic_frame(O):
+    from orb_slam_cuda_amd.synth import synth_frame
+    W, H = 640, 240
+    cfg = O.config(nfeatures=600, width=W, height=H)
+    img = synth_frame(3, W, H)
+    st = O.tie_stats(cfg, img)
+    kp, _ = O.extract(cfg, img)
+    per_level = np.bincount(kp["octave"], minlength=8)
+    assert set(np.unique(st["events"])) <= {0, 1}
+    for l in range(8):
+        if st["events"][l]:
+            assert 2 <= st["nodes"][l] <= st["kps"][l] <= per_level[l]
+        else:
+            assert st["nodes"][l] == st["kps"][l] == 0
