@@ -11,16 +11,33 @@ One step = one batch of B frames resident in HBM:
     check) used by monocular initialisation.
 Frame t-1 of the first frame of a batch is the last frame of the previous
 batch (carried on device), so every step does B extractions + B matches.
+Step k processes batch k mod (pool / B) of a resident pool of synthetic
+frames larger than the 256 MB MALL (--pool, default 640 frames = 308 MB),
+so level 0 streams from HBM instead of staying in the last-level cache.
 
-Two streams: the matching of batch k (a few wide workgroups per frame pair)
-runs on its own stream, overlapping the extraction of batch k+1; outputs are
-triple-buffered and ordered by events (see step()). --serial runs everything
-on one stream.
+Streams: the matching of batch k (a few wide workgroups per frame pair) runs
+on its own stream, overlapping the extraction of batch k+1; outputs are
+triple-buffered and ordered by events (see MonoPipeline.step). --serial runs
+everything on one stream.
 
-Multi-GPU: one process per GPU, frames sharded by rank (each rank streams its
-own synthetic sequence), no data-path collective ("weak" scaling). The
-barrier and the max-over-ranks of the timed region go through
-torch.distributed with the gloo backend (control plane only).
+Extra legs in the same JSON line (rank 0, N = 1; skipped with --no-latency /
+--no-host-stream):
+  * "latency": the call Tracking makes per frame, orbx_extract on ONE host
+    1241x376 image (host in, host keypoints + descriptors out; pinned
+    staging, captured hipGraph) and the host SearchForInitialization call,
+    median / p99 over 200 calls, beside the oracle's single-thread latency;
+  * "host_stream": the same C3 pipeline fed from pinned host memory every
+    step (H2D of each batch on a copy stream, keypoints / descriptors /
+    matches copied back), PCIe-inclusive frames/s.
+
+Multi-GPU: one process per GPU. `--gpus N` without a torchrun environment
+spawns N worker processes (multiprocessing "spawn", before this process
+touches the GPU); under torchrun (RANK set) each rank is one worker and
+--gpus must equal WORLD_SIZE. Each rank selects device LOCAL_RANK before any
+allocation, streams its own synthetic sequence and matches within its shard:
+no data-path collective ("weak" scaling). The barrier, the max-over-ranks of
+the timed region and the per-rank figures go through torch.distributed with
+the gloo backend (control plane only).
 
 Prints ONE JSON line (rank 0). Per-kernel durations are measured live with
 HIP events recorded on the launch stream around every stage of every step.
@@ -31,6 +48,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
 import sys
 import time
 
@@ -51,6 +69,7 @@ STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_t
 KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
            "hamming_top2": "hamming_top2_mfma_kernel", "search_init": "search_init_kernel"}
+KP, DS = 28, 32  # bytes of one orbx_kp (cv::KeyPoint) and one descriptor
 
 CONFIGS = {
     "kitti": dict(W=1241, H=376, nfeatures=2000,
@@ -61,7 +80,8 @@ CONFIGS = {
                             "left/right extraction on separate HIP streams + Frame::ComputeStereoMatches"),
     "euroc": dict(W=752, H=480, nfeatures=1000,
                   workload="C5: EuRoC-shaped 752x480 mono u8, nFeatures=1000, 8 levels x1.2, "
-                           "extract + match vs t-1 (dense Hamming top-2 + SearchForInitialization)"),
+                           "extract + match vs t-1 (dense Hamming top-2 + SearchForInitialization), "
+                           "one sequence per GPU"),
 }
 
 
@@ -88,12 +108,14 @@ def algorithmic_bytes(W, H, nkp):
     }
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs of this node, one worker process each")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--pool", type=int, default=640,
+                    help="resident synthetic frames per GPU, cycled batch by batch (> the 256 MB MALL)")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="frame-parallel oracle workers for cpu_baseline (0 = the host's CPU share, OMP_NUM_THREADS)")
@@ -110,180 +132,392 @@ def main():
                     help="2: SearchForInitialization on its own stream, beside the dense top-2")
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
                     help="stream that copies a batch's last frame for the next batch's first pair")
-    args = ap.parse_args()
+    ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency leg")
+    ap.add_argument("--no-host-stream", action="store_true", help="skip the host-streamed throughput leg")
+    ap.add_argument("--host-steps", type=int, default=30, help="timed steps of the host-streamed leg")
+    ap.add_argument("--spawn", action="store_true", help="use the worker launcher even for --gpus 1")
+    ap.add_argument("--stub-worker", action="store_true", help=argparse.SUPPRESS)  # launcher tests (CPU)
+    return ap.parse_args(argv)
 
+
+# --------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def visible_gpus() -> int:
+    """GPUs this node exposes, counted without initialising HIP in this process
+    (torch.cuda.device_count() does not initialise the runtime on this image)."""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+def _worker_entry(argv, rank, world, port):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    worker(parse_args(argv))
+
+
+def launch(args, argv) -> int:
+    """One worker process per GPU (spawned before this process makes any GPU
+    call); returns the first non-zero worker exit code, or 0."""
+    import multiprocessing as mp
+    N = args.gpus
+    if not args.stub_worker:
+        n = visible_gpus()
+        if N > n:
+            raise SystemExit(f"bench.py: --gpus {N} but only {n} GPU(s) visible; refusing to oversubscribe")
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_entry, args=(argv, r, N, port), daemon=False) for r in range(N)]
+    for p in procs:
+        p.start()
+    code = 0
+    for p in procs:
+        p.join()
+        if p.exitcode != 0 and code == 0:
+            code = p.exitcode if p.exitcode > 0 else 1
+            for q in procs:  # a dead rank would leave the others blocked in the barrier
+                if q.is_alive():
+                    q.terminate()
+    return code
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "RANK" not in os.environ and (args.gpus > 1 or args.spawn):
+        code = launch(args, argv)
+        if code:
+            raise SystemExit(code)
+        return
+    worker(args)
+
+
+def aggregate(frames_rank: int, wall_rank: float, dist, world: int) -> dict:
+    """Whole-job figures: value = frames of all ranks / the slowest rank's time."""
+    from orb_slam_cuda_amd import sharding
+    wall = sharding.max_over_ranks(wall_rank, dist)
+    frames = int(round(sharding.sum_over_ranks(float(frames_rank), dist)))
+    per_rank = [frames_rank / wall_rank]
+    if dist is not None:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, round(frames_rank / wall_rank, 2))
+    return {"value": frames / wall, "wall": wall, "frames": frames, "per_rank": [round(v, 2) for v in per_rank]}
+
+
+def worker(args):
     from orb_slam_cuda_amd import sharding
     rank, world, local = sharding.rank_info()
-    # control plane only (gloo); initialised before liborbx loads so one HIP runtime is in the process
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    # control plane only (gloo), initialised before liborbx loads so one HIP runtime is in the process
     dist = sharding.init_control_plane()
+    try:
+        if args.stub_worker:
+            return run_stub(args, rank, world, dist)
+        from orb_slam_cuda_amd import _lib
+        L = _lib.lib()
+        ndev = _lib.device_count()
+        if local >= ndev:
+            raise SystemExit(f"bench.py: rank {rank} needs device {local}, only {ndev} visible")
+        # the device is selected before ANY allocation, stream or event of this process
+        _lib.check(L.orbx_set_device(local))
+        cfg = CONFIGS[args.config]
+        if cfg.get("stereo"):
+            run_stereo(args, cfg, rank, world, local, dist)
+        else:
+            run_mono(args, cfg, rank, world, local, dist)
+    finally:
+        if dist is not None:
+            dist.destroy_process_group()
 
-    import orb_slam_cuda_amd as pkg
-    from orb_slam_cuda_amd import _lib
-    from orb_slam_cuda_amd.synth import SynthSequence
 
-    L = _lib.lib()
-    cfg = CONFIGS[args.config]
-    if cfg.get("stereo"):
-        return run_stereo(args, cfg, rank, world, local, dist)
-    W, H, NF, B = cfg["W"], cfg["H"], cfg["nfeatures"], args.batch
-    pitch = (W + 63) & ~63
+def run_stub(args, rank, world, dist):
+    """CPU stand-in for the GPU work (launcher tests): rank r 'processes'
+    batch x steps frames in (1 + r) x 10 ms; everything else is the real
+    control plane and reporting path."""
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (1 + rank))
+    wall = time.perf_counter() - t0
+    agg = aggregate(args.batch * args.steps, wall, dist, world)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(agg["value"], 2), "unit": "frames/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "per_rank_frames_per_s": agg["per_rank"],
+                          "frames_total": agg["frames"], "data": "stub (no GPU work)"}), flush=True)
 
-    seq = SynthSequence(sharding.sequence_seed(rank), W, H)
-    frames = seq.frames(B)
-    host = np.zeros((B, H, pitch), np.uint8)
-    host[:, :, :W] = frames
-    d_frames = _lib.DeviceArray(host.nbytes)
-    check = _lib.check
-    check(L.orbx_set_device(local))
-    d_frames.upload(host)
 
-    S = args.split
-    if S < 1 or B % S:
-        raise SystemExit("--split must divide --batch")
-    BS = B // S  # frames per extraction launch
-    exts = [pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=BS) for _ in range(S)]
-    ext = exts[0]
-    cap = ext.frame_capacity
-    KP, DS = 28, 32
-    # three output sets: batch k writes set k % 3, slots 1..B, and its last
-    # frame is copied into slot 0 of set (k+1) % 3 (frame t-1 of the next
-    # batch's first frame).
-    NS = 3
-    d_kps = [_lib.DeviceArray((B + 1) * cap * KP) for _ in range(NS)]
-    d_desc = [_lib.DeviceArray((B + 1) * cap * DS) for _ in range(NS)]
-    d_counts = [_lib.DeviceArray((B + 1) * 4) for _ in range(NS)]
-    for d in d_counts:
-        d.zero()
-    matcher = pkg.ORBmatcher(0.9, True, device=local, max_pairs=B, max_kps=cap)
-    d_bi, d_bd, d_sd = (_lib.DeviceArray(B * cap * 4) for _ in range(3))
-    d_m12 = _lib.DeviceArray(B * cap * 4)
-    d_nm = _lib.DeviceArray(B * 4)
-    # the extraction stream may ask the dispatcher for priority (--priority):
-    # it is the critical path, matching fills the compute units it leaves idle
-    prio = 1 if args.priority else None
-    s_exts = [_lib.Stream(prio) for _ in range(S)]
-    s_ext = s_exts[0]
-    s_match = _lib.Stream(0 if args.priority else None) if not args.serial else s_ext
-    two_match = args.match_streams == 2 and not args.serial and not args.no_match and args.carry == "match"
-    s_init = _lib.Stream(0 if args.priority else None) if two_match else s_match
-    bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
-    vp = lambda a: C.c_void_p(a)
-    n_ev = 12  # 6 extraction stage marks (extract stream) + 3 matching marks + 2 BoW marks (match stream) + init start
-    voc = None
-    if args.bow:
-        from orb_slam_cuda_amd.synth import synthetic_vocabulary
-        voc = pkg.ORBVocabulary.from_arrays(synthetic_vocabulary(10, 6, seed=1), device=local)
-        d_bw, d_bn, d_fn, d_fi, d_fnn = (_lib.DeviceArray(B * cap * 4), _lib.DeviceArray(B * 4),
-                                         _lib.DeviceArray(B * cap * 4), _lib.DeviceArray(B * cap * 4),
-                                         _lib.DeviceArray(B * 4))
-        d_bv = _lib.DeviceArray(B * cap * 8)
-        d_fo = _lib.DeviceArray(B * (cap + 1) * 4)
-        d_vw = (_lib.DeviceArray(B * cap * 4), _lib.DeviceArray(B * cap * 4), _lib.DeviceArray(B * cap * 8))
+# --------------------------------------------------------------------------- mono pipeline
+class MonoPipeline:
+    """The C3 / C5 step: extraction of a batch on S streams, matching of the
+    same batch against t-1 on the matching stream, overlapping the next
+    batch's extraction. Input either from a resident device pool (default)
+    or from pinned host memory (host=True: H2D per batch on a copy stream,
+    results copied back on a second one)."""
 
-    def step(k, evs, ev_ext, ev_done):
-        """Batch k: extraction on s_ext; carry copy and matching of the same
-        batch on s_match, overlapping the extraction of batch k+1 (--serial:
-        one stream, no overlap). Extraction k waits for matching k-3 (the
-        last reader of set k % 3); matching k waits for extraction k."""
+    NS = 3  # output sets: batch k writes set k % 3
+
+    def __init__(self, args, cfg, local, frames_pool, host=False, need_events=True):
+        import orb_slam_cuda_amd as pkg
+        from orb_slam_cuda_amd import _lib
+        self.args, self.cfg, self.host = args, cfg, host
+        self.L, self.check, self._lib = _lib.lib(), _lib.check, _lib
+        W, H, NF, B = cfg["W"], cfg["H"], cfg["nfeatures"], args.batch
+        self.W, self.H, self.B = W, H, B
+        self.pitch = pitch = (W + 63) & ~63
+        self.fbytes = H * pitch
+        npool = len(frames_pool)
+        if npool % B:
+            raise SystemExit("--pool must be a multiple of --batch")
+        self.nbatches = npool // B
+        if host:
+            self.h_pool = _lib.HostArray((npool, H, pitch), np.uint8)
+            self.h_pool.a[:, :, :W] = frames_pool
+            self.d_in = [_lib.DeviceArray(B * self.fbytes) for _ in range(self.NS)]  # input ring
+        else:
+            self.d_pool = _lib.DeviceArray(npool * self.fbytes)
+            chunk = np.zeros((B, H, pitch), np.uint8)
+            for b in range(self.nbatches):
+                chunk[:, :, :W] = frames_pool[b * B:(b + 1) * B]
+                self.d_pool.upload(chunk, b * B * self.fbytes)
+        S = args.split
+        if S < 1 or B % S:
+            raise SystemExit("--split must divide --batch")
+        self.S, self.BS = S, B // S
+        self.exts = [pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=self.BS) for _ in range(S)]
+        self.cap = cap = self.exts[0].frame_capacity
+        NS = self.NS
+        DA = _lib.DeviceArray
+        self.d_kps = [DA((B + 1) * cap * KP) for _ in range(NS)]
+        self.d_desc = [DA((B + 1) * cap * DS) for _ in range(NS)]
+        self.d_counts = [DA((B + 1) * 4) for _ in range(NS)]
+        for d in self.d_counts:
+            d.zero()
+        self.matcher = pkg.ORBmatcher(0.9, True, device=local, max_pairs=B, max_kps=cap)
+        self.d_bi, self.d_bd, self.d_sd, self.d_m12 = ([DA(B * cap * 4) for _ in range(NS)] for _ in range(4))
+        self.d_nm = [DA(B * 4) for _ in range(NS)]
+        if host:
+            HA = _lib.HostArray
+            self.h_kps = [HA(B * cap * KP, np.uint8) for _ in range(NS)]
+            self.h_desc = [HA(B * cap * DS, np.uint8) for _ in range(NS)]
+            self.h_counts = [HA(B, np.int32) for _ in range(NS)]
+            self.h_m12 = [HA(B * cap, np.int32) for _ in range(NS)]
+            self.h_nm = [HA(B, np.int32) for _ in range(NS)]
+            self.s_h2d, self.s_d2h = _lib.Stream(), _lib.Stream()
+        prio = 1 if args.priority else None
+        self.s_exts = [_lib.Stream(prio) for _ in range(S)]
+        self.s_ext = self.s_exts[0]
+        self.s_match = _lib.Stream(0 if args.priority else None) if not args.serial else self.s_ext
+        self.two_match = (args.match_streams == 2 and not args.serial and not args.no_match
+                          and args.carry == "match" and not host)
+        self.s_init = _lib.Stream(0 if args.priority else None) if self.two_match else self.s_match
+        self.bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
+        self.voc = None
+        if args.bow and not host:
+            from orb_slam_cuda_amd.synth import synthetic_vocabulary
+            self.voc = pkg.ORBVocabulary.from_arrays(synthetic_vocabulary(10, 6, seed=1), device=local)
+            self.d_bw, self.d_bn, self.d_fn, self.d_fi, self.d_fnn = (DA(B * cap * 4), DA(B * 4), DA(B * cap * 4),
+                                                                      DA(B * cap * 4), DA(B * 4))
+            self.d_bv = DA(B * cap * 8)
+            self.d_fo = DA(B * (cap + 1) * 4)
+            self.d_vw = (DA(B * cap * 4), DA(B * cap * 4), DA(B * cap * 8))
+        self.need_events = need_events
+        self.ev = {}
+
+    def _event(self, name, k):
+        e = self.ev.get((name, k))
+        if e is None:
+            e = self.ev[(name, k)] = self._lib.Event()
+        return e
+
+    def alloc_events(self, total):
+        E = self._lib.Event
+        n_ev = 12  # 6 extraction stage marks + 3 matching marks + 2 BoW marks + init start
+        self.evsets = [[E() for _ in range(n_ev)] for _ in range(total)] if self.need_events else None
+        self.ev_ext = [E() for _ in range(total)]
+        self.ev_done = [E() for _ in range(total)]
+        self.ev_done2 = [E() for _ in range(total)]
+        self.ev_carry = [E() for _ in range(total)]
+        self.ev_part = [[E() for _ in range(self.S)] for _ in range(total)]
+        if self.host:
+            self.ev_in = [E() for _ in range(total)]
+            self.ev_out = [E() for _ in range(total)]
+
+    def frames_ptr(self, k):
+        if self.host:
+            return self.d_in[k % self.NS].ptr
+        return self.d_pool.ptr + (k % self.nbatches) * self.B * self.fbytes
+
+    def step(self, k):
+        """Batch k: extraction on the extraction streams; carry copy and
+        matching of the same batch on s_match, overlapping the extraction of
+        batch k+1 (--serial: one stream). Extraction k waits for matching k-3
+        (the last reader of set k % 3); matching k waits for extraction k."""
+        a, L, check = self.args, self.L, self.check
+        vp = C.c_void_p
+        B, BS, cap, NS = self.B, self.BS, self.cap, self.NS
         b, nb = k % NS, (k + 1) % NS
-        # the batch is cut into S contiguous parts, one extractor and stream each
-        for h, (ex, se) in enumerate(zip(exts, s_exts)):
-            if h == 0:
+        evs = self.evsets[k] if self.evsets is not None else None
+        if self.host:
+            # H2D of batch k into input slot k % 3, after extraction k-3 read it
+            if k >= NS:
+                self.s_h2d.wait(self.ev_ext[k - NS])
+            src = self.h_pool.ptr + (k % self.nbatches) * B * self.fbytes
+            check(L.orbx_memcpy_htod_async(vp(self.d_in[k % NS].ptr), vp(src), B * self.fbytes, self.s_h2d.s))
+            self.ev_in[k].record(self.s_h2d)
+        fp = self.frames_ptr(k)
+        for h, (ex, se) in enumerate(zip(self.exts, self.s_exts)):
+            if h == 0 and evs is not None:
                 arr = (C.c_void_p * 6)(*[e.e.value for e in evs[:6]])
                 check(L.orbx_set_stage_events(ex.handle, arr))
-            if not args.serial and k >= 3:
-                se.wait(ev_done[k - 3])  # matching k-3 was the last reader of set k % 3
-                if two_match:
-                    se.wait(ev_done2[k - 3])
-            sv = se if not args.serial else s_ext
-            check(L.orbx_extract_batch(ex.handle, vp(d_frames.ptr + h * BS * H * pitch), BS, H * pitch, pitch,
-                                       vp(d_kps[b].ptr + (1 + h * BS) * cap * KP),
-                                       vp(d_desc[b].ptr + (1 + h * BS) * cap * DS),
-                                       vp(d_counts[b].ptr + 4 * (1 + h * BS)), sv.s))
-            if h > 0 and not args.serial:
-                ev_part[k][h].record(se)
-                s_ext.wait(ev_part[k][h])
-        def carry(st):
-            check(L.orbx_memcpy_dtod_async(vp(d_kps[nb].ptr), vp(d_kps[b].ptr + B * cap * KP), cap * KP, st.s))
-            check(L.orbx_memcpy_dtod_async(vp(d_desc[nb].ptr), vp(d_desc[b].ptr + B * cap * DS), cap * DS, st.s))
-            check(L.orbx_memcpy_dtod_async(vp(d_counts[nb].ptr), vp(d_counts[b].ptr + B * 4), 4, st.s))
+            sv = se if not a.serial else self.s_ext
+            if self.host:
+                sv.wait(self.ev_in[k])
+            if not a.serial and k >= NS:
+                sv.wait(self.ev_done[k - NS])  # matching k-3 was the last reader of set k % 3
+                if self.two_match:
+                    sv.wait(self.ev_done2[k - NS])
+                if self.host:
+                    sv.wait(self.ev_out[k - NS])  # and the read-back of batch k-3
+            check(L.orbx_extract_batch(ex.handle, vp(fp + h * BS * self.fbytes), BS, self.fbytes, self.pitch,
+                                       vp(self.d_kps[b].ptr + (1 + h * BS) * cap * KP),
+                                       vp(self.d_desc[b].ptr + (1 + h * BS) * cap * DS),
+                                       vp(self.d_counts[b].ptr + 4 * (1 + h * BS)), sv.s))
+            if h > 0 and not a.serial:
+                self.ev_part[k][h].record(se)
+                self.s_ext.wait(self.ev_part[k][h])
 
-        if args.carry == "ext" or args.serial:
+        def carry(st):
+            check(L.orbx_memcpy_dtod_async(vp(self.d_kps[nb].ptr), vp(self.d_kps[b].ptr + B * cap * KP), cap * KP, st.s))
+            check(L.orbx_memcpy_dtod_async(vp(self.d_desc[nb].ptr), vp(self.d_desc[b].ptr + B * cap * DS), cap * DS,
+                                           st.s))
+            check(L.orbx_memcpy_dtod_async(vp(self.d_counts[nb].ptr), vp(self.d_counts[b].ptr + B * 4), 4, st.s))
+
+        s_match, s_init = self.s_match, self.s_init
+        if a.carry == "ext" or a.serial:
             # slot 0 of set (k+1) % 3 was last read by matching k-2
-            if k >= 2 and not args.serial:
-                s_ext.wait(ev_done[k - 2])
-            carry(s_ext)
-        ev_ext[k].record(s_ext)
-        if not args.serial:
-            s_match.wait(ev_ext[k])
-        if args.carry == "match" and not args.serial:
-            if two_match and k >= 2:
-                s_match.wait(ev_done2[k - 2])  # SearchForInitialization k-2 also read set (k+1) % 3
+            if k >= 2 and not a.serial:
+                self.s_ext.wait(self.ev_done[k - 2])
+            carry(self.s_ext)
+        self.ev_ext[k].record(self.s_ext)
+        if not a.serial:
+            s_match.wait(self.ev_ext[k])
+        if a.carry == "match" and not a.serial:
+            if self.two_match and k >= 2:
+                s_match.wait(self.ev_done2[k - 2])  # SearchForInitialization k-2 also read set (k+1) % 3
             carry(s_match)  # in order after matching k-2, the last reader of set (k+1) % 3
-            ev_carry[k].record(s_match)
-        if voc is not None:
+            self.ev_carry[k].record(s_match)
+        if self.voc is not None:
             evs[9].record(s_match)
             # Frame::ComputeBoW of the batch's frames (slots 1..B), levelsup 4 (src/Frame.cc:398)
-            check(L.orbv_transform_batch(voc.handle, vp(d_desc[b].ptr + cap * DS), cap * DS, vp(d_counts[b].ptr + 4),
-                                         B, cap, 4, vp(d_bw.ptr), vp(d_bv.ptr), vp(d_bn.ptr), vp(d_fn.ptr),
-                                         vp(d_fo.ptr), vp(d_fi.ptr), vp(d_fnn.ptr), vp(d_vw[0].ptr), vp(d_vw[1].ptr),
-                                         vp(d_vw[2].ptr), s_match.s), vocabulary=True)
+            check(L.orbv_transform_batch(self.voc.handle, vp(self.d_desc[b].ptr + cap * DS), cap * DS,
+                                         vp(self.d_counts[b].ptr + 4), B, cap, 4, vp(self.d_bw.ptr), vp(self.d_bv.ptr),
+                                         vp(self.d_bn.ptr), vp(self.d_fn.ptr), vp(self.d_fo.ptr), vp(self.d_fi.ptr),
+                                         vp(self.d_fnn.ptr), vp(self.d_vw[0].ptr), vp(self.d_vw[1].ptr),
+                                         vp(self.d_vw[2].ptr), s_match.s), vocabulary=True)
             evs[10].record(s_match)
-        evs[6].record(s_match)
-        if not args.no_match:
+        if evs is not None:
+            evs[6].record(s_match)
+        if not a.no_match:
             # query = frame t (slots 1..B), candidates = frame t-1 (slots 0..B-1)
-            check(L.orbm_hamming_top2(matcher.handle, vp(d_desc[b].ptr + cap * DS), cap * DS,
-                                      vp(d_counts[b].ptr + 4), cap, vp(d_desc[b].ptr), cap * DS,
-                                      vp(d_counts[b].ptr), B, vp(d_bi.ptr), vp(d_bd.ptr), vp(d_sd.ptr),
-                                      s_match.s), matcher=True)
-            evs[7].record(s_match)
-            if two_match:  # after batch k's extraction and the carry into its slot 0 (step k-1)
-                s_init.wait(ev_ext[k])
+            check(L.orbm_hamming_top2(self.matcher.handle, vp(self.d_desc[b].ptr + cap * DS), cap * DS,
+                                      vp(self.d_counts[b].ptr + 4), cap, vp(self.d_desc[b].ptr), cap * DS,
+                                      vp(self.d_counts[b].ptr), B, vp(self.d_bi[b].ptr), vp(self.d_bd[b].ptr),
+                                      vp(self.d_sd[b].ptr), s_match.s), matcher=True)
+            if evs is not None:
+                evs[7].record(s_match)
+            if self.two_match:  # after batch k's extraction and the carry into its slot 0 (step k-1)
+                s_init.wait(self.ev_ext[k])
                 if k >= 1:
-                    s_init.wait(ev_carry[k - 1])
-            evs[11].record(s_init)
+                    s_init.wait(self.ev_carry[k - 1])
+            if evs is not None:
+                evs[11].record(s_init)
             check(L.orbm_search_for_initialization_batch(
-                matcher.handle, vp(d_kps[b].ptr), vp(d_desc[b].ptr), vp(d_counts[b].ptr),
-                vp(d_kps[b].ptr + cap * KP), vp(d_desc[b].ptr + cap * DS), vp(d_counts[b].ptr + 4), cap, B,
-                bounds, None, 100, C.c_float(0.9), 1, vp(d_m12.ptr), vp(d_nm.ptr), s_init.s), matcher=True)
-        evs[8].record(s_init)
-        ev_done[k].record(s_match)
-        if two_match:
-            ev_done2[k].record(s_init)
+                self.matcher.handle, vp(self.d_kps[b].ptr), vp(self.d_desc[b].ptr), vp(self.d_counts[b].ptr),
+                vp(self.d_kps[b].ptr + cap * KP), vp(self.d_desc[b].ptr + cap * DS), vp(self.d_counts[b].ptr + 4),
+                cap, B, self.bounds, None, 100, C.c_float(0.9), 1, vp(self.d_m12[b].ptr), vp(self.d_nm[b].ptr),
+                s_init.s), matcher=True)
+        if evs is not None:
+            evs[8].record(s_init)
+        self.ev_done[k].record(s_match)
+        if self.two_match:
+            self.ev_done2[k].record(s_init)
+        if self.host:
+            # read back batch k's keypoints, descriptors, counts and matches
+            d2h = self.s_d2h
+            d2h.wait(self.ev_done[k])
+            cp = lambda dst, src, n: check(L.orbx_memcpy_dtoh_async(vp(dst), vp(src), n, d2h.s))
+            cp(self.h_kps[b].ptr, self.d_kps[b].ptr + cap * KP, B * cap * KP)
+            cp(self.h_desc[b].ptr, self.d_desc[b].ptr + cap * DS, B * cap * DS)
+            cp(self.h_counts[b].ptr, self.d_counts[b].ptr + 4, B * 4)
+            if not a.no_match:
+                cp(self.h_m12[b].ptr, self.d_m12[b].ptr, B * cap * 4)
+                cp(self.h_nm[b].ptr, self.d_nm[b].ptr, B * 4)
+            self.ev_out[k].record(d2h)
 
-    total_steps = args.warmup + args.steps
-    evsets = [[_lib.Event() for _ in range(n_ev)] for _ in range(total_steps)]
-    ev_ext = [_lib.Event() for _ in range(total_steps)]
-    ev_done = [_lib.Event() for _ in range(total_steps)]
-    ev_done2 = [_lib.Event() for _ in range(total_steps)]
-    ev_carry = [_lib.Event() for _ in range(total_steps)]
-    ev_part = [[_lib.Event() for _ in range(S)] for _ in range(total_steps)]
-    def sync_all():
-        for se in s_exts:
+    def sync_all(self):
+        for se in self.s_exts:
             se.synchronize()
-        s_match.synchronize()
-        s_init.synchronize()
+        self.s_match.synchronize()
+        self.s_init.synchronize()
+        if self.host:
+            self.s_h2d.synchronize()
+            self.s_d2h.synchronize()
 
-    for k in range(args.warmup):
-        step(k, evsets[k], ev_ext, ev_done)
-    sync_all()
-    if dist is not None:
-        dist.barrier()
-    sync_all()
-    t0 = time.perf_counter()
-    for k in range(args.warmup, total_steps):
-        step(k, evsets[k], ev_ext, ev_done)
-    t_issue = time.perf_counter()  # host time to enqueue the timed steps (launch-bound if close to wall)
-    sync_all()
-    t1 = time.perf_counter()
-    if dist is not None:
-        dist.barrier()
-    wall = sharding.max_over_ranks(t1 - t0, dist)
-    timed = evsets[args.warmup:]
+    def run(self, warmup, steps, dist):
+        total = warmup + steps
+        self.alloc_events(total)
+        for k in range(warmup):
+            self.step(k)
+        self.sync_all()
+        if dist is not None:
+            dist.barrier()
+        self.sync_all()
+        t0 = time.perf_counter()
+        for k in range(warmup, total):
+            self.step(k)
+        t_issue = time.perf_counter()
+        self.sync_all()
+        t1 = time.perf_counter()
+        if dist is not None:
+            dist.barrier()
+        self.total = total
+        return t1 - t0, t_issue - t0
+
+    def check_status(self):
+        bad = {f"extractor{i}": e.status() for i, e in enumerate(self.exts)}
+        bad["matcher"] = self.matcher.status()
+        bad = {k: v for k, v in bad.items() if v}
+        if bad:
+            raise RuntimeError(f"device status words set after the timed region: {bad}")
+
+    def last_set(self):
+        return (self.total - 1) % self.NS
+
+
+def run_mono(args, cfg, rank, world, local, dist):
+    from orb_slam_cuda_amd import sharding
+    from orb_slam_cuda_amd.synth import SynthSequence
+    W, H, NF, B = cfg["W"], cfg["H"], cfg["nfeatures"], args.batch
+    pool = max(B, (args.pool // B) * B)
+    frames = SynthSequence(sharding.sequence_seed(rank), W, H).frames(pool)
+    pipe = MonoPipeline(args, cfg, local, frames)
+    wall_rank, issue = pipe.run(args.warmup, args.steps, dist)
+    agg = aggregate(B * args.steps, wall_rank, dist, world)
+    pipe.check_status()
+    BS, S, cap = pipe.BS, pipe.S, pipe.cap
+    timed = pipe.evsets[args.warmup:]
     ev_ms = timed[0][0].elapsed_ms(timed[-1][8])
     STAGES_RUN = STAGES + (["bow_transform"] if args.bow else [])
-
-    # per-stage average durations over the timed steps (ms per launch-group, B frames),
+    # per-stage average durations over the timed steps (ms per launch-group, BS frames),
     # each bracketed by events on the stream its kernels run on
     st = {s: 0.0 for s in STAGES_RUN}
     for evs in timed:
@@ -295,49 +529,42 @@ def main():
             st["hamming_top2"] += evs[6].elapsed_ms(evs[7])
             st["search_init"] += evs[11].elapsed_ms(evs[8])
     st = {s: v / args.steps for s, v in st.items()}
-
-    nm = d_nm.download(B, np.int32)
-    nkp_mean = float(d_counts[(total_steps - 1) % NS].download(B + 1, np.int32)[1:].mean())
-    frames_total = B * args.steps * world
-    value = frames_total / wall
+    ls = pipe.last_set()
+    nm = pipe.d_nm[ls].download(B, np.int32)
+    cnt = pipe.d_counts[ls].download(B + 1, np.int32).astype(np.int64)
+    nkp_mean = float(cnt[1:].mean())
+    # quadtree tie-rule exposure over the last batch (orbx_get_tie_stats)
+    ties = np.concatenate([e.tie_stats(0, BS) for e in pipe.exts])  # (B, L, 3)
+    tie = {"events_per_frame": round(float(ties[:, :, 0].sum(1).mean()), 2),
+           "kept_keypoints_per_frame": round(float(ties[:, :, 2].sum(1).mean()), 1),
+           "fraction_of_kept": round(float(ties[:, :, 2].sum() / max(1, cnt[1:].sum())), 4),
+           "levels_with_event_frac": round(float((ties[:, :, 0] > 0).mean()), 3),
+           "frames": int(len(ties))}
     ab = algorithmic_bytes(W, H, nkp_mean)
     extract_ms = sum(st[s] for s in STAGES[:5])
     dominant = max(STAGES_RUN, key=lambda s: st[s])
     # roofline of the pyramid+FAST pass and of the dominant kernel
     pf_ms = st["pyramid"] + st["fast_grid"]
     pf_gbs = ab["pyr_fast_pass"] * BS / (pf_ms * 1e-3) / 1e9
-    roof = None
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
                   "orient_brief": ab["orient_brief"]}
     # the roofline kernel is FAST: the longest extraction kernel when each runs
-    # alone (profiles/r01_serial_kernel_stats.csv) and the one whose event time
-    # in this pipelined run matches its rocprofv3 average; the event pairs of
-    # the pyramid and the blur also hold their wait for compute units that the
+    # alone (profiles/*serial_kernel_stats.csv) and the one whose event time in
+    # this pipelined run matches its rocprofv3 average; the event pairs of the
+    # pyramid and the blur also hold their wait for compute units that the
     # other streams occupy, which a by-time pick would report as their duration
     rk = "fast_grid"
-    def pmc_bytes(kernel):
-        """HBM-side bytes per launch of `kernel` from the committed PMC passes (profiles/)."""
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        try:
-            pmc = json.load(open(pmc_path))
-        except Exception:
-            return None
-        want = kernel.split(" ")[0]  # profile keys carry template arguments ("fast_cells_kernel<44>")
-        return next((v.get("bytes_per_launch") for k, v in pmc.items() if k.split("<")[0] == want), None)
-
     traffic = pmc_bytes(KERNELS[rk])
     ach = hbm_stages[rk] * BS / (st[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
             "algorithmic_bytes_per_launch": int(hbm_stages[rk] * BS),
             "avg_launch_ms": round(st[rk], 4)}
-
     # the dense matcher runs on the matrix cores: algorithmic work = one 256-element +-1 dot
     # product per (query, candidate) pair = 512 FLOP, against the dense FP4 MFMA peak; the
     # per-pair top-2 update (v_min + v_med3) is reported against the VALU lane-op peak
     match_roof = None
     if not args.no_match and st["hamming_top2"] > 0:
-        cnt = d_counts[(total_steps - 1) % NS].download(B + 1, np.int32).astype(np.int64)
         pairs = int((cnt[1:] * cnt[:-1]).sum())
         sec = st["hamming_top2"] * 1e-3
         tf = 512.0 * pairs / sec / 1e12
@@ -347,40 +574,159 @@ def main():
                       "traffic": pmc_bytes(KERNELS["hamming_top2"]),
                       "pairs_per_launch": pairs, "pairs_per_s": round(pairs / sec, 1),
                       "avg_launch_ms": round(st["hamming_top2"], 4)}
-
-    cpu = cpu1 = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    lat = host = cpu = cpu1 = None
+    solo = world == 1
+    if rank == 0 and solo and not args.no_latency:
+        lat = latency_leg(cfg, local, frames[:32], args.no_match)
+    if rank == 0 and solo and not args.no_host_stream and args.host_steps > 0:
+        host = host_stream_leg(args, cfg, local, frames)
+    if rank == 0 and solo and args.cpu_sample > 0:
         sample = frames if args.cpu_sample <= len(frames) else seq_cpu(rank, W, H, args.cpu_sample)
         cpu1 = cpu_baseline(sample, cfg, args.cpu_sample, args.no_match)
         nt = args.cpu_threads if args.cpu_threads > 0 else cpu_threads_default()
         cpu = cpu_baseline(sample, cfg, args.cpu_sample, args.no_match, nt) if nt > 1 else cpu1
+        if lat is not None:
+            lat["cpu_oracle"] = cpu_latency(frames[:16], cfg, args.no_match)
 
     if rank == 0:
+        workload = (cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only")
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "metric": METRIC, "value": round(agg["value"], 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(agg["wall"] / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (seeded shapes + noise sequence, orb_slam_cuda_amd/synth.py)",
-            "config": {"workload": (cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only")
-                                   + (" + Frame::ComputeBoW (synthetic k10 L6 vocabulary)" if args.bow else ""),
+            "data": "synthetic (seeded shapes + noise sequence, orb_slam_cuda_amd/synth.py), "
+                    f"{pool} resident frames per GPU cycled batch by batch",
+            "config": {"workload": workload + (" + Frame::ComputeBoW (synthetic k10 L6 vocabulary)" if args.bow else ""),
                        "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
-                       "frames_per_step_per_gpu": B, "parallelism": f"frame-sharded x{world}, no collectives",
+                       "frames_per_step_per_gpu": B, "resident_pool_frames": pool,
+                       "parallelism": f"frame-sharded x{world}, one process per GPU, no collectives",
                        "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS},
+            "per_rank_frames_per_s": agg["per_rank"],
             "roofline": roof,
             "match_roofline": match_roof,
             "cpu_baseline": cpu,
             "cpu_baseline_1thread": cpu1,
+            "latency": lat,
+            "host_stream": host,
+            "quadtree_tie_straddle": tie,
             "pyr_fast_pass_hbm_gbs": round(pf_gbs, 1),
             "dominant_kernel": KERNELS[dominant],
             "stage_ms_per_step": {s: round(v, 4) for s, v in st.items()},
             "extract_only_frames_per_s": round(BS / (extract_ms * 1e-3), 1),
-            "host_issue_ms_per_step": round((t_issue - t0) / args.steps * 1e3, 4), "event_ms_per_step": round(ev_ms / args.steps, 4),
+            "host_issue_ms_per_step": round(issue / args.steps * 1e3, 4), "event_ms_per_step": round(ev_ms / args.steps, 4),
             "keypoints_per_frame": round(nkp_mean, 1),
-            "init_matches_per_pair": round(float(nm[1:].mean()), 1),
+            "init_matches_per_pair": round(float(nm.mean()), 1),
         }
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+
+
+def pmc_bytes(kernel):
+    """HBM-side bytes per launch of `kernel` from the committed PMC passes (profiles/)."""
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        pmc = json.load(open(pmc_path))
+    except Exception:
+        return None
+    want = kernel.split(" ")[0]  # profile keys carry template arguments ("fast_cells_kernel<44>")
+    return next((v.get("bytes_per_launch") for k, v in pmc.items() if k.split("<")[0] == want), None)
+
+
+def host_stream_leg(args, cfg, local, frames):
+    """The C3 pipeline fed from pinned host memory: every batch crosses PCIe
+    (H2D on a copy stream, overlapped with the previous batch's compute) and
+    its keypoints, descriptors, counts and matches come back (D2H on a second
+    copy stream). PCIe-inclusive throughput; never `value`."""
+    pipe = MonoPipeline(args, cfg, local, frames, host=True, need_events=False)
+    wall, _ = pipe.run(min(args.warmup, 10), args.host_steps, None)
+    pipe.check_status()
+    B, cap = pipe.B, pipe.cap
+    h2d = B * pipe.fbytes
+    d2h = B * (cap * (KP + DS) + 4) + (0 if args.no_match else B * (cap + 1) * 4)
+    return {"value": round(B * args.host_steps / wall, 2), "unit": "frames/s", "steps": args.host_steps,
+            "ms_per_step": round(wall / args.host_steps * 1e3, 4),
+            "pcie_gb_per_s": round((h2d + d2h) * args.host_steps / wall / 1e9, 2),
+            "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
+            "what": f"pool of {len(frames)} frames in pinned host memory, batch uploaded per step, "
+                    "keypoints + descriptors + counts" + ("" if args.no_match else " + matches") + " read back"}
+
+
+def latency_leg(cfg, local, frames, no_match, n=200, warm=20):
+    """orbx_extract (the synchronous single-image call the reference's
+    Tracking makes, src/Frame.cc:246-252) and the host SearchForInitialization,
+    median / p99 over n calls after warm calls."""
+    import orb_slam_cuda_amd as pkg
+    from orb_slam_cuda_amd import _lib
+    W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
+    L = _lib.lib()
+    ext = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local)
+    cap = ext.frame_capacity
+    imgs = [np.ascontiguousarray(f) for f in frames]
+    kps = [np.empty(cap, pkg.KP_DTYPE) for _ in imgs]
+    desc = [np.empty((cap, 32), np.uint8) for _ in imgs]
+    ns = [0] * len(imgs)
+    n_c = C.c_int(0)
+
+    def one(i):
+        j = i % len(imgs)
+        _lib.check(L.orbx_extract(ext.handle, _lib.ptr(imgs[j]), W, H, W, _lib.ptr(kps[j]), cap, _lib.ptr(desc[j]),
+                                  C.byref(n_c)))
+        ns[j] = n_c.value
+
+    for i in range(warm):
+        one(i)
+    t = []
+    for i in range(n):
+        t0 = time.perf_counter()
+        one(i)
+        t.append(time.perf_counter() - t0)
+    t = np.array(t) * 1e3
+    out = {"extract_ms": {"median": round(float(np.median(t)), 4), "p99": round(float(np.percentile(t, 99)), 4),
+                          "calls": n},
+           "what": f"orbx_extract, one host {W}x{H} u8 image in, host keypoints + descriptors out "
+                   "(pinned staging, H2D + 5 kernels + D2H as one replayed hipGraph, one sync)"}
+    if not no_match:
+        m = pkg.ORBmatcher(0.9, True, device=local, max_kps=cap)
+        b = _lib.GridBounds(0.0, float(W), 0.0, float(H))
+        m12 = np.empty(cap, np.int32)
+        nm = C.c_int(0)
+        ts = []
+        for i in range(warm + n):
+            j = i % (len(imgs) - 1)
+            k1, d1, k2, d2 = kps[j][:ns[j]], desc[j][:ns[j]], kps[j + 1][:ns[j + 1]], desc[j + 1][:ns[j + 1]]
+            prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1), np.float32)
+            t0 = time.perf_counter()
+            _lib.check(L.orbm_search_for_initialization(m.handle, _lib.ptr(k1), _lib.ptr(d1), len(k1), _lib.ptr(k2),
+                                                        _lib.ptr(d2), len(k2), b, _lib.ptr(prev), 100, C.c_float(0.9),
+                                                        1, _lib.ptr(m12), C.byref(nm)), matcher=True)
+            if i >= warm:
+                ts.append(time.perf_counter() - t0)
+        ts = np.array(ts) * 1e3
+        out["search_init_ms"] = {"median": round(float(np.median(ts)), 4),
+                                 "p99": round(float(np.percentile(ts, 99)), 4), "calls": n}
+    return out
+
+
+def cpu_latency(frames, cfg, no_match):
+    """The oracle's single-thread latency of the same calls (median over the frames)."""
+    from oracle import oracle as O
+    W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
+    oc = O.config(nfeatures=NF, width=W, height=H)
+    te, ts, prev = [], [], None
+    for fr in frames:
+        t0 = time.perf_counter()
+        kp, desc = O.extract(oc, fr)
+        te.append(time.perf_counter() - t0)
+        if prev is not None and not no_match:
+            pk, pd = prev
+            t0 = time.perf_counter()
+            O.search_for_initialization(pk, pd, kp, desc, (0, W, 0, H), np.stack([pk["x"], pk["y"]], 1), 100, 0.9, True)
+            ts.append(time.perf_counter() - t0)
+        prev = (kp, desc)
+    out = {"extract_ms_median": round(float(np.median(te)) * 1e3, 3), "frames": len(frames), "cores": 1,
+           "kind": "port"}
+    if ts:
+        out["search_init_ms_median"] = round(float(np.median(ts)) * 1e3, 3)
+    return out
 
 
 STEREO_METRIC = "stereo pairs/s ORB extract (left+right) + ComputeStereoMatches, 2x1241x376 nFeatures=2000"
@@ -392,8 +738,9 @@ def run_stereo(args, cfg, rank, world, local, dist):
     one stream and right frames on another (two ORBextractor handles, as
     Frame's mpORBextractorLeft / mpORBextractorRight), then ComputeStereoMatches
     of the B pairs on the left stream once both are done. Two handle sets
-    alternate between steps so that the stereo matching of step k (which reads
-    step k's pyramids) overlaps the extraction of step k+1."""
+    (each with its own matcher) alternate between steps so that the stereo
+    matching of step k (which reads step k's pyramids) overlaps the
+    extraction of step k+1."""
     import orb_slam_cuda_amd as pkg
     from orb_slam_cuda_amd import _lib, sharding
     from orb_slam_cuda_amd.synth import stereo_pair
@@ -402,7 +749,6 @@ def run_stereo(args, cfg, rank, world, local, dist):
     check = _lib.check
     W, H, NF, B = cfg["W"], cfg["H"], cfg["nfeatures"], args.batch
     pitch = (W + 63) & ~63
-    check(L.orbx_set_device(local))
     base = sharding.sequence_seed(rank)
     pairs = [stereo_pair(base + i, W, H) for i in range(B)]
     host = np.zeros((2, B, H, pitch), np.uint8)
@@ -412,7 +758,7 @@ def run_stereo(args, cfg, rank, world, local, dist):
     d_frames = _lib.DeviceArray(host.nbytes)
     d_frames.upload(host)
     fb = B * H * pitch  # bytes of one side's frames
-    KP, DS, NSET = 28, 32, 2
+    NSET = 2
     sets = []
     s_one = _lib.Stream() if args.serial else None  # --serial: every launch on one stream
     for _ in range(NSET):
@@ -421,11 +767,11 @@ def run_stereo(args, cfg, rank, world, local, dist):
         cap = eL.frame_capacity
         sL = s_one or _lib.Stream()
         sets.append(dict(eL=eL, eR=eR, sL=sL, sR=s_one or _lib.Stream(),
+                         m=pkg.ORBmatcher(device=local, max_pairs=B, max_kps=cap),
                          kps=_lib.DeviceArray(2 * B * cap * KP), desc=_lib.DeviceArray(2 * B * cap * DS),
                          n=_lib.DeviceArray(2 * B * 4), u=_lib.DeviceArray(B * cap * 4),
                          d=_lib.DeviceArray(B * cap * 4), kept=_lib.DeviceArray(B * 4)))
     cap = sets[0]["eL"].frame_capacity
-    matcher = pkg.ORBmatcher(device=local, max_pairs=B, max_kps=cap)
     vp = lambda a: C.c_void_p(a)
     total = args.warmup + args.steps
     # per step: 6 extraction stage marks (left stream) + stereo start/end + right-done + done
@@ -446,7 +792,7 @@ def run_stereo(args, cfg, rank, world, local, dist):
         st["sL"].wait(ev[8])
         ev[6].record(st["sL"])
         check(L.orbm_compute_stereo_matches_batch(
-            matcher.handle, st["eL"].handle, 0, st["eR"].handle, 0, vp(st["kps"].ptr), vp(st["desc"].ptr),
+            st["m"].handle, st["eL"].handle, 0, st["eR"].handle, 0, vp(st["kps"].ptr), vp(st["desc"].ptr),
             vp(st["n"].ptr), vp(st["kps"].ptr + B * cap * KP), vp(st["desc"].ptr + B * cap * DS),
             vp(st["n"].ptr + B * 4), cap, B, C.c_float(MB), C.c_float(MBF), vp(st["u"].ptr), vp(st["d"].ptr),
             vp(st["kept"].ptr), st["sL"].s), matcher=True)
@@ -471,7 +817,13 @@ def run_stereo(args, cfg, rank, world, local, dist):
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
-    wall = sharding.max_over_ranks(t1 - t0, dist)
+    agg = aggregate(B * args.steps, t1 - t0, dist, world)
+    for st in sets:
+        for h in (st["eL"], st["eR"]):
+            if h.status():
+                raise RuntimeError("extractor device status word set")
+        if st["m"].status():
+            raise RuntimeError("matcher device status word set")
     timed = evs[args.warmup:]
     stages = STAGES[:5] + ["stereo"]
     sm = {s: 0.0 for s in stages}
@@ -483,29 +835,29 @@ def run_stereo(args, cfg, rank, world, local, dist):
     last = sets[(total - 1) % NSET]
     kept = last["kept"].download(B, np.int32)
     nkp = last["n"].download(2 * B, np.int32)
-    value = B * args.steps * world / wall
     ab = algorithmic_bytes(W, H, float(nkp.mean()))
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
                   "orient_brief": ab["orient_brief"]}
-    rk = max(hbm_stages, key=lambda s: sm[s])
+    rk = "fast_grid"
     ach = hbm_stages[rk] * B / (sm[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_bytes(KERNELS[rk]),
             "algorithmic_bytes_per_launch": int(hbm_stages[rk] * B), "avg_launch_ms": round(sm[rk], 4)}
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline_stereo(pairs, cfg, max(1, args.cpu_sample // 2))
     if rank == 0:
         out = {
-            "metric": STEREO_METRIC, "value": round(value, 2), "unit": "stereo pairs/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "metric": STEREO_METRIC, "value": round(agg["value"], 2), "unit": "stereo pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(agg["wall"] / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic rectified pairs (orb_slam_cuda_amd/synth.py stereo_pair)",
             "config": {"workload": cfg["workload"], "frame": f"2x{W}x{H}", "nfeatures": NF, "nlevels": 8,
                        "scale_factor": 1.2, "pairs_per_step_per_gpu": B,
-                       "parallelism": f"pair-sharded x{world}, no collectives",
+                       "parallelism": f"pair-sharded x{world}, one process per GPU, no collectives",
                        "streams": 1 if args.serial else 2 * NSET,
                        "mb": MB, "mbf": MBF},
+            "per_rank_pairs_per_s": agg["per_rank"],
             "roofline": roof,
             "cpu_baseline": cpu,
             "stage_ms_per_step": {s: round(v, 4) for s, v in sm.items()},
@@ -513,8 +865,6 @@ def run_stereo(args, cfg, rank, world, local, dist):
             "stereo_matches_per_pair": round(float(kept.mean()), 1),
         }
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 def cpu_baseline_stereo(pairs, cfg, n):
@@ -567,8 +917,8 @@ def cpu_baseline(frames, cfg, n, no_match, threads=1):
 
     threads == 1: one thread over n consecutive frames.
     threads > 1: independent frame-parallel workers, one per core, each over its
-    own run of n // threads consecutive frames, aggregate frames/s over the wall
-    clock; the oracle's C calls release the GIL.
+    own run of n consecutive frames, aggregate frames/s over the wall clock
+    (SURVEY 8(d) (ii)); the oracle's C calls release the GIL.
     """
     from oracle import oracle as O
     W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
@@ -583,8 +933,10 @@ def cpu_baseline(frames, cfg, n, no_match, threads=1):
                 "sample": f"{n} consecutive frames of the same synthetic sequence, oracle extract"
                           + ("" if no_match else what) + f", single thread, {dt:.1f} s"}
     from concurrent.futures import ThreadPoolExecutor
-    per = max(2, n // threads)
-    chunks = [frames[(k * per) % max(1, len(frames) - per):][:per] for k in range(threads)]
+    # every worker runs as many frames as the single-thread sample (about
+    # 10 s of CPU work each, so the aggregate is not a sub-second blip)
+    per = max(2, n)
+    chunks = [frames[(k * 37) % max(1, len(frames) - per):][:per] for k in range(threads)]
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
         list(ex.map(lambda c: _cpu_run(O, oc, c, W, no_match), chunks))

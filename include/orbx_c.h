@@ -626,6 +626,12 @@ int orbx_memcpy_htod(void* dst, const void* src, size_t bytes);
 int orbx_memcpy_dtoh(void* dst, const void* src, size_t bytes);
 int orbx_memset(void* dst, int value, size_t bytes);
 int orbx_memcpy_dtod_async(void* dst, const void* src, size_t bytes, void* stream);
+/* Pinned (page-locked) host memory and asynchronous host<->device copies on
+ * a stream: host-streamed input (frames uploaded per batch) and read-back. */
+int orbx_host_alloc(void** p, size_t bytes);
+int orbx_host_free(void* p);
+int orbx_memcpy_htod_async(void* dst, const void* src, size_t bytes, void* stream);
+int orbx_memcpy_dtoh_async(void* dst, const void* src, size_t bytes, void* stream);
 int orbx_stream_create(void** stream);
 /* A stream whose work the dispatcher prefers (high = 1) or defers (high = 0)
  * when both compete for compute units (hipStreamCreateWithPriority). */

@@ -188,6 +188,10 @@ def lib() -> C.CDLL:
         L.orbx_memcpy_dtoh.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.orbx_memset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
         L.orbx_memcpy_dtod_async.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.orbx_memcpy_htod_async.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.orbx_memcpy_dtoh_async.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.orbx_host_alloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        L.orbx_host_free.argtypes = [C.c_void_p]
         L.orbx_stream_create.argtypes = [C.POINTER(C.c_void_p)]
         L.orbx_stream_create_priority.argtypes = [C.POINTER(C.c_void_p), C.c_int]
         L.orbx_stream_destroy.argtypes = [C.c_void_p]
@@ -270,6 +274,29 @@ class DeviceArray:
     def __del__(self):
         if getattr(self, "p", None) and self.p.value and _lib is not None:
             _lib.orbx_free(self.p)
+            self.p = C.c_void_p(0)
+
+
+class HostArray:
+    """Owning pinned host allocation (hipHostMalloc) viewed as a numpy array."""
+
+    def __init__(self, shape, dtype):
+        self.dtype = np.dtype(dtype)
+        self.shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        self.p = C.c_void_p(0)
+        check(lib().orbx_host_alloc(C.byref(self.p), max(self.nbytes, 1)))
+        buf = (C.c_uint8 * max(self.nbytes, 1)).from_address(self.p.value)
+        self.a = np.frombuffer(buf, np.uint8, self.nbytes).view(self.dtype).reshape(self.shape)
+
+    @property
+    def ptr(self) -> int:
+        return self.p.value
+
+    def __del__(self):
+        if getattr(self, "p", None) and self.p.value and _lib is not None:
+            self.a = None
+            _lib.orbx_host_free(self.p)
             self.p = C.c_void_p(0)
 
 

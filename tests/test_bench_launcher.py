@@ -1,0 +1,60 @@
+"""CPU tests of bench.py's multi-GPU launcher and reporting path: `--gpus N`
+spawns N worker processes that join the gloo control plane, and rank 0
+reports the whole-job aggregate. The GPU work is replaced by a stub worker
+(--stub-worker); everything else is the code the 8-GPU run executes."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_spawns_n_workers_and_aggregates(n):
+    pytest.importorskip("torch")
+    r = _run(["--gpus", str(n), "--steps", "5", "--warmup", "1", "--batch", "8", "--stub-worker"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # one JSON line, from rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n
+    assert out["frames_total"] == n * 8 * 5
+    per = out["per_rank_frames_per_s"]
+    assert len(per) == n and all(v > 0 for v in per)
+    # rank r sleeps (1 + r) x 10 ms: the job time is the slowest rank's
+    assert per[0] > per[-1]
+    assert out["value"] <= sum(per) + 1e-6
+    assert abs(out["value"] - out["frames_total"] / (out["frames_total"] / n / per[-1])) / out["value"] < 0.05
+
+
+def test_gpus_must_match_torchrun_world():
+    pytest.importorskip("torch")
+    r = _run(["--gpus", "2", "--stub-worker"], {"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
+
+
+def test_launcher_refuses_to_oversubscribe():
+    pytest.importorskip("torch")
+    import torch
+    n = torch.cuda.device_count()
+    r = _run(["--gpus", str(n + 1), "--spawn", "--steps", "1", "--warmup", "0"])
+    assert r.returncode != 0 and "oversubscribe" in (r.stderr + r.stdout)
+
+
+def test_parse_defaults():
+    sys.path.insert(0, ROOT)
+    import bench
+    a = bench.parse_args([])
+    assert a.gpus == 1 and a.batch == 64 and a.pool % a.batch == 0 and a.pool * 1280 * 376 > 256 * 2 ** 20
