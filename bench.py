@@ -66,7 +66,11 @@ MFMA_FP4_PEAK_TFLOPS = 10066.3
 # VALU lane-op peak: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (the top-2 update costs 2 lane-ops per pair)
 VALU_PEAK_TOPS = 78.6
 STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_top2", "search_init"]
+# the fused front path (orbx_front_path): event pairs 0-1 bracket front_band_kernel (pyramid +
+# blur + FAST + NMS), 1-2 nothing, 2-3 cell_compact_kernel
+FRONT_STAGES = ["front", None, "cell_compact", "quadtree", "orient_brief", "hamming_top2", "search_init"]
 KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
+           "front": "front_band_kernel", "cell_compact": "cell_compact_kernel",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
            "hamming_top2": "hamming_top2_mfma_kernel", "search_init": "search_init_kernel"}
 KP, DS = 28, 32  # bytes of one orbx_kp (cv::KeyPoint) and one descriptor
@@ -105,6 +109,11 @@ def algorithmic_bytes(W, H, nkp):
         "fast_grid": sum(P),                                           # read every level once
         "pyr_fast_pass": P[0] + sum(P[:7]) + sum(P[1:]) + sum(P),      # BASELINE.md B_pf
         "orient_brief": nkp * (2 * 31 * 31 + 60),                      # patch gathers + outputs
+        # fused front kernel: read level 0, write levels 1..7 and the blur of
+        # every level, write the two NMS bit rows of the detection rectangle
+        "front": P[0] + sum(P[1:]) + sum(P) + sum(((w - 38 + 31) // 32 + 2) * 8 * (h - 38)
+                                               for w, h in level_sizes(W, H)),
+        "cell_compact": sum(((w - 38 + 31) // 32 + 2) * 8 * (h - 38) for w, h in level_sizes(W, H)),
     }
 
 
@@ -516,13 +525,18 @@ def run_mono(args, cfg, rank, world, local, dist):
     BS, S, cap = pipe.BS, pipe.S, pipe.cap
     timed = pipe.evsets[args.warmup:]
     ev_ms = timed[0][0].elapsed_ms(timed[-1][8])
-    STAGES_RUN = STAGES + (["bow_transform"] if args.bow else [])
+    front = pipe.exts[0].front_path
+    names = FRONT_STAGES if front else STAGES
+    ext_stages = [n for n in names[:5] if n]
+    STAGES_RUN = ext_stages + (["hamming_top2", "search_init"] if not args.no_match else []) \
+        + (["bow_transform"] if args.bow else [])
     # per-stage average durations over the timed steps (ms per launch-group, BS frames),
     # each bracketed by events on the stream its kernels run on
     st = {s: 0.0 for s in STAGES_RUN}
     for evs in timed:
-        for i, s in enumerate(STAGES[:5]):
-            st[s] += evs[i].elapsed_ms(evs[i + 1])
+        for i, s in enumerate(names[:5]):
+            if s:
+                st[s] += evs[i].elapsed_ms(evs[i + 1])
         if args.bow:
             st["bow_transform"] += evs[9].elapsed_ms(evs[10])
         if not args.no_match:
@@ -541,19 +555,18 @@ def run_mono(args, cfg, rank, world, local, dist):
            "levels_with_event_frac": round(float((ties[:, :, 0] > 0).mean()), 3),
            "frames": int(len(ties))}
     ab = algorithmic_bytes(W, H, nkp_mean)
-    extract_ms = sum(st[s] for s in STAGES[:5])
+    extract_ms = sum(st[s] for s in ext_stages)
     dominant = max(STAGES_RUN, key=lambda s: st[s])
-    # roofline of the pyramid+FAST pass and of the dominant kernel
-    pf_ms = st["pyramid"] + st["fast_grid"]
+    # roofline of the pyramid+FAST pass: the kernels that run it
+    pf_ms = st["front"] if front else st["pyramid"] + st["fast_grid"]
     pf_gbs = ab["pyr_fast_pass"] * BS / (pf_ms * 1e-3) / 1e9
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
-                  "orient_brief": ab["orient_brief"]}
-    # the roofline kernel is FAST: the longest extraction kernel when each runs
-    # alone (profiles/*serial_kernel_stats.csv) and the one whose event time in
-    # this pipelined run matches its rocprofv3 average; the event pairs of the
-    # pyramid and the blur also hold their wait for compute units that the
-    # other streams occupy, which a by-time pick would report as their duration
-    rk = "fast_grid"
+                  "orient_brief": ab["orient_brief"], "front": ab["front"], "cell_compact": ab["cell_compact"]}
+    # the roofline kernel: the fused front kernel (pyramid + blur + FAST + NMS,
+    # the longest extraction kernel), or FAST on the per-stage path (the
+    # longest one alone, whose event time in the pipelined run matches its
+    # rocprofv3 average)
+    rk = "front" if front else "fast_grid"
     traffic = pmc_bytes(KERNELS[rk])
     ach = hbm_stages[rk] * BS / (st[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -825,11 +838,14 @@ def run_stereo(args, cfg, rank, world, local, dist):
         if st["m"].status():
             raise RuntimeError("matcher device status word set")
     timed = evs[args.warmup:]
-    stages = STAGES[:5] + ["stereo"]
+    front = sets[0]["eL"].front_path
+    names = FRONT_STAGES if front else STAGES
+    stages = [n for n in names[:5] if n] + ["stereo"]
     sm = {s: 0.0 for s in stages}
     for ev in timed:
-        for i, s in enumerate(STAGES[:5]):
-            sm[s] += ev[i].elapsed_ms(ev[i + 1])
+        for i, s in enumerate(names[:5]):
+            if s:
+                sm[s] += ev[i].elapsed_ms(ev[i + 1])
         sm["stereo"] += ev[6].elapsed_ms(ev[7])
     sm = {s: v / args.steps for s, v in sm.items()}
     last = sets[(total - 1) % NSET]
@@ -837,8 +853,8 @@ def run_stereo(args, cfg, rank, world, local, dist):
     nkp = last["n"].download(2 * B, np.int32)
     ab = algorithmic_bytes(W, H, float(nkp.mean()))
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
-                  "orient_brief": ab["orient_brief"]}
-    rk = "fast_grid"
+                  "orient_brief": ab["orient_brief"], "front": ab["front"], "cell_compact": ab["cell_compact"]}
+    rk = "front" if front else "fast_grid"
     ach = hbm_stages[rk] * B / (sm[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_bytes(KERNELS[rk]),

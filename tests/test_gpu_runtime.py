@@ -47,6 +47,15 @@ def test_tie_stats_batch(pkg, O):
     assert ext.status() == 0
 
 
+def test_front_path_is_planned_for_the_bench_shapes(pkg):
+    """The fused front kernel holds KITTI (nF 2000 and the 4000 init extractor)
+    and EuRoC plans, unless ORBX_FRONT=0 forces the per-stage kernels."""
+    import os
+    want = os.environ.get("ORBX_FRONT", "1") != "0"
+    for nf, W, H, B in ((2000, 1241, 376, 32), (4000, 1241, 376, 1), (1000, 752, 480, 32), (500, 640, 240, 1)):
+        assert pkg.ORBextractor(nf, 1.2, 8, 20, 7, W, H, max_batch=B).front_path == want
+
+
 def test_small_handle_does_not_shrink_lds_limit(pkg, O):
     """A handle with a small plan created after a large one must not lower the
     per-kernel LDS limit the large one launches with."""
