@@ -66,11 +66,11 @@ MFMA_FP4_PEAK_TFLOPS = 10066.3
 # VALU lane-op peak: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (the top-2 update costs 2 lane-ops per pair)
 VALU_PEAK_TOPS = 78.6
 STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_top2", "search_init"]
-# the fused front path (orbx_front_path): event pairs 0-1 bracket front_band_kernel (pyramid +
-# blur + FAST + NMS), 1-2 nothing, 2-3 cell_compact_kernel
-FRONT_STAGES = ["front", None, "cell_compact", "quadtree", "orient_brief", "hamming_top2", "search_init"]
+# the fused path (orbx_front_path): event pairs 0-1 bracket the pyramid, 1-2 nothing, 2-3
+# front_tile_kernel (blur + FAST + NMS + per-cell threshold choice per tile)
+FRONT_STAGES = ["pyramid", None, "blur_fast", "quadtree", "orient_brief", "hamming_top2", "search_init"]
 KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
-           "front": "front_band_kernel", "cell_compact": "cell_compact_kernel",
+           "blur_fast": "front_tile_kernel",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
            "hamming_top2": "hamming_top2_mfma_kernel", "search_init": "search_init_kernel"}
 KP, DS = 28, 32  # bytes of one orbx_kp (cv::KeyPoint) and one descriptor
@@ -109,11 +109,8 @@ def algorithmic_bytes(W, H, nkp):
         "fast_grid": sum(P),                                           # read every level once
         "pyr_fast_pass": P[0] + sum(P[:7]) + sum(P[1:]) + sum(P),      # BASELINE.md B_pf
         "orient_brief": nkp * (2 * 31 * 31 + 60),                      # patch gathers + outputs
-        # fused front kernel: read level 0, write levels 1..7 and the blur of
-        # every level, write the two NMS bit rows of the detection rectangle
-        "front": P[0] + sum(P[1:]) + sum(P) + sum(((w - 38 + 31) // 32 + 2) * 8 * (h - 38)
-                                               for w, h in level_sizes(W, H)),
-        "cell_compact": sum(((w - 38 + 31) // 32 + 2) * 8 * (h - 38) for w, h in level_sizes(W, H)),
+        # fused blur + FAST tiles: read every level once, write its blur
+        "blur_fast": 2 * sum(P),
     }
 
 
@@ -558,15 +555,14 @@ def run_mono(args, cfg, rank, world, local, dist):
     extract_ms = sum(st[s] for s in ext_stages)
     dominant = max(STAGES_RUN, key=lambda s: st[s])
     # roofline of the pyramid+FAST pass: the kernels that run it
-    pf_ms = st["front"] if front else st["pyramid"] + st["fast_grid"]
+    pf_ms = st["pyramid"] + (st["blur_fast"] if front else st["fast_grid"])
     pf_gbs = ab["pyr_fast_pass"] * BS / (pf_ms * 1e-3) / 1e9
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
-                  "orient_brief": ab["orient_brief"], "front": ab["front"], "cell_compact": ab["cell_compact"]}
-    # the roofline kernel: the fused front kernel (pyramid + blur + FAST + NMS,
-    # the longest extraction kernel), or FAST on the per-stage path (the
-    # longest one alone, whose event time in the pipelined run matches its
-    # rocprofv3 average)
-    rk = "front" if front else "fast_grid"
+                  "orient_brief": ab["orient_brief"], "blur_fast": ab["blur_fast"]}
+    # the roofline kernel: the fused blur + FAST tiles (the longest extraction
+    # kernel), or FAST on the per-stage path (the longest one alone, whose
+    # event time in the pipelined run matches its rocprofv3 average)
+    rk = "blur_fast" if front else "fast_grid"
     traffic = pmc_bytes(KERNELS[rk])
     ach = hbm_stages[rk] * BS / (st[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -853,8 +849,8 @@ def run_stereo(args, cfg, rank, world, local, dist):
     nkp = last["n"].download(2 * B, np.int32)
     ab = algorithmic_bytes(W, H, float(nkp.mean()))
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
-                  "orient_brief": ab["orient_brief"], "front": ab["front"], "cell_compact": ab["cell_compact"]}
-    rk = "front" if front else "fast_grid"
+                  "orient_brief": ab["orient_brief"], "blur_fast": ab["blur_fast"]}
+    rk = "blur_fast" if front else "fast_grid"
     ach = hbm_stages[rk] * B / (sm[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_bytes(KERNELS[rk]),

@@ -174,10 +174,11 @@ int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out);
  * Waits for the device; `reset` != 0 clears it. orbx_extract checks and clears
  * it itself; batch callers (orbx_extract_batch) poll it here. */
 int orbx_get_status(orbx_handle h, int reset, int* status);
-/* 1 if the handle's plan runs the fused front kernel (pyramid + blur + FAST +
- * NMS per row band, then the per-cell compaction), 0 for the per-stage
- * kernels (ORBX_FRONT=0 in the environment, or a plan the front kernel's LDS
- * cannot hold). Both produce identical outputs. */
+/* 1 if the handle's plan runs the fused blur + FAST tiles (one pass per
+ * (level, FAST cell row, chunk of cells): GaussianBlur, FAST, NMS and the
+ * per-cell threshold choice), 0 for the separate blur and per-cell FAST
+ * kernels (ORBX_FRONT=0 in the environment, or tiles that do not fit LDS).
+ * Both produce identical outputs. */
 int orbx_front_path(orbx_handle h);
 /* The rBRIEF test table the kernels use (bit_pattern_31_,
  * src/ORBextractor.cc:236-494): 1024 ints in the reference's flat order

@@ -73,8 +73,20 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
   return a;
 }
 
+// Workgroup barrier that orders LDS only. __syncthreads() is a workgroup
+// release/acquire fence on all memory: on gfx950 it first waits for every
+// outstanding global store of the thread (s_waitcnt vmcnt(0)), which stalls a
+// kernel that streams results to HBM between LDS phases. Use this one where
+// no thread reads global data another thread of the workgroup wrote.
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Exclusive scan of a[0..n) in LDS by NT threads; returns the total.
-template <int NT>
+// LDS_ONLY: the barriers order LDS only (lds_sync).
+template <int NT, bool LDS_ONLY = false>
 __device__ int block_scan_excl(int* a, int n, int* s_tmp) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int per = (n + NT - 1) / NT;
@@ -83,7 +95,7 @@ __device__ int block_scan_excl(int* a, int n, int* s_tmp) {
   for (int i = b; i < e; ++i) sum += a[i];
   const int x = wave_incl_scan_dpp(sum);
   if (lane == 63) s_tmp[w] = x;
-  __syncthreads();
+  if (LDS_ONLY) lds_sync(); else __syncthreads();
   int wpre = 0, total = 0;
 #pragma unroll
   for (int i = 0; i < NT / 64; ++i) {
@@ -97,7 +109,7 @@ __device__ int block_scan_excl(int* a, int n, int* s_tmp) {
     a[i] = run;
     run += v;
   }
-  __syncthreads();
+  if (LDS_ONLY) lds_sync(); else __syncthreads();
   return total;
 }
 
@@ -109,11 +121,8 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
 int launch_quadtree(const ExtractParams& P, const ExtractBuffers& X, int batch, hipStream_t s);
 int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const ExtractBuffers& X, orbx_kp* kps,
                         uint8_t* desc, int* counts, int batch, hipStream_t s);
-int launch_front(const ExtractParams& P, const LevelPtrs& lp, const ExtractBuffers& X, int batch, hipStream_t s);
-int launch_cell_compact(const ExtractParams& P, const ExtractBuffers& X, int batch, hipStream_t s);
-bool front_cells_fit(const ExtractParams& P);
-size_t front_lds_bytes(const ExtractParams& P);
-const void* front_kernel_ptr();
+int launch_front_tiles(const ExtractParams& P, const LevelPtrs& lp, const ExtractBuffers& X, int batch,
+                       hipStream_t s);
 size_t quadtree_lds_bytes(const ExtractParams& P);
 size_t pyr_band_lds_bytes(const ExtractParams& P);
 const void* pyr_band_kernel_ptr();

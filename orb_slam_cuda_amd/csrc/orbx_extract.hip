@@ -1,20 +1,18 @@
 // orbx_extract.hip — the batched ORBextractor::operator() pipeline for gfx950.
 //
-// For a batch of B frames, all on one stream, no host round trip. Front path
-// (default when the plan fits, P.front):
-//   launch_front         (1)  ComputePyramid + GaussianBlur 7x7 +   orbx_front.hip
-//                             FAST scores + per-cell NMS, per band
-//   launch_cell_compact  (1)  per-cell threshold choice, key lists  orbx_front.hip
-// per-stage path (ORBX_FRONT=0, or a plan the front kernel cannot hold):
+// For a batch of B frames, all on one stream, no host round trip:
 //   launch_pyramid       (1, or L-1 launches) ComputePyramid        orbx_pyramid.hip
+//   fused path (default when the tiles fit LDS, P.front):
+//   launch_front_tiles   (1)  GaussianBlur 7x7 + per-cell FAST +    orbx_front.hip
+//                             NMS + threshold choice, per tile
+//   per-stage path (ORBX_FRONT=0):
 //   launch_blur          (1)  GaussianBlur 7x7 s=2                  orbx_blur.hip
 //   launch_fast          (1)  per-cell FAST + NMS                   orbx_fast.hip
-// then both:
 //   launch_quadtree      (1)  DistributeOctTree                     orbx_quadtree.hip
 //   launch_orient_brief  (1)  IC_Angle + rBRIEF + scale/assemble    orbx_brief.hip
 // Optional events (caller-owned or the handle's ORBX_TIMING ones) bracket
-// every stage on the launch stream (front path: ev[0..1] the front kernel,
-// ev[1..2] empty, ev[2..3] the cell compaction).
+// every stage on the launch stream (fused path: ev[1..2] is empty and
+// ev[2..3] brackets the blur + FAST tiles).
 #include "orbx_device.cuh"
 
 namespace orbx {
@@ -41,14 +39,12 @@ int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_
   };
   int rc;
   rec(0);
+  if ((rc = launch_pyramid(Q, lp, X.rtab, batch, stream))) return rc;
+  rec(1);
   if (P.front) {
-    if ((rc = launch_front(Q, lp, X, batch, stream))) return rc;
-    rec(1);
     rec(2);
-    if ((rc = launch_cell_compact(Q, X, batch, stream))) return rc;
+    if ((rc = launch_front_tiles(Q, lp, X, batch, stream))) return rc;
   } else {
-    if ((rc = launch_pyramid(Q, lp, X.rtab, batch, stream))) return rc;
-    rec(1);
     if ((rc = launch_blur(Q, lp, X.blur, batch, stream))) return rc;
     rec(2);
     if ((rc = launch_fast(Q, lp, X.cells, X.slots, X.cell_counts, batch, stream))) return rc;

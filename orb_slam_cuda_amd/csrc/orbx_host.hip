@@ -28,9 +28,8 @@ size_t quadtree_lds_bytes(const ExtractParams& P);
 extern const void* quadtree_kernel_ptr();
 size_t pyr_band_lds_bytes(const ExtractParams& P);
 extern const void* pyr_band_kernel_ptr();
-size_t front_lds_bytes(const ExtractParams& P);
-extern const void* front_kernel_ptr();
-bool front_cells_fit(const ExtractParams& P);
+int plan_tiles(ExtractParams& P, std::vector<int4>& tl, int target_px);
+extern const void* front_tile_kernel_ptr();
 }  // namespace orbx
 
 using namespace orbx;
@@ -77,8 +76,9 @@ struct Plan {
   ExtractParams P{};
   std::vector<CellGeom> cells;
   std::vector<int2> rtab;
-  DeviceBuf pyr, blur, score, bitmaps, rtab_d, cells_d, umax_d, slots, cell_counts, qkeys, qcounts, qties, qscratch,
-      qnscratch, err;
+  std::vector<int4> tiles;
+  DeviceBuf pyr, blur, tiles_d, rtab_d, cells_d, umax_d, slots, cell_counts, qkeys, qcounts, qties, qscratch, qnscratch,
+      err;
 };
 
 }  // namespace
@@ -295,100 +295,6 @@ static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
   select_pyr_plan(P, def);
 }
 
-// Row bands of the fused front kernel (orbx_front.hip front_band_kernel): the
-// same ownership partition as the band pyramid (bands of R rows of the last
-// level, walked up the resize chain), but every level also needs its owned
-// rows +-4 (the 7x7 blur reads +-3 rows, FAST's ring 3 and its NMS 1 more),
-// so a band computes [own_lo - 4, own_hi + 4] plus the source rows of the
-// next level's computed rows. Level l's rows live in LDS buffer l & 1, its
-// FAST score rows in the other one. R shrinks until the band fits 2
-// workgroups per CU (else 1); several R are kept and the launch picks one.
-static int front_lds_fixed() { return 8 * 2 * 128 * 4; }  // per-wave survivor / detection rings
-
-static void plan_front(ExtractParams& P, std::vector<int2>& rtab) {
-  P.front = 0;
-  P.fr_nplans = 0;
-  const int L = P.L;
-  for (int l = 0; l < L; ++l) {
-    P.lv[l].fpitch = (kFrontPad + P.lv[l].w + 8 + 15) & ~15;
-    if (P.lv[l].dx1 <= P.lv[l].dx0 || P.lv[l].dy1 <= P.lv[l].dy0) return;
-  }
-  auto src_lo = [&](int l, int y) { return P.lv[l].area2x ? 2 * y : (rtab[P.lv[l].ytab + y].x & 0xFFFF); };
-  auto src_hi = [&](int l, int y) { return P.lv[l].area2x ? 2 * y + 1 : (rtab[P.lv[l].ytab + y].x >> 16); };
-  const int HL = P.lv[L - 1].h;
-  const size_t budgets[2] = {78 * 1024, 160 * 1024 - 1024};
-  const int R0 = std::max(1, (HL + 17) / 18);
-  for (int pass = 0; pass < 2 && P.fr_nplans == 0; ++pass)
-    for (int R = pass == 0 ? R0 + 8 : R0; R >= std::max(1, R0 / 3) && P.fr_nplans < 6; --R) {
-      const int nb = (HL + R - 1) / R;
-      std::vector<int> lo((size_t)nb * L), ohi((size_t)nb * L), clo((size_t)nb * L), chi((size_t)nb * L);
-      for (int b = 0; b < nb; ++b) {
-        lo[b * L + L - 1] = b * R;
-        ohi[b * L + L - 1] = std::min((b + 1) * R, HL) - 1;
-      }
-      for (int l = L - 2; l >= 0; --l)
-        for (int b = 0; b < nb; ++b) lo[b * L + l] = b == 0 ? 0 : src_lo(l + 1, lo[b * L + l + 1]);
-      for (int l = L - 2; l >= 0; --l)
-        for (int b = 0; b < nb; ++b) ohi[b * L + l] = b + 1 < nb ? lo[(b + 1) * L + l] - 1 : P.lv[l].h - 1;
-      for (int b = 0; b < nb; ++b)
-        for (int l = L - 1; l >= 0; --l) {
-          const int i = b * L + l, h = P.lv[l].h;
-          int cl = INT_MAX, ch = INT_MIN;
-          if (lo[i] <= ohi[i]) {
-            cl = std::max(0, lo[i] - 4);
-            ch = std::min(h - 1, ohi[i] + 4);
-          }
-          if (l + 1 < L && clo[i + 1] <= chi[i + 1]) {
-            cl = std::min(cl, src_lo(l + 1, clo[i + 1]));
-            ch = std::max(ch, src_hi(l + 1, chi[i + 1]));
-          }
-          if (cl > ch) {  // nothing owned or needed at this level: an empty range
-            cl = 1;
-            ch = 0;
-          }
-          clo[i] = cl;
-          chi[i] = ch;
-        }
-      size_t need[2] = {0, 0}, ybytes = 0;
-      long long cost = 0;
-      for (int b = 0; b < nb; ++b) {
-        size_t s = 0;
-        long long c = 0;
-        for (int l = 0; l < L; ++l) {
-          const int i = b * L + l;
-          const size_t fp = P.lv[l].fpitch;
-          need[l & 1] = std::max(need[l & 1], (size_t)(chi[i] - clo[i] + 1) * fp);
-          need[(l + 1) & 1] = std::max(need[(l + 1) & 1], (size_t)std::max(ohi[i] - lo[i] + 5, 1) * fp);
-          if (l >= 1) s += (size_t)(chi[i] - clo[i] + 1) * 8;
-          c += (long long)(chi[i] - clo[i] + 1) * P.lv[l].w;
-        }
-        ybytes = std::max(ybytes, s);
-        cost = std::max(cost, c);
-      }
-      need[0] = (need[0] + 15) & ~(size_t)15;
-      need[1] = (need[1] + 15) & ~(size_t)15;
-      ybytes = (ybytes + 15) & ~(size_t)15;
-      if (need[0] + need[1] + ybytes + front_lds_fixed() > budgets[pass]) continue;
-      if (P.fr_nplans > 0 && P.fr_plan[P.fr_nplans - 1].nbands == nb) continue;
-      ExtractParams::PyrPlan& q = P.fr_plan[P.fr_nplans++];
-      q.nbands = nb;
-      q.lds_a = (int)need[0];
-      q.lds_b = (int)need[1];
-      q.lds_y = (int)ybytes;
-      q.bands = (int)rtab.size();
-      q.cost = (int)std::min<long long>(cost, INT_MAX);
-      for (int b = 0; b < nb; ++b)
-        for (int l = 0; l < L; ++l) {
-          rtab.push_back(make_int2(clo[b * L + l], chi[b * L + l]));
-          rtab.push_back(make_int2(lo[b * L + l], ohi[b * L + l]));
-        }
-      if (pass == 1) break;
-    }
-  if (P.fr_nplans == 0) return;
-  P.front = 1;
-  select_front_plan(P, 0);
-}
-
 static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   Plan& pl = h->plan;
   const orbx_config& c = h->cfg;
@@ -405,7 +311,7 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   pl.cells.clear();
   pl.rtab.clear();
   long long lvl_off = 0;  // level planes [l][B][h][pitch], same offsets in pyramid and blur
-  int slot = 0, kbase = 0, maxnodes = 0, maxcells = 0, bm_words = 0, cell_rows = 0;
+  int slot = 0, kbase = 0, maxnodes = 0, maxcells = 0;
   bool front_geom_ok = true;
   for (int l = 0; l < L; ++l) {
     LevelGeom& g = P.lv[l];
@@ -471,11 +377,7 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     g.dy0 = g.minBY + 3;
     g.dx1 = std::min(g.minBX + g.nCols * g.wCell + 3, g.maxBX - 3);
     g.dy1 = std::min(g.minBY + g.nRows * g.hCell + 3, g.maxBY - 3);
-    g.bm_ndw = g.dx1 > g.dx0 ? (g.dx1 - g.dx0 + 31) / 32 + 2 : 2;
-    g.bm_off = bm_words;
-    bm_words += std::max(g.dy1 - g.dy0, 0) * 2 * g.bm_ndw;
-    cell_rows += g.nRows;
-    for (int c = 0; c < g.ncells; ++c) {  // the front path relies on this band geometry
+    for (int c = 0; c < g.ncells; ++c) {  // the fused tiles rely on this band geometry
       const CellGeom& cg = pl.cells[g.cell0 + c];
       if (!cg.cap) continue;
       const int i = c / g.nCols, j = c % g.nCols;
@@ -533,12 +435,13 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     }
   }
   plan_band_pyramid(P, pl.rtab);
-  P.bm_per_frame = bm_words;
-  P.cr_per_frame = cell_rows;
-  if (front_geom_ok && front_cells_fit(P)) plan_front(P, pl.rtab);
   {
-    const char* e = getenv("ORBX_FRONT");  // 0: the per-stage kernels (A/B and the legacy path's tests)
-    if (e && e[0] == '0') P.front = 0;
+    // the fused blur + FAST tiles are opt-in (ORBX_FRONT=1): identical
+    // outputs, but measured slower than the separate blur and per-cell FAST
+    // kernels (barrier-bound phases at 12-24 waves per CU)
+    const char* e = getenv("ORBX_FRONT");
+    const char* px = getenv("ORBX_TILE_PX");  // tile width experiments
+    P.front = e && e[0] == '1' && front_geom_ok && plan_tiles(P, pl.tiles, px ? atoi(px) : 256) > 0;
   }
   if (maxnodes > 65000) return fail(ORBX_EINVAL, "nfeatures too large for the quadtree node table");
   P.slots_per_frame = slot;
@@ -564,8 +467,7 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   int rc;
   if ((rc = pl.pyr.alloc((size_t)lvl_off))) return rc;
   if ((rc = pl.blur.alloc((size_t)lvl_off))) return rc;
-  if ((rc = pl.score.alloc(P.front ? (size_t)lvl_off : 0))) return rc;
-  if ((rc = pl.bitmaps.alloc(P.front ? (size_t)B * P.bm_per_frame * 4 + 16 : 0))) return rc;
+  if ((rc = pl.tiles_d.alloc(P.front ? pl.tiles.size() * sizeof(int4) : 0))) return rc;
   if ((rc = pl.rtab_d.alloc(std::max<size_t>(pl.rtab.size(), 1) * sizeof(int2)))) return rc;
   if ((rc = pl.cells_d.alloc(pl.cells.size() * sizeof(CellGeom)))) return rc;
   if ((rc = pl.umax_d.alloc(16 * sizeof(int)))) return rc;
@@ -596,14 +498,9 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
       return fail(ORBX_EDEVICE, "LDS limit of pyr_band_kernel: %s", hipGetErrorString(hipGetLastError()));
   }
   if (P.front) {
-    size_t mx = 0;
-    for (int i = 0; i < P.fr_nplans; ++i) {
-      ExtractParams Q = P;
-      select_front_plan(Q, i);
-      mx = std::max(mx, front_lds_bytes(Q));
-    }
-    if (raise_lds_limit(front_kernel_ptr(), mx))
-      return fail(ORBX_EDEVICE, "LDS limit of front_band_kernel: %s", hipGetErrorString(hipGetLastError()));
+    HIP_OK(hipMemcpy(pl.tiles_d.p, pl.tiles.data(), pl.tiles.size() * sizeof(int4), hipMemcpyHostToDevice));
+    if (raise_lds_limit(front_tile_kernel_ptr(), (size_t)P.tl_lds))
+      return fail(ORBX_EDEVICE, "LDS limit of front_tile_kernel: %s", hipGetErrorString(hipGetLastError()));
   }
   if (raise_lds_limit(quadtree_kernel_ptr(), quadtree_lds_bytes(P)))
     return fail(ORBX_EDEVICE, "LDS limit of quadtree_kernel: %s", hipGetErrorString(hipGetLastError()));
@@ -614,8 +511,7 @@ static ExtractBuffers buffers_of(const Plan& pl) {
   ExtractBuffers X;
   X.pyr = pl.pyr.as<uint8_t>();
   X.blur = pl.blur.as<uint8_t>();
-  X.score = pl.score.as<uint8_t>();
-  X.bitmaps = pl.bitmaps.as<uint32_t>();
+  X.tiles = pl.tiles_d.as<int4>();
   X.rtab = pl.rtab_d.as<int2>();
   X.cells = pl.cells_d.as<CellGeom>();
   X.umax = pl.umax_d.as<int>();

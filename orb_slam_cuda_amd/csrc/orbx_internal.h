@@ -49,14 +49,9 @@ struct LevelGeom {
   float scale;           // mvScaleFactor[l]
   float size;            // (float)(int)(PATCH_SIZE * mvScaleFactor[l])
   int xtab2;             // band pyramid column table: {sx, a0 | a1 << 16}, replicate folded in
-  // fused front kernel (orbx_front.hip)
-  int fpitch;            // LDS row pitch: kFrontPad bytes of left pad + w + right pad
+  // fused blur + FAST tiles (orbx_front.hip)
   int dx0, dx1, dy0, dy1;  // detection rectangle: the union of the FAST cell bands
-  int bm_ndw;            // dwords per bitmap row (ceil((dx1 - dx0) / 32) + 2 zero pad)
-  int bm_off;            // this level's bitmap rows inside a frame's bitmaps (dwords)
 };
-
-constexpr int kFrontPad = 16;  // left pad of a front-kernel LDS row (x = -3..-1 for the blur)
 
 struct CellGeom {
   int16_t c0, r0, c1, r1;  // ROI [c0,c1) x [r0,r1) in level coordinates
@@ -88,27 +83,15 @@ struct ExtractParams {
     int cost;  // largest per-band pixel count over the levels (level 0 staged + computed rows)
   } pyr_plan[6];
   int pyr_nplans;
-  // fused front kernel (orbx_front.hip): one workgroup per (frame, band) builds
-  // the band's pyramid rows, blurs them, scores FAST and runs the per-cell NMS
-  int front;                   // 1 = front path planned (else the per-stage kernels)
-  int fr_nbands, fr_bands;     // bands per frame; int2 offset in the resize table ({comp}, {own} per level)
-  int fr_lds_a, fr_lds_b, fr_lds_y;
-  PyrPlan fr_plan[6];
-  int fr_nplans;
-  int bm_per_frame;            // dwords of NMS bitmaps per frame (2 maps per detection row)
-  int cr_per_frame;            // FAST cell rows per frame (cell_compact_kernel workgroups)
+  // fused blur + FAST path (orbx_front.hip): one workgroup per (frame, level,
+  // FAST cell row, chunk of cells) blurs its tile and runs FAST, NMS and the
+  // per-cell threshold choice from one LDS copy of it
+  int front;                   // 1 = fused tiles planned (else the blur and per-cell FAST kernels)
+  int tl_per_frame;            // tiles per frame
+  int tl_lds;                  // LDS bytes of the largest tile
   int gauss[7];                // 7-tap Gaussian fixed-point kernel (sum 257)
   LevelGeom lv[kMaxLevels];
 };
-
-inline void select_front_plan(ExtractParams& P, int i) {
-  const ExtractParams::PyrPlan& q = P.fr_plan[i];
-  P.fr_nbands = q.nbands;
-  P.fr_bands = q.bands;
-  P.fr_lds_a = q.lds_a;
-  P.fr_lds_b = q.lds_b;
-  P.fr_lds_y = q.lds_y;
-}
 
 inline void select_pyr_plan(ExtractParams& P, int i) {
   const ExtractParams::PyrPlan& q = P.pyr_plan[i];
@@ -167,8 +150,7 @@ struct ExtractBuffers {
   uint16_t* qnode_scratch;
   long long qscratch_per_fl;  // entries per (frame, level)
   int* err;            // device error word
-  uint8_t* score;      // front path: FAST scores of the NMS survivors, level planes as blur
-  uint32_t* bitmaps;   // front path: per detection row {kept at iniThFAST, kept at minThFAST} bit rows
+  const int4* tiles;   // fused path: 2 int4 per tile ({level, cell row, j0, j1}, {owned blur rect})
 };
 
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames,

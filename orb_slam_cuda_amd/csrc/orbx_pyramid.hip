@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams
     for (int q = 0; q < 8; ++q) nxt[q] = rtab[g.xtab2 + min(4 * (gi + (q >> 2) * G) + (q & 3), g.w - 1)];
   };
   fetch_cols(1);
-  __syncthreads();
+  lds_sync();  // LDS only: the owned rows written to HBM are not read back here
   if (dbg && tid == 0) dbg[blockIdx.x * 16] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
 
   // ---- levels 1 .. L-1: thread -> 8 output columns (two runs of 4), rows strided
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams
         band_rows<false>(P, lp, l, f, src, dst, s_yt + yoff, cs.x, cd, own, r0, rstep, xa, xb, sx, a0v, a1v);
     }
     yoff += cd.y - cd.x + 1;
-    __syncthreads();
+    lds_sync();
     if (dbg && tid == 0) dbg[blockIdx.x * 16 + l] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
   }
 }

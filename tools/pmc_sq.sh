@@ -5,7 +5,7 @@ set -e
 OUT=$GRAFT_REPO_ROOT/$1; shift
 mkdir -p $OUT
 cd /tmp; export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
-ARGS="--steps 3 --warmup 1 --cpu-sample 0 --serial $*"
+ARGS="--steps 3 --warmup 1 --cpu-sample 0 --serial --pool 64 --no-latency --no-host-stream $*"
 i=0
 for grp in \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
