@@ -70,7 +70,7 @@ STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_t
 # front_tile_kernel (blur + FAST + NMS + per-cell threshold choice per tile)
 FRONT_STAGES = ["pyramid", None, "blur_fast", "quadtree", "orient_brief", "hamming_top2", "search_init"]
 KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
-           "blur_fast": "front_tile_kernel",
+           "blur_fast": "front_tile_kernel", "bow_match": "search_bow_kernel<512>",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
            "hamming_top2": "hamming_top2_mfma_kernel", "search_init": "search_init_kernel"}
 KP, DS = 28, 32  # bytes of one orbx_kp (cv::KeyPoint) and one descriptor
@@ -134,6 +134,8 @@ def parse_args(argv=None):
                     help="high-priority extraction streams, low-priority matching stream")
     ap.add_argument("--bow", action="store_true",
                     help="also Frame::ComputeBoW every frame (synthetic ORBvoc-shaped vocabulary, k 10 L 6)")
+    ap.add_argument("--bow-match", action="store_true",
+                    help="also SearchByBoW of every frame against its predecessor as reference keyframe (implies --bow)")
     ap.add_argument("--match-streams", type=int, choices=[1, 2], default=1,
                     help="2: SearchForInitialization on its own stream, beside the dense top-2")
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
@@ -327,14 +329,22 @@ class MonoPipeline:
         self.s_init = _lib.Stream(0 if args.priority else None) if self.two_match else self.s_match
         self.bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
         self.voc = None
-        if args.bow and not host:
+        self.bow_match = args.bow_match and not host
+        if (args.bow or args.bow_match) and not host:
             from orb_slam_cuda_amd.synth import synthetic_vocabulary
             self.voc = pkg.ORBVocabulary.from_arrays(synthetic_vocabulary(10, 6, seed=1), device=local)
-            self.d_bw, self.d_bn, self.d_fn, self.d_fi, self.d_fnn = (DA(B * cap * 4), DA(B * 4), DA(B * cap * 4),
-                                                                      DA(B * cap * 4), DA(B * 4))
-            self.d_bv = DA(B * cap * 8)
-            self.d_fo = DA(B * (cap + 1) * 4)
-            self.d_vw = (DA(B * cap * 4), DA(B * cap * 4), DA(B * cap * 8))
+            # BoW of slots 0..B (slot 0 = frame t-1 of the batch's first frame) when
+            # SearchByBoW matches every frame against its predecessor as the reference keyframe
+            NB1 = B + 1
+            self.d_bw, self.d_bn, self.d_fn, self.d_fi, self.d_fnn = (DA(NB1 * cap * 4), DA(NB1 * 4),
+                                                                      DA(NB1 * cap * 4), DA(NB1 * cap * 4),
+                                                                      DA(NB1 * 4))
+            self.d_bv = DA(NB1 * cap * 8)
+            self.d_fo = DA(NB1 * (cap + 1) * 4)
+            self.d_vw = (DA(NB1 * cap * 4), DA(NB1 * cap * 4), DA(NB1 * cap * 8))
+            if self.bow_match:
+                self.bow_matcher = pkg.ORBmatcher(0.7, True, device=local, max_pairs=B, max_kps=cap)
+                self.d_bow_out, self.d_bow_nm = DA(B * cap * 4), DA(B * 4)
         self.need_events = need_events
         self.ev = {}
 
@@ -346,7 +356,7 @@ class MonoPipeline:
 
     def alloc_events(self, total):
         E = self._lib.Event
-        n_ev = 12  # 6 extraction stage marks + 3 matching marks + 2 BoW marks + init start
+        n_ev = 13  # 6 extraction stage marks + 3 matching marks + 2 BoW marks + init start + BoW match end
         self.evsets = [[E() for _ in range(n_ev)] for _ in range(total)] if self.need_events else None
         self.ev_ext = [E() for _ in range(total)]
         self.ev_done = [E() for _ in range(total)]
@@ -423,13 +433,30 @@ class MonoPipeline:
             self.ev_carry[k].record(s_match)
         if self.voc is not None:
             evs[9].record(s_match)
-            # Frame::ComputeBoW of the batch's frames (slots 1..B), levelsup 4 (src/Frame.cc:398)
-            check(L.orbv_transform_batch(self.voc.handle, vp(self.d_desc[b].ptr + cap * DS), cap * DS,
-                                         vp(self.d_counts[b].ptr + 4), B, cap, 4, vp(self.d_bw.ptr), vp(self.d_bv.ptr),
-                                         vp(self.d_bn.ptr), vp(self.d_fn.ptr), vp(self.d_fo.ptr), vp(self.d_fi.ptr),
-                                         vp(self.d_fnn.ptr), vp(self.d_vw[0].ptr), vp(self.d_vw[1].ptr),
-                                         vp(self.d_vw[2].ptr), s_match.s), vocabulary=True)
+            # Frame::ComputeBoW (src/Frame.cc:394-401, levelsup 4) of the batch's frames
+            # (slots 1..B; with --bow-match also slot 0, the reference keyframe of slot 1)
+            s0 = 0 if self.bow_match else 1
+            check(L.orbv_transform_batch(self.voc.handle, vp(self.d_desc[b].ptr + s0 * cap * DS), cap * DS,
+                                         vp(self.d_counts[b].ptr + 4 * s0), B + 1 - s0, cap, 4, vp(self.d_bw.ptr),
+                                         vp(self.d_bv.ptr), vp(self.d_bn.ptr), vp(self.d_fn.ptr), vp(self.d_fo.ptr),
+                                         vp(self.d_fi.ptr), vp(self.d_fnn.ptr), vp(self.d_vw[0].ptr),
+                                         vp(self.d_vw[1].ptr), vp(self.d_vw[2].ptr), s_match.s), vocabulary=True)
             evs[10].record(s_match)
+            if self.bow_match:
+                # SearchByBoW(KF, F) of frame t against frame t-1 as the reference keyframe, every
+                # keyframe feature with a MapPoint (Tracking::TrackReferenceKeyFrame, ratio 0.7,
+                # src/Tracking.cc:839-842), all B pairs in one launch
+                ofs = lambda d, k, pitch, size: vp(d.ptr + k * pitch * size)
+                sides = []
+                for side in (0, 1):
+                    sides += [ofs(self.d_kps[b], side, cap, KP), ofs(self.d_desc[b], side, cap, DS),
+                              ofs(self.d_counts[b], side, 1, 4), None, ofs(self.d_fn, side, cap, 4),
+                              ofs(self.d_fo, side, cap + 1, 4), ofs(self.d_fi, side, cap, 4),
+                              ofs(self.d_fnn, side, 1, 4)]
+                check(L.orbm_search_by_bow_batch(self.bow_matcher.handle, B, cap, cap, *sides, C.c_float(0.7), 1, 0,
+                                                 vp(self.d_bow_out.ptr), vp(self.d_bow_nm.ptr), s_match.s),
+                      matcher=True)
+                evs[12].record(s_match)
         if evs is not None:
             evs[6].record(s_match)
         if not a.no_match:
@@ -501,6 +528,8 @@ class MonoPipeline:
     def check_status(self):
         bad = {f"extractor{i}": e.status() for i, e in enumerate(self.exts)}
         bad["matcher"] = self.matcher.status()
+        if getattr(self, "bow_match", False):
+            bad["bow_matcher"] = self.bow_matcher.status()
         bad = {k: v for k, v in bad.items() if v}
         if bad:
             raise RuntimeError(f"device status words set after the timed region: {bad}")
@@ -526,7 +555,7 @@ def run_mono(args, cfg, rank, world, local, dist):
     names = FRONT_STAGES if front else STAGES
     ext_stages = [n for n in names[:5] if n]
     STAGES_RUN = ext_stages + (["hamming_top2", "search_init"] if not args.no_match else []) \
-        + (["bow_transform"] if args.bow else [])
+        + (["bow_transform"] if (args.bow or args.bow_match) else []) + (["bow_match"] if args.bow_match else [])
     # per-stage average durations over the timed steps (ms per launch-group, BS frames),
     # each bracketed by events on the stream its kernels run on
     st = {s: 0.0 for s in STAGES_RUN}
@@ -534,8 +563,10 @@ def run_mono(args, cfg, rank, world, local, dist):
         for i, s in enumerate(names[:5]):
             if s:
                 st[s] += evs[i].elapsed_ms(evs[i + 1])
-        if args.bow:
+        if args.bow or args.bow_match:
             st["bow_transform"] += evs[9].elapsed_ms(evs[10])
+        if args.bow_match:
+            st["bow_match"] += evs[10].elapsed_ms(evs[12])
         if not args.no_match:
             st["hamming_top2"] += evs[6].elapsed_ms(evs[7])
             st["search_init"] += evs[11].elapsed_ms(evs[8])
@@ -605,7 +636,8 @@ def run_mono(args, cfg, rank, world, local, dist):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded shapes + noise sequence, orb_slam_cuda_amd/synth.py), "
                     f"{pool} resident frames per GPU cycled batch by batch",
-            "config": {"workload": workload + (" + Frame::ComputeBoW (synthetic k10 L6 vocabulary)" if args.bow else ""),
+            "config": {"workload": workload + (" + Frame::ComputeBoW (synthetic k10 L6 vocabulary)" if (args.bow or args.bow_match) else "")
+                                   + (" + SearchByBoW(KF t-1, F t)" if args.bow_match else ""),
                        "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
                        "frames_per_step_per_gpu": B, "resident_pool_frames": pool,
                        "parallelism": f"frame-sharded x{world}, one process per GPU, no collectives",
@@ -625,6 +657,8 @@ def run_mono(args, cfg, rank, world, local, dist):
             "host_issue_ms_per_step": round(issue / args.steps * 1e3, 4), "event_ms_per_step": round(ev_ms / args.steps, 4),
             "keypoints_per_frame": round(nkp_mean, 1),
             "init_matches_per_pair": round(float(nm.mean()), 1),
+            "bow_matches_per_pair": (round(float(pipe.d_bow_nm.download(B, np.int32).mean()), 1)
+                                     if args.bow_match else None),
         }
         print(json.dumps(out), flush=True)
 

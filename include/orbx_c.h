@@ -498,6 +498,26 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
                        orbm_feature_vector fvB, float nnratio, int check_ori,
                        int kf_vs_kf, int* out, int* nmatches);
 
+/* Batched device-resident SearchByBoW over `pairs` (A, B) pairs on `stream`,
+ * one workgroup per pair (Tracking::TrackReferenceKeyFrame calls the KF-F
+ * form once per frame, src/Tracking.cc:839-842; relocalisation once per
+ * candidate, :1445). Pair p: keypoints (orbx_kp, angles read from them),
+ * descriptors (32 B rows) and MapPoint masks at p*kp_pitch of each side
+ * (d_mpA/d_mpB NULL = every feature has one; d_mpB is read for kf_vs_kf
+ * only), counts d_nA[p]/d_nB[p]; FeatureVectors as CSR at p*node_pitch
+ * (offsets at p*(node_pitch+1)), d_nnA[p]/d_nnB[p] nodes: exactly the layout
+ * orbv_transform_batch writes (node_pitch = its cap). Output at p*kp_pitch:
+ * kf_vs_kf = 0: out[iB] = matched A index or -1 (vpMapPointMatches);
+ * kf_vs_kf = 1: out[iA] = matched B index or -1; d_nmatches[p]. */
+int orbm_search_by_bow_batch(orbm_handle m, int pairs, int kp_pitch, int node_pitch,
+                             const orbx_kp* d_kpA, const uint8_t* d_descA, const int* d_nA,
+                             const uint8_t* d_mpA, const uint32_t* d_nodesA, const int* d_offA,
+                             const int* d_idxA, const int* d_nnA, const orbx_kp* d_kpB,
+                             const uint8_t* d_descB, const int* d_nB, const uint8_t* d_mpB,
+                             const uint32_t* d_nodesB, const int* d_offB, const int* d_idxB,
+                             const int* d_nnB, float nnratio, int check_ori, int kf_vs_kf,
+                             int* d_out, int* d_nmatches, void* stream);
+
 /* Frame::ComputeStereoMatches (src/Frame.cc:465-639) on host buffers
  * (synchronous). kpL/descL = mvKeys/mDescriptors of the left image, kpR/descR
  * = mvKeysRight/mDescriptorsRight; the SAD refinement reads mvImagePyramid of

@@ -124,6 +124,8 @@ def lib() -> C.CDLL:
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, FeatureVectorC, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_int, FeatureVectorC, C.c_float, C.c_int, C.c_int, C.c_void_p,
             C.POINTER(C.c_int)]
+        L.orbm_search_by_bow_batch.argtypes = ([C.c_void_p, C.c_int, C.c_int, C.c_int] + [C.c_void_p] * 16
+                                               + [C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
         L.orbm_compute_stereo_matches.argtypes = [
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
             C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]

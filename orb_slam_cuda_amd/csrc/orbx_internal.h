@@ -171,12 +171,7 @@ int launch_search_init(const MatchBuffers& M, const orbx_kp* kp1, const uint8_t*
                        const int* n1, const orbx_kp* kp2, const uint8_t* desc2, const int* n2,
                        int kp_pitch, int pairs, orbm_grid_bounds b, float* prev_xy, int window,
                        float nnratio, int check_ori, int* matches12, int* nmatches, void* stream);
-int launch_search_bow(const uint8_t* descA, const float* angleA, const uint8_t* mpA, int nA,
-                      const uint32_t* nodesA, const int* offA, const int* idxA, int nnA,
-                      const uint8_t* descB, const float* angleB, const uint8_t* mpB, int nB,
-                      const uint32_t* nodesB, const int* offB, const int* idxB, int nnB,
-                      float nnratio, int check_ori, int kf_vs_kf, int* out, int* nmatches,
-                      int* scratch, void* stream);
+
 
 // orbx_stereo.hip — Frame::ComputeStereoMatches over a batch of rectified pairs.
 // Pyramid pointers address pair 0; pair p's level l is at base[l] + p * fstride[l].

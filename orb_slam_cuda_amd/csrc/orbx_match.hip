@@ -445,47 +445,189 @@ __device__ __forceinline__ Top2 wave_top2(bool valid, int dist, int pos) {
 }
 
 // ------------------------------------------------------------ SearchByBoW
-// One block; shared vocabulary nodes are independent (DBoW2 puts every
-// feature in exactly one node), so each wave takes whole nodes and runs the
-// reference's greedy per-node loop with the best/second reduction across
-// lanes. scratch: [nnA] shared-node partner index.
-__global__ __launch_bounds__(256) void search_bow_kernel(
-    const uint8_t* __restrict__ descA, const float* __restrict__ angleA, const uint8_t* __restrict__ mpA, int nA,
-    const uint32_t* __restrict__ nodesA, const int* __restrict__ offA, const int* __restrict__ idxA, int nnA,
-    const uint8_t* __restrict__ descB, const float* __restrict__ angleB, const uint8_t* __restrict__ mpB, int nB,
-    const uint32_t* __restrict__ nodesB, const int* __restrict__ offB, const int* __restrict__ idxB, int nnB,
-    float nnratio, int check_ori, int kf_vs_kf, int* __restrict__ out, int* __restrict__ nmatches,
-    int* __restrict__ binOf /* nA or nB entries */) {
-  __shared__ int s_hist[32];
-  __shared__ int s_var[8];
+// One workgroup per (A, B) pair, batched over the grid. Shared vocabulary
+// nodes are independent (DBoW2 puts every feature in exactly one node, so a
+// node's B features are touched by that node's A features only), so each
+// wave takes whole nodes and runs the reference's greedy per-node loop with
+// the best/second reduction across lanes; the rotation histogram is the
+// workgroup's. binOf: per-pair scratch [nout] of histogram bins.
+struct BowSide {
+  const uint8_t* desc;  // pair p: desc + p * kp_pitch * 32
+  const float* angle;   // keypoint i's angle at angle[p * kp_pitch * angle_stride + i * angle_stride]
+  int angle_stride;     // 1 for an angle array, 7 for orbx_kp records
+  const uint8_t* mp;    // has a (good) MapPoint, or null = all
+  const int* n;         // features per pair
+  const uint32_t* nodes;  // FeatureVector CSR: pair p at p * node_pitch (off: p * (node_pitch + 1))
+  const int* off;
+  const int* idx;
+  const int* nn;        // nodes per pair
+  long long kp_pitch, node_pitch;
+};
+
+constexpr int kBowGroups = 4;    // workgroups per pair (node ranges)
+constexpr int kBowThreads = 256;
+constexpr int kBowMaxB = 256;    // B features of a node held in registers (4 chunks of 64 lanes)
+
+// Grid: pairs x G workgroups; workgroup g of a pair takes its nodes g, g+G, ...
+// through a wave-level work queue. A node's B features are touched by that
+// node's A features only (DBoW2 puts every feature in one node), so the taken
+// bits of a workgroup's nodes are private to it; the rotation histogram and
+// the match count are the pair's (global atomics, hist[0..29] bins, hist[30]
+// count), and search_bow_finalize_kernel applies ComputeThreeMaxima after.
+template <int NT>
+__global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, float nnratio, int check_ori,
+                                                        int kf_vs_kf, int G, int* __restrict__ out_all,
+                                                        long long out_pitch, int* __restrict__ bin_all,
+                                                        int* __restrict__ hist_all) {
+  constexpr int kWaves = NT / 64;
   __shared__ uint32_t s_taken_[2048];  // one bit per B feature: matched (vbMatched2 / vpMapPointMatches set)
+  __shared__ uint32_t s_nodesB[2048];  // the pair's B node ids (binary searches in LDS)
+  __shared__ uint32_t s_adesc[kWaves][64][8];  // per wave: a chunk of the node's A descriptors
+  __shared__ int s_aidx[kWaves][64];           // and their feature index, -1 without a MapPoint
+  __shared__ int s_bidx[kWaves][kBowMaxB];     // the node's B feature indices in node order
+  __shared__ int s_queue;
   volatile uint32_t* s_taken = s_taken_;
+  const int p = blockIdx.x / G, g = blockIdx.x - p * G;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int nout = kf_vs_kf ? nA : nB;
-  for (int i = tid; i < 2048; i += 256) s_taken_[i] = 0;
-  for (int i = tid; i < nout; i += 256) {
-    out[i] = -1;
-    binOf[i] = -1;
-  }
-  if (tid < 32) s_hist[tid] = 0;
-  if (tid == 0) s_var[0] = 0;
+  const int nnA = A.nn[p], nnB = B.nn[p];
+  const uint8_t* descA = A.desc + p * A.kp_pitch * 32;
+  const uint8_t* descB = B.desc + p * B.kp_pitch * 32;
+  const float* angA = A.angle + p * A.kp_pitch * A.angle_stride;
+  const float* angB = B.angle + p * B.kp_pitch * B.angle_stride;
+  const uint8_t* mpA = A.mp ? A.mp + p * A.kp_pitch : nullptr;
+  const uint8_t* mpB = B.mp ? B.mp + p * B.kp_pitch : nullptr;
+  const uint32_t* nodesA = A.nodes + p * A.node_pitch;
+  const uint32_t* nodesB = B.nodes + p * B.node_pitch;
+  const int* offA = A.off + p * (A.node_pitch + 1);
+  const int* offB = B.off + p * (B.node_pitch + 1);
+  const int* idxA = A.idx + p * A.node_pitch;
+  const int* idxB = B.idx + p * B.node_pitch;
+  int* out = out_all + p * out_pitch;
+  int* binOf = bin_all + p * out_pitch;
+  int* hist = hist_all + p * 32;
+  for (int i = tid; i < 2048; i += NT) s_taken_[i] = 0;
+  const bool nodes_lds = nnB <= 2048;
+  if (nodes_lds)
+    for (int i = tid; i < nnB; i += NT) s_nodesB[i] = nodesB[i];
+  if (tid == 0) s_queue = 0;
   __syncthreads();
   const float factor = 1.0f / kHistoLength;
-  for (int ka = wv; ka < nnA; ka += 4) {
-    // lower_bound of nodesA[ka] in nodesB
+  // an accepted match: output, taken bit, the pair's count and rotation histogram (one lane)
+  auto accept = [&](int idx1, int bestIdx2) {
+    int histIdx;
+    if (kf_vs_kf) {
+      out[idx1] = bestIdx2;
+      histIdx = idx1;
+    } else {
+      out[bestIdx2] = idx1;
+      histIdx = bestIdx2;
+    }
+    atomicOr((unsigned*)&s_taken[bestIdx2 >> 5], 1u << (bestIdx2 & 31));
+    atomicAdd(&hist[30], 1);
+    if (check_ori) {
+      float rot = __fsub_rn(angA[(long long)idx1 * A.angle_stride], angB[(long long)bestIdx2 * B.angle_stride]);
+      if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+      int bin = (int)roundf(__fmul_rn(rot, factor));
+      if (bin == kHistoLength) bin = 0;
+      binOf[histIdx] = bin;
+      atomicAdd(&hist[bin], 1);
+    }
+  };
+  for (;;) {
+    int qi = 0;
+    if (lane == 0) qi = atomicAdd(&s_queue, 1);
+    const int ka = g + G * __builtin_amdgcn_readfirstlane(qi);
+    if (ka >= nnA) break;
+    // lower_bound of nodesA[ka] in nodesB (the lock-step walk of :180-264 meets exactly the shared ids)
     const uint32_t id = nodesA[ka];
     int lo = 0, hi = nnB;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (nodesB[mid] < id) lo = mid + 1;
+      if ((nodes_lds ? s_nodesB[mid] : nodesB[mid]) < id) lo = mid + 1;
       else hi = mid;
     }
-    if (lo >= nnB || nodesB[lo] != id) continue;
-    const int kb = lo;
-    const int b0 = offB[kb], b1 = offB[kb + 1];
-    for (int pa = offA[ka]; pa < offA[ka + 1]; ++pa) {
+    if (lo >= nnB || (nodes_lds ? s_nodesB[lo] : nodesB[lo]) != id) continue;
+    const int b0 = offB[lo], b1 = offB[lo + 1];
+    const int a0i = offA[ka], a1i = offA[ka + 1];
+    const int nbn = b1 - b0;
+    if (nbn <= kBowMaxB) {
+      // the node's B descriptors in registers (lane l holds positions l, l+64,
+      // ...), A descriptors staged 64 at a time in LDS and read back as
+      // broadcasts: the greedy loop over A waits on no global load
+      constexpr int kC = kBowMaxB / 64;
+      uint4 q0[kC], q1[kC];
+      int bidx[kC];
+      bool bok[kC];
+#pragma unroll
+      for (int c = 0; c < kC; ++c) {
+        const int pos = c * 64 + lane;
+        bidx[c] = -1;
+        bok[c] = false;
+        q0[c] = q1[c] = make_uint4(0, 0, 0, 0);
+        if (pos < nbn) {
+          const int i2 = idxB[b0 + pos];
+          bidx[c] = i2;
+          bok[c] = !kf_vs_kf || !mpB || mpB[i2] != 0;
+          const uint4* d2 = (const uint4*)(descB + (long long)i2 * 32);
+          q0[c] = d2[0];
+          q1[c] = d2[1];
+          s_bidx[wv][pos] = i2;
+        }
+      }
+      for (int ac = a0i; ac < a1i; ac += 64) {
+        const int nan_ = min(64, a1i - ac);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < nan_) {
+          const int i1 = idxA[ac + lane];
+          const bool ok = !mpA || mpA[i1];
+          const uint4* d1 = (const uint4*)(descA + (long long)i1 * 32);
+          const uint4 v0 = d1[0], v1 = d1[1];
+          uint32_t* w = s_adesc[wv][lane];
+          w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w;
+          w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
+          s_aidx[wv][lane] = ok ? i1 : -1;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int i = 0; i < nan_; ++i) {
+          const int idx1 = s_aidx[wv][i];
+          if (idx1 < 0) continue;  // (:191-197) uniform
+          const uint32_t* w = s_adesc[wv][i];
+          const uint4 a0 = make_uint4(w[0], w[1], w[2], w[3]), a1 = make_uint4(w[4], w[5], w[6], w[7]);
+          // per lane the two smallest (distance << 16 | position) keys over its
+          // chunks, then the wave's: position order = the node vector's order,
+          // so equal distances resolve to the earlier candidate as in :211-226
+          uint32_t k1 = 0x7FFFFFFFu, k2 = 0x7FFFFFFFu;
+#pragma unroll
+          for (int c = 0; c < kC; ++c) {
+            if (c * 64 >= nbn) break;  // uniform
+            const int i2 = bidx[c];
+            const bool valid = i2 >= 0 && bok[c] && !((s_taken[i2 >> 5] >> (i2 & 31)) & 1u);
+            if (valid) {
+              const uint32_t key = ((uint32_t)hamming256(a0, a1, q0[c], q1[c]) << 16) | (uint32_t)(c * 64 + lane);
+              k2 = min(k2, max(k1, key));
+              k1 = min(k1, key);
+            }
+          }
+          const uint32_t m1 = (uint32_t)wave_min((int)k1);
+          const uint32_t m2 = (uint32_t)wave_min((int)(k1 == m1 ? k2 : k1));
+          // merged with the initial best = second = 256 of the reference loop
+          const int d1 = m1 == 0x7FFFFFFFu ? 256 : min((int)(m1 >> 16), 256);
+          const int d2 = m2 == 0x7FFFFFFFu ? 256 : min((int)(m2 >> 16), 256);
+          const bool pass = kf_vs_kf ? (d1 < kThLow) : (d1 <= kThLow);
+          if (pass && (float)d1 < __fmul_rn(nnratio, (float)d2)) {
+            if (lane == 0) accept(idx1, s_bidx[wv][m1 & 0xFFFF]);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+      }
+      continue;
+    }
+    // very large nodes: candidates streamed from global memory 64 at a time
+    for (int pa = a0i; pa < a1i; ++pa) {
       const int idx1 = idxA[pa];
-      if (!mpA[idx1]) continue;
+      if (mpA && !mpA[idx1]) continue;
       const uint4* d1 = (const uint4*)(descA + (long long)idx1 * 32);
       const uint4 a0 = d1[0], a1 = d1[1];
       Top2 acc{256, -1, 256};
@@ -496,7 +638,7 @@ __global__ __launch_bounds__(256) void search_bow_kernel(
         if (q < b1) {
           idx2 = idxB[q];
           const bool taken = (s_taken[idx2 >> 5] >> (idx2 & 31)) & 1u;
-          valid = !taken && (!kf_vs_kf || mpB[idx2] != 0);
+          valid = !taken && (!kf_vs_kf || !mpB || mpB[idx2] != 0);
           if (valid) {
             const uint4* d2 = (const uint4*)(descB + (long long)idx2 * 32);
             dist = hamming256(a0, a1, d2[0], d2[1]);
@@ -512,38 +654,29 @@ __global__ __launch_bounds__(256) void search_bow_kernel(
       }
       const bool pass = kf_vs_kf ? (acc.best < kThLow) : (acc.best <= kThLow);
       if (pass && (float)acc.best < __fmul_rn(nnratio, (float)acc.second)) {
-        if (lane == 0) {
-          const int bestIdx2 = acc.pos;
-          int histIdx;
-          if (kf_vs_kf) {
-            out[idx1] = bestIdx2;
-            histIdx = idx1;
-          } else {
-            out[bestIdx2] = idx1;
-            histIdx = bestIdx2;
-          }
-          atomicOr((unsigned*)&s_taken[bestIdx2 >> 5], 1u << (bestIdx2 & 31));
-          atomicAdd(&s_var[0], 1);
-          if (check_ori) {
-            float rot = __fsub_rn(angleA[idx1], angleB[bestIdx2]);
-            if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-            int bin = (int)roundf(__fmul_rn(rot, factor));
-            if (bin == kHistoLength) bin = 0;
-            binOf[histIdx] = bin;
-            atomicAdd(&s_hist[bin], 1);
-          }
-        }
+        if (lane == 0) accept(idx1, acc.pos);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
       }
     }
   }
-  __syncthreads();
+}
+
+// Rotation consistency (src/ORBmatcher.cc:267-285, ComputeThreeMaxima :1601-1642)
+// and the final count, one workgroup per pair.
+__global__ __launch_bounds__(256) void search_bow_finalize_kernel(const int* __restrict__ nA, const int* __restrict__ nB,
+                                                                  int kf_vs_kf, int check_ori, int* __restrict__ out_all,
+                                                                  long long out_pitch, const int* __restrict__ bin_all,
+                                                                  int* __restrict__ hist_all, int* __restrict__ nmatches) {
+  __shared__ int s_var[4];
+  const int p = blockIdx.x, tid = threadIdx.x;
+  int* hist = hist_all + p * 32;
+  const int nout = kf_vs_kf ? nA[p] : min(nB[p], 65536);
   if (check_ori) {
     if (tid == 0) {
       int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
       for (int i = 0; i < kHistoLength; i++) {
-        const int s = s_hist[i];
+        const int s = hist[i];
         if (s > max1) {
           max3 = max2; max2 = max1; max1 = s;
           ind3 = ind2; ind2 = ind1; ind1 = i;
@@ -561,21 +694,43 @@ __global__ __launch_bounds__(256) void search_bow_kernel(
       } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
         ind3 = -1;
       }
-      s_var[1] = ind1;
-      s_var[2] = ind2;
-      s_var[3] = ind3;
+      s_var[0] = ind1;
+      s_var[1] = ind2;
+      s_var[2] = ind3;
+      s_var[3] = 0;
     }
     __syncthreads();
-    const int ind1 = s_var[1], ind2 = s_var[2], ind3 = s_var[3];
+    const int ind1 = s_var[0], ind2 = s_var[1], ind3 = s_var[2];
+    int* out = out_all + p * out_pitch;
+    const int* binOf = bin_all + p * out_pitch;
+    int removed = 0;
     for (int i = tid; i < nout; i += 256) {
       const int b = binOf[i];
       if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
       out[i] = -1;
-      atomicSub(&s_var[0], 1);
+      ++removed;
     }
+    if (removed) atomicAdd(&s_var[3], removed);
     __syncthreads();
+    if (tid == 0) nmatches[p] = hist[30] - s_var[3];
+  } else if (tid == 0) {
+    nmatches[p] = hist[30];
   }
-  if (tid == 0) *nmatches = s_var[0];
+}
+
+int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnratio, int check_ori, int kf_vs_kf,
+                      int* out, long long out_pitch, int* nmatches, int* bin_scratch, int* hist_scratch, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  // outputs and bins start at -1 (0xFF bytes), histograms and counts at 0
+  if (hipMemsetAsync(out, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
+      hipMemsetAsync(bin_scratch, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
+      hipMemsetAsync(hist_scratch, 0, (size_t)pairs * 32 * 4, s) != hipSuccess)
+    return ORBX_EDEVICE;
+  hipLaunchKernelGGL(search_bow_kernel<kBowThreads>, dim3(pairs * kBowGroups), dim3(kBowThreads), 0, s, A, B, nnratio,
+                     check_ori, kf_vs_kf, kBowGroups, out, out_pitch, bin_scratch, hist_scratch);
+  hipLaunchKernelGGL(search_bow_finalize_kernel, dim3(pairs), dim3(256), 0, s, A.n, B.n, kf_vs_kf, check_ori, out,
+                     out_pitch, bin_scratch, hist_scratch, nmatches);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
 // ------------------------------------------------------------ launchers
@@ -631,7 +786,8 @@ struct orbx_matcher {
   long long cand_cap = 0;
   uint32_t* cand = nullptr;
   int* err = nullptr;
-  int* stereo_sad = nullptr;  // [max_pairs][max_kps] SAD per left keypoint (-1 = none)
+  int* stereo_sad = nullptr;  // [max_pairs][max_kps] SAD per left keypoint (-1 = none); SearchByBoW bins
+  int* bow_hist = nullptr;    // [max_pairs][32] SearchByBoW rotation histogram (+ match count)
   int* pose_picks = nullptr;  // pose-projection picks per point (frames x mp_pitch)
   size_t pose_picks_cap = 0;
   hipStream_t stream = nullptr;
@@ -667,7 +823,8 @@ int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out) {
   m->cand_cap = std::min<long long>((long long)max_kps * max_kps, 4ll << 20);
   if (hipMalloc(&m->cand, (size_t)max_pairs * m->cand_cap * 4) != hipSuccess ||
       hipMalloc(&m->err, 16) != hipSuccess ||
-      hipMalloc(&m->stereo_sad, (size_t)max_pairs * max_kps * 4) != hipSuccess) {
+      hipMalloc(&m->stereo_sad, (size_t)max_pairs * max_kps * 4) != hipSuccess ||
+      hipMalloc(&m->bow_hist, (size_t)max_pairs * 32 * 4) != hipSuccess) {
     orbm_destroy(m);
     return mfail(ORBX_ENOMEM, "matcher workspace allocation failed");
   }
@@ -685,6 +842,7 @@ int orbm_destroy(orbm_handle m) {
   if (m->cand) (void)hipFree(m->cand);
   if (m->err) (void)hipFree(m->err);
   if (m->stereo_sad) (void)hipFree(m->stereo_sad);
+  if (m->bow_hist) (void)hipFree(m->bow_hist);
   if (m->pose_picks) (void)hipFree(m->pose_picks);
   if (m->stage) (void)hipFree(m->stage);
   if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -860,14 +1018,14 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
                        r16((size_t)(fvA.n_nodes + 1) * 4), r16((size_t)ia * 4), r16((size_t)nB * 32),
                        r16((size_t)nB * 4), r16((size_t)nB), r16((size_t)fvB.n_nodes * 4),
                        r16((size_t)(fvB.n_nodes + 1) * 4), r16((size_t)ib * 4), r16((size_t)nout * 4),
-                       r16((size_t)nout * 4), 16};
+                       r16((size_t)nout * 4), 16, 16, 128};
   size_t tot = 0;
   for (size_t v : sz) tot += v;
   int rc;
   if ((rc = stage_reserve(m, tot))) return rc;
   uint8_t* p = (uint8_t*)m->stage;
-  void* d[15];
-  for (int i = 0; i < 15; ++i) {
+  void* d[17];
+  for (int i = 0; i < 17; ++i) {
     d[i] = p;
     p += sz[i];
   }
@@ -877,26 +1035,54 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
     if (n && src) MHIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));
     return ORBX_OK;
   };
-  std::vector<uint8_t> mpBdef;
-  if (!mpB) mpBdef.assign(std::max(nB, 1), 1), mpB = mpBdef.data();
+  const int hn[4] = {nA, nB, fvA.n_nodes, fvB.n_nodes};
   if ((rc = up(d[0], descA, (size_t)nA * 32)) || (rc = up(d[1], angleA, (size_t)nA * 4)) ||
       (rc = up(d[2], mpA, (size_t)nA)) || (rc = up(d[3], fvA.nodes, (size_t)fvA.n_nodes * 4)) ||
       (rc = up(d[4], fvA.off, (size_t)(fvA.n_nodes + 1) * 4)) || (rc = up(d[5], fvA.idx, (size_t)ia * 4)) ||
       (rc = up(d[6], descB, (size_t)nB * 32)) || (rc = up(d[7], angleB, (size_t)nB * 4)) ||
       (rc = up(d[8], mpB, (size_t)nB)) || (rc = up(d[9], fvB.nodes, (size_t)fvB.n_nodes * 4)) ||
-      (rc = up(d[10], fvB.off, (size_t)(fvB.n_nodes + 1) * 4)) || (rc = up(d[11], fvB.idx, (size_t)ib * 4)))
+      (rc = up(d[10], fvB.off, (size_t)(fvB.n_nodes + 1) * 4)) || (rc = up(d[11], fvB.idx, (size_t)ib * 4)) ||
+      (rc = up(d[15], hn, sizeof hn)))
     return rc;
-  hipLaunchKernelGGL(search_bow_kernel, dim3(1), dim3(256), 0, st, (const uint8_t*)d[0], (const float*)d[1],
-                     (const uint8_t*)d[2], nA, (const uint32_t*)d[3], (const int*)d[4], (const int*)d[5],
-                     fvA.n_nodes, (const uint8_t*)d[6], (const float*)d[7], (const uint8_t*)d[8], nB,
-                     (const uint32_t*)d[9], (const int*)d[10], (const int*)d[11], fvB.n_nodes, nnratio, check_ori,
-                     kf_vs_kf, (int*)d[12], (int*)d[14], (int*)d[13]);
-  MHIP(hipGetLastError());
+  const int* dn = (const int*)d[15];
+  BowSide A{(const uint8_t*)d[0], (const float*)d[1], 1, mpA ? (const uint8_t*)d[2] : nullptr, dn,
+            (const uint32_t*)d[3], (const int*)d[4], (const int*)d[5], dn + 2, 0, 0};
+  BowSide B{(const uint8_t*)d[6], (const float*)d[7], 1, mpB ? (const uint8_t*)d[8] : nullptr, dn + 1,
+            (const uint32_t*)d[9], (const int*)d[10], (const int*)d[11], dn + 3, 0, 0};
+  if ((rc = launch_search_bow(A, B, 1, nnratio, check_ori, kf_vs_kf, (int*)d[12], std::max(nout, 1), (int*)d[14],
+                              (int*)d[13], (int*)d[16], st)))
+    return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
   int nm = 0;
   MHIP(hipMemcpyAsync(&nm, d[14], 4, hipMemcpyDeviceToHost, st));
   if (nout) MHIP(hipMemcpyAsync(out, d[12], (size_t)nout * 4, hipMemcpyDeviceToHost, st));
   MHIP(hipStreamSynchronize(st));
   *nmatches = nm;
+  return ORBX_OK;
+}
+
+int orbm_search_by_bow_batch(orbm_handle m, int pairs, int kp_pitch, int node_pitch, const orbx_kp* d_kpA,
+                             const uint8_t* d_descA, const int* d_nA, const uint8_t* d_mpA, const uint32_t* d_nodesA,
+                             const int* d_offA, const int* d_idxA, const int* d_nnA, const orbx_kp* d_kpB,
+                             const uint8_t* d_descB, const int* d_nB, const uint8_t* d_mpB, const uint32_t* d_nodesB,
+                             const int* d_offB, const int* d_idxB, const int* d_nnB, float nnratio, int check_ori,
+                             int kf_vs_kf, int* d_out, int* d_nmatches, void* stream) {
+  if (!m || pairs < 1 || kp_pitch < 1 || node_pitch < 1 || !d_kpA || !d_descA || !d_nA || !d_nodesA || !d_offA ||
+      !d_idxA || !d_nnA || !d_kpB || !d_descB || !d_nB || !d_nodesB || !d_offB || !d_idxB || !d_nnB || !d_out ||
+      !d_nmatches)
+    return mfail(ORBX_EINVAL, "bad argument");
+  if (pairs > m->max_pairs || kp_pitch > m->max_kps)
+    return mfail(ORBX_ECAPACITY, "pairs/kp_pitch above the matcher's max_pairs/max_kps");
+  if (kp_pitch > 65536) return mfail(ORBX_EINVAL, "kp_pitch must be <= 65536");
+  MHIP(hipSetDevice(m->device));
+  // angles straight from the orbx_kp records (cv::KeyPoint::angle, float 3 of 7)
+  BowSide A{d_descA, (const float*)d_kpA + 3, 7, d_mpA, d_nA, d_nodesA, d_offA, d_idxA, d_nnA, kp_pitch, node_pitch};
+  BowSide B{d_descB, (const float*)d_kpB + 3, 7, d_mpB, d_nB, d_nodesB, d_offB, d_idxB, d_nnB, kp_pitch, node_pitch};
+  hipStream_t s = (hipStream_t)stream;
+  if (m->ws.before(s)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
+  const int rc = launch_search_bow(A, B, pairs, nnratio, check_ori, kf_vs_kf, d_out, kp_pitch, d_nmatches,
+                                   m->stereo_sad, m->bow_hist, stream);
+  if (rc) return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
+  if (m->ws.after(s)) return mfail(ORBX_EDEVICE, "event record failed");
   return ORBX_OK;
 }
 
