@@ -1,0 +1,63 @@
+// Source-compatible replacement for the reference's include/ORBextractor.h
+// (:75-197): the same class, constructor, operator() and getters, with the
+// VisionWorks graph members (:119-196) replaced by one liborbx handle. Frame,
+// Tracking and the rest compile against it unchanged.
+#ifndef ORBEXTRACTOR_H
+#define ORBEXTRACTOR_H
+
+#include <list>
+#include <vector>
+
+#include <opencv2/core/core.hpp>
+
+#include "orbx_c.h"
+
+namespace ORB_SLAM2 {
+
+class ORBextractor {
+ public:
+  enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
+
+  ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST, int width, int height);
+  ~ORBextractor();
+  ORBextractor(const ORBextractor&) = delete;
+  ORBextractor& operator=(const ORBextractor&) = delete;
+
+  // Compute the ORB features and descriptors on an image (mask ignored, as
+  // in the reference).
+  void operator()(cv::InputArray image, cv::InputArray mask, std::vector<cv::KeyPoint>& keypoints,
+                  cv::OutputArray descriptors);
+
+  int inline GetLevels() { return nlevels; }
+  float inline GetScaleFactor() { return (float)scaleFactor; }
+  std::vector<float> inline GetScaleFactors() { return mvScaleFactor; }
+  std::vector<float> inline GetInverseScaleFactors() { return mvInvScaleFactor; }
+  std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2; }
+  std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
+
+  std::vector<cv::Mat> mvImagePyramid;
+
+  // Per-stage device times of the last call, named as the reference's
+  // GetTime records ("Pyramid/Resize", "FAST+Grid", ...).
+  int GetStageTimes(std::vector<float>& ms, std::vector<const char*>& names);
+
+ protected:
+  int nfeatures;
+  double scaleFactor;
+  int nlevels;
+  int iniThFAST;
+  int minThFAST;
+
+  std::vector<int> mnFeaturesPerLevel;
+  std::vector<float> mvScaleFactor;
+  std::vector<float> mvInvScaleFactor;
+  std::vector<float> mvLevelSigma2;
+  std::vector<float> mvInvLevelSigma2;
+
+  orbx_handle h_ = nullptr;
+  int cap_ = 0;
+};
+
+}  // namespace ORB_SLAM2
+
+#endif

@@ -1,0 +1,87 @@
+// ORBextractor over liborbx: replaces the reference's src/ORBextractor.cc
+// (constructor :496-560, operator() :1538-1548 / CPU branch :1710-1808).
+#include "ORBextractor.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace ORB_SLAM2 {
+
+static void orbx_check(int rc) {
+  if (rc != ORBX_OK) throw std::runtime_error(std::string("liborbx: ") + orbx_last_error());  // NVXIO_SAFE_CALL
+}
+
+static_assert(sizeof(cv::KeyPoint) == sizeof(orbx_kp), "cv::KeyPoint must be layout-identical to orbx_kp");
+
+ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST,
+                           int width, int height)
+    : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
+      minThFAST(_minThFAST) {
+  orbx_config c = {};
+  c.nfeatures = _nfeatures;
+  c.scale_factor = _scaleFactor;
+  c.nlevels = _nlevels;
+  c.ini_th_fast = _iniThFAST;
+  c.min_th_fast = _minThFAST;
+  c.width = width;
+  c.height = height;
+  c.device = 0;
+  c.max_batch = 1;
+  c.scale_mode = ORBX_SCALE_U;
+  c.pattern_mode = ORBX_PATTERN_FORK;
+  orbx_check(orbx_create(&c, &h_));
+  mvScaleFactor.resize(nlevels);
+  mvInvScaleFactor.resize(nlevels);
+  mvLevelSigma2.resize(nlevels);
+  mvInvLevelSigma2.resize(nlevels);
+  orbx_check(orbx_get_scales(h_, mvScaleFactor.data(), mvInvScaleFactor.data(), mvLevelSigma2.data(),
+                             mvInvLevelSigma2.data()));
+  std::vector<int> lw(nlevels), lh(nlevels);
+  mnFeaturesPerLevel.resize(nlevels);
+  int nl = 0;
+  orbx_check(orbx_get_levels_info(h_, &nl, lw.data(), lh.data(), mnFeaturesPerLevel.data()));
+  cap_ = orbx_frame_capacity(h_);
+  if (cap_ <= 0) throw std::runtime_error("liborbx: bad frame capacity");
+}
+
+ORBextractor::~ORBextractor() {
+  if (h_) orbx_destroy(h_);
+}
+
+void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask*/, std::vector<cv::KeyPoint>& _keypoints,
+                              cv::OutputArray _descriptors) {
+  if (_image.empty()) return;  // :1542-1543
+  cv::Mat image = _image.getMat();
+  assert(image.type() == CV_8UC1);  // :1546
+  _keypoints.resize(cap_);
+  cv::Mat desc(cap_, 32, CV_8U);
+  int n = 0;
+  orbx_check(orbx_extract(h_, image.data, image.cols, image.rows, image.step,
+                          reinterpret_cast<orbx_kp*>(_keypoints.data()), cap_, desc.data, &n));
+  _keypoints.resize(n);
+  if (n == 0)
+    _descriptors.release();  // :1716-1717
+  else
+    desc.rowRange(0, n).copyTo(_descriptors);  // _descriptors.create(nkeypoints, 32, CV_8U) :1719
+  // mvImagePyramid: read by Frame::ComputeStereoMatches (src/Frame.cc:472-579)
+  mvImagePyramid.resize(nlevels);
+  std::vector<int> lw(nlevels), lh(nlevels), nfl(nlevels);
+  int nl = 0;
+  orbx_check(orbx_get_levels_info(h_, &nl, lw.data(), lh.data(), nfl.data()));
+  for (int l = 0; l < nlevels; ++l) {
+    mvImagePyramid[l].create(lh[l], lw[l], CV_8U);
+    orbx_check(orbx_get_level(h_, /*frame=*/0, l, /*blurred=*/0, mvImagePyramid[l].data, mvImagePyramid[l].step));
+  }
+}
+
+int ORBextractor::GetStageTimes(std::vector<float>& ms, std::vector<const char*>& names) {
+  ms.assign(16, 0.f);
+  names.assign(16, nullptr);
+  int n = 0;
+  orbx_check(orbx_get_stage_times(h_, ms.data(), names.data(), 16, &n));
+  ms.resize(n);
+  names.resize(n);
+  return n;
+}
+
+}  // namespace ORB_SLAM2
