@@ -70,7 +70,7 @@ STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_t
 # front_tile_kernel (blur + FAST + NMS + per-cell threshold choice per tile)
 FRONT_STAGES = ["pyramid", None, "blur_fast", "quadtree", "orient_brief", "hamming_top2", "search_init"]
 KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
-           "blur_fast": "front_tile_kernel", "bow_match": "search_bow_kernel<512>",
+           "blur_fast": "front_tile_kernel", "bow_match": "search_bow_kernel<256>",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
            "hamming_top2": "hamming_top2_mfma_kernel", "search_init": "search_init_kernel"}
 KP, DS = 28, 32  # bytes of one orbx_kp (cv::KeyPoint) and one descriptor

@@ -445,12 +445,28 @@ __device__ __forceinline__ Top2 wave_top2(bool valid, int dist, int pos) {
 }
 
 // ------------------------------------------------------------ SearchByBoW
-// One workgroup per (A, B) pair, batched over the grid. Shared vocabulary
-// nodes are independent (DBoW2 puts every feature in exactly one node, so a
-// node's B features are touched by that node's A features only), so each
-// wave takes whole nodes and runs the reference's greedy per-node loop with
-// the best/second reduction across lanes; the rotation histogram is the
-// workgroup's. binOf: per-pair scratch [nout] of histogram bins.
+// Grid: pairs x G workgroups; workgroup g of a pair takes the pair's A nodes
+// [g*nnA/G, (g+1)*nnA/G). Shared vocabulary nodes are independent: DBoW2 puts
+// every feature in exactly one node, so a node's B features are touched by
+// that node's A features only, the taken bits of a workgroup's nodes are
+// private to it, and only the rotation histogram and the match count are the
+// pair's (global atomics: hist[0..29] bins, hist[30] count;
+// search_bow_finalize_kernel applies ComputeThreeMaxima after).
+//
+// Inside a node the reference is greedy (src/ORBmatcher.cc:186-262): A rows in
+// node order, each taking the best untaken B row. The workgroup splits that
+// into
+//  (1) a data-parallel pass, one lane per A row: the node's B rows (staged in
+//      LDS in node order, static filter applied) are scanned once and the
+//      row's K smallest keys (distance << 16 | position in the node) kept;
+//  (2) the greedy pass, one lane per node, in A order: the first two untaken
+//      keys of the row's list ARE the reference's bestDist1/bestIdx and
+//      bestDist2 (keys order ties by node position, as the strict `<` of
+//      :211-226 does), so the pass is a few register operations per row; a
+//      row whose list has fewer than two untaken keys left while it had more
+//      than K candidates rescans its node (rare).
+// A workgroup whose node range does not fit the LDS tables falls back to the
+// per-wave greedy (a wave per node, the best/second reduced across lanes).
 struct BowSide {
   const uint8_t* desc;  // pair p: desc + p * kp_pitch * 32
   const float* angle;   // keypoint i's angle at angle[p * kp_pitch * angle_stride + i * angle_stride]
@@ -464,32 +480,65 @@ struct BowSide {
   long long kp_pitch, node_pitch;
 };
 
-constexpr int kBowGroups = 4;    // workgroups per pair (node ranges)
+#ifndef ORBX_BOW_GROUPS
+#define ORBX_BOW_GROUPS 8
+#endif
+constexpr int kBowGroups = ORBX_BOW_GROUPS;  // workgroups per pair (node ranges)
 constexpr int kBowThreads = 256;
-constexpr int kBowMaxB = 256;    // B features of a node held in registers (4 chunks of 64 lanes)
+constexpr int kBowK = 8;         // smallest keys kept per A row
+constexpr int kBowCapB = 768;    // B rows staged per workgroup
+constexpr int kBowCapA = 768;    // A rows per workgroup
+constexpr int kBowCapN = 256;    // nodes per workgroup
+constexpr int kBowMaxB = 256;    // fallback: B features of a node held in registers (4 chunks of 64 lanes)
+constexpr uint32_t kBowNone = 0xFFFFFFFFu;
+#ifndef ORBX_BOW_ROUNDS
+#define ORBX_BOW_ROUNDS 16
+#endif
+constexpr int kBowRounds = ORBX_BOW_ROUNDS;  // greedy fixed-point rounds before the sequential pass (0: sequential only)
 
-// Grid: pairs x G workgroups; workgroup g of a pair takes its nodes g, g+G, ...
-// through a wave-level work queue. A node's B features are touched by that
-// node's A features only (DBoW2 puts every feature in one node), so the taken
-// bits of a workgroup's nodes are private to it; the rotation histogram and
-// the match count are the pair's (global atomics, hist[0..29] bins, hist[30]
-// count), and search_bow_finalize_kernel applies ComputeThreeMaxima after.
+struct BowTables {  // the two-pass layout
+  uint32_t bdesc[kBowCapB][8];  // the range's B rows, node by node
+  int bidx[kBowCapB];           // their feature index, -1 = not a candidate (KF-KF without a good MapPoint)
+  uint4 top[kBowCapA][2];       // per A row its kBowK = 8 smallest keys, ascending (kBowNone = empty)
+  int nv[kBowCapA];             // candidates the row saw, -1 = row skipped (no good MapPoint);
+                                // after the greedy pass: the matched staged position, or -1
+  int match[kBowCapA];          // greedy rounds: the row's current choice (staged position, -1 = none)
+  int claim[kBowCapB];          // greedy rounds: first row (in range order) choosing the position
+  int rq[kBowCapA];             // the row's node: B rows [rq & 0xFFFF, rq >> 16)
+  int boff[kBowCapN + 1];       // node j's B rows at [boff[j], boff[j+1])
+  int aoff[kBowCapN + 1];       // node j's A rows at [aoff[j], aoff[j+1]) (relative to the range)
+  int bsrc[kBowCapN];           // node j's B CSR start
+  uint32_t taken[kBowCapB / 32];  // by staged position
+};
+struct BowFallback {  // the per-wave layout
+  uint32_t taken[2048];  // one bit per B feature
+  uint32_t adesc[kBowThreads / 64][64][8];
+  int aidx[kBowThreads / 64][64];
+  int bidx[kBowThreads / 64][kBowMaxB];
+};
+union BowLds {
+  BowTables t;
+  BowFallback f;
+};
+
 template <int NT>
 __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, float nnratio, int check_ori,
                                                         int kf_vs_kf, int G, int* __restrict__ out_all,
                                                         long long out_pitch, int* __restrict__ bin_all,
-                                                        int* __restrict__ hist_all) {
+                                                        int* __restrict__ hist_all, int* dbg) {
   constexpr int kWaves = NT / 64;
-  __shared__ uint32_t s_taken_[2048];  // one bit per B feature: matched (vbMatched2 / vpMapPointMatches set)
-  __shared__ uint32_t s_nodesB[2048];  // the pair's B node ids (binary searches in LDS)
-  __shared__ uint32_t s_adesc[kWaves][64][8];  // per wave: a chunk of the node's A descriptors
-  __shared__ int s_aidx[kWaves][64];           // and their feature index, -1 without a MapPoint
-  __shared__ int s_bidx[kWaves][kBowMaxB];     // the node's B feature indices in node order
+  const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](int k, int v) {  // diagnostics only (ORBX_BOW_PROF=1): per-workgroup phase cycles
+    if (dbg && threadIdx.x == 0) dbg[blockIdx.x * 8 + k] = v < 0 ? (int)(__builtin_amdgcn_s_memtime() - t_begin) : v;
+  };
+  __shared__ BowLds S;
+  __shared__ int s_scan[kWaves + 1];
+  __shared__ int s_hist[32];
   __shared__ int s_queue;
-  volatile uint32_t* s_taken = s_taken_;
   const int p = blockIdx.x / G, g = blockIdx.x - p * G;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nnA = A.nn[p], nnB = B.nn[p];
+  const int k0 = (int)((long long)g * nnA / G), k1 = (int)((long long)(g + 1) * nnA / G), nk = k1 - k0;
   const uint8_t* descA = A.desc + p * A.kp_pitch * 32;
   const uint8_t* descB = B.desc + p * B.kp_pitch * 32;
   const float* angA = A.angle + p * A.kp_pitch * A.angle_stride;
@@ -505,15 +554,10 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
   int* out = out_all + p * out_pitch;
   int* binOf = bin_all + p * out_pitch;
   int* hist = hist_all + p * 32;
-  for (int i = tid; i < 2048; i += NT) s_taken_[i] = 0;
-  const bool nodes_lds = nnB <= 2048;
-  if (nodes_lds)
-    for (int i = tid; i < nnB; i += NT) s_nodesB[i] = nodesB[i];
-  if (tid == 0) s_queue = 0;
-  __syncthreads();
+  if (nk <= 0) return;
   const float factor = 1.0f / kHistoLength;
-  // an accepted match: output, taken bit, the pair's count and rotation histogram (one lane)
-  auto accept = [&](int idx1, int bestIdx2) {
+  // an accepted match: output, the pair's count and rotation histogram
+  auto accept = [&](int idx1, int bestIdx2, int* h) {
     int histIdx;
     if (kf_vs_kf) {
       out[idx1] = bestIdx2;
@@ -522,31 +566,326 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
       out[bestIdx2] = idx1;
       histIdx = bestIdx2;
     }
-    atomicOr((unsigned*)&s_taken[bestIdx2 >> 5], 1u << (bestIdx2 & 31));
-    atomicAdd(&hist[30], 1);
+    atomicAdd(&h[30], 1);
     if (check_ori) {
       float rot = __fsub_rn(angA[(long long)idx1 * A.angle_stride], angB[(long long)bestIdx2 * B.angle_stride]);
       if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
       int bin = (int)roundf(__fmul_rn(rot, factor));
       if (bin == kHistoLength) bin = 0;
       binOf[histIdx] = bin;
-      atomicAdd(&hist[bin], 1);
+      atomicAdd(&h[bin], 1);
     }
   };
-  for (;;) {
-    int qi = 0;
-    if (lane == 0) qi = atomicAdd(&s_queue, 1);
-    const int ka = g + G * __builtin_amdgcn_readfirstlane(qi);
-    if (ka >= nnA) break;
-    // lower_bound of nodesA[ka] in nodesB (the lock-step walk of :180-264 meets exactly the shared ids)
-    const uint32_t id = nodesA[ka];
+  // lower_bound of a node id in B's node list (the lock-step walk of :180-264
+  // meets exactly the shared ids); -1 when B lacks it
+  auto find_b = [&](uint32_t id) {
     int lo = 0, hi = nnB;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if ((nodes_lds ? s_nodesB[mid] : nodesB[mid]) < id) lo = mid + 1;
+      if (nodesB[mid] < id) lo = mid + 1;
       else hi = mid;
     }
-    if (lo >= nnB || (nodes_lds ? s_nodesB[lo] : nodesB[lo]) != id) continue;
+    return (lo < nnB && nodesB[lo] == id) ? lo : -1;
+  };
+  const int a_base = offA[k0], na = offA[k1] - a_base;
+
+  // ---- node table: B node per A node, staged B offsets (block scan of counts)
+  bool fits = nk <= kBowCapN && na <= kBowCapA;
+  if (fits) {
+    int carry = 0;
+    for (int j0 = 0; j0 < nk; j0 += NT) {
+      const int j = j0 + tid;
+      int cnt = 0, src = 0;
+      if (j < nk) {
+        const int kb = find_b(nodesA[k0 + j]);
+        if (kb >= 0) {
+          src = offB[kb];
+          cnt = offB[kb + 1] - src;
+        }
+        S.t.bsrc[j] = src;
+        S.t.aoff[j + 1] = offA[k0 + j + 1] - a_base;
+      }
+      const int incl = wave_incl_scan_dpp(cnt);
+      if (lane == 63) s_scan[wv] = incl;
+      __syncthreads();
+      int before = carry;
+      for (int w = 0; w < wv; ++w) before += s_scan[w];
+      if (j < nk) S.t.boff[j + 1] = before + incl;
+      int tot = 0;
+      for (int w = 0; w < kWaves; ++w) tot += s_scan[w];
+      carry += tot;
+      __syncthreads();
+    }
+    if (tid == 0) S.t.boff[0] = S.t.aoff[0] = 0;
+    fits = carry <= kBowCapB;  // uniform
+  }
+  stamp(1, -1);
+  if (fits) {
+    __syncthreads();
+    const int nb = S.t.boff[nk];
+    for (int i = tid; i < kBowCapB / 32; i += NT) S.t.taken[i] = 0;
+    // ---- stage the range's B rows in node order (static filter: KF-KF needs a good MapPoint)
+    for (int i = tid; i < nb; i += NT) {
+      int lo = 0, hi = nk;  // node j with boff[j] <= i < boff[j+1]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (S.t.boff[mid] <= i) lo = mid;
+        else hi = mid;
+      }
+      const int i2 = idxB[S.t.bsrc[lo] + (i - S.t.boff[lo])];
+      const bool ok = !kf_vs_kf || !mpB || mpB[i2] != 0;
+      const uint4* d2 = (const uint4*)(descB + (long long)i2 * 32);
+      const uint4 v0 = d2[0], v1 = d2[1];
+      *(uint4*)&S.t.bdesc[i][0] = v0;
+      *(uint4*)&S.t.bdesc[i][4] = v1;
+      S.t.bidx[i] = ok ? i2 : -1;
+    }
+    __syncthreads();
+    stamp(2, -1);
+    // ---- (1) per A row, its kBowK smallest keys over the node's candidates
+    for (int ia = tid; ia < na; ia += NT) {
+      int lo = 0, hi = nk;  // node j with aoff[j] <= ia < aoff[j+1]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (S.t.aoff[mid] <= ia) lo = mid;
+        else hi = mid;
+      }
+      const int i1 = idxA[a_base + ia];
+      uint32_t t0 = kBowNone, t1 = kBowNone, t2 = kBowNone, t3 = kBowNone;
+      uint32_t t4 = kBowNone, t5 = kBowNone, t6 = kBowNone, t7 = kBowNone;
+      int nv = -1;
+      if (!mpA || mpA[i1]) {  // (:191-197)
+        nv = 0;
+        const uint4* d1 = (const uint4*)(descA + (long long)i1 * 32);
+        const uint4 a0 = d1[0], a1 = d1[1];
+        const int q0 = S.t.boff[lo], q1 = S.t.boff[lo + 1];
+        auto insert = [&](uint32_t key) {  // into the ascending t0..t7
+          uint32_t m;
+          m = min(t0, key); key = max(t0, key); t0 = m;
+          m = min(t1, key); key = max(t1, key); t1 = m;
+          m = min(t2, key); key = max(t2, key); t2 = m;
+          m = min(t3, key); key = max(t3, key); t3 = m;
+          m = min(t4, key); key = max(t4, key); t4 = m;
+          m = min(t5, key); key = max(t5, key); t5 = m;
+          m = min(t6, key); key = max(t6, key); t6 = m;
+          t7 = min(t7, key);
+        };
+        // two candidates per step: their LDS reads are in flight together
+        int q = q0;
+        for (; q + 1 < q1; q += 2) {
+          const int okA = S.t.bidx[q], okB = S.t.bidx[q + 1];
+          const uint4 b0 = *(const uint4*)&S.t.bdesc[q][0], b1 = *(const uint4*)&S.t.bdesc[q][4];
+          const uint4 c0 = *(const uint4*)&S.t.bdesc[q + 1][0], c1 = *(const uint4*)&S.t.bdesc[q + 1][4];
+          const uint32_t kA = ((uint32_t)hamming256(a0, a1, b0, b1) << 16) | (uint32_t)(q - q0);
+          const uint32_t kB = ((uint32_t)hamming256(a0, a1, c0, c1) << 16) | (uint32_t)(q + 1 - q0);
+          if (okA >= 0) insert(kA), ++nv;
+          if (okB >= 0) insert(kB), ++nv;
+        }
+        if (q < q1 && S.t.bidx[q] >= 0) {
+          ++nv;
+          insert(((uint32_t)hamming256(a0, a1, *(const uint4*)&S.t.bdesc[q][0], *(const uint4*)&S.t.bdesc[q][4]) << 16) |
+                 (uint32_t)(q - q0));
+        }
+      }
+      S.t.top[ia][0] = make_uint4(t0, t1, t2, t3);
+      S.t.top[ia][1] = make_uint4(t4, t5, t6, t7);
+      S.t.nv[ia] = nv;
+      S.t.rq[ia] = S.t.boff[lo] | (S.t.boff[lo + 1] << 16);
+    }
+    __syncthreads();
+    stamp(3, -1);
+    // ---- (2) the greedy pass as a fixed point (Jacobi rounds). Row i's
+    // decision depends only on which of its candidates earlier rows of its
+    // node took; every round recomputes all rows in parallel from the previous
+    // round's choices (a position counts as taken for row i when a row before
+    // i chose it: claim = the first such row). Row 1 of a node is right in
+    // round 0 and row i by round i - 1, and a round without changes is the
+    // unique fixed point = the sequential result, so the rounds stop there.
+    // Rows with a decision changing after kBowRounds rounds fall back to the
+    // sequential pass below.
+    auto decide = [&](int ia, auto&& taken) -> int {  // staged position or -1
+      const int nv = S.t.nv[ia];
+      if (nv < 0) return -1;
+      const int rq = S.t.rq[ia], q0 = rq & 0xFFFF, q1 = rq >> 16;
+      if (q0 == q1) return -1;
+      const uint4 tA = S.t.top[ia][0], tB = S.t.top[ia][1];
+      const uint32_t keys[kBowK] = {tA.x, tA.y, tA.z, tA.w, tB.x, tB.y, tB.z, tB.w};
+      int d1 = 256, d2 = 256, p1 = -1, found = 0;
+#pragma unroll
+      for (int k = 0; k < kBowK; ++k) {
+        const uint32_t key = keys[k];
+        if (key == kBowNone || found == 2 || taken(ia, q0 + (int)(key & 0xFFFF))) continue;
+        if (found == 0) {
+          d1 = (int)(key >> 16);
+          p1 = q0 + (int)(key & 0xFFFF);
+        } else {
+          d2 = (int)(key >> 16);
+        }
+        ++found;
+      }
+      if (found < 2 && nv > kBowK) {
+        // the list ran out under taken rows: rescan the node (strict < of :211-226)
+        const int i1 = idxA[a_base + ia];
+        const uint4* da = (const uint4*)(descA + (long long)i1 * 32);
+        const uint4 a0 = da[0], a1 = da[1];
+        d1 = 256;
+        d2 = 256;
+        p1 = -1;
+        for (int q = q0; q < q1; ++q) {
+          if (S.t.bidx[q] < 0 || taken(ia, q)) continue;
+          const int dist = hamming256(a0, a1, *(const uint4*)&S.t.bdesc[q][0], *(const uint4*)&S.t.bdesc[q][4]);
+          if (dist < d1) {
+            d2 = d1;
+            d1 = dist;
+            p1 = q;
+          } else if (dist < d2) {
+            d2 = dist;
+          }
+        }
+      }
+      // d1 = 256 never passes; with d1 < 256 the reference's bestIdx is set
+      const bool pass = kf_vs_kf ? (d1 < kThLow) : (d1 <= kThLow);
+      return (pass && (float)d1 < __fmul_rn(nnratio, (float)min(d2, 256))) ? p1 : -1;
+    };
+    const int nb_ = S.t.boff[nk];
+    for (int ia = tid; ia < na; ia += NT) S.t.match[ia] = decide(ia, [](int, int) { return false; });
+    bool settled = false;
+    for (int round = 0; round < kBowRounds && !settled; ++round) {
+      for (int q = tid; q < nb_; q += NT) S.t.claim[q] = INT_MAX;
+      __syncthreads();
+      for (int ia = tid; ia < na; ia += NT) {
+        const int q = S.t.match[ia];
+        if (q >= 0) atomicMin(&S.t.claim[q], ia);
+      }
+      __syncthreads();
+      int changed = 0;
+      for (int ia = tid; ia < na; ia += NT) {
+        const int m = decide(ia, [&](int row, int q) { return S.t.claim[q] < row; });
+        if (m != S.t.match[ia]) {
+          S.t.match[ia] = m;
+          changed = 1;
+        }
+      }
+      settled = !__syncthreads_or(changed);
+    }
+    if (settled) {
+      for (int ia = tid; ia < na; ia += NT) S.t.nv[ia] = S.t.match[ia];
+    } else {
+      // sequential: one lane per node, A rows in node order, taken sets in registers
+      for (int j = tid; j < nk; j += NT) {
+        const int q0 = S.t.boff[j], q1 = S.t.boff[j + 1];
+        if (q0 == q1) {  // node absent from B (or empty)
+          for (int ia = S.t.aoff[j]; ia < S.t.aoff[j + 1]; ++ia) S.t.nv[ia] = -1;
+          continue;
+        }
+        const bool reg = q1 - q0 <= 128;
+        uint64_t tk0 = 0, tk1 = 0;  // taken positions 0..63, 64..127 (reg)
+        auto taken = [&](int r) -> bool {  // r: position in the node
+          if (reg) return ((((r & 64) ? tk1 : tk0) >> (r & 63)) & 1ull) != 0;
+          const int q = q0 + r;
+          return (S.t.taken[q >> 5] >> (q & 31)) & 1u;
+        };
+        const int r0 = S.t.aoff[j], r1 = S.t.aoff[j + 1];
+        uint4 nxA = S.t.top[r0][0], nxB = S.t.top[r0][1];
+        int nxt_nv = S.t.nv[r0];
+        for (int ia = r0; ia < r1; ++ia) {
+          const uint4 tA = nxA, tB = nxB;
+          const int nv = nxt_nv;
+          if (ia + 1 < r1) {
+            nxA = S.t.top[ia + 1][0];
+            nxB = S.t.top[ia + 1][1];
+            nxt_nv = S.t.nv[ia + 1];
+          }
+          int res = -1;
+          if (nv >= 0) {
+            int d1 = 256, d2 = 256, r1st = -1, found = 0;
+            const uint32_t keys[kBowK] = {tA.x, tA.y, tA.z, tA.w, tB.x, tB.y, tB.z, tB.w};
+  #pragma unroll
+            for (int k = 0; k < kBowK; ++k) {
+              const uint32_t key = keys[k];
+              if (key == kBowNone || found == 2 || taken((int)(key & 0xFFFF))) continue;
+              if (found == 0) {
+                d1 = (int)(key >> 16);
+                r1st = (int)(key & 0xFFFF);
+              } else {
+                d2 = (int)(key >> 16);
+              }
+              ++found;
+            }
+            if (found < 2 && nv > kBowK) {
+              // the list ran out under taken rows: rescan the node (strict < of :211-226)
+              const int i1 = idxA[a_base + ia];
+              const uint4* da = (const uint4*)(descA + (long long)i1 * 32);
+              const uint4 a0 = da[0], a1 = da[1];
+              d1 = 256;
+              d2 = 256;
+              r1st = -1;
+              for (int r = 0; r < q1 - q0; ++r) {
+                if (S.t.bidx[q0 + r] < 0 || taken(r)) continue;
+                const int dist = hamming256(a0, a1, *(const uint4*)&S.t.bdesc[q0 + r][0],
+                                            *(const uint4*)&S.t.bdesc[q0 + r][4]);
+                if (dist < d1) {
+                  d2 = d1;
+                  d1 = dist;
+                  r1st = r;
+                } else if (dist < d2) {
+                  d2 = dist;
+                }
+              }
+            }
+            // d1 = 256 never passes; with d1 < 256 the reference's bestIdx is set
+            const bool pass = kf_vs_kf ? (d1 < kThLow) : (d1 <= kThLow);
+            if (pass && (float)d1 < __fmul_rn(nnratio, (float)min(d2, 256))) {
+              res = q0 + r1st;
+              if (reg) {
+                const uint64_t bit = 1ull << (r1st & 63);
+                tk0 |= (r1st & 64) ? 0ull : bit;
+                tk1 |= (r1st & 64) ? bit : 0ull;
+              } else {
+                atomicOr(&S.t.taken[res >> 5], 1u << (res & 31));
+              }
+            }
+          }
+          S.t.nv[ia] = res;
+        }
+      }
+    }
+    __syncthreads();
+    stamp(4, -1);
+    // ---- the accepted matches: outputs, then count and rotation histogram
+    // summed in LDS first (one global atomic per bin per workgroup)
+    if (tid < 32) s_hist[tid] = 0;
+    __syncthreads();
+    for (int ia = tid; ia < na; ia += NT) {
+      const int q = S.t.nv[ia];
+      if (q >= 0) accept(idxA[a_base + ia], S.t.bidx[q], s_hist);
+    }
+    __syncthreads();
+    if (tid < 32 && s_hist[tid]) atomicAdd(&hist[tid], s_hist[tid]);
+    if (dbg) {
+      __syncthreads();
+      stamp(0, -1);
+      stamp(5, nk);
+      stamp(6, na);
+      stamp(7, S.t.boff[nk]);
+    }
+    return;
+  }
+
+  // ---- fallback: a wave per node through a queue, best/second reduced across lanes
+  stamp(5, -nk);
+  __syncthreads();
+  volatile uint32_t* s_taken = S.f.taken;
+  for (int i = tid; i < 2048; i += NT) S.f.taken[i] = 0;
+  if (tid == 0) s_queue = 0;
+  __syncthreads();
+  for (;;) {
+    int qi = 0;
+    if (lane == 0) qi = atomicAdd(&s_queue, 1);
+    const int ka = k0 + __builtin_amdgcn_readfirstlane(qi);
+    if (ka >= k1) break;
+    const int lo = find_b(nodesA[ka]);
+    if (lo < 0) continue;
     const int b0 = offB[lo], b1 = offB[lo + 1];
     const int a0i = offA[ka], a1i = offA[ka + 1];
     const int nbn = b1 - b0;
@@ -571,7 +910,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
           const uint4* d2 = (const uint4*)(descB + (long long)i2 * 32);
           q0[c] = d2[0];
           q1[c] = d2[1];
-          s_bidx[wv][pos] = i2;
+          S.f.bidx[wv][pos] = i2;
         }
       }
       for (int ac = a0i; ac < a1i; ac += 64) {
@@ -582,17 +921,17 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
           const bool ok = !mpA || mpA[i1];
           const uint4* d1 = (const uint4*)(descA + (long long)i1 * 32);
           const uint4 v0 = d1[0], v1 = d1[1];
-          uint32_t* w = s_adesc[wv][lane];
+          uint32_t* w = S.f.adesc[wv][lane];
           w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w;
           w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
-          s_aidx[wv][lane] = ok ? i1 : -1;
+          S.f.aidx[wv][lane] = ok ? i1 : -1;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         for (int i = 0; i < nan_; ++i) {
-          const int idx1 = s_aidx[wv][i];
+          const int idx1 = S.f.aidx[wv][i];
           if (idx1 < 0) continue;  // (:191-197) uniform
-          const uint32_t* w = s_adesc[wv][i];
+          const uint32_t* w = S.f.adesc[wv][i];
           const uint4 a0 = make_uint4(w[0], w[1], w[2], w[3]), a1 = make_uint4(w[4], w[5], w[6], w[7]);
           // per lane the two smallest (distance << 16 | position) keys over its
           // chunks, then the wave's: position order = the node vector's order,
@@ -616,7 +955,11 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
           const int d2 = m2 == 0x7FFFFFFFu ? 256 : min((int)(m2 >> 16), 256);
           const bool pass = kf_vs_kf ? (d1 < kThLow) : (d1 <= kThLow);
           if (pass && (float)d1 < __fmul_rn(nnratio, (float)d2)) {
-            if (lane == 0) accept(idx1, s_bidx[wv][m1 & 0xFFFF]);
+            if (lane == 0) {
+              const int i2 = S.f.bidx[wv][m1 & 0xFFFF];
+              atomicOr((unsigned*)&s_taken[i2 >> 5], 1u << (i2 & 31));
+              accept(idx1, i2, hist);
+            }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
           }
@@ -631,8 +974,8 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
       const uint4* d1 = (const uint4*)(descA + (long long)idx1 * 32);
       const uint4 a0 = d1[0], a1 = d1[1];
       Top2 acc{256, -1, 256};
-      for (int cb = b0; cb < b1; cb += 64) {
-        const int q = cb + lane;
+      for (int q0 = b0; q0 < b1; q0 += 64) {
+        const int q = q0 + lane;
         bool valid = false;
         int dist = 0, idx2 = -1;
         if (q < b1) {
@@ -645,16 +988,20 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
           }
         }
         const Top2 t = wave_top2(valid, dist, idx2);
-        const int nb = min(acc.best, t.best);
-        const int npos = (acc.best <= t.best) ? acc.pos : t.pos;
-        const int nsec = min(min(max(acc.best, t.best), acc.second), t.second);
-        acc.best = nb;
-        acc.pos = npos;
-        acc.second = nsec;
+        if (t.best < acc.best) {
+          acc.second = min(acc.best, t.second);
+          acc.best = t.best;
+          acc.pos = t.pos;
+        } else {
+          acc.second = min(acc.second, t.best);
+        }
       }
       const bool pass = kf_vs_kf ? (acc.best < kThLow) : (acc.best <= kThLow);
       if (pass && (float)acc.best < __fmul_rn(nnratio, (float)acc.second)) {
-        if (lane == 0) accept(idx1, acc.pos);
+        if (lane == 0) {
+          atomicOr((unsigned*)&s_taken[acc.pos >> 5], 1u << (acc.pos & 31));
+          accept(idx1, acc.pos, hist);
+        }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
       }
@@ -726,8 +1073,26 @@ int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnrat
       hipMemsetAsync(bin_scratch, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
       hipMemsetAsync(hist_scratch, 0, (size_t)pairs * 32 * 4, s) != hipSuccess)
     return ORBX_EDEVICE;
-  hipLaunchKernelGGL(search_bow_kernel<kBowThreads>, dim3(pairs * kBowGroups), dim3(kBowThreads), 0, s, A, B, nnratio,
-                     check_ori, kf_vs_kf, kBowGroups, out, out_pitch, bin_scratch, hist_scratch);
+  static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_BOW_PROF=1)
+  static const bool prof = getenv("ORBX_BOW_PROF") && getenv("ORBX_BOW_PROF")[0] == '1';
+  const int nwg = pairs * kBowGroups;
+  if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)65536 * 32);
+  if (prof) (void)hipMemsetAsync(dbg, 0, (size_t)nwg * 32, s);
+  hipLaunchKernelGGL(search_bow_kernel<kBowThreads>, dim3(nwg), dim3(kBowThreads), 0, s, A, B, nnratio,
+                     check_ori, kf_vs_kf, kBowGroups, out, out_pitch, bin_scratch, hist_scratch, prof ? dbg : nullptr);
+  if (prof) {
+    std::vector<int> h((size_t)nwg * 8);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), dbg, h.size() * 4, hipMemcpyDeviceToHost);
+    double t[8] = {0}, mx[8] = {0};
+    int nfb = 0;
+    for (int w = 0; w < nwg; ++w) {
+      if (h[w * 8 + 5] < 0) ++nfb;
+      for (int k = 0; k < 8; ++k) t[k] += h[w * 8 + k], mx[k] = std::max(mx[k], (double)h[w * 8 + k]);
+    }
+    fprintf(stderr, "bow: %d WGs (%d fallback); avg/max cycles at: table %.0f/%.0f staged %.0f/%.0f top %.0f/%.0f greedy %.0f/%.0f end %.0f/%.0f; avg nodes %.1f rows A %.1f B %.1f\n",
+            nwg, nfb, t[1] / nwg, mx[1], t[2] / nwg, mx[2], t[3] / nwg, mx[3], t[4] / nwg, mx[4], t[0] / nwg, mx[0], t[5] / nwg, t[6] / nwg, t[7] / nwg);
+  }
   hipLaunchKernelGGL(search_bow_finalize_kernel, dim3(pairs), dim3(256), 0, s, A.n, B.n, kf_vs_kf, check_ori, out,
                      out_pitch, bin_scratch, hist_scratch, nmatches);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;

@@ -11,10 +11,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def voc(pkg):
+@pytest.fixture(scope="module", params=[(10, 6), (4, 5), (2, 4)], ids=["k10L6", "k4L5", "k2L4"])
+def voc(pkg, request):
+    """k10 L6: ~100 FeatureVector nodes of ~20 features (the two-pass path);
+    k4 L5: 4 nodes of ~500 (long greedy chains, top-list rescans); k2 L4: the
+    root only, one node of ~2000 (over the LDS tables: the per-wave fallback
+    with candidates streamed from global memory)."""
     from orb_slam_cuda_amd.synth import synthetic_vocabulary
-    v = synthetic_vocabulary(10, 6, seed=1)
+    k, L = request.param
+    v = synthetic_vocabulary(k, L, seed=1)
     return v, pkg.ORBVocabulary.from_arrays(v)
 
 
