@@ -42,7 +42,6 @@ namespace orbx {
 #define ORBX_TILE_THREADS 512
 #endif
 constexpr int kTlThreads = ORBX_TILE_THREADS;
-constexpr int kTlWaves = kTlThreads / 64;
 constexpr int kTlList = 2048;  // FAST survivors / detections handled per pass (u16 entries)
 
 typedef unsigned short tl_us2_t __attribute__((ext_vector_type(2)));

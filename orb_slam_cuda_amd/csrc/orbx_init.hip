@@ -105,6 +105,18 @@ __device__ __forceinline__ void row_top2(uint32_t& k1, uint32_t& k2) {
   row_top2_step<kDppMirror>(k1, k2);
 }
 
+// vMatchedDistance[i2] at i1's turn: the smallest distance of an earlier
+// query's claim on i2 in the snapshot (INT_MAX if none)
+__device__ __forceinline__ int init_claim_md(const LDSP int* head, const LDSP int* nxt, int i2, int i1) {
+  int md = INT_MAX;
+  for (int hd = head[i2]; hd >= 0;) {
+    const int x = nxt[hd];
+    if (hd < i1) md = min(md, x & 511);
+    hd = (x >> 9) - 1;
+  }
+  return md;
+}
+
 struct InitShared {
   LDSP int* cell;     // [kInitCells + 1] first sorted position of each cell
   LDSP int* cof;      // [K] cell of each F2 keypoint (sort), then head[i2] (rounds), md[i2] (fallback)
@@ -261,6 +273,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
     if (S.coff[i + 1] > S.coff[i]) S.queue[lds_atomic_add(&S.var[7], 1)] = i;
   __syncthreads();
   const int nq = S.var[7];
+  init_stamp(P, 6);
   bool converged = false;
   for (int round = 0; round < kInitMaxRounds; ++round) {
     if (S.var[6] == 0) {
@@ -272,37 +285,33 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
     if (tid == 0) S.var[6] = 0;
     __syncthreads();
     int changed = 0;
-    // a 16-lane row per query: lane l scans candidates c0 + l, c0 + l + 16, ...
-    // keeping the two smallest (distance << 22 | position) keys; the row merge
-    // gives the sequential scan's best (earliest on equal distances) and second
-    for (int g = tid >> 4; g < nq; g += kInitThreads / 16) {
-      const int l16 = tid & 15;
-      const int i1 = S.queue[g];
-      const int c0 = S.coff[i1], c1 = S.coff[i1 + 1];
-      uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
-      for (int c = c0 + l16; c < c1; c += 16) {
-        const uint32_t e = cand[c];
-        const int i2 = (int)(e & 0x7FFFFF), dist = (int)(e >> 23);
-        int md = INT_MAX;  // vMatchedDistance[i2] at i1's turn
-        for (int hd = head[i2]; hd >= 0;) {
-          const int x = nxt[hd];
-          if (hd < i1) md = min(md, x & 511);
-          hd = (x >> 9) - 1;
+    {
+      // a 16-lane row per query: lane l scans candidates c0 + l, c0 + l + 16, ...
+      // keeping the two smallest (distance << 22 | position) keys; the row merge
+      // gives the sequential scan's best (earliest on equal distances) and second
+      for (int g = tid >> 4; g < nq; g += kInitThreads / 16) {
+        const int l16 = tid & 15;
+        const int i1 = S.queue[g];
+        const int c0 = S.coff[i1], c1 = S.coff[i1 + 1];
+        uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
+        for (int c = c0 + l16; c < c1; c += 16) {
+          const uint32_t e = cand[c];
+          const int i2 = (int)(e & 0x7FFFFF), dist = (int)(e >> 23);
+          if (init_claim_md(head, nxt, i2, i1) <= dist) continue;  // (:444-445)
+          const uint32_t key = ((uint32_t)dist << 22) | (uint32_t)(c - c0);
+          k2 = min(k2, max(k1, key));
+          k1 = min(k1, key);
         }
-        if (md <= dist) continue;  // (:444-445)
-        const uint32_t key = ((uint32_t)dist << 22) | (uint32_t)(c - c0);
-        k2 = min(k2, max(k1, key));
-        k1 = min(k1, key);
-      }
-      row_top2(k1, k2);
-      const int best = k1 == 0xFFFFFFFFu ? INT_MAX : (int)(k1 >> 22);
-      const int best2 = k2 == 0xFFFFFFFFu ? INT_MAX : (int)(k2 >> 22);
-      const bool ok = best <= kInitThLow && (float)best < __fmul_rn((float)best2, P.nnratio);
-      if (l16 == 0) {
-        const int r = ok ? ((int)(cand[c0 + (k1 & 0x3FFFFF)] & 0x7FFFFF) << 9 | best) : -1;
-        if (res[i1] != r) {
-          res[i1] = r;
-          changed = 1;
+        row_top2(k1, k2);
+        const int best = k1 == 0xFFFFFFFFu ? INT_MAX : (int)(k1 >> 22);
+        const int best2 = k2 == 0xFFFFFFFFu ? INT_MAX : (int)(k2 >> 22);
+        const bool ok = best <= kInitThLow && (float)best < __fmul_rn((float)best2, P.nnratio);
+        if (l16 == 0) {
+          const int r = ok ? ((int)(cand[c0 + (k1 & 0x3FFFFF)] & 0x7FFFFF) << 9 | best) : -1;
+          if (res[i1] != r) {
+            res[i1] = r;
+            changed = 1;
+          }
         }
       }
     }
@@ -321,7 +330,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
     }
     __syncthreads();
   }
-  init_stamp(P, 6);
+  init_stamp(P, 7);
   if (P.prof && tid == 0) P.prof[blockIdx.x * 16 + 12] = converged ? 1 : 0;
   if (converged) {
     // the latest accepting query keeps each i2 (earlier ones were stolen
@@ -395,6 +404,134 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
   __syncthreads();
 }
 
+// Rotation consistency (src/ORBmatcher.cc:473-512, ComputeThreeMaxima
+// :1601-1642) and the outputs: vnMatches12 and the vbPrevMatched update
+// (:515-517). src[i1] = the i2 every accepting query entered into rotHist
+// (-1 if none), m12 = vnMatches12 after the steals, var[0] = the match count;
+// hist[0..30) zeroed.
+template <int NT>
+__device__ void init_finish(const InitParams& P, LDSP int* src, LDSP int* m12, LDSP int* hist, LDSP int* var,
+                            const orbx_kp* __restrict__ kp1, const orbx_kp* __restrict__ kp2, int n1, float* prev,
+                            int* m12_out, int* nmatches_out) {
+  const int tid = threadIdx.x;
+  const float factor = 1.0f / kInitHisto;
+  if (P.check_ori) {
+    for (int i = tid; i < n1; i += NT) {
+      const int j = src[i];
+      int bin = -1;
+      if (j >= 0) {
+        float rot = __fsub_rn(kp1[i].angle, kp2[j].angle);
+        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+        bin = (int)roundf(__fmul_rn(rot, factor));
+        if (bin == kInitHisto) bin = 0;
+        lds_atomic_add(&hist[bin], 1);
+      }
+      src[i] = bin;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+      for (int i = 0; i < kInitHisto; i++) {
+        const int s = hist[i];
+        if (s > max1) {
+          max3 = max2; max2 = max1; max1 = s;
+          ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+          max3 = max2; max2 = s;
+          ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+          max3 = s;
+          ind3 = i;
+        }
+      }
+      if (max2 < __fmul_rn(0.1f, (float)max1)) {
+        ind2 = -1;
+        ind3 = -1;
+      } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
+        ind3 = -1;
+      }
+      var[1] = ind1;
+      var[2] = ind2;
+      var[3] = ind3;
+    }
+    __syncthreads();
+    const int ind1 = var[1], ind2 = var[2], ind3 = var[3];
+    int rej = 0;
+    for (int i = tid; i < n1; i += NT) {
+      const int b = src[i];
+      if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
+      if (m12[i] >= 0) {
+        m12[i] = -1;
+        ++rej;
+      }
+    }
+    rej = wave_sum_dpp(rej);
+    if ((tid & 63) == 0 && rej) lds_atomic_add(&var[0], -rej);
+    __syncthreads();
+  }
+  for (int i = tid; i < n1; i += NT) {
+    const int j = m12[i];
+    m12_out[i] = j;
+    if (prev && j >= 0) {
+      prev[2 * i] = kp2[j].x;
+      prev[2 * i + 1] = kp2[j].y;
+    }
+  }
+  if (tid == 0) *nmatches_out = var[0];
+}
+
+// Frame::AssignFeaturesToGrid for F2's octave-0 keypoints (the only ones
+// GetFeaturesInArea(.., 0, 0) returns), as a counting sort by cell, stable in
+// index order: cell[c] = first sorted position of cell c (column-major cells,
+// so a window column is one run), pos / idx / (d0: descriptors at kD0Stride
+// words, when d0_words can hold them) in sorted order. slot / members are
+// scratch of n2 entries. Returns n0; no trailing barrier.
+template <int NT>
+__device__ int init_build_grid(const InitParams& P, const orbx_kp* __restrict__ kp2, const uint8_t* __restrict__ desc2,
+                               int n2, LDSP int* cell, LDSP int* cof, LDSP float* pos, LDSP int* idx, LDSP int* slot,
+                               LDSP int* members, LDSP int* tmp, LDSP uint32_t* d0, int d0_words, bool* d0_lds) {
+  const int tid = threadIdx.x;
+  for (int c = tid; c <= kInitCells; c += NT) cell[c] = 0;
+  __syncthreads();
+  for (int i = tid; i < n2; i += NT) {
+    const orbx_kp k = kp2[i];
+    int c = -1;
+    if (!(k.octave == 0 && init_pos_in_grid(k.x, k.y, P, &c))) c = -1;
+    cof[i] = c;
+    if (c >= 0) slot[i] = lds_atomic_add(&cell[c], 1);
+  }
+  __syncthreads();
+  const int n0 = init_scan<NT>(cell, kInitCells + 1, tmp);
+  const bool dl = kD0Stride * n0 <= d0_words;
+  *d0_lds = dl;
+  for (int i = tid; i < n2; i += NT) {
+    const int c = cof[i];
+    if (c >= 0) members[cell[c] + slot[i]] = i;
+  }
+  __syncthreads();
+  // stable placement: rank inside the cell = members with a smaller index
+  // (cells hold a handful of octave-0 keypoints)
+  for (int i = tid; i < n2; i += NT) {
+    const int c = cof[i];
+    if (c < 0) continue;
+    const int b = cell[c], e = cell[c + 1];
+    int p = b;
+    for (int q = b; q < e; ++q) p += members[q] < i ? 1 : 0;
+    const orbx_kp k = kp2[i];
+    pos[2 * p] = k.x;
+    pos[2 * p + 1] = k.y;
+    idx[p] = i;
+    if (dl) {
+      const uint4* d = (const uint4*)(desc2 + (size_t)i * 32);
+      const uint4 u = d[0], v = d[1];
+      LDSP uint32_t* w = d0 + kD0Stride * p;
+      w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+      w[4] = v.x; w[5] = v.y; w[6] = v.z; w[7] = v.w;
+    }
+  }
+  return n0;
+}
+
 __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     InitParams P, const orbx_kp* __restrict__ kp1_all, const uint8_t* __restrict__ desc1_all,
     const int* __restrict__ n1_all, const orbx_kp* __restrict__ kp2_all, const uint8_t* __restrict__ desc2_all,
@@ -435,54 +572,16 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   LDSP uint32_t* tail = (LDSP uint32_t*)sp;  // P.cand_lds entries: descriptors, then candidates
 
   init_stamp(P, 0);
-  // ---- phase 0: counting sort of F2's octave-0 keypoints by cell (the only
-  // ones GetFeaturesInArea(.., 0, 0) returns), stable in index order
-  for (int c = tid; c <= kInitCells; c += kInitThreads) S.cell[c] = 0;
   if (tid < 32) {
     S.hist[tid] = 0;
     S.var[tid] = 0;
   }
-  __syncthreads();
-  LDSP int* slot = S.src;     // arrival slot of each F2 keypoint in its cell (free until phase 3)
-  LDSP int* members = S.queue;  // cell members in arrival order (free until phase 3)
-  for (int i = tid; i < n2; i += kInitThreads) {
-    const orbx_kp k = kp2[i];
-    int c = -1;
-    if (!(k.octave == 0 && init_pos_in_grid(k.x, k.y, P, &c))) c = -1;
-    S.cof[i] = c;
-    if (c >= 0) slot[i] = lds_atomic_add(&S.cell[c], 1);
-  }
-  __syncthreads();
-  const int n0 = init_scan<kInitThreads>(S.cell, kInitCells + 1, S.tmp);
-  const bool d0_lds = kD0Stride * n0 <= P.cand_lds / 2;
+  bool d0_lds = false;
+  const int n0 = init_build_grid<kInitThreads>(P, kp2, desc2, n2, S.cell, S.cof, S.pos, S.idx, S.src, S.queue, S.tmp,
+                                               tail, P.cand_lds / 2, &d0_lds);
   S.d0 = tail;
   S.cand = tail + (d0_lds ? kD0Stride * n0 : 0);
   const int cand_lds = P.cand_lds - (d0_lds ? kD0Stride * n0 : 0);
-  for (int i = tid; i < n2; i += kInitThreads) {
-    const int c = S.cof[i];
-    if (c >= 0) members[S.cell[c] + slot[i]] = i;
-  }
-  __syncthreads();
-  // stable placement: rank inside the cell = members with a smaller index
-  // (cells hold a handful of octave-0 keypoints)
-  for (int i = tid; i < n2; i += kInitThreads) {
-    const int c = S.cof[i];
-    if (c < 0) continue;
-    const int b = S.cell[c], e = S.cell[c + 1];
-    int p = b;
-    for (int q = b; q < e; ++q) p += members[q] < i ? 1 : 0;
-    const orbx_kp k = kp2[i];
-    S.pos[2 * p] = k.x;
-    S.pos[2 * p + 1] = k.y;
-    S.idx[p] = i;
-    if (d0_lds) {
-      const uint4* d = (const uint4*)(desc2 + (size_t)i * 32);
-      const uint4 u = d[0], v = d[1];
-      LDSP uint32_t* w = S.d0 + kD0Stride * p;
-      w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
-      w[4] = v.x; w[5] = v.y; w[6] = v.z; w[7] = v.w;
-    }
-  }
   // F1's octave-0 queries, compacted in index order
   for (int i = tid; i <= n1; i += kInitThreads) S.coff[i] = 0;
   __syncthreads();
@@ -560,74 +659,8 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
       init_solve<uint32_t*, false>(P, S, c, kp1, desc1, desc2, prev, n1, n2, nq0, total);
   }
   if (P.stop == 3) return;
-  LDSP int* m12 = S.qlist;  // vnMatches12
-  // rotation consistency (src/ORBmatcher.cc:473-512, ComputeThreeMaxima :1601-1642)
-  const float factor = 1.0f / kInitHisto;
-  if (P.check_ori) {
-    for (int i = tid; i < n1; i += kInitThreads) {
-      const int j = S.src[i];
-      int bin = -1;
-      if (j >= 0) {
-        float rot = __fsub_rn(kp1[i].angle, kp2[j].angle);
-        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-        bin = (int)roundf(__fmul_rn(rot, factor));
-        if (bin == kInitHisto) bin = 0;
-        lds_atomic_add(&S.hist[bin], 1);
-      }
-      S.src[i] = bin;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-      for (int i = 0; i < kInitHisto; i++) {
-        const int s = S.hist[i];
-        if (s > max1) {
-          max3 = max2; max2 = max1; max1 = s;
-          ind3 = ind2; ind2 = ind1; ind1 = i;
-        } else if (s > max2) {
-          max3 = max2; max2 = s;
-          ind3 = ind2; ind2 = i;
-        } else if (s > max3) {
-          max3 = s;
-          ind3 = i;
-        }
-      }
-      if (max2 < __fmul_rn(0.1f, (float)max1)) {
-        ind2 = -1;
-        ind3 = -1;
-      } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
-        ind3 = -1;
-      }
-      S.var[1] = ind1;
-      S.var[2] = ind2;
-      S.var[3] = ind3;
-    }
-    __syncthreads();
-    const int ind1 = S.var[1], ind2 = S.var[2], ind3 = S.var[3];
-    int rej = 0;
-    for (int i = tid; i < n1; i += kInitThreads) {
-      const int b = S.src[i];
-      if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
-      if (m12[i] >= 0) {
-        m12[i] = -1;
-        ++rej;
-      }
-    }
-    rej = wave_sum_dpp(rej);
-    if ((tid & 63) == 0 && rej) lds_atomic_add(&S.var[0], -rej);
-    __syncthreads();
-  }
-  // outputs: vnMatches12 and the vbPrevMatched update (:515-517)
-  for (int i = tid; i < n1; i += kInitThreads) {
-    const int j = m12[i];
-    m12_out[i] = j;
-    if (prev && j >= 0) {
-      prev[2 * i] = kp2[j].x;
-      prev[2 * i + 1] = kp2[j].y;
-    }
-  }
-  if (tid == 0) nmatches[pr] = S.var[0];
-  init_stamp(P, 7);
+  init_finish<kInitThreads>(P, S.src, S.qlist, S.hist, S.var, kp1, kp2, n1, prev, m12_out, nmatches + pr);
+  init_stamp(P, 8);
 }
 
 int launch_search_init(const InitParams& P0, const orbx_kp* kp1, const uint8_t* desc1, const int* n1,
@@ -635,7 +668,7 @@ int launch_search_init(const InitParams& P0, const orbx_kp* kp1, const uint8_t* 
                        int* matches12, int* nmatches, int* err, int pairs, void* stream) {
   InitParams P = P0;
   const size_t fixed = init_lds_fixed_bytes(P.kp_pitch);
-  // sorted positions are 12-bit fields of the phase-2 entries
+  // sorted positions and i2 are 12-bit fields of the candidate entries / keys
   if (P.kp_pitch > 4096 || fixed + 4096 > kInitLdsBudget) return ORBX_ECAPACITY;
   P.cand_lds = (int)((kInitLdsBudget - fixed) / 4) & ~15;
   if (raise_lds_limit((const void*)search_init_kernel, kInitLdsBudget)) return ORBX_EDEVICE;

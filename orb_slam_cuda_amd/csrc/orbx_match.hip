@@ -1271,30 +1271,31 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
   static long long* prof = nullptr;  // ORBX_INIT_PROF: phase clocks of every pair, averaged after the call
   const bool do_prof = getenv("ORBX_INIT_PROF") != nullptr;
   if (do_prof) {
+    if (pairs > 4096) return mfail(ORBX_EINVAL, "ORBX_INIT_PROF: at most 4096 pairs");
     if (!prof) MHIP(hipMalloc(&prof, (size_t)4096 * 16 * 8));
     MHIP(hipMemset(prof, 0, (size_t)pairs * 16 * 8));
     P.prof = prof;
   }
   if (m->ws.before((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
-  const int rc = launch_search_init(P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, d_prev_xy, m->cand, d_matches12,
-                                    d_nmatches, m->err, pairs, stream);
+  const int rc = launch_search_init(P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, d_prev_xy, m->cand,
+                                    d_matches12, d_nmatches, m->err, pairs, stream);
   if (!rc && m->ws.after((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "event record failed");
   if (do_prof && !rc) {
     std::vector<long long> h((size_t)pairs * 16);
     MHIP(hipStreamSynchronize((hipStream_t)stream));
     MHIP(hipMemcpy(h.data(), prof, h.size() * 8, hipMemcpyDeviceToHost));
-    double ph[8] = {0}, rounds = 0, conv = 0, tot = 0;
+    double ph[9] = {0}, rounds = 0, conv = 0, tot = 0;
     for (int q = 0; q < pairs; ++q) {
-      for (int k = 1; k < 8; ++k)
+      for (int k = 1; k < 9; ++k)
         if (h[q * 16 + k]) ph[k] += (double)(h[q * 16 + k] - h[q * 16]);
       rounds += h[q * 16 + 11];
       conv += h[q * 16 + 12];
       tot += h[q * 16 + 13];
     }
     fprintf(stderr, "search_init phases (avg clocks from start): sort %.0f qlist %.0f count %.0f walk %.0f dist %.0f "
-            "rounds %.0f end %.0f | rounds %.1f converged %.2f candidates %.0f\n", ph[1] / pairs, ph[2] / pairs,
-            ph[3] / pairs, ph[4] / pairs, ph[5] / pairs, ph[6] / pairs, ph[7] / pairs, rounds / pairs, conv / pairs,
-            tot / pairs);
+            "rounds %.0f end %.0f | rounds %.1f converged %.2f candidates %.0f\n", ph[1] / pairs,
+            ph[2] / pairs, ph[3] / pairs, ph[4] / pairs, ph[5] / pairs, ph[7] / pairs, ph[8] / pairs,
+            rounds / pairs, conv / pairs, tot / pairs);
   }
   if (rc == ORBX_ECAPACITY)
     return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization's LDS grid", kp_pitch);

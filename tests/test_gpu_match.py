@@ -13,6 +13,8 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 
+
+
 def _pair(O, seed, W=1241, H=376, nf=2000):
     from orb_slam_cuda_amd.synth import SynthSequence
     fr = SynthSequence(seed, W, H).frames(2)
@@ -305,3 +307,28 @@ def test_search_for_initialization_contention(pkg, O, seed, ratio):
                                        pkg.Frame.from_extraction(k2, d2, W, H), p, v12, 100)
         r12, rnm, rprev = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), prev, 100, ratio, ori)
         assert nm == rnm and np.array_equal(np.array(v12, np.int32), r12) and np.array_equal(p, rprev)
+
+
+def test_search_for_initialization_overflow_then_recovers(pkg, O):
+    """More candidates than the per-pair list area (4 M entries): 2100 x 2100
+    level-0 keypoints in one window. The call reports ECAPACITY rather than
+    truncating; the next call on the same matcher is exact again."""
+    W, H = 1241, 376
+    rng = np.random.default_rng(9)
+    n = 2100
+    k1 = _kps(pkg, rng.uniform(500, 560, n), rng.uniform(150, 210, n))
+    k2 = _kps(pkg, rng.uniform(500, 560, n), rng.uniform(150, 210, n))
+    d1 = rng.integers(0, 256, (n, 32), np.uint8)
+    d2 = rng.integers(0, 256, (n, 32), np.uint8)
+    m = pkg.ORBmatcher(0.9, True, max_kps=n)
+    F1, F2 = pkg.Frame.from_extraction(k1, d1, W, H), pkg.Frame.from_extraction(k2, d2, W, H)
+    with pytest.raises(pkg.OrbxError):
+        m.SearchForInitialization(F1, F2, np.stack([k1["x"], k1["y"]], 1).astype(np.float32), None, 100)
+    (a1, e1), (a2, e2) = _pair(O, 5)
+    prev = np.stack([a1["x"], a1["y"]], 1).astype(np.float32)
+    v12 = []
+    nm = m.SearchForInitialization(pkg.Frame.from_extraction(a1, e1, W, H), pkg.Frame.from_extraction(a2, e2, W, H),
+                                   prev, v12, 100)
+    r12, rnm, rprev = O.search_for_initialization(a1, e1, a2, e2, (0, W, 0, H), np.stack([a1["x"], a1["y"]], 1),
+                                                  100, 0.9, True)
+    assert nm == rnm and np.array_equal(np.array(v12, np.int32), r12) and np.array_equal(prev, rprev)

@@ -52,5 +52,5 @@ for _ in range(N):
     run()
 e1.record(s)
 s.synchronize()
-print(f"{which} pairs={B} stop={os.environ.get('ORBX_INIT_STOP', '0')} ms_per_call={e0.elapsed_ms(e1) / N:.4f} "
+print(f"{which} cap={cap} pairs={B} stop={os.environ.get('ORBX_INIT_STOP', '0')} ms_per_call={e0.elapsed_ms(e1) / N:.4f} "
       f"matches_mean={d_nm.download(B, np.int32).mean():.1f}")
