@@ -22,6 +22,7 @@
 // unless it is empty, and writes the keys in row-major order (the order
 // cv::FAST emits them) into the cell's fixed slot range. Every compaction is
 // an ordered ballot compaction, so row-major order is preserved throughout.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -30,6 +31,8 @@
 #include "orbx_fastcore.cuh"
 
 namespace orbx {
+
+#define LDSP __attribute__((address_space(3)))
 
 // ROI row stride in LDS: 44 when every cell ROI fits 3 + rw <= 44 bytes (cells
 // of <= 35 px, KITTI and EuRoC: staged with dword loads from the dword below
@@ -41,6 +44,10 @@ namespace orbx {
 constexpr int kTightE = ORBX_FAST_TIGHT_E;
 constexpr int kRoiTight = kTightE == 4 ? 44 : 48, kRoiWide = 80;
 
+// 24-bit multiply (full-rate v_mul_u32_u24; the compiler cannot prove the
+// operand ranges and otherwise picks the quarter-rate 32/64-bit forms)
+__device__ __forceinline__ int u24mul(int a, int b) { return (int)__umul24((unsigned)a, (unsigned)b); }
+
 // Bresenham ring of radius 3, k = 0..15 (cv::makeOffsets, pattern 16)
 template <int kRoiStride>
 __device__ __forceinline__ int ring_off(int k) {
@@ -50,7 +57,7 @@ __device__ __forceinline__ int ring_off(int k) {
 }
 
 template <int kRoiStride>
-__device__ __forceinline__ void ring_masks(const uint8_t* c, int lo, int hi, uint32_t* dark, uint32_t* bright) {
+__device__ __forceinline__ void ring_masks(const LDSP uint8_t* c, int lo, int hi, uint32_t* dark, uint32_t* bright) {
   uint32_t dk = 0, br = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -66,7 +73,7 @@ __device__ __forceinline__ void ring_masks(const uint8_t* c, int lo, int hi, uin
 #define ORBX_FAST_PK 1  // packed-u16 compass pre-test (0: the scalar form, for A/B)
 #endif
 #ifndef ORBX_FAST_WAVES
-#define ORBX_FAST_WAVES 6  // VGPR budget: 6 waves per SIMD (<= 80 VGPRs)
+#define ORBX_FAST_WAVES 8  // VGPR budget: 8 waves per SIMD (<= 64 VGPRs; 41 used)
 #endif
 template <int kRoiStride>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WAVES))) void fast_cells_kernel(ExtractParams P, LevelPtrs lp,
@@ -101,14 +108,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     if (lane == 0) *cnt = 0;
     return;
   }
-  unsigned char* sp = smem;
-  auto take = [&](size_t bytes) { unsigned char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
-  uint8_t* roi = (uint8_t*)take((size_t)P.fast_rh_max * kRoiStride);
+  // LDS-typed pointers: 32-bit offsets in every address computation
+  LDSP unsigned char* sp = (LDSP unsigned char*)smem;
+  auto take = [&](size_t bytes) { LDSP unsigned char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
+  LDSP uint8_t* roi = (LDSP uint8_t*)take((size_t)P.fast_rh_max * kRoiStride);
   // score map with a zero ring, row stride bw + 1: the right border of a row
   // is the left border of the next, which no score is ever written to
-  uint8_t* sc = (uint8_t*)take((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1);
-  uint16_t* list = (uint16_t*)take(2ull * P.fast_bw_max * P.fast_bh_max);
-  uint64_t* ball = (uint64_t*)take(16ull * ((P.fast_bw_max * P.fast_bh_max + 63) / 64));
+  LDSP uint8_t* sc = (LDSP uint8_t*)take((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1);
+  LDSP uint16_t* list = (LDSP uint16_t*)take(2ull * P.fast_bw_max * P.fast_bh_max);
+  // the NMS ballots live in the ROI's LDS: the ROI is dead once the scores are
+  // written (phase (d) reads only the list and the score map)
+  LDSP uint64_t* ball = (LDSP uint64_t*)roi;
 
   const int l = cg.level;
   const LevelGeom& g = P.lv[l];
@@ -123,23 +133,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     // qwords per row), kK per lane in flight
     typedef unsigned int piece_t __attribute__((ext_vector_type(kTightE / 4)));
     constexpr int kK = kTightE == 4 ? 8 : 5;
-    const int nd = (cg.c1 - a0 + kTightE - 1) / kTightE, total = rh * nd;
+    // a fixed kPR pieces per staged row, so the lane -> (row, piece) split is
+    // a division by a constant; pieces past the ROI's last one (nd) and rows
+    // past the last (rh) reload that piece / row (same bytes, same LDS slot)
+    constexpr int kPR = kRoiStride / kTightE;
+    const int nd = (cg.c1 - a0 + kTightE - 1) / kTightE, total = rh * kPR;
     piece_t v[kK];
     int ro[kK], lo[kK];
 #pragma unroll
     for (int k = 0; k < kK; ++k) {
-      const int i = min(lane + 64 * k, total - 1);
-      const int r = i / nd, d = i - r * nd;
+      const int i = lane + 64 * k, q = i / kPR;
+      const int r = min(q, rh - 1), d = min(i - q * kPR, nd - 1);
       ro[k] = r * kRoiStride + kTightE * d;
-      lo[k] = r * pitch + kTightE * d;
+      lo[k] = (int)__umul24((unsigned)r, (unsigned)pitch) + kTightE * d;
     }
 #pragma unroll
     for (int k = 0; k < kK; ++k) v[k] = *(const piece_t*)(rows + a0 + lo[k]);
 #pragma unroll
-    for (int k = 0; k < kK; ++k) *(piece_t*)(roi + ro[k]) = v[k];
+    for (int k = 0; k < kK; ++k) *(LDSP piece_t*)(roi + ro[k]) = v[k];
     for (int i = lane + 64 * kK; i < total; i += 64) {
-      const int r = i / nd, d = i - r * nd;
-      *(piece_t*)(roi + r * kRoiStride + kTightE * d) = *(const piece_t*)(rows + (long long)r * pitch + a0 + kTightE * d);
+      const int q = i / kPR;
+      const int r = min(q, rh - 1), d = min(i - q * kPR, nd - 1);
+      *(LDSP piece_t*)(roi + r * kRoiStride + kTightE * d) =
+          *(const piece_t*)(rows + (int)__umul24((unsigned)r, (unsigned)pitch) + a0 + kTightE * d);
     }
   } else if (lp.aligned16[l]) {
     // the ROI's 16-byte chunks, 4 per lane (tall cells loop for the rest)
@@ -157,17 +173,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = *(const u32x4*)(rows + a0 + lo[k]);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) *(u32x4*)(roi + ro[k]) = v[k];
+    for (int k = 0; k < 4; ++k) *(LDSP u32x4*)(roi + ro[k]) = v[k];
     for (int i = lane + 256; i < total; i += 64) {
       const int r = i / nch, ch = i - r * nch;
-      *(uint4*)(roi + r * kRoiStride + ch * 16) = *(const uint4*)(rows + (long long)r * pitch + a0 + ch * 16);
+      *(LDSP u32x4*)(roi + r * kRoiStride + ch * 16) = *(const u32x4*)(rows + (long long)r * pitch + a0 + ch * 16);
     }
   } else {
     for (int r = 0; r < rh; ++r)
       for (int c = lane; c < rw; c += 64) roi[r * kRoiStride + ox + c] = rows[(long long)r * pitch + cg.c0 + c];
   }
   const int sw = bw + 1;
-  for (int i = lane; i < (sw * (bh + 2) + 1 + 3) >> 2; i += 64) ((uint32_t*)sc)[i] = 0;
+  for (int i = lane; i < (sw * (bh + 2) + 1 + 3) >> 2; i += 64) ((LDSP uint32_t*)sc)[i] = 0;
   __syncthreads();
   stamp(0);
 
@@ -175,7 +191,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   const bool two = bw <= 32;  // 2 rows x 32 lanes, else 1 row x 64 lanes (bw <= 59)
   const int lr = two ? (lane >> 5) : 0, lc = two ? (lane & 31) : lane;
   const int rstep = two ? 2 : 1;
-  const uint8_t* band = roi + 3 * kRoiStride + ox + 3;  // band pixel (0,0)
+  const LDSP uint8_t* band = roi + 3 * kRoiStride + ox + 3;  // band pixel (0,0)
 
   // (a) compass pre-test over all band pixels, row-major ordered compaction;
   // four row groups per step so their LDS reads are in flight together
@@ -189,8 +205,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
 #pragma unroll
     for (int q = 0; q < 4; q += 2) {
       const int byA = by0 + q * rstep + lr, byB = byA + rstep;
-      const uint8_t* cA = band + min(byA, bh - 1) * kRoiStride + min(lc, bw - 1);
-      const uint8_t* cB = band + min(byB, bh - 1) * kRoiStride + min(lc, bw - 1);
+      const LDSP uint8_t* cA = band + u24mul(min(byA, bh - 1), kRoiStride) + min(lc, bw - 1);
+      const LDSP uint8_t* cB = band + u24mul(min(byB, bh - 1), kRoiStride) + min(lc, bw - 1);
       auto pk = [](int lo, int hi) { return (u16x2){(unsigned short)lo, (unsigned short)hi}; };
       const u16x2 v = pk(cA[0], cB[0]);
       const u16x2 n0 = pk(cA[3 * kRoiStride], cB[3 * kRoiStride]), n4 = pk(cA[3], cB[3]);
@@ -210,7 +226,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int by = by0 + q * rstep + lr;
-      const uint8_t* c = band + min(by, bh - 1) * kRoiStride + min(lc, bw - 1);
+      const LDSP uint8_t* c = band + u24mul(min(by, bh - 1), kRoiStride) + min(lc, bw - 1);
       const int v = c[0];
       const int n0 = c[3 * kRoiStride], n4 = c[3], n8 = c[-3 * kRoiStride], n12 = c[-3];
       // >= 2 of the 4 compass pixels darker than v - t  <=>  their 2nd smallest is;
@@ -238,7 +254,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     const int e = i < n1 ? list[i] : 0;
     bool det = false;
     if (i < n1) {
-      const uint8_t* c = band + (e >> 8) * kRoiStride + (e & 255);
+      const LDSP uint8_t* c = band + u24mul(e >> 8, kRoiStride) + (e & 255);
       const int v = c[0];
       uint32_t dk, br;
       ring_masks<kRoiStride>(c, v - t, v + t, &dk, &br);
@@ -252,12 +268,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   // (c) FAST scores of the detected pixels
   for (int i = lane; i < n2; i += 64) {
     const int e = list[i];
-    const uint8_t* c = band + (e >> 8) * kRoiStride + (e & 255);
+    const LDSP uint8_t* c = band + u24mul(e >> 8, kRoiStride) + (e & 255);
     const int v = c[0];
     int d[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) d[k] = v - c[ring_off<kRoiStride>(k)];
-    sc[((e >> 8) + 1) * sw + (e & 255) + 1] = (uint8_t)corner_score16(d, t);
+    sc[u24mul((e >> 8) + 1, sw) + (e & 255) + 1] = (uint8_t)corner_score16(d, t);
   }
   __syncthreads();
   stamp(3);
@@ -270,7 +286,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     bool ki = false, km = false;
     if (i < n2) {
       const int e = list[i];
-      const uint8_t* q = sc + ((e >> 8) + 1) * sw + (e & 255) + 1;
+      const LDSP uint8_t* q = sc + u24mul((e >> 8) + 1, sw) + (e & 255) + 1;
       const int s = q[0];
       bool gi = s >= ti && s > 0, gm = s >= tm && s > 0;
       const int nbv[8] = {q[-1], q[1], q[-sw - 1], q[-sw], q[-sw + 1], q[sw - 1], q[sw], q[sw + 1]};
@@ -319,8 +335,8 @@ size_t fast_lds_bytes(const ExtractParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t band = (size_t)P.fast_bw_max * P.fast_bh_max;
   const int stride = fast_tight(P) ? kRoiTight : kRoiWide;
-  return r16((size_t)P.fast_rh_max * stride) + r16((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1) +
-         r16(2 * band) + r16(16 * ((band + 63) / 64));
+  return r16(std::max((size_t)P.fast_rh_max * stride, 16 * ((band + 63) / 64))) +
+         r16((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1) + r16(2 * band);
 }
 
 int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cells, uint32_t* slots,
@@ -330,12 +346,17 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
   const int nwg = P.ncells_total * batch;
   if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)nwg * 32);
   if (prof) (void)hipMemsetAsync(dbg, 0, (size_t)nwg * 32, s);
-  if (fast_tight(P))
-    hipLaunchKernelGGL(fast_cells_kernel<kRoiTight>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
-                       lp, cells, slots, cell_counts, prof ? dbg : nullptr);
-  else
-    hipLaunchKernelGGL(fast_cells_kernel<kRoiWide>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
-                       lp, cells, slots, cell_counts, prof ? dbg : nullptr);
+  // diagnostics: ORBX_FAST_TWICE=1 runs the (idempotent) kernel twice, so the
+  // second run's phase clocks show FAST on cache-warm levels
+  static const int reps = getenv("ORBX_FAST_TWICE") && getenv("ORBX_FAST_TWICE")[0] == '1' ? 2 : 1;
+  for (int rep = 0; rep < reps; ++rep) {
+    if (fast_tight(P))
+      hipLaunchKernelGGL(fast_cells_kernel<kRoiTight>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
+                         lp, cells, slots, cell_counts, prof ? dbg : nullptr);
+    else
+      hipLaunchKernelGGL(fast_cells_kernel<kRoiWide>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
+                         lp, cells, slots, cell_counts, prof ? dbg : nullptr);
+  }
   if (prof) {
     std::vector<int> h((size_t)nwg * 8);
     (void)hipStreamSynchronize(s);
