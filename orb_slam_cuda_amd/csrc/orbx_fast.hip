@@ -56,17 +56,105 @@ __device__ __forceinline__ int ring_off(int k) {
   return ry[k] * kRoiStride + rx[k];
 }
 
+// 16-bit dark / bright masks of the ring (bit k: ring pixel k < lo / > hi),
+// two ring pixels (k, k + 8) per packed u16x2 register: saturating subtract,
+// min with 1, shift into bit k of each half (v_pk_sub_u16 clamp, v_pk_min_u16,
+// v_lshl_or_b32 per pair instead of a compare + select + shift per pixel)
+// packed u16x2 ops as written: the compiler turns min(sub_sat(a, b), 1) back
+// into a compare + select per half
+__device__ __forceinline__ uint32_t pk_sub_sat_u16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 template <int kRoiStride>
 __device__ __forceinline__ void ring_masks(const LDSP uint8_t* c, int lo, int hi, uint32_t* dark, uint32_t* bright) {
+  const uint32_t l16 = (uint32_t)max(lo, 0), h16 = (uint32_t)hi;  // lo < 0: nothing is darker
+  const uint32_t vl = l16 | (l16 << 16), vh = h16 | (h16 << 16), one = 0x00010001u;
   uint32_t dk = 0, br = 0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int x = c[ring_off<kRoiStride>(k)];
-    dk |= (uint32_t)(x < lo) << k;
-    br |= (uint32_t)(x > hi) << k;
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t x = (uint32_t)c[ring_off<kRoiStride>(k)] | ((uint32_t)c[ring_off<kRoiStride>(k + 8)] << 16);
+    dk |= pk_min_u16(pk_sub_sat_u16(vl, x), one) << k;
+    br |= pk_min_u16(pk_sub_sat_u16(x, vh), one) << k;
   }
-  *dark = dk;
-  *bright = br;
+  *dark = (dk & 0xFFu) | ((dk >> 8) & 0xFF00u);
+  *bright = (br & 0xFFu) | ((br >> 8) & 0xFF00u);
+}
+
+// (a) of the tight-stride kernel on dword LDS reads: a lane tests 4
+// horizontally adjacent band pixels (G = ceil(bw / 4) lanes per band row,
+// 64 / G rows per pass). Band pixel (y, x) is ROI byte (y + 3) * 44 + OX + 3 + x
+// (OX = the cell's byte offset in its first staged dword, a template
+// parameter so every byte extraction is one v_alignbyte_b32 with a constant
+// shift). Pixels split into even / odd u16x2 pairs for the packed compass
+// network; per-pixel ballots give the row-major ordered compaction.
+template <int OX>
+__device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* list, int bw, int bh, int t,
+                                        int lane) {
+  constexpr int S = kRoiTight;
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  // byte offsets, from the group's first dword, of the group's centres, +3 and -3 neighbours
+  constexpr int kC = OX + 3, kN4 = OX + 6, kN12 = OX;
+  auto ext = [](const uint32_t* d, int o) -> uint32_t {
+    return (o & 3) == 0 ? d[o >> 2] : __builtin_amdgcn_alignbyte(d[(o >> 2) + 1], d[o >> 2], o & 3);
+  };
+  auto bits = [](uint32_t x) { return __builtin_bit_cast(u16x2, x); };
+  const int G = (bw + 3) >> 2, RP = 64 / G;
+  const int r = lane / G, g = lane - r * G, x = 4 * g;
+  const bool lane_ok = r < RP;
+  uint64_t colm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) colm[j] = __ballot(lane_ok && x + j < bw);
+  const uint64_t lt = lanemask_lt(lane);
+  const u16x2 tt = {(unsigned short)t, (unsigned short)t};
+  int n1 = 0;
+  for (int by0 = 0; by0 < bh; by0 += RP) {
+    const int by = by0 + r;
+    const uint64_t rowm = __ballot(by < bh);
+    const LDSP uint32_t* rc = (const LDSP uint32_t*)(roi + u24mul(min(by, bh - 1) + 3, S)) + g;
+    const LDSP uint32_t* ru = rc - 3 * S / 4;  // 3 rows up: ring pixel 8
+    const LDSP uint32_t* rd = rc + 3 * S / 4;  // 3 rows down: ring pixel 0
+    uint32_t dc[4], du[2], dd[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dc[k] = k <= ((kN4 + 3) >> 2) ? rc[k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      du[k] = (kC >> 2) + k <= ((kC + 3) >> 2) ? ru[(kC >> 2) + k] : 0u;
+      dd[k] = (kC >> 2) + k <= ((kC + 3) >> 2) ? rd[(kC >> 2) + k] : 0u;
+    }
+    const uint32_t v4 = ext(dc, kC), n4 = ext(dc, kN4), n12 = ext(dc, kN12);
+    const uint32_t n8 = ext(du, kC & 3), n0 = ext(dd, kC & 3);
+    u16x2 any[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // h = 0: pixels 0 and 2, h = 1: pixels 1 and 3
+      const uint32_t sh = 8 * h;
+      const u16x2 v = bits((v4 >> sh) & 0x00FF00FFu);
+      const u16x2 a0 = bits((n0 >> sh) & 0x00FF00FFu), a4 = bits((n4 >> sh) & 0x00FF00FFu);
+      const u16x2 a8 = bits((n8 >> sh) & 0x00FF00FFu), a12 = bits((n12 >> sh) & 0x00FF00FFu);
+      const u16x2 s1 = __builtin_elementwise_min(a0, a4), l1 = __builtin_elementwise_max(a0, a4);
+      const u16x2 s2 = __builtin_elementwise_min(a8, a12), l2 = __builtin_elementwise_max(a8, a12);
+      const u16x2 a = __builtin_elementwise_max(s1, s2), b = __builtin_elementwise_min(l1, l2);
+      const u16x2 dk = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), __builtin_elementwise_min(a, b));
+      const u16x2 br = __builtin_elementwise_sub_sat(__builtin_elementwise_max(a, b), v + tt);
+      any[h] = dk | br;
+    }
+    const uint64_t m0 = __ballot(any[0].x != 0) & colm[0] & rowm, m1 = __ballot(any[1].x != 0) & colm[1] & rowm;
+    const uint64_t m2 = __ballot(any[0].y != 0) & colm[2] & rowm, m3 = __ballot(any[1].y != 0) & colm[3] & rowm;
+    int pos = n1 + mbcnt64(m0) + mbcnt64(m1) + mbcnt64(m2) + mbcnt64(m3);
+    const uint16_t e = (uint16_t)((by << 8) | x);
+    if ((m0 >> lane) & 1) list[pos++] = e;
+    if ((m1 >> lane) & 1) list[pos++] = (uint16_t)(e + 1);
+    if ((m2 >> lane) & 1) list[pos++] = (uint16_t)(e + 2);
+    if ((m3 >> lane) & 1) list[pos] = (uint16_t)(e + 3);
+    n1 += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+  }
+  return n1;
 }
 
 #ifndef ORBX_FAST_PK
@@ -193,57 +281,66 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   const int rstep = two ? 2 : 1;
   const LDSP uint8_t* band = roi + 3 * kRoiStride + ox + 3;  // band pixel (0,0)
 
-  // (a) compass pre-test over all band pixels, row-major ordered compaction;
-  // four row groups per step so their LDS reads are in flight together
+  // (a) compass pre-test over all band pixels, row-major ordered compaction
   int n1 = 0;
-  for (int by0 = 0; by0 < bh; by0 += 4 * rstep) {
-    bool fl[4];
-#if ORBX_FAST_PK
-    // two row groups per packed u16x2 register: the min/max network, the
-    // thresholds (saturating subtract) and the tests run as v_pk_* ops
-    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int q = 0; q < 4; q += 2) {
-      const int byA = by0 + q * rstep + lr, byB = byA + rstep;
-      const LDSP uint8_t* cA = band + u24mul(min(byA, bh - 1), kRoiStride) + min(lc, bw - 1);
-      const LDSP uint8_t* cB = band + u24mul(min(byB, bh - 1), kRoiStride) + min(lc, bw - 1);
-      auto pk = [](int lo, int hi) { return (u16x2){(unsigned short)lo, (unsigned short)hi}; };
-      const u16x2 v = pk(cA[0], cB[0]);
-      const u16x2 n0 = pk(cA[3 * kRoiStride], cB[3 * kRoiStride]), n4 = pk(cA[3], cB[3]);
-      const u16x2 n8 = pk(cA[-3 * kRoiStride], cB[-3 * kRoiStride]), n12 = pk(cA[-3], cB[-3]);
-      const u16x2 s1 = __builtin_elementwise_min(n0, n4), l1 = __builtin_elementwise_max(n0, n4);
-      const u16x2 s2 = __builtin_elementwise_min(n8, n12), l2 = __builtin_elementwise_max(n8, n12);
-      const u16x2 a = __builtin_elementwise_max(s1, s2), b = __builtin_elementwise_min(l1, l2);
-      const u16x2 tt = {(unsigned short)t, (unsigned short)t};
-      // min(a,b) < v - t  <=>  sat(sat(v - t) - min(a,b)) != 0;  max(a,b) > v + t  <=>  sat(max(a,b) - (v + t)) != 0
-      const u16x2 dk = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), __builtin_elementwise_min(a, b));
-      const u16x2 br = __builtin_elementwise_sub_sat(__builtin_elementwise_max(a, b), v + tt);
-      const u16x2 any = dk | br;
-      fl[q] = (int)(byA < bh) & (int)(lc < bw) & (int)(any.x != 0);
-      fl[q + 1] = (int)(byB < bh) & (int)(lc < bw) & (int)(any.y != 0);
+  if constexpr (kTight && kTightE == 4) {
+    switch (ox) {
+      case 0: n1 = compass4<0>(roi, list, bw, bh, t, lane); break;
+      case 1: n1 = compass4<1>(roi, list, bw, bh, t, lane); break;
+      case 2: n1 = compass4<2>(roi, list, bw, bh, t, lane); break;
+      default: n1 = compass4<3>(roi, list, bw, bh, t, lane); break;
     }
+  } else {
+    // four row groups per step so their LDS reads are in flight together
+    for (int by0 = 0; by0 < bh; by0 += 4 * rstep) {
+      bool fl[4];
+#if ORBX_FAST_PK
+      // two row groups per packed u16x2 register: the min/max network, the
+      // thresholds (saturating subtract) and the tests run as v_pk_* ops
+      typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int q = 0; q < 4; q += 2) {
+        const int byA = by0 + q * rstep + lr, byB = byA + rstep;
+        const LDSP uint8_t* cA = band + u24mul(min(byA, bh - 1), kRoiStride) + min(lc, bw - 1);
+        const LDSP uint8_t* cB = band + u24mul(min(byB, bh - 1), kRoiStride) + min(lc, bw - 1);
+        auto pk = [](int lo, int hi) { return (u16x2){(unsigned short)lo, (unsigned short)hi}; };
+        const u16x2 v = pk(cA[0], cB[0]);
+        const u16x2 n0 = pk(cA[3 * kRoiStride], cB[3 * kRoiStride]), n4 = pk(cA[3], cB[3]);
+        const u16x2 n8 = pk(cA[-3 * kRoiStride], cB[-3 * kRoiStride]), n12 = pk(cA[-3], cB[-3]);
+        const u16x2 s1 = __builtin_elementwise_min(n0, n4), l1 = __builtin_elementwise_max(n0, n4);
+        const u16x2 s2 = __builtin_elementwise_min(n8, n12), l2 = __builtin_elementwise_max(n8, n12);
+        const u16x2 a = __builtin_elementwise_max(s1, s2), b = __builtin_elementwise_min(l1, l2);
+        const u16x2 tt = {(unsigned short)t, (unsigned short)t};
+        // min(a,b) < v - t  <=>  sat(sat(v - t) - min(a,b)) != 0;  max(a,b) > v + t  <=>  sat(max(a,b) - (v + t)) != 0
+        const u16x2 dk = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), __builtin_elementwise_min(a, b));
+        const u16x2 br = __builtin_elementwise_sub_sat(__builtin_elementwise_max(a, b), v + tt);
+        const u16x2 any = dk | br;
+        fl[q] = (int)(byA < bh) & (int)(lc < bw) & (int)(any.x != 0);
+        fl[q + 1] = (int)(byB < bh) & (int)(lc < bw) & (int)(any.y != 0);
+      }
 #else
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int by = by0 + q * rstep + lr;
-      const LDSP uint8_t* c = band + u24mul(min(by, bh - 1), kRoiStride) + min(lc, bw - 1);
-      const int v = c[0];
-      const int n0 = c[3 * kRoiStride], n4 = c[3], n8 = c[-3 * kRoiStride], n12 = c[-3];
-      // >= 2 of the 4 compass pixels darker than v - t  <=>  their 2nd smallest is;
-      // >= 2 brighter than v + t  <=>  their 2nd largest is
-      const int s1 = min(n0, n4), l1 = max(n0, n4), s2 = min(n8, n12), l2 = max(n8, n12);
-      const int a = max(s1, s2), b = min(l1, l2);
-      // bitwise, not short-circuit: the reads are clamped, so all four row
-      // groups' loads can be in flight before the first use
-      fl[q] = (int)(by < bh) & (int)(lc < bw) & ((int)(min(a, b) < v - t) | (int)(max(a, b) > v + t));
-    }
+      for (int q = 0; q < 4; ++q) {
+        const int by = by0 + q * rstep + lr;
+        const LDSP uint8_t* c = band + u24mul(min(by, bh - 1), kRoiStride) + min(lc, bw - 1);
+        const int v = c[0];
+        const int n0 = c[3 * kRoiStride], n4 = c[3], n8 = c[-3 * kRoiStride], n12 = c[-3];
+        // >= 2 of the 4 compass pixels darker than v - t  <=>  their 2nd smallest is;
+        // >= 2 brighter than v + t  <=>  their 2nd largest is
+        const int s1 = min(n0, n4), l1 = max(n0, n4), s2 = min(n8, n12), l2 = max(n8, n12);
+        const int a = max(s1, s2), b = min(l1, l2);
+        // bitwise, not short-circuit: the reads are clamped, so all four row
+        // groups' loads can be in flight before the first use
+        fl[q] = (int)(by < bh) & (int)(lc < bw) & ((int)(min(a, b) < v - t) | (int)(max(a, b) > v + t));
+      }
 #endif
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int by = by0 + q * rstep + lr;
-      const uint64_t m = __ballot(fl[q]);
-      if (fl[q]) list[n1 + mbcnt64(m)] = (uint16_t)((by << 8) | lc);
-      n1 += __popcll(m);
+      for (int q = 0; q < 4; ++q) {
+        const int by = by0 + q * rstep + lr;
+        const uint64_t m = __ballot(fl[q]);
+        if (fl[q]) list[n1 + mbcnt64(m)] = (uint16_t)((by << 8) | lc);
+        n1 += __popcll(m);
+      }
     }
   }
   stamp(1);
