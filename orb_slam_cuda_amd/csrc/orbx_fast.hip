@@ -111,7 +111,6 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
   uint64_t colm[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) colm[j] = __ballot(lane_ok && x + j < bw);
-  const uint64_t lt = lanemask_lt(lane);
   const u16x2 tt = {(unsigned short)t, (unsigned short)t};
   int n1 = 0;
   for (int by0 = 0; by0 < bh; by0 += RP) {
@@ -211,7 +210,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   const int l = cg.level;
   const LevelGeom& g = P.lv[l];
   const int pitch = lp.pitch[l];
+#ifdef ORBX_FAST_SAMEROI  // diagnostics (tools/variant.sh): every cell of a level stages frame 0's first ROI
+  const uint8_t* rows = lp.base[l] + (long long)g.minBY * pitch + (g.minBX - cg.c0);
+#else
   const uint8_t* rows = lp.base[l] + f * lp.fstride[l] + (long long)cg.r0 * pitch;
+#endif
   constexpr bool kTight = kRoiStride == kRoiTight;
   const int a0 = kTight ? (cg.c0 & ~(kTightE - 1)) : (cg.c0 & ~15), ox = cg.c0 - a0;
   // unpredicated staging: lanes past the last piece load and store it again
@@ -236,7 +239,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
       lo[k] = (int)__umul24((unsigned)r, (unsigned)pitch) + kTightE * d;
     }
 #pragma unroll
-    for (int k = 0; k < kK; ++k) v[k] = *(const piece_t*)(rows + a0 + lo[k]);
+    for (int k = 0; k < kK; ++k) {
+#ifdef ORBX_FAST_NOLOAD  // diagnostics: no global loads (synthetic bytes)
+      v[k] = (piece_t)(0x01010101u * (uint32_t)((lane * 37 + k * 11 + cell) & 255));
+#else
+      v[k] = *(const piece_t*)(rows + a0 + lo[k]);
+#endif
+    }
 #pragma unroll
     for (int k = 0; k < kK; ++k) *(LDSP piece_t*)(roi + ro[k]) = v[k];
     for (int i = lane + 64 * kK; i < total; i += 64) {
