@@ -107,14 +107,14 @@ __global__ __launch_bounds__(256) void pyr_resize_kernel(
       } else {
         int D0, D1;
         if (!rep[q]) {
-          D0 = r0[s] * a0v[q] + r0[s + 1] * a1v[q];
-          D1 = r1[s] * a0v[q] + r1[s + 1] * a1v[q];
+          D0 = __mul24((int)r0[s], a0v[q]) + __mul24((int)r0[s + 1], a1v[q]);
+          D1 = __mul24((int)r1[s], a0v[q]) + __mul24((int)r1[s + 1], a1v[q]);
         } else {
           D0 = r0[s] * 2048;
           D1 = r1[s] * 2048;
         }
         const int b0 = (short)(yt.y & 0xFFFF), b1 = (short)(yt.y >> 16);
-        v[q] = sat_u8((D0 * b0 + D1 * b1 + (1 << 21)) >> 22);
+        v[q] = sat_u8((__mul24(D0, b0) + __mul24(D1, b1) + (1 << 21)) >> 22);
       }
     }
     const uint32_t packed = pack4_u8(v[0], v[1], v[2], v[3]);
@@ -153,8 +153,8 @@ __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtr
   uint8_t* G0 = (uint8_t*)lp.base[l] + f * lp.fstride[l];
   for (int r = cd.x + r0; r <= cd.y; r += rstep) {
     const int2 yt = yt_rows[r - cd.x];
-    const uint8_t* s0 = src + ((yt.x & 0xFFFF) - src_lo) * spitch;
-    const uint8_t* s1 = src + ((yt.x >> 16) - src_lo) * spitch;
+    const uint8_t* s0 = src + __mul24((yt.x & 0xFFFF) - src_lo, spitch);
+    const uint8_t* s1 = src + __mul24((yt.x >> 16) - src_lo, spitch);
     int p00[8], p01[8], p10[8], p11[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -169,15 +169,17 @@ __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtr
       for (int q = 0; q < 8; ++q) v[q] = (p00[q] + p01[q] + p10[q] + p11[q] + 2) >> 2;
     } else {
       const int b0 = (short)(yt.y & 0xFFFF), b1 = (short)(yt.y >> 16);
+      // every factor fits 24 bits (u8 x 11-bit coefficients, D < 2^20): full-rate
+      // v_mad_i32_i24 instead of the quarter-rate 32-bit multiply
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int D0 = p00[q] * a0v[q] + p01[q] * a1v[q];
-        const int D1 = p10[q] * a0v[q] + p11[q] * a1v[q];
-        v[q] = sat_u8((D0 * b0 + D1 * b1 + (1 << 21)) >> 22);
+        const int D0 = __mul24(p00[q], a0v[q]) + __mul24(p01[q], a1v[q]);
+        const int D1 = __mul24(p10[q], a0v[q]) + __mul24(p11[q], a1v[q]);
+        v[q] = sat_u8((__mul24(D0, b0) + __mul24(D1, b1) + (1 << 21)) >> 22);
       }
     }
     const uint32_t pa = pack4_u8(v[0], v[1], v[2], v[3]), pb = pack4_u8(v[4], v[5], v[6], v[7]);
-    uint8_t* lrow = dst + (r - cd.x) * g.lpitch;
+    uint8_t* lrow = dst + __mul24(r - cd.x, g.lpitch);
     *(uint32_t*)(lrow + xa) = pa;
     *(uint32_t*)(lrow + xb) = pb;
     if (r >= own.x && r <= own.y) {
