@@ -68,14 +68,14 @@ def test_stage_probes(pkg, O):
                                       (151, 499), (126, 416), (105, 346)]
 
 
-@pytest.mark.parametrize("name", ["kitti_s0", "euroc_s3"])
+@pytest.mark.parametrize("name", ["kitti_s0", "euroc_s3", "kitti_s4_modeF"])
 def test_golden_vectors(pkg, name):
     from orb_slam_cuda_amd.synth import synth_frame
     g = np.load(os.path.join(GOLDEN, f"extract_{name}.npz"))
     W, H = int(g["W"]), int(g["H"])
     img = synth_frame(int(g["seed"]), W, H)
     assert sha(img) == str(g["image_sha"])
-    ext = pkg.ORBextractor(int(g["nfeatures"]), 1.2, 8, 20, 7, W, H)
+    ext = pkg.ORBextractor(int(g["nfeatures"]), 1.2, 8, 20, 7, W, H, scale_mode="UF"[int(g["scale_mode"])])
     kp, desc = ext(img)
     assert np.array_equal(kp.view(np.uint8).reshape(len(kp), 28), g["keypoints"])
     assert np.array_equal(desc, g["descriptors"])
@@ -232,3 +232,29 @@ def test_full_batch_properties(pkg):
     one = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H)
     kp10, _ = one(frames[10])
     assert np.array_equal(kps[10, :n[10]].view(np.uint8), kp10.view(np.uint8))
+
+
+def test_batch_mode_f_parity(pkg, O):
+    """The fork's buildGraph scale override (scale_mode F, src/ORBextractor.cc:674-680,
+    what the reference as written always computes) through the device batch API:
+    every frame of a batch equals the oracle in mode F."""
+    from orb_slam_cuda_amd import _lib
+    from orb_slam_cuda_amd.synth import SynthSequence
+    W, H, B = 1241, 376, 8
+    frames = SynthSequence(44, W, H).frames(B)
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H, max_batch=B, scale_mode="F")
+    cap = ext.frame_capacity
+    host = np.ascontiguousarray(frames)
+    d_in = _lib.DeviceArray(host.nbytes)
+    d_in.upload(host)
+    d_kp, d_desc, d_n = _lib.DeviceArray(B * cap * 28), _lib.DeviceArray(B * cap * 32), _lib.DeviceArray(B * 4)
+    s = _lib.Stream()
+    ext.extract_batch_device(d_in.ptr, B, H * W, W, d_kp.ptr, d_desc.ptr, d_n.ptr, s)
+    s.synchronize()
+    n = d_n.download(B, np.int32)
+    kps = d_kp.download(B * cap, pkg.KP_DTYPE).reshape(B, cap)
+    descs = d_desc.download((B, cap, 32), np.uint8)
+    cfg = oracle_cfg(O, 2000, W, H, scale_mode="F")
+    for i in range(B):
+        rkp, rdesc = O.extract(cfg, frames[i])
+        assert_same(kps[i, :n[i]], descs[i, :n[i]], rkp, rdesc)

@@ -217,14 +217,14 @@ def test_search_by_bow_matches_refpy(O, kf_vs_kf):
 
 
 # ----------------------------------------------------------- golden vectors
-@pytest.mark.parametrize("name", ["kitti_s0", "euroc_s3"])
+@pytest.mark.parametrize("name", ["kitti_s0", "euroc_s3", "kitti_s4_modeF"])
 def test_golden_extract(O, name):
     from orb_slam_cuda_amd.synth import synth_frame
     g = np.load(os.path.join(GOLDEN, f"extract_{name}.npz"))
     W, H = int(g["W"]), int(g["H"])
     img = synth_frame(int(g["seed"]), W, H)
     assert sha(img) == str(g["image_sha"]), "synthetic generator changed; regenerate goldens"
-    cfg = O.config(nfeatures=int(g["nfeatures"]), width=W, height=H)
+    cfg = O.config(nfeatures=int(g["nfeatures"]), width=W, height=H, scale_mode=int(g["scale_mode"]))
     kp, desc = O.extract(cfg, img)
     assert np.array_equal(kp.view(np.uint8).reshape(len(kp), 28), g["keypoints"])
     assert np.array_equal(desc, g["descriptors"])
