@@ -132,6 +132,9 @@ def parse_args(argv=None):
     ap.add_argument("--split", type=int, default=2, help="extraction launches (and streams) per batch")
     ap.add_argument("--priority", action="store_true",
                     help="high-priority extraction streams, low-priority matching stream")
+    ap.add_argument("--no-match-priority", dest="match_priority", action="store_false",
+                    help="matching stream(s) at normal priority (default: high, so the matcher's "
+                         "one-workgroup-per-pair kernels get CUs as the extraction kernels drain them)")
     ap.add_argument("--bow", action="store_true",
                     help="also Frame::ComputeBoW every frame (synthetic ORBvoc-shaped vocabulary, k 10 L 6)")
     ap.add_argument("--bow-match", action="store_true",
@@ -323,10 +326,11 @@ class MonoPipeline:
         prio = 1 if args.priority else None
         self.s_exts = [_lib.Stream(prio) for _ in range(S)]
         self.s_ext = self.s_exts[0]
-        self.s_match = _lib.Stream(0 if args.priority else None) if not args.serial else self.s_ext
+        mprio = 0 if args.priority else (1 if args.match_priority else None)
+        self.s_match = _lib.Stream(mprio) if not args.serial else self.s_ext
         self.two_match = (args.match_streams == 2 and not args.serial and not args.no_match
                           and args.carry == "match" and not host)
-        self.s_init = _lib.Stream(0 if args.priority else None) if self.two_match else self.s_match
+        self.s_init = _lib.Stream(mprio) if self.two_match else self.s_match
         self.bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
         self.voc = None
         self.bow_match = args.bow_match and not host
@@ -641,7 +645,9 @@ def run_mono(args, cfg, rank, world, local, dist):
                        "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
                        "frames_per_step_per_gpu": B, "resident_pool_frames": pool,
                        "parallelism": f"frame-sharded x{world}, one process per GPU, no collectives",
-                       "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS},
+                       "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS,
+                       "match_stream_priority": ("low" if args.priority else "high" if args.match_priority
+                                                 else "normal")},
             "per_rank_frames_per_s": agg["per_rank"],
             "roofline": roof,
             "match_roofline": match_roof,
