@@ -606,6 +606,13 @@ def run_mono(args, cfg, rank, world, local, dist):
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
             "algorithmic_bytes_per_launch": int(hbm_stages[rk] * BS),
             "avg_launch_ms": round(st[rk], 4)}
+    # the same kernel against VALU issue (it is latency / issue bound, not HBM bound):
+    # its committed SQ_INSTS_VALU per launch over this run's launch time
+    vi = sq_valu(KERNELS[rk])
+    if vi and BS == SQ_LAUNCH_FRAMES:
+        roof["valu_issue"] = {"wave_instr_per_launch": int(vi), "achieved_T_per_s": round(vi / (st[rk] * 1e-3) / 1e12, 4),
+                              "peak_T_per_s": VALU_ISSUE_PEAK_T, "frac": round(vi / (st[rk] * 1e-3) / 1e12 / VALU_ISSUE_PEAK_T, 4),
+                              "source": "profiles/sq_valu.json (tools/pmc_sq.sh, serial run)"}
     # the dense matcher runs on the matrix cores: algorithmic work = one 256-element +-1 dot
     # product per (query, candidate) pair = 512 FLOP, against the dense FP4 MFMA peak; the
     # per-pair top-2 update (v_min + v_med3) is reported against the VALU lane-op peak
@@ -669,6 +676,20 @@ def run_mono(args, cfg, rank, world, local, dist):
                                      if args.bow_match else None),
         }
         print(json.dumps(out), flush=True)
+
+
+SQ_LAUNCH_FRAMES = 32   # frames per extraction launch of the committed SQ counter run
+VALU_ISSUE_PEAK_T = 1.2288  # wave64 VALU instructions/s: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles
+
+
+def sq_valu(kernel):
+    """VALU wave-instructions per launch of `kernel` from the committed SQ counters (profiles/)."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "sq_valu.json")))
+    except Exception:
+        return None
+    want = kernel.split(" ")[0]
+    return next((v.get("valu_per_launch") for k, v in d.items() if k.split("<")[0] == want), None)
 
 
 def pmc_bytes(kernel):
