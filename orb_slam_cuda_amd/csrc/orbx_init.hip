@@ -24,7 +24,9 @@
 //      (per-i2 claim lists); a round without change is the fixed point. Past
 //      kInitMaxRounds one lane runs the sequential greedy instead;
 //   4. the latest acceptor keeps each i2, rotation consistency, outputs.
+#include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "orbx_device.cuh"
 #include "orbx_wave.cuh"
@@ -670,7 +672,12 @@ int launch_search_init(const InitParams& P0, const orbx_kp* kp1, const uint8_t* 
   const size_t fixed = init_lds_fixed_bytes(P.kp_pitch);
   // sorted positions and i2 are 12-bit fields of the candidate entries / keys
   if (P.kp_pitch > 4096 || fixed + 4096 > kInitLdsBudget) return ORBX_ECAPACITY;
-  P.cand_lds = (int)((kInitLdsBudget - fixed) / 4) & ~15;
+  // LDS request: the whole CU by default; ORBX_INIT_LDS_KB caps it (candidates and
+  // F2's descriptors then spill to global memory) so a workgroup can start on a CU
+  // that extraction workgroups still partly occupy
+  static const int cap_kb = getenv("ORBX_INIT_LDS_KB") ? atoi(getenv("ORBX_INIT_LDS_KB")) : 0;
+  const size_t budget = cap_kb > 0 ? std::min(kInitLdsBudget, std::max(fixed + 64, (size_t)cap_kb * 1024)) : kInitLdsBudget;
+  P.cand_lds = (int)((budget - fixed) / 4) & ~15;
   if (raise_lds_limit((const void*)search_init_kernel, kInitLdsBudget)) return ORBX_EDEVICE;
   const size_t lds = fixed + (size_t)P.cand_lds * 4;
   hipLaunchKernelGGL(search_init_kernel, dim3(pairs), dim3(kInitThreads), lds, (hipStream_t)stream, P, kp1, desc1, n1,
