@@ -639,7 +639,7 @@ def run_mono(args, cfg, rank, world, local, dist):
         nt = args.cpu_threads if args.cpu_threads > 0 else cpu_threads_default()
         cpu = cpu_baseline(sample, cfg, args.cpu_sample, args.no_match, nt) if nt > 1 else cpu1
         if lat is not None:
-            lat["cpu_oracle"] = cpu_latency(frames[:16], cfg, args.no_match)
+            lat["cpu_oracle"] = cpu_latency(frames[:220], cfg, args.no_match)
 
     if rank == 0:
         workload = (cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only")
@@ -778,8 +778,9 @@ def latency_leg(cfg, local, frames, no_match, n=200, warm=20):
     return out
 
 
-def cpu_latency(frames, cfg, no_match):
-    """The oracle's single-thread latency of the same calls (median over the frames)."""
+def cpu_latency(frames, cfg, no_match, warm=20):
+    """The oracle's single-thread latency of the same calls: median over the
+    frames after `warm` warm-up frames (>= 200 frames)."""
     from oracle import oracle as O
     W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
     oc = O.config(nfeatures=NF, width=W, height=H)
@@ -794,7 +795,9 @@ def cpu_latency(frames, cfg, no_match):
             O.search_for_initialization(pk, pd, kp, desc, (0, W, 0, H), np.stack([pk["x"], pk["y"]], 1), 100, 0.9, True)
             ts.append(time.perf_counter() - t0)
         prev = (kp, desc)
-    out = {"extract_ms_median": round(float(np.median(te)) * 1e3, 3), "frames": len(frames), "cores": 1,
+    w = min(warm, max(0, len(te) - 1))
+    te, ts = te[w:], ts[w:]
+    out = {"extract_ms_median": round(float(np.median(te)) * 1e3, 3), "frames": len(te), "warmup": w, "cores": 1,
            "kind": "port"}
     if ts:
         out["search_init_ms_median"] = round(float(np.median(ts)) * 1e3, 3)
