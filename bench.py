@@ -778,6 +778,17 @@ def latency_leg(cfg, local, frames, no_match, n=200, warm=20):
     return out
 
 
+def cpu_model():
+    """The host CPU's model name (report it beside the CPU baseline)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_latency(frames, cfg, no_match, warm=20):
     """The oracle's single-thread latency of the same calls: median over the
     frames after `warm` warm-up frames (>= 200 frames)."""
@@ -1007,7 +1018,7 @@ def cpu_baseline(frames, cfg, n, no_match, threads=1):
         t0 = time.perf_counter()
         _cpu_run(O, oc, frames[:n], W, no_match)
         dt = time.perf_counter() - t0
-        return {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+        return {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
                 "sample": f"{n} consecutive frames of the same synthetic sequence, oracle extract"
                           + ("" if no_match else what) + f", single thread, {dt:.1f} s"}
     from concurrent.futures import ThreadPoolExecutor
@@ -1020,7 +1031,7 @@ def cpu_baseline(frames, cfg, n, no_match, threads=1):
         list(ex.map(lambda c: _cpu_run(O, oc, c, W, no_match), chunks))
     dt = time.perf_counter() - t0
     tot = sum(len(c) for c in chunks)
-    return {"value": round(tot / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+    return {"value": round(tot / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{threads} frame-parallel oracle workers x {per} consecutive frames of the synthetic sequence, "
                       "oracle extract" + ("" if no_match else what) + f", {dt:.1f} s wall"}
 
