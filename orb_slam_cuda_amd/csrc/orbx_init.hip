@@ -38,7 +38,15 @@ constexpr int kInitCells = kInitGridCols * kInitGridRows;
 constexpr int kInitHisto = 30;  // HISTO_LENGTH
 constexpr int kInitThLow = 50;  // TH_LOW
 constexpr int kInitMaxRounds = 48;
-constexpr int kD0Stride = 9;  // words per staged F2 descriptor: odd, so random rows spread over the LDS banks
+constexpr int kD0Stride = 9;
+#ifndef ORBX_INIT_ROUND_LANES
+#define ORBX_INIT_ROUND_LANES 4
+#endif
+constexpr int kRoundLanes = ORBX_INIT_ROUND_LANES;  // lanes per query in the Jacobi rounds
+#ifndef ORBX_INIT_WIN_LANES
+#define ORBX_INIT_WIN_LANES 4
+#endif
+constexpr int kWinLanes = ORBX_INIT_WIN_LANES;  // lanes per query in the window count / list phases  // words per staged F2 descriptor: odd, so random rows spread over the LDS banks
 
 #define LDSP __attribute__((address_space(3)))
 
@@ -78,19 +86,35 @@ __device__ __forceinline__ int init_hamming(uint4 a0, uint4 a1, uint4 b0, uint4 
          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-// 16-lane row (one query) helpers on DPP; all 16 lanes of the row must be active
-__device__ __forceinline__ int row_incl_scan(int v) {
-  v += dpp_i<kDppShr1>(0, v);
-  v += dpp_i<kDppShr2>(0, v);
-  v += dpp_i<kDppShr4>(0, v);
-  v += dpp_i<kDppShr8>(0, v);
+// DPP helpers over groups of G lanes (1, 2, 4, 8 or 16) inside a 16-lane row;
+// every lane of a group must be active
+template <int G>
+__device__ __forceinline__ int group_incl_scan(int v) {
+  if (G == 1) return v;
+  const int lg = threadIdx.x & (G - 1);
+  int t = dpp_i<kDppShr1>(0, v);
+  v += lg >= 1 ? t : 0;
+  if (G == 2) return v;
+  t = dpp_i<kDppShr2>(0, v);
+  v += lg >= 2 ? t : 0;
+  if (G > 4) {
+    t = dpp_i<kDppShr4>(0, v);
+    v += lg >= 4 ? t : 0;
+  }
+  if (G > 8) {
+    t = dpp_i<kDppShr8>(0, v);
+    v += lg >= 8 ? t : 0;
+  }
   return v;
 }
-__device__ __forceinline__ int row_sum(int v) {
+template <int G>
+__device__ __forceinline__ int group_sum(int v) {
+  if (G == 1) return v;
   v += dpp_i<kDppQuad1032>(0, v);
+  if (G == 2) return v;
   v += dpp_i<kDppQuad2301>(0, v);
-  v += dpp_i<kDppHalfMirror>(0, v);
-  v += dpp_i<kDppMirror>(0, v);
+  if (G > 4) v += dpp_i<kDppHalfMirror>(0, v);
+  if (G > 8) v += dpp_i<kDppMirror>(0, v);
   return v;
 }
 // (k1, k2) = the two smallest keys of the row
@@ -100,11 +124,14 @@ __device__ __forceinline__ void row_top2_step(uint32_t& k1, uint32_t& k2) {
   k2 = min(min(max(k1, o1), k2), o2);
   k1 = min(k1, o1);
 }
+template <int G = 16>
 __device__ __forceinline__ void row_top2(uint32_t& k1, uint32_t& k2) {
+  if (G == 1) return;
   row_top2_step<kDppQuad1032>(k1, k2);
+  if (G == 2) return;
   row_top2_step<kDppQuad2301>(k1, k2);
-  row_top2_step<kDppHalfMirror>(k1, k2);
-  row_top2_step<kDppMirror>(k1, k2);
+  if (G > 4) row_top2_step<kDppHalfMirror>(k1, k2);
+  if (G > 8) row_top2_step<kDppMirror>(k1, k2);
 }
 
 // vMatchedDistance[i2] at i1's turn: the smallest distance of an earlier
@@ -183,17 +210,17 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
   // ---- phase 2a: candidate lists in reference order: a 16-lane row per
   // query, a lane per window column; column c's entries follow the entries of
   // columns < c (row prefix sum), each (query slot << 12 | sorted position)
-  for (int g = tid >> 4; g < nq0; g += kInitThreads / 16) {
-    const int l16 = tid & 15;
+  for (int g = tid / kWinLanes; g < nq0; g += kInitThreads / kWinLanes) {
+    const int l16 = tid & (kWinLanes - 1);
     const int i1 = S.qlist[g];
     const int off = S.coff[i1];
-    if (off == S.coff[i1 + 1]) continue;  // row-uniform
+    if (off == S.coff[i1 + 1]) continue;  // group-uniform
     const float x = S.src_f[g], y = S.queue_f[g];
     int cx0, cx1, cy0, cy1;
     init_window(x, y, P, cx0, cx1, cy0, cy1);
     const int ncol = cx1 - cx0 + 1;
     int base = off;
-    for (int c0 = 0; c0 < ncol; c0 += 16) {
+    for (int c0 = 0; c0 < ncol; c0 += kWinLanes) {
       const int ci = c0 + l16;
       int pb = 0, pe = 0, own = 0;
       if (ci < ncol) {
@@ -205,13 +232,13 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
           own += (fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r) ? 1 : 0;
         }
       }
-      int o = base + row_incl_scan(own) - own;
+      int o = base + group_incl_scan<kWinLanes>(own) - own;
       for (int p = pb; p < pe; ++p) {
         const float qx = S.pos[2 * p], qy = S.pos[2 * p + 1];
         if (fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r)
           cand[o++] = ((uint32_t)g << 12) | (uint32_t)p;
       }
-      base += row_sum(own);
+      base += group_sum<kWinLanes>(own);
     }
   }
   __syncthreads();
@@ -291,12 +318,13 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
       // a 16-lane row per query: lane l scans candidates c0 + l, c0 + l + 16, ...
       // keeping the two smallest (distance << 22 | position) keys; the row merge
       // gives the sequential scan's best (earliest on equal distances) and second
-      for (int g = tid >> 4; g < nq; g += kInitThreads / 16) {
-        const int l16 = tid & 15;
+      // kRoundLanes lanes per query (a DPP row holds 16 / kRoundLanes queries)
+      for (int g = tid / kRoundLanes; g < nq; g += kInitThreads / kRoundLanes) {
+        const int l16 = tid & (kRoundLanes - 1);
         const int i1 = S.queue[g];
         const int c0 = S.coff[i1], c1 = S.coff[i1 + 1];
         uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
-        for (int c = c0 + l16; c < c1; c += 16) {
+        for (int c = c0 + l16; c < c1; c += kRoundLanes) {
           const uint32_t e = cand[c];
           const int i2 = (int)(e & 0x7FFFFF), dist = (int)(e >> 23);
           if (init_claim_md(head, nxt, i2, i1) <= dist) continue;  // (:444-445)
@@ -304,7 +332,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
           k2 = min(k2, max(k1, key));
           k1 = min(k1, key);
         }
-        row_top2(k1, k2);
+        row_top2<kRoundLanes>(k1, k2);
         const int best = k1 == 0xFFFFFFFFu ? INT_MAX : (int)(k1 >> 22);
         const int best2 = k2 == 0xFFFFFFFFu ? INT_MAX : (int)(k2 >> 22);
         const bool ok = best <= kInitThLow && (float)best < __fmul_rn((float)best2, P.nnratio);
@@ -431,30 +459,31 @@ __device__ void init_finish(const InitParams& P, LDSP int* src, LDSP int* m12, L
       src[i] = bin;
     }
     __syncthreads();
-    if (tid == 0) {
-      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-      for (int i = 0; i < kInitHisto; i++) {
-        const int s = hist[i];
-        if (s > max1) {
-          max3 = max2; max2 = max1; max1 = s;
-          ind3 = ind2; ind2 = ind1; ind1 = i;
-        } else if (s > max2) {
-          max3 = max2; max2 = s;
-          ind3 = ind2; ind2 = i;
-        } else if (s > max3) {
-          max3 = s;
-          ind3 = i;
+    if (tid < 64) {
+      // ComputeThreeMaxima's sequential scan (strict >, first index wins) is a
+      // stable top-3 of the positive bins by (count desc, index asc): three wave
+      // maxima of (count << 8 | 255 - bin), each excluding the previous winner
+      int key = tid < kInitHisto && hist[tid] > 0 ? (hist[tid] << 8) | (255 - tid) : 0;
+      int top[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        top[k] = INT_MAX - wave_min_dpp(INT_MAX - key);
+        if (key == top[k]) key = 0;
+      }
+      if (tid == 0) {
+        const int max1 = top[0] >> 8, max2 = top[1] >> 8, max3 = top[2] >> 8;
+        int ind1 = max1 ? 255 - (top[0] & 255) : -1, ind2 = max2 ? 255 - (top[1] & 255) : -1,
+            ind3 = max3 ? 255 - (top[2] & 255) : -1;
+        if (max2 < __fmul_rn(0.1f, (float)max1)) {
+          ind2 = -1;
+          ind3 = -1;
+        } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
+          ind3 = -1;
         }
+        var[1] = ind1;
+        var[2] = ind2;
+        var[3] = ind3;
       }
-      if (max2 < __fmul_rn(0.1f, (float)max1)) {
-        ind2 = -1;
-        ind3 = -1;
-      } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
-        ind3 = -1;
-      }
-      var[1] = ind1;
-      var[2] = ind2;
-      var[3] = ind3;
     }
     __syncthreads();
     const int ind1 = var[1], ind2 = var[2], ind3 = var[3];
@@ -616,13 +645,13 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   init_stamp(P, 2);
   // ---- phase 1: candidate counts (Frame::GetFeaturesInArea(x, y, r, 0, 0));
   // one 16-lane row per query, a lane per window column
-  for (int g = tid >> 4; g < nq0; g += kInitThreads / 16) {
-    const int l16 = tid & 15;
+  for (int g = tid / kWinLanes; g < nq0; g += kInitThreads / kWinLanes) {
+    const int l16 = tid & (kWinLanes - 1);
     const int i1 = S.qlist[g];
     const float x = qx[g], y = qy[g];
     int cx0, cx1, cy0, cy1, cnt = 0;
     const int ncol = init_window(x, y, P, cx0, cx1, cy0, cy1) ? cx1 - cx0 + 1 : 0;
-    for (int ci = l16; ci < ncol; ci += 16) {
+    for (int ci = l16; ci < ncol; ci += kWinLanes) {
       const int ix = cx0 + ci;
       const int pe = S.cell[ix * kInitGridRows + cy1 + 1];
       for (int p = S.cell[ix * kInitGridRows + cy0]; p < pe; ++p) {
@@ -630,7 +659,7 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
         cnt += (fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r) ? 1 : 0;
       }
     }
-    cnt = row_sum(cnt);
+    cnt = group_sum<kWinLanes>(cnt);
     if (l16 == 0) S.coff[i1] = cnt;
   }
   __syncthreads();
