@@ -46,7 +46,8 @@ constexpr int kRoundLanes = ORBX_INIT_ROUND_LANES;  // lanes per query in the Ja
 #ifndef ORBX_INIT_WIN_LANES
 #define ORBX_INIT_WIN_LANES 4
 #endif
-constexpr int kWinLanes = ORBX_INIT_WIN_LANES;  // lanes per query in the window count / list phases  // words per staged F2 descriptor: odd, so random rows spread over the LDS banks
+constexpr int kWinLanes = ORBX_INIT_WIN_LANES;
+constexpr uint32_t kInitVoid = 0xFFFFFFFFu;  // list slot of a window-cell keypoint outside the r-square  // lanes per query in the window count / list phases  // words per staged F2 descriptor: odd, so random rows spread over the LDS banks
 
 #define LDSP __attribute__((address_space(3)))
 
@@ -222,21 +223,22 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
     int base = off;
     for (int c0 = 0; c0 < ncol; c0 += kWinLanes) {
       const int ci = c0 + l16;
-      int pb = 0, pe = 0, own = 0;
+      int pb = 0, pe = 0;
       if (ci < ncol) {
         const int ix = cx0 + ci;
         pb = S.cell[ix * kInitGridRows + cy0];
         pe = S.cell[ix * kInitGridRows + cy1 + 1];
-        for (int p = pb; p < pe; ++p) {
-          const float qx = S.pos[2 * p], qy = S.pos[2 * p + 1];
-          own += (fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r) ? 1 : 0;
-        }
       }
+      const int own = pe - pb;
       int o = base + group_incl_scan<kWinLanes>(own) - own;
+      // one slot per keypoint of the column's cells; those outside the
+      // |dx|, |dy| < r square stay in the list as kInitVoid (skipped by every
+      // later pass), so the list keeps the reference's candidate order
       for (int p = pb; p < pe; ++p) {
         const float qx = S.pos[2 * p], qy = S.pos[2 * p + 1];
-        if (fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r)
-          cand[o++] = ((uint32_t)g << 12) | (uint32_t)p;
+        cand[o++] = fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r
+                        ? ((uint32_t)g << 12) | (uint32_t)p
+                        : kInitVoid;
       }
       base += group_sum<kWinLanes>(own);
     }
@@ -258,6 +260,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
   // the entry becomes (i2 | distance << 23)
   for (int c = tid; c < total; c += kInitThreads) {
     const uint32_t e = cand[c];
+    if (e == kInitVoid) continue;
     const int g = (int)(e >> 12), p = (int)(e & 0xFFF);
     uint4 a0, a1;
     if (qd_lds) {
@@ -326,6 +329,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
         uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
         for (int c = c0 + l16; c < c1; c += kRoundLanes) {
           const uint32_t e = cand[c];
+          if (e == kInitVoid) continue;
           const int i2 = (int)(e & 0x7FFFFF), dist = (int)(e >> 23);
           if (init_claim_md(head, nxt, i2, i1) <= dist) continue;  // (:444-445)
           const uint32_t key = ((uint32_t)dist << 22) | (uint32_t)(c - c0);
@@ -407,6 +411,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
       int best = INT_MAX, best2 = INT_MAX, bidx = -1;
       for (int c = S.coff[i1]; c < c1; ++c) {
         const uint32_t e = cand[c];
+        if (e == kInitVoid) continue;
         const int i2 = (int)(e & 0x7FFFFF), dist = (int)(e >> 23);
         if (md[i2] <= dist) continue;
         if (dist < best) {
@@ -607,12 +612,11 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     S.hist[tid] = 0;
     S.var[tid] = 0;
   }
-  bool d0_lds = false;
+  bool d0_unused = false;
+  // F2's descriptors are staged after the list sizes are known (the tail goes
+  // to the candidate lists first, then to the descriptors)
   const int n0 = init_build_grid<kInitThreads>(P, kp2, desc2, n2, S.cell, S.cof, S.pos, S.idx, S.src, S.queue, S.tmp,
-                                               tail, P.cand_lds / 2, &d0_lds);
-  S.d0 = tail;
-  S.cand = tail + (d0_lds ? kD0Stride * n0 : 0);
-  const int cand_lds = P.cand_lds - (d0_lds ? kD0Stride * n0 : 0);
+                                               tail, 0, &d0_unused);
   // F1's octave-0 queries, compacted in index order
   for (int i = tid; i <= n1; i += kInitThreads) S.coff[i] = 0;
   __syncthreads();
@@ -643,8 +647,10 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   }
   __syncthreads();
   init_stamp(P, 2);
-  // ---- phase 1: candidate counts (Frame::GetFeaturesInArea(x, y, r, 0, 0));
-  // one 16-lane row per query, a lane per window column
+  // ---- phase 1: list slots per query = the keypoints of its window's cells
+  // (Frame::GetFeaturesInArea(x, y, r, 0, 0) before the |dx|, |dy| < r test:
+  // a column's cells are one run of sorted positions, so no position is read
+  // here); kWinLanes lanes per query, a lane per window column
   for (int g = tid / kWinLanes; g < nq0; g += kInitThreads / kWinLanes) {
     const int l16 = tid & (kWinLanes - 1);
     const int i1 = S.qlist[g];
@@ -653,11 +659,7 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     const int ncol = init_window(x, y, P, cx0, cx1, cy0, cy1) ? cx1 - cx0 + 1 : 0;
     for (int ci = l16; ci < ncol; ci += kWinLanes) {
       const int ix = cx0 + ci;
-      const int pe = S.cell[ix * kInitGridRows + cy1 + 1];
-      for (int p = S.cell[ix * kInitGridRows + cy0]; p < pe; ++p) {
-        const float qx = S.pos[2 * p], qy = S.pos[2 * p + 1];
-        cnt += (fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r) ? 1 : 0;
-      }
+      cnt += S.cell[ix * kInitGridRows + cy1 + 1] - S.cell[ix * kInitGridRows + cy0];
     }
     cnt = group_sum<kWinLanes>(cnt);
     if (l16 == 0) S.coff[i1] = cnt;
@@ -667,7 +669,7 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   init_stamp(P, 3);
   if (P.prof && tid == 0) P.prof[blockIdx.x * 16 + 13] = total;
   if (P.stop == 2) return;
-  if (total > cand_lds && total > P.cand_cap) {
+  if (total > P.cand_lds && total > P.cand_cap) {
     // overflow is reported (status bit 8), never truncated: the pair gets no
     // matches rather than stale outputs of an earlier call
     for (int i = tid; i < min(n1, K); i += kInitThreads) m12_out[i] = -1;
@@ -677,7 +679,21 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     }
     return;
   }
-  if (total <= cand_lds) {
+  // tail layout: [candidate lists (if they fit) | F2 descriptors (if they fit)]
+  const bool cand_in_lds = total <= P.cand_lds;
+  const int d0_at = cand_in_lds ? ((total + 15) & ~15) : 0;
+  const bool d0_lds = d0_at + kD0Stride * n0 <= P.cand_lds;
+  S.cand = tail;
+  S.d0 = tail + d0_at;
+  if (d0_lds) {
+    for (int t = tid; t < 2 * n0; t += kInitThreads) {
+      const int p = t >> 1, h = t & 1;
+      const uint4 u = ((const uint4*)(desc2 + (size_t)S.idx[p] * 32))[h];
+      LDSP uint32_t* w = S.d0 + kD0Stride * p + 4 * h;
+      w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+    }
+  }
+  if (cand_in_lds) {
     if (d0_lds)
       init_solve<LDSP uint32_t*, true>(P, S, S.cand, kp1, desc1, desc2, prev, n1, n2, nq0, total);
     else
