@@ -351,6 +351,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
     }
     if (changed) S.var[6] = 1;
     __syncthreads();
+    const long long t_snap = P.prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
     // snapshot of this round's outcomes as per-i2 claim lists
     for (int i = tid; i < n2; i += kInitThreads) head[i] = -1;
     __syncthreads();
@@ -363,6 +364,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
                   (r & 511);
     }
     __syncthreads();
+    if (P.prof && tid == 0) P.prof[blockIdx.x * 16 + 9] += (long long)__builtin_amdgcn_s_memtime() - t_snap;
   }
   init_stamp(P, 7);
   if (P.prof && tid == 0) P.prof[blockIdx.x * 16 + 12] = converged ? 1 : 0;

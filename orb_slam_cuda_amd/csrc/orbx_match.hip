@@ -1284,18 +1284,19 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
     std::vector<long long> h((size_t)pairs * 16);
     MHIP(hipStreamSynchronize((hipStream_t)stream));
     MHIP(hipMemcpy(h.data(), prof, h.size() * 8, hipMemcpyDeviceToHost));
-    double ph[9] = {0}, rounds = 0, conv = 0, tot = 0;
+    double ph[9] = {0}, rounds = 0, conv = 0, tot = 0, snap = 0;
     for (int q = 0; q < pairs; ++q) {
       for (int k = 1; k < 9; ++k)
         if (h[q * 16 + k]) ph[k] += (double)(h[q * 16 + k] - h[q * 16]);
       rounds += h[q * 16 + 11];
+      snap += h[q * 16 + 9];
       conv += h[q * 16 + 12];
       tot += h[q * 16 + 13];
     }
     fprintf(stderr, "search_init phases (avg clocks from start): sort %.0f qlist %.0f count %.0f walk %.0f dist %.0f "
-            "rounds %.0f end %.0f | rounds %.1f converged %.2f candidates %.0f\n", ph[1] / pairs,
+            "rounds %.0f end %.0f | rounds %.1f converged %.2f candidates %.0f snapshots %.0f\n", ph[1] / pairs,
             ph[2] / pairs, ph[3] / pairs, ph[4] / pairs, ph[5] / pairs, ph[7] / pairs, ph[8] / pairs,
-            rounds / pairs, conv / pairs, tot / pairs);
+            rounds / pairs, conv / pairs, tot / pairs, snap / pairs);
   }
   if (rc == ORBX_ECAPACITY)
     return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization's LDS grid", kp_pitch);
