@@ -521,13 +521,12 @@ __device__ void init_finish(const InitParams& P, LDSP int* src, LDSP int* m12, L
 // Frame::AssignFeaturesToGrid for F2's octave-0 keypoints (the only ones
 // GetFeaturesInArea(.., 0, 0) returns), as a counting sort by cell, stable in
 // index order: cell[c] = first sorted position of cell c (column-major cells,
-// so a window column is one run), pos / idx / (d0: descriptors at kD0Stride
-// words, when d0_words can hold them) in sorted order. slot / members are
-// scratch of n2 entries. Returns n0; no trailing barrier.
+// so a window column is one run), pos / idx in sorted order. slot / members
+// are scratch of n2 entries. Returns n0; no trailing barrier.
 template <int NT>
-__device__ int init_build_grid(const InitParams& P, const orbx_kp* __restrict__ kp2, const uint8_t* __restrict__ desc2,
-                               int n2, LDSP int* cell, LDSP int* cof, LDSP float* pos, LDSP int* idx, LDSP int* slot,
-                               LDSP int* members, LDSP int* tmp, LDSP uint32_t* d0, int d0_words, bool* d0_lds) {
+__device__ int init_build_grid(const InitParams& P, const orbx_kp* __restrict__ kp2, int n2, LDSP int* cell,
+                               LDSP int* cof, LDSP float* pos, LDSP int* idx, LDSP int* slot, LDSP int* members,
+                               LDSP int* tmp) {
   const int tid = threadIdx.x;
   for (int c = tid; c <= kInitCells; c += NT) cell[c] = 0;
   __syncthreads();
@@ -540,8 +539,6 @@ __device__ int init_build_grid(const InitParams& P, const orbx_kp* __restrict__ 
   }
   __syncthreads();
   const int n0 = init_scan<NT>(cell, kInitCells + 1, tmp);
-  const bool dl = kD0Stride * n0 <= d0_words;
-  *d0_lds = dl;
   for (int i = tid; i < n2; i += NT) {
     const int c = cof[i];
     if (c >= 0) members[cell[c] + slot[i]] = i;
@@ -559,13 +556,6 @@ __device__ int init_build_grid(const InitParams& P, const orbx_kp* __restrict__ 
     pos[2 * p] = k.x;
     pos[2 * p + 1] = k.y;
     idx[p] = i;
-    if (dl) {
-      const uint4* d = (const uint4*)(desc2 + (size_t)i * 32);
-      const uint4 u = d[0], v = d[1];
-      LDSP uint32_t* w = d0 + kD0Stride * p;
-      w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
-      w[4] = v.x; w[5] = v.y; w[6] = v.z; w[7] = v.w;
-    }
   }
   return n0;
 }
@@ -614,11 +604,9 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
     S.hist[tid] = 0;
     S.var[tid] = 0;
   }
-  bool d0_unused = false;
   // F2's descriptors are staged after the list sizes are known (the tail goes
   // to the candidate lists first, then to the descriptors)
-  const int n0 = init_build_grid<kInitThreads>(P, kp2, desc2, n2, S.cell, S.cof, S.pos, S.idx, S.src, S.queue, S.tmp,
-                                               tail, 0, &d0_unused);
+  const int n0 = init_build_grid<kInitThreads>(P, kp2, n2, S.cell, S.cof, S.pos, S.idx, S.src, S.queue, S.tmp);
   // F1's octave-0 queries, compacted in index order
   for (int i = tid; i <= n1; i += kInitThreads) S.coff[i] = 0;
   __syncthreads();
