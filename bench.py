@@ -627,6 +627,12 @@ def run_mono(args, cfg, rank, world, local, dist):
                       "traffic": pmc_bytes(KERNELS["hamming_top2"]),
                       "pairs_per_launch": pairs, "pairs_per_s": round(pairs / sec, 1),
                       "avg_launch_ms": round(st["hamming_top2"], 4)}
+    bow_nm = (round(float(pipe.d_bow_nm.download(B, np.int32).mean()), 1) if args.bow_match else None)
+    # release the timed pipeline (its streams hold hardware queues) before the extra legs
+    pipe.sync_all()
+    del pipe, timed
+    import gc
+    gc.collect()
     lat = host = cpu = cpu1 = None
     solo = world == 1
     if rank == 0 and solo and not args.no_latency:
@@ -672,8 +678,7 @@ def run_mono(args, cfg, rank, world, local, dist):
             "host_issue_ms_per_step": round(issue / args.steps * 1e3, 4), "event_ms_per_step": round(ev_ms / args.steps, 4),
             "keypoints_per_frame": round(nkp_mean, 1),
             "init_matches_per_pair": round(float(nm.mean()), 1),
-            "bow_matches_per_pair": (round(float(pipe.d_bow_nm.download(B, np.int32).mean()), 1)
-                                     if args.bow_match else None),
+            "bow_matches_per_pair": bow_nm,
         }
         print(json.dumps(out), flush=True)
 

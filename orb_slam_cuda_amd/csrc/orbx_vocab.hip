@@ -16,7 +16,7 @@
 // NodeId the FeatureVector carries).
 //
 // Kernels:
-//   voc_descend_kernel<GL>  GL lanes per descriptor (16 when k <= 16, else 32):
+//   voc_descend_kernel<GL>  GL lanes per descriptor (8 when k <= 16, else 32):
 //                           at each level lane c takes child c (c += GL), the
 //                           (dist << 16 | c) minimum over the group picks the
 //                           child; one 32-byte gather per lane per level.
@@ -80,8 +80,15 @@ __global__ __launch_bounds__(256) void voc_descend_kernel(VocDev V, const uint8_
                     __popc(b.x ^ q1.x) + __popc(b.y ^ q1.y) + __popc(b.z ^ q1.z) + __popc(b.w ^ q1.w);
       best = min(best, (d << 16) | c);
     }
+    if (GL <= 16) {  // group minimum on DPP (quad, half-row, row), no LDS round trip
+      best = min(best, dpp_i<kDppQuad1032>(INT_MAX, best));
+      best = min(best, dpp_i<kDppQuad2301>(INT_MAX, best));
+      if (GL > 4) best = min(best, dpp_i<kDppHalfMirror>(INT_MAX, best));
+      if (GL > 8) best = min(best, dpp_i<kDppMirror>(INT_MAX, best));
+    } else {
 #pragma unroll
-    for (int o = GL / 2; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, GL));
+      for (int o = GL / 2; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, GL));
+    }
     node = cf.x + (best & 0xFFFF);
     if (level == nid_level) {
       nid = V.orig[node];
@@ -466,12 +473,20 @@ int orbv_transform_batch(orbv_handle v, const uint8_t* d_desc, size_t desc_pitch
   const VocDev V{v->child, v->desc, v->word, v->weight, v->orig};
   const int nid_level = v->L - levelsup;
   if (v->n_words > 0) {
-    if (v->max_children <= 16) {
-      const long long groups = (long long)nf;
+    static const int gl_env = getenv("ORBX_VOC_GL") ? atoi(getenv("ORBX_VOC_GL")) : 0;  // A/B
+    const long long groups = (long long)nf;
+    if (v->max_children <= 16 && gl_env != 16 && gl_env != 4) {
+      // 8 lanes per descriptor: k <= 16 children take one or two passes, and a
+      // wave serves 8 descriptors instead of 4 (16 lanes left 6 of them idle at k = 10)
+      hipLaunchKernelGGL(voc_descend_kernel<8>, dim3((unsigned)((groups * 8 + 255) / 256)), dim3(256), 0, st, V,
+                         d_desc, desc_pitch, d_n, frames, cap, nid_level, d_word_ids, d_node_ids, d_weights);
+    } else if (v->max_children <= 16 && gl_env == 4) {
+      hipLaunchKernelGGL(voc_descend_kernel<4>, dim3((unsigned)((groups * 4 + 255) / 256)), dim3(256), 0, st, V,
+                         d_desc, desc_pitch, d_n, frames, cap, nid_level, d_word_ids, d_node_ids, d_weights);
+    } else if (v->max_children <= 16) {
       hipLaunchKernelGGL(voc_descend_kernel<16>, dim3((unsigned)((groups * 16 + 255) / 256)), dim3(256), 0, st, V,
                          d_desc, desc_pitch, d_n, frames, cap, nid_level, d_word_ids, d_node_ids, d_weights);
     } else {
-      const long long groups = (long long)nf;
       hipLaunchKernelGGL(voc_descend_kernel<32>, dim3((unsigned)((groups * 32 + 255) / 256)), dim3(256), 0, st, V,
                          d_desc, desc_pitch, d_n, frames, cap, nid_level, d_word_ids, d_node_ids, d_weights);
     }
