@@ -125,6 +125,68 @@ __device__ void bitonic_sort64(uint64_t* s, int S) {
   }
 }
 
+// The same sort for S = 4 * kAsThreads keys held in registers, 4 per thread
+// (thread t: keys 4t .. 4t+3): partners 1 or 2 apart are in the thread,
+// partners 4 .. 128 apart in the same wave (64-bit lane exchange), and only
+// the stages 256 .. S/2 apart go through LDS with a barrier (6 of the 66 for
+// S = 2048, instead of a barrier per stage).
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ void bitonic_sort64_reg(uint64_t* s) {
+  constexpr int S = 4 * kAsThreads;
+  const int t = threadIdx.x;
+  uint64_t v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = s[4 * t + q];
+  for (int k = 2; k <= S; k <<= 1) {
+    int j = k >> 1;
+    if (j >= 4 * 64) {  // partners in other waves: through LDS
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[4 * t + q] = v[q];
+      __syncthreads();
+      for (; j >= 4 * 64; j >>= 1) {
+        for (int u = t; u < S / 2; u += kAsThreads) {
+          const int i = 2 * u - (u & (j - 1));
+          const int l = i + j;
+          const uint64_t a = s[i], b = s[l];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            s[i] = b;
+            s[l] = a;
+          }
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = s[4 * t + q];
+    }
+    for (; j >= 4; j >>= 1) {  // partner thread t ^ (j / 4), same wave
+      const bool lower = (t & (j >> 2)) == 0, up = ((4 * t) & k) == 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t b = shfl_xor64(v[q], j >> 2);
+        v[q] = (up == lower) ? (v[q] < b ? v[q] : b) : (v[q] < b ? b : v[q]);
+      }
+    }
+    for (; j >= 1; j >>= 1) {  // partner in the thread
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q & j) continue;
+        const bool up = ((4 * t + q) & k) == 0;
+        const uint64_t a = v[q], b = v[q | j];
+        const bool sw = (a > b) == up;
+        v[q] = sw ? b : a;
+        v[q | j] = sw ? a : b;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s[4 * t + q] = v[q];
+  __syncthreads();
+}
+
 // run heads of the sorted valid keys (high 32 bits change): returns the number
 // of runs; s_head[t] = run index of a head, -1 otherwise. Keys == ~0 are invalid
 // and sorted last.
@@ -159,7 +221,7 @@ __global__ __launch_bounds__(kAsThreads) void voc_assemble_kernel(
     int cap, int S, const int* __restrict__ d_n, const uint32_t* __restrict__ word, const uint32_t* __restrict__ nid,
     const double* __restrict__ w, int tf, int must, int l2, int nwords, uint32_t* __restrict__ bow_words,
     double* __restrict__ bow_values, int* __restrict__ bow_n, uint32_t* __restrict__ fv_nodes,
-    int* __restrict__ fv_off, int* __restrict__ fv_idx, int* __restrict__ fv_n) {
+    int* __restrict__ fv_off, int* __restrict__ fv_idx, int* __restrict__ fv_n, int stop) {
   extern __shared__ __attribute__((aligned(16))) uint64_t s_key[];  // [S]
   int* s_head = (int*)(s_key + S);                                   // [S]
   __shared__ int s_tmp[kAsThreads / 64];
@@ -169,40 +231,46 @@ __global__ __launch_bounds__(kAsThreads) void voc_assemble_kernel(
   const int n = nwords > 0 ? d_n[f] : 0;  // if(empty()) return (:1131-1134)
   const size_t base = (size_t)f * cap;
 
-  // ---- FeatureVector: (node, feature) ascending = std::map order, push_back order
-  if (tid == 0) s_m = 0;
-  for (int i = tid; i < S; i += kAsThreads)
-    s_key[i] = (i < n && w[base + i] > 0) ? ((uint64_t)nid[base + i] << 32) | (uint32_t)i : ~0ull;
-  __syncthreads();
-  bitonic_sort64(s_key, S);
-  int runs = mark_runs(s_key, S, s_head, s_tmp);
-  for (int t = tid; t < S; t += kAsThreads) {
-    const uint64_t k = s_key[t];
-    if (k == ~0ull) {
-      if (t == 0 || s_key[t - 1] != ~0ull) s_m = t;  // number of valid features
-      continue;
+  // blockIdx.y = 0: the FeatureVector, 1: the BowVector (independent halves,
+  // each in its own workgroup so that the two run side by side)
+  if (blockIdx.y == 0) {
+    // ---- FeatureVector: (node, feature) ascending = std::map order, push_back order
+    if (tid == 0) s_m = 0;
+    for (int i = tid; i < S; i += kAsThreads)
+      s_key[i] = (i < n && w[base + i] > 0) ? ((uint64_t)nid[base + i] << 32) | (uint32_t)i : ~0ull;
+    __syncthreads();
+    if (S == 4 * kAsThreads) bitonic_sort64_reg(s_key); else bitonic_sort64(s_key, S);
+    int runs = mark_runs(s_key, S, s_head, s_tmp);
+    for (int t = tid; t < S; t += kAsThreads) {
+      const uint64_t k = s_key[t];
+      if (k == ~0ull) {
+        if (t == 0 || s_key[t - 1] != ~0ull) s_m = t;  // number of valid features
+        continue;
+      }
+      fv_idx[base + t] = (int)(uint32_t)k;
+      const int r = s_head[t];
+      if (r >= 0) {
+        fv_nodes[base + r] = (uint32_t)(k >> 32);
+        fv_off[(size_t)f * (cap + 1) + r] = t;
+      }
     }
-    fv_idx[base + t] = (int)(uint32_t)k;
-    const int r = s_head[t];
-    if (r >= 0) {
-      fv_nodes[base + r] = (uint32_t)(k >> 32);
-      fv_off[(size_t)f * (cap + 1) + r] = t;
+    __syncthreads();
+    const int m = (s_key[S - 1] != ~0ull) ? S : s_m;
+    if (tid == 0) {
+      fv_off[(size_t)f * (cap + 1) + runs] = m;
+      fv_n[f] = runs;
     }
+    __syncthreads();
+    return;
   }
-  __syncthreads();
-  const int m = (s_key[S - 1] != ~0ull) ? S : s_m;
-  if (tid == 0) {
-    fv_off[(size_t)f * (cap + 1) + runs] = m;
-    fv_n[f] = runs;
-  }
-  __syncthreads();
+  if (stop == 2) return;  // diagnostics (ORBX_VOC_STOP=2): FeatureVector only
 
   // ---- BowVector: (word, feature) ascending; value = weights added in feature order
   for (int i = tid; i < S; i += kAsThreads)
     s_key[i] = (i < n && w[base + i] > 0) ? ((uint64_t)word[base + i] << 32) | (uint32_t)i : ~0ull;
   __syncthreads();
-  bitonic_sort64(s_key, S);
-  runs = mark_runs(s_key, S, s_head, s_tmp);
+  if (S == 4 * kAsThreads) bitonic_sort64_reg(s_key); else bitonic_sort64(s_key, S);
+  const int runs = mark_runs(s_key, S, s_head, s_tmp);
   double* s_val = (double*)s_key;  // values overwrite the keys after they are read below
   double v_mine[16];  // S <= 8192 = 16 keys per thread
   int r_mine[16], nm = 0;
@@ -229,6 +297,7 @@ __global__ __launch_bounds__(kAsThreads) void voc_assemble_kernel(
     for (int r = tid; r < runs; r += kAsThreads) s_val[r] /= nd;
     __syncthreads();
   }
+  if (stop == 3) return;  // diagnostics (ORBX_VOC_STOP=3): no normalisation
   if (must) {
     if (tid == 0) {
       double norm = 0.0;
@@ -502,9 +571,10 @@ int orbv_transform_batch(orbv_handle v, const uint8_t* d_desc, size_t desc_pitch
   int l1 = v->scoring != 1;
   const int must = v->scoring != 5;
   const int tf = v->weighting == 0 || v->weighting == 1;
-  hipLaunchKernelGGL(voc_assemble_kernel, dim3(frames), dim3(kAsThreads), lds, st, cap, S, d_n, d_word_ids, d_node_ids,
+  hipLaunchKernelGGL(voc_assemble_kernel, dim3(frames, 2), dim3(kAsThreads), lds, st, cap, S, d_n, d_word_ids, d_node_ids,
                      d_weights, tf, must, !l1, v->n_words, d_bow_words, d_bow_values, d_bow_n, d_fv_nodes, d_fv_off,
-                     d_fv_idx, d_fv_n);
+                     d_fv_idx, d_fv_n,
+                     getenv("ORBX_VOC_STOP") ? atoi(getenv("ORBX_VOC_STOP")) : 0);
   VHIP(hipGetLastError());
   return ORBX_OK;
 }
