@@ -119,7 +119,10 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1, help="GPUs of this node, one worker process each")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=64, help="frames per batch per GPU (2 extraction launches of 32)")
+    ap.add_argument("--batches-per-step", type=int, default=4,
+                    help="batches per timed step (a step is 4 x 64 frames by default, so a short --steps "
+                         "run still times the pipeline's steady state rather than its fill and drain)")
     ap.add_argument("--pool", type=int, default=640,
                     help="resident synthetic frames per GPU, cycled batch by batch (> the 256 MB MALL)")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
@@ -551,11 +554,12 @@ def run_mono(args, cfg, rank, world, local, dist):
     pool = max(B, (args.pool // B) * B)
     frames = SynthSequence(sharding.sequence_seed(rank), W, H).frames(pool)
     pipe = MonoPipeline(args, cfg, local, frames)
-    wall_rank, issue = pipe.run(args.warmup, args.steps, dist)
-    agg = aggregate(B * args.steps, wall_rank, dist, world)
+    SUB = max(1, args.batches_per_step)
+    wall_rank, issue = pipe.run(args.warmup * SUB, args.steps * SUB, dist)
+    agg = aggregate(B * SUB * args.steps, wall_rank, dist, world)
     pipe.check_status()
     BS, S, cap = pipe.BS, pipe.S, pipe.cap
-    timed = pipe.evsets[args.warmup:]
+    timed = pipe.evsets[args.warmup * SUB:]
     ev_ms = timed[0][0].elapsed_ms(timed[-1][8])
     front = pipe.exts[0].front_path
     names = FRONT_STAGES if front else STAGES
@@ -576,7 +580,7 @@ def run_mono(args, cfg, rank, world, local, dist):
         if not args.no_match:
             st["hamming_top2"] += evs[6].elapsed_ms(evs[7])
             st["search_init"] += evs[11].elapsed_ms(evs[8])
-    st = {s: v / args.steps for s, v in st.items()}
+    st = {s: v / len(timed) for s, v in st.items()}  # per batch (per launch group)
     ls = pipe.last_set()
     nm = pipe.d_nm[ls].download(B, np.int32)
     cnt = pipe.d_counts[ls].download(B + 1, np.int32).astype(np.int64)
@@ -658,7 +662,8 @@ def run_mono(args, cfg, rank, world, local, dist):
             "config": {"workload": workload + (" + Frame::ComputeBoW (synthetic k10 L6 vocabulary)" if (args.bow or args.bow_match) else "")
                                    + (" + SearchByBoW(KF t-1, F t)" if args.bow_match else ""),
                        "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
-                       "frames_per_step_per_gpu": B, "resident_pool_frames": pool,
+                       "frames_per_step_per_gpu": B * SUB, "batches_per_step": SUB, "frames_per_batch": B,
+                       "resident_pool_frames": pool,
                        "parallelism": f"frame-sharded x{world}, one process per GPU, no collectives",
                        "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS,
                        "match_stream_priority": ("low" if args.priority else "high" if args.match_priority
@@ -673,7 +678,7 @@ def run_mono(args, cfg, rank, world, local, dist):
             "quadtree_tie_straddle": tie,
             "pyr_fast_pass_hbm_gbs": round(pf_gbs, 1),
             "dominant_kernel": KERNELS[dominant],
-            "stage_ms_per_step": {s: round(v, 4) for s, v in st.items()},
+            "stage_ms_per_batch": {s: round(v, 4) for s, v in st.items()},
             "extract_only_frames_per_s": round(BS / (extract_ms * 1e-3), 1),
             "host_issue_ms_per_step": round(issue / args.steps * 1e3, 4), "event_ms_per_step": round(ev_ms / args.steps, 4),
             "keypoints_per_frame": round(nkp_mean, 1),

@@ -15,5 +15,5 @@ for MODE in 1 0; do
 done
 for MODE in 1 0 1 0; do
   ORBX_FRONT=$MODE timeout -k 10 200 python3 bench.py --steps 100 --warmup 20 --cpu-sample 0 --no-latency --no-host-stream > $OUT/bench$MODE.log 2>&1
-  python3 -c "import json;d=json.loads(open('$OUT/bench$MODE.log').read().strip().splitlines()[-1]);print('FRONT=$MODE VALUE',d['value'],d['ms_per_step'],d['stage_ms_per_step'],d['roofline']['frac'])"
+  python3 -c "import json;d=json.loads(open('$OUT/bench$MODE.log').read().strip().splitlines()[-1]);print('FRONT=$MODE VALUE',d['value'],d['ms_per_step'],d['stage_ms_per_batch'],d['roofline']['frac'])"
 done

@@ -13,5 +13,5 @@ for v in names:
     except (OSError, ValueError, IndexError) as e:
         print(v, "incomplete:", e)
         continue
-    st = " ".join("%s=%.1f" % (k[:6], 1000 * x) for k, x in s["stage_ms_per_step"].items())
+    st = " ".join("%s=%.1f" % (k[:6], 1000 * x) for k, x in s["stage_ms_per_batch"].items())
     print("%-8s %-22s serial %7.0f  pipe %7.0f %7.0f  | %s" % (v, t[:22], s["value"], b[0], b[1], st))
