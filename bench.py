@@ -3,7 +3,8 @@
 
 Workload (BASELINE.json configs[2], "C3"): KITTI-shaped 1241x376 mono u8
 frames, nFeatures=2000, 8 levels, scale 1.2, iniThFAST 20 / minThFAST 7.
-One step = one batch of B frames resident in HBM:
+One step = --batches-per-step (4) consecutive batches of B (64) frames
+resident in HBM; per batch:
   * ORBextractor::operator() on all B frames (orbx_extract_batch), and
   * for every frame t, matching against frame t-1: the dense brute-force
     2000 x 2000 Hamming best/second search (orbm_hamming_top2) and the exact
