@@ -11,8 +11,8 @@ resident in HBM; per batch:
     ORBmatcher::SearchForInitialization (window 100, ratio 0.9, rotation
     check) used by monocular initialisation.
 Frame t-1 of the first frame of a batch is the last frame of the previous
-batch (carried on device), so every step does B extractions + B matches.
-Step k processes batch k mod (pool / B) of a resident pool of synthetic
+batch (carried on device), so every batch does B extractions + B matches.
+Batch k processes slot k mod (pool / B) of a resident pool of synthetic
 frames larger than the 256 MB MALL (--pool, default 640 frames = 308 MB),
 so level 0 streams from HBM instead of staying in the last-level cache.
 
