@@ -454,9 +454,13 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   P.max_cells_level = maxcells;
   P.kcap_lds = 0;
   {
-    // keep the LDS footprint near 64 KiB so two quadtree blocks fit one CU
+    const char* e = getenv("ORBX_QT_GENERIC");  // tests: the generic rounds on any plan
+    P.qt_lean = maxnodes < 16384 && !(e && e[0] == '1');
+  }
+  {
+    // keep the LDS footprint at 80 KiB so two quadtree blocks fit one CU
     const size_t base = quadtree_lds_bytes(P);
-    const size_t budget = 64 * 1024;
+    const size_t budget = 80 * 1024;
     P.kcap_lds = base < budget ? (int)((budget - base) / 6) & ~15 : 0;
   }
   pl.P = P;

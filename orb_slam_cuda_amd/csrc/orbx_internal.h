@@ -67,6 +67,7 @@ struct ExtractParams {
   int maxnodes, sortn;         // quadtree node-table size, bitonic size (pow2)
   int max_cells_level;         // largest ncells of any level
   int kcap_lds;                // quadtree keys kept in LDS up to this count
+  int qt_lean;                 // quadtree: lean rounds (packed 16-bit key nodes, maxnodes < 16384), else the generic ones
   int fast_rh_max;             // largest FAST cell ROI height
   int fast_bw_max, fast_bh_max;  // largest FAST detection band
   int pattern_upstream;

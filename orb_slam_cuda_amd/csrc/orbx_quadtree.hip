@@ -57,7 +57,10 @@ __device__ __forceinline__ QNode child_box(const QNode& nd, int q) {
 
 __device__ __forceinline__ int nonempty(int4 c) { return (c.x > 0) + (c.y > 0) + (c.z > 0) + (c.w > 0); }
 
-__global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, const int* __restrict__ cell_counts,
+#ifndef ORBX_QT_MINW
+#define ORBX_QT_MINW 1
+#endif
+__global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(ExtractParams P, const int* __restrict__ cell_counts,
                                                               const uint32_t* __restrict__ slots,
                                                               const CellGeom* __restrict__ cells,
                                                               uint32_t* __restrict__ qscratch,
@@ -100,6 +103,9 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   int* coff = (int*)take(4ull * (P.max_cells_level + 1));
   int* s_soff = (int*)take(4ull * (P.max_cells_level + 1));  // cell slot offsets
   int2* s_mid = (int2*)take(8ull * MN);  // halves() of every node of this round
+  int4* cc2 = (int4*)take(16ull * MN);    // register-resident rounds: next list's child counts
+  int2* s_mid2 = (int2*)take(8ull * MN);  // ... and its halves()
+  int* s_wave = (int*)take(256);          // ... per-wave partials (scan totals, splits, T, expandable)
   int* s_tmp = (int*)take(64);
   int* s_var = (int*)take(64);
   uint32_t* lkeys = (uint32_t*)take(4ull * P.kcap_lds);
@@ -107,7 +113,12 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
 
   // ---- the level's FAST keys in reference order (cells row-major, FAST order inside)
   const int* cntp = cell_counts + (long long)f * P.ncells_total + g.cell0;
-  for (int c = tid; c < g.ncells; c += kQtThreads) coff[c] = cntp[c];
+  // cell counts and slot offsets are independent loads: one memory latency
+  for (int c = tid; c < g.ncells; c += kQtThreads) {
+    const int cnt = cntp[c], so = cells[g.cell0 + c].slot_off;
+    coff[c] = cnt;
+    s_soff[c] = so;
+  }
   __syncthreads();
   const int K = block_scan_excl<kQtThreads>(coff, g.ncells, s_tmp);
   const unsigned long long t_scan = __builtin_amdgcn_s_memtime();
@@ -120,15 +131,20 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   const uint32_t* fslots = slots + (long long)f * P.slots_per_frame;
   {
     // gather the K keys: cell c's keys (slot_off(c) .. + count) go to coff[c] ..
-    for (int c = tid; c < g.ncells; c += kQtThreads) s_soff[c] = cells[g.cell0 + c].slot_off;
     if (tid == 0) coff[g.ncells] = K;
     __syncthreads();
-    // per cell: its keys are one contiguous slot run; loads in groups of
-    // four so that a thread's memory latencies overlap
+    // per cell: its keys are one contiguous slot run; the first eight are
+    // loaded together (most cells hold fewer), the rest in groups of four
     for (int c = tid; c < g.ncells; c += kQtThreads) {
       const int b = coff[c], n = coff[c + 1] - b;
       const uint32_t* src = fslots + s_soff[c];
-      int i = 0;
+      uint32_t v8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v8[i] = i < n ? src[i] : 0u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (i < n) keys[b + i] = v8[i];
+      int i = 8;
       for (; i + 4 <= n; i += 4) {
         const uint32_t v0 = src[i], v1 = src[i + 1], v2 = src[i + 2], v3 = src[i + 3];
         keys[b + i] = v0;
@@ -145,13 +161,10 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
   int* rootCnt = tA;  // nIni <= MN
   for (int i = tid; i < nIni; i += kQtThreads) rootCnt[i] = 0;
   __syncthreads();
-  for (int k = tid; k < K; k += kQtThreads) {
-    const int r = (int)__fdiv_rn((float)key_x(keys[k]), g.hX);  // vpIniNodes[kp.pt.x/hX]
-    knode[k] = (uint16_t)r;
-    atomicAdd(&rootCnt[r], 1);
-  }
-  __syncthreads();
-  if (tid == 0) {
+  // the non-empty roots in column order (one lane: nIni is a handful);
+  // rootCnt[i] becomes the root's list position, -1 if empty (erased)
+  auto build_roots = [&](bool reg) {
+    if (tid != 0) return;
     int n = 0;
     for (int i = 0; i < nIni; ++i) {
       const int c = rootCnt[i];
@@ -164,20 +177,370 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
         nodeA[n] = nd;
         nkA[n] = c;
         seqA[n] = 0;
+        if (reg) {
+          int mx, my;
+          halves(nd, &mx, &my);
+          s_mid[n] = make_int2(mx, my);
+          cc[n] = make_int4(0, 0, 0, 0);
+        }
         rootCnt[i] = n++;
       } else {
-        rootCnt[i] = -1;  // empty roots are erased
+        rootCnt[i] = -1;
       }
     }
     s_var[0] = n;  // list size
     s_var[1] = 0;  // sorted-phase flag
     s_var[6] = s_var[7] = s_var[8] = 0;  // tie-straddle events / group nodes / kept keys
+  };
+  const int N = g.N;
+  uint32_t* out = qkeys + (long long)f * P.kp_per_frame + g.kbase;
+  auto write_tail = [&](int size, unsigned long long t_rounds) {
+    if (tid == 0) {
+      qcounts[f * P.L + l] = min(size, g.kcap);
+      int* qt = qties + ((long long)f * P.L + l) * 4;
+      qt[0] = s_var[6];
+      qt[1] = s_var[7];
+      qt[2] = s_var[8];
+      qt[3] = 0;
+      if (size > g.kcap) atomicOr(err, 4);
+    }
+    if (dbg && tid == 0) {  // diagnostics only (ORBX_QT_PROF=1)
+      int* d = dbg + (blockIdx.y * gridDim.x + blockIdx.x) * 8;
+      d[0] = (int)(t_rounds - t_begin);
+      d[1] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
+      d[2] = dbg_rounds;
+      d[3] = dbg_sorted;
+      d[4] = K;
+      d[5] = size;
+      d[6] = (int)(t_scan - t_begin);
+      d[7] = (int)(t_gather - t_begin);
+      int* dp = dbg + gridDim.x * gridDim.y * 8 + (blockIdx.y * gridDim.x + blockIdx.x) * 8;
+      dp[0] = (int)dbg_p0;
+      dp[1] = (int)dbg_p1;
+      dp[2] = (int)dbg_p2;
+      dp[3] = (int)dbg_p3;
+      dp[4] = (int)dbg_p4;
+    }
+  };
+  if (P.qt_lean) {
+    // ---- lean rounds. A key's node and its quadrant in that node are one
+    // packed 16-bit entry (node << 2 | q); the next round's child counts are
+    // added while the keys are re-homed, and the node-order scan runs over
+    // per-thread chunks of the list with per-wave partials: four barriers
+    // per breadth round (the generic path below takes nine). Key passes take
+    // four keys per thread at a time so that their LDS latencies overlap.
+    const int lane = tid & 63, wv = tid >> 6;
+    constexpr int NW = kQtThreads / 64;
+    for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
+      uint32_t kk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) kk[u] = k0 + u * kQtThreads < K ? keys[k0 + u * kQtThreads] : 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (k0 + u * kQtThreads < K) {
+          const int r = (int)__fdiv_rn((float)key_x(kk[u]), g.hX);  // vpIniNodes[kp.pt.x/hX]
+          knode[k0 + u * kQtThreads] = (uint16_t)r;
+          atomicAdd(&rootCnt[r], 1);
+        }
+      }
+    }
+    __syncthreads();
+    build_roots(true);
+    __syncthreads();
+    QNode* nA = nodeA;
+    QNode* nB = nodeB;
+    int* kA = nkA;
+    int* kB = nkB;
+    int* qA = seqA;
+    int* qB = seqB;
+    int4* cA = cc;
+    int4* cB = cc2;
+    int2* mA = s_mid;
+    int2* mB = s_mid2;
+    // first child counts: a key counts into its node's quadrant if the node holds > 1 key
+    for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
+      uint32_t kk[4];
+      int n[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool in = k0 + u * kQtThreads < K;
+        kk[u] = in ? keys[k0 + u * kQtThreads] : 0u;
+        n[u] = in ? knode[k0 + u * kQtThreads] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) n[u] = rootCnt[n[u]];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (k0 + u * kQtThreads < K) {
+          const int2 md = mA[n[u]];
+          const int q = (key_x(kk[u]) >= md.x ? 1 : 0) + (key_y(kk[u]) >= md.y ? 2 : 0);
+          if (kA[n[u]] > 1) atomicAdd(((int*)&cA[n[u]]) + q, 1);
+          knode[k0 + u * kQtThreads] = (uint16_t)((n[u] << 2) | q);
+        }
+      }
+    }
+    int size = s_var[0];
+    bool sorted_phase = false;
+    lds_sync();
+    for (int round = 0; round < 64; ++round) {
+      ph(-1);
+      dbg_sorted += sorted_phase;
+      const int per = (size + kQtThreads - 1) / kQtThreads;
+      const int nb = min(tid * per, size), ne = min(nb + per, size);
+      int expand = 0;
+      // the next list: a kept node moves to pos; a split node's non-empty
+      // children take base, base + 1, ... as n4 n3 n2 n1 (creation order
+      // j * 4 + q), and cA[n] becomes their positions
+      auto place_kept = [&](int n, int pos) {
+        nB[pos] = nA[n];
+        kB[pos] = kA[n];
+        qB[pos] = qA[n];
+        mB[pos] = mA[n];
+        cB[pos] = make_int4(0, 0, 0, 0);
+        tB[n] = pos;
+      };
+      auto place_split = [&](int n, int j, int base) {
+        const int4 c = cA[n];
+        const QNode nd = nA[n];
+        const int2 md = mA[n];
+        const int cnts[4] = {c.x, c.y, c.z, c.w};
+        int pos4[4];
+        int after = 0;
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+          pos4[q] = -1;
+          if (cnts[q] > 0) {
+            const int pos = base + after++;
+            QNode cb;
+            cb.x0 = (q & 1) ? md.x : nd.x0;
+            cb.x1 = (q & 1) ? nd.x1 : md.x;
+            cb.y0 = (q & 2) ? md.y : nd.y0;
+            cb.y1 = (q & 2) ? nd.y1 : md.y;
+            int mx, my;
+            halves(cb, &mx, &my);
+            nB[pos] = cb;
+            kB[pos] = cnts[q];
+            qB[pos] = j * 4 + q;
+            mB[pos] = make_int2(mx, my);
+            cB[pos] = make_int4(0, 0, 0, 0);
+            expand += cnts[q] > 1;
+            pos4[q] = pos;
+          }
+        }
+        cA[n] = make_int4(pos4[0], pos4[1], pos4[2], pos4[3]);
+      };
+      int m = 0, T = 0;
+      if (!sorted_phase) {
+        // breadth round (see the generic path): packed scan value per node,
+        // candidates-before (low half) and sum of (children - 1) over them (high half)
+        int sum = 0;
+        for (int n = nb; n < ne; ++n) {
+          const int v = kA[n] > 1 ? ((nonempty(cA[n]) - 1) << 16) | 1 : 0;
+          tA[n] = v;
+          sum += v;
+        }
+        const int x = wave_incl_scan_dpp(sum);
+        if (lane == 63) s_wave[wv] = x;
+        lds_sync();
+        int run = x - sum;
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+          if (i < wv) run += s_wave[i];
+        int splits = 0, tmax = 0;
+        for (int n = nb; n < ne; ++n) {
+          const int v = tA[n], E = run >> 16, C = run & 0xFFFF;
+          int j = -1;
+          if (v && size + E < N) {
+            j = C;
+            ++splits;
+            tmax = max(tmax, E + C + nonempty(cA[n]));
+          }
+          rank[n] = j;
+          tA[n] = run;
+          run += v;
+        }
+        splits = wave_sum_dpp(splits);
+        tmax = INT_MAX - wave_min_dpp(INT_MAX - tmax);
+        if (lane == 0) {
+          s_wave[16 + wv] = splits;
+          s_wave[32 + wv] = tmax;
+        }
+        lds_sync();
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+          m += s_wave[16 + i];
+          T = max(T, s_wave[32 + i]);
+        }
+        ph(1);
+        for (int n = nb; n < ne; ++n) {
+          const int j = rank[n], v = tA[n];
+          if (j < 0) place_kept(n, T + n - min(v & 0xFFFF, m));
+          else place_split(n, j, T - ((v >> 16) + (v & 0xFFFF) + nonempty(cA[n])));
+        }
+      } else {
+        // sorted round: candidates by (size, creation) descending, each
+        // counting the larger keys (keys are distinct)
+        unsigned long long* s_key = (unsigned long long*)nB;  // free until the table step
+        for (int i = tid; i < size; i += kQtThreads) {
+          s_key[i] = kA[i] > 1
+                         ? ((unsigned long long)kA[i] << 40) | ((unsigned long long)qA[i] << 16) | (unsigned long long)i
+                         : 0ull;
+          s_sort[i] = 0;
+          rank[i] = -1;
+        }
+        lds_sync();
+        int cands = 0;
+        for (int i = tid; i < size; i += kQtThreads) {
+          const unsigned long long ki = s_key[i];
+          if (ki) {
+            int r = 0, j = 0;
+            for (; j + 8 <= size; j += 8) {  // eight broadcast keys in flight
+              unsigned long long v[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) v[u] = s_key[j + u];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) r += v[u] > ki ? 1 : 0;
+            }
+            for (; j < size; ++j) r += s_key[j] > ki ? 1 : 0;
+            s_sort[r] = ki;
+            ++cands;
+          }
+        }
+        cands = wave_sum_dpp(cands);
+        if (lane == 0) s_wave[16 + wv] = cands;
+        lds_sync();
+        int ncand = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) ncand += s_wave[16 + i];
+        for (int j = tid; j < ncand; j += kQtThreads) tA[j] = nonempty(cA[(int)(s_sort[j] & 0xFFFF)]) - 1;
+        lds_sync();
+        block_scan_excl<kQtThreads, true>(tA, ncand, s_tmp);  // tA[j] = children - 1 summed over ranks < j
+        // split ranks: the prefix with size + tA[j] < N
+        int splits = 0;
+        for (int j = tid; j < ncand; j += kQtThreads) {
+          if (size + tA[j] < N) {
+            const int n = (int)(s_sort[j] & 0xFFFF);
+            rank[n] = j;
+            ord[j] = n;
+            ++splits;
+          }
+        }
+        splits = wave_sum_dpp(splits);
+        if (lane == 0) s_wave[32 + wv] = splits;
+        lds_sync();
+#pragma unroll
+        for (int i = 0; i < NW; ++i) m += s_wave[32 + i];
+        // children block size: sum over the split ranks of their children
+        if (m > 0) T = tA[m - 1] + nonempty(cA[ord[m - 1]]) - 1 + m;
+        ph(4);
+        // tie-straddle exposure (generic path)
+        if (m > 0 && m < ncand && (s_sort[m - 1] >> 40) == (s_sort[m] >> 40)) {
+          const unsigned long long sz = s_sort[m - 1] >> 40;
+          for (int j = tid; j < ncand; j += kQtThreads) {
+            const unsigned long long key = s_sort[j];
+            if ((key >> 40) == sz) {
+              atomicAdd(&s_var[7], 1);
+              atomicAdd(&s_var[8], j < m ? nonempty(cA[(int)(key & 0xFFFF)]) : 1);
+            }
+          }
+          if (tid == 0) s_var[6] += 1;
+        }
+        for (int n = tid; n < size; n += kQtThreads) tB[n] = rank[n] < 0 ? 1 : 0;
+        lds_sync();
+        block_scan_excl<kQtThreads, true>(tB, size, s_tmp);  // kept nodes keep their order after the children
+        for (int n = nb; n < ne; ++n) {
+          const int j = rank[n];
+          if (j < 0) place_kept(n, T + tB[n]);
+          else place_split(n, j, T - (tA[j] + j + nonempty(cA[n])));
+        }
+      }
+      expand = wave_sum_dpp(expand);
+      if (lane == 0) s_wave[48 + wv] = expand;
+      lds_sync();
+      ph(2);
+      int nExp = 0;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) nExp += s_wave[48 + i];
+      const int newSize = T + (size - m);
+      // finish when the list reached N or a round changed nothing (src/ORBextractor.cc:1011, 1093)
+      const bool finish = newSize >= N || newSize == size;
+      // re-home the keys, counting them into the next list's children
+      for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
+        uint32_t kk[4];
+        int pk[4], nn[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool in = k0 + u * kQtThreads < K;
+          kk[u] = in ? keys[k0 + u * kQtThreads] : 0u;
+          pk[u] = in ? knode[k0 + u * kQtThreads] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int n = pk[u] >> 2;
+          nn[u] = rank[n] < 0 ? tB[n] : ((const int*)&cA[n])[pk[u] & 3];
+        }
+        if (!finish) {
+          int2 md[4];
+          int big[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            big[u] = kB[nn[u]];
+            md[u] = mB[nn[u]];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (k0 + u * kQtThreads < K) {
+              const int q = (key_x(kk[u]) >= md[u].x ? 1 : 0) + (key_y(kk[u]) >= md[u].y ? 2 : 0);
+              if (big[u] > 1) atomicAdd(((int*)&cB[nn[u]]) + q, 1);
+              knode[k0 + u * kQtThreads] = (uint16_t)((nn[u] << 2) | q);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (k0 + u * kQtThreads < K) knode[k0 + u * kQtThreads] = (uint16_t)(nn[u] << 2);
+        }
+      }
+      // the breadth phase ends once one more full round would overshoot N (:1015)
+      if (!finish && !sorted_phase && newSize + 3 * nExp > N) sorted_phase = true;
+      size = newSize;
+      {
+        QNode* t0 = nA; nA = nB; nB = t0;
+        int* t1 = kA; kA = kB; kB = t1;
+        int* t2 = qA; qA = qB; qB = t2;
+        int4* t3 = cA; cA = cB; cB = t3;
+        int2* t4 = mA; mA = mB; mB = t4;
+      }
+      lds_sync();
+      ph(3);
+      dbg_rounds++;
+      if (finish) break;
+      if (round == 63 && tid == 0) atomicOr(err, 2);
+    }
+    const unsigned long long t_rounds = __builtin_amdgcn_s_memtime();
+    // ---- keep the best key per node: max FAST score, first in key order
+    for (int n = tid; n < size; n += kQtThreads) s_sort[n] = 0;
+    lds_sync();
+    for (int k = tid; k < K; k += kQtThreads)
+      atomicMax(&s_sort[knode[k] >> 2],
+                ((unsigned long long)key_score(keys[k]) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)k));
+    lds_sync();
+    for (int n = tid; n < size && n < g.kcap; n += kQtThreads)
+      out[n] = keys[0xFFFFFFFFu - (uint32_t)(s_sort[n] & 0xFFFFFFFFull)];
+    write_tail(size, t_rounds);
+    return;
   }
+  for (int k = tid; k < K; k += kQtThreads) {
+    const int r = (int)__fdiv_rn((float)key_x(keys[k]), g.hX);  // vpIniNodes[kp.pt.x/hX]
+    knode[k] = (uint16_t)r;
+    atomicAdd(&rootCnt[r], 1);
+  }
+  __syncthreads();
+  build_roots(false);
   __syncthreads();
   for (int k = tid; k < K; k += kQtThreads) knode[k] = (uint16_t)rootCnt[knode[k]];
   __syncthreads();
 
-  const int N = g.N;
   // node tables ping-pong between rounds (A = this round's list, B = the next)
   QNode* nA = nodeA;
   QNode* nB = nodeB;
@@ -446,42 +809,17 @@ __global__ __launch_bounds__(kQtThreads) void quadtree_kernel(ExtractParams P, c
     atomicMax(&s_sort[knode[k]], v);
   }
   __syncthreads();
-  uint32_t* out = qkeys + (long long)f * P.kp_per_frame + g.kbase;
   for (int n = tid; n < size && n < g.kcap; n += kQtThreads)
     out[n] = keys[0xFFFFFFFFu - (uint32_t)(s_sort[n] & 0xFFFFFFFFull)];
-  if (tid == 0) {
-    qcounts[f * P.L + l] = min(size, g.kcap);
-    int* qt = qties + ((long long)f * P.L + l) * 4;
-    qt[0] = s_var[6];
-    qt[1] = s_var[7];
-    qt[2] = s_var[8];
-    qt[3] = 0;
-    if (size > g.kcap) atomicOr(err, 4);
-  }
-  if (dbg && tid == 0) {  // diagnostics only (ORBX_QT_PROF=1)
-    int* d = dbg + (blockIdx.y * gridDim.x + blockIdx.x) * 8;
-    d[0] = (int)(t_rounds - t_begin);
-    d[1] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
-    d[2] = dbg_rounds;
-    d[3] = dbg_sorted;
-    d[4] = K;
-    d[5] = size;
-    d[6] = (int)(t_scan - t_begin);
-    d[7] = (int)(t_gather - t_begin);
-    int* dp = dbg + gridDim.x * gridDim.y * 8 + (blockIdx.y * gridDim.x + blockIdx.x) * 8;
-    dp[0] = (int)dbg_p0;
-    dp[1] = (int)dbg_p1;
-    dp[2] = (int)dbg_p2;
-    dp[3] = (int)dbg_p3;
-    dp[4] = (int)dbg_p4;
-  }
+  write_tail(size, t_rounds);
 }
 
 size_t quadtree_lds_bytes(const ExtractParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t MN = P.maxnodes, SN = P.sortn;
   return r16(8 * SN) + 2 * r16(sizeof(QNode) * MN) + 4 * r16(4 * MN) + r16(16 * MN) + 2 * r16(4 * (MN + 1)) +
-         2 * r16(4 * MN) + 2 * r16(4 * (P.max_cells_level + 1)) + r16(8 * MN) + 2 * r16(64) +
+         2 * r16(4 * MN) + 2 * r16(4 * (P.max_cells_level + 1)) + r16(8 * MN) + r16(16 * MN) + r16(8 * MN) + 256 +
+         2 * r16(64) +
          r16(4ull * P.kcap_lds) + r16(2ull * P.kcap_lds);
 }
 

@@ -123,6 +123,20 @@ def test_dense_noise_uses_global_quadtree_path(pkg, O):
     assert_same(kp, desc, rkp, rdesc)
 
 
+def test_generic_quadtree_rounds(pkg, O, monkeypatch):
+    # the generic quadtree rounds (plans whose node table does not fit the lean
+    # rounds' 16-bit packing) on a normal frame and on dense noise
+    from orb_slam_cuda_amd.synth import synth_frame
+    monkeypatch.setenv("ORBX_QT_GENERIC", "1")
+    W, H = 1241, 376
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H)
+    rng = np.random.default_rng(5)
+    for img in (synth_frame(33, W, H), rng.integers(0, 256, size=(H, W), dtype=np.uint8)):
+        kp, desc = ext(img)
+        rkp, rdesc = O.extract(oracle_cfg(O, 2000, W, H), img)
+        assert_same(kp, desc, rkp, rdesc)
+
+
 def test_edge_images(pkg, O):
     W, H = 640, 360
     ext = pkg.ORBextractor(1000, 1.2, 8, 20, 7, W, H)
