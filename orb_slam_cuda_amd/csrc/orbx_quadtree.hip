@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
   int2* s_mid = (int2*)take(8ull * MN);  // halves() of every node of this round
   int4* cc2 = (int4*)take(16ull * MN);    // register-resident rounds: next list's child counts
   int2* s_mid2 = (int2*)take(8ull * MN);  // ... and its halves()
-  int* s_wave = (int*)take(256);          // ... per-wave partials (scan totals, splits, T, expandable)
+  int* s_wave = (int*)take(512);          // ... per-wave partials (scan totals, counts, sums; 16 each)
   int* s_tmp = (int*)take(64);
   int* s_var = (int*)take(64);
   uint32_t* lkeys = (uint32_t*)take(4ull * P.kcap_lds);
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
       dp[4] = (int)dbg_p4;
     }
   };
-  if (P.qt_lean) {
+  if (P.qt_lean && K < 65536) {  // sort keys pack a node's key count in 16 bits
     // ---- lean rounds. A key's node and its quadrant in that node are one
     // packed 16-bit entry (node << 2 | q); the next round's child counts are
     // added while the keys are re-homed, and the node-order scan runs over
@@ -231,6 +231,8 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
     // four keys per thread at a time so that their LDS latencies overlap.
     const int lane = tid & 63, wv = tid >> 6;
     constexpr int NW = kQtThreads / 64;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    uint32_t* s_key = (uint32_t*)ord;  // sorted rounds: size << 16 | creation per node
     for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
       uint32_t kk[4];
 #pragma unroll
@@ -298,6 +300,7 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
         mB[pos] = mA[n];
         cB[pos] = make_int4(0, 0, 0, 0);
         tB[n] = pos;
+        rank[n] = -1;  // the re-homing reads kept nodes' positions from tB (sorted rounds keep ranked candidates too)
       };
       auto place_split = [&](int n, int j, int base) {
         const int4 c = cA[n];
@@ -378,33 +381,33 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
           else place_split(n, j, T - ((v >> 16) + (v & 0xFFFF) + nonempty(cA[n])));
         }
       } else {
-        // sorted round: candidates by (size, creation) descending, each
-        // counting the larger keys (keys are distinct)
-        unsigned long long* s_key = (unsigned long long*)nB;  // free until the table step
-        for (int i = tid; i < size; i += kQtThreads) {
-          s_key[i] = kA[i] > 1
-                         ? ((unsigned long long)kA[i] << 40) | ((unsigned long long)qA[i] << 16) | (unsigned long long)i
-                         : 0ull;
-          s_sort[i] = 0;
-          rank[i] = -1;
-        }
-        lds_sync();
+        // sorted round: the candidates (nodes with > 1 key; after a round
+        // that did not finish, all of them children of that round) by (size,
+        // creation) descending. s_key, filled while the keys were re-homed,
+        // holds size << 16 | creation, distinct among the candidates, 0 for
+        // the others; each candidate counts the larger keys.
+        int* s_pos = (int*)s_sort;  // sorted rank -> node
         int cands = 0;
         for (int i = tid; i < size; i += kQtThreads) {
-          const unsigned long long ki = s_key[i];
+          const uint32_t ki = s_key[i];
+          int r = -1;
           if (ki) {
-            int r = 0, j = 0;
-            for (; j + 8 <= size; j += 8) {  // eight broadcast keys in flight
-              unsigned long long v[8];
+            r = 0;
+            int j = 0;
+            for (; j + 16 <= size; j += 16) {  // sixteen broadcast keys in flight
+              u32x4 v[4];
 #pragma unroll
-              for (int u = 0; u < 8; ++u) v[u] = s_key[j + u];
+              for (int u = 0; u < 4; ++u) v[u] = *(const u32x4*)(s_key + j + 4 * u);
 #pragma unroll
-              for (int u = 0; u < 8; ++u) r += v[u] > ki ? 1 : 0;
+              for (int u = 0; u < 4; ++u)
+                r += (v[u].x > ki ? 1 : 0) + (v[u].y > ki ? 1 : 0) + (v[u].z > ki ? 1 : 0) + (v[u].w > ki ? 1 : 0);
             }
             for (; j < size; ++j) r += s_key[j] > ki ? 1 : 0;
-            s_sort[r] = ki;
+            s_pos[r] = i;
+            tA[r] = nonempty(cA[i]) - 1;
             ++cands;
           }
+          rank[i] = r;
         }
         cands = wave_sum_dpp(cands);
         if (lane == 0) s_wave[16 + wv] = cands;
@@ -412,46 +415,68 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
         int ncand = 0;
 #pragma unroll
         for (int i = 0; i < NW; ++i) ncand += s_wave[16 + i];
-        for (int j = tid; j < ncand; j += kQtThreads) tA[j] = nonempty(cA[(int)(s_sort[j] & 0xFFFF)]) - 1;
+        // split ranks: the prefix of ranks j with size + E_j < N, E_j = sum
+        // of (children - 1) over the ranks before j (per-thread rank chunks)
+        const int cper = (ncand + kQtThreads - 1) / kQtThreads;
+        const int cb = min(tid * cper, ncand), ce = min(cb + cper, ncand);
+        int csum = 0;
+        for (int j = cb; j < ce; ++j) csum += tA[j];
+        const int cx = wave_incl_scan_dpp(csum);
+        if (lane == 63) s_wave[wv] = cx;
         lds_sync();
-        block_scan_excl<kQtThreads, true>(tA, ncand, s_tmp);  // tA[j] = children - 1 summed over ranks < j
-        // split ranks: the prefix with size + tA[j] < N
-        int splits = 0;
-        for (int j = tid; j < ncand; j += kQtThreads) {
-          if (size + tA[j] < N) {
-            const int n = (int)(s_sort[j] & 0xFFFF);
-            rank[n] = j;
-            ord[j] = n;
+        int run = cx - csum;
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+          if (i < wv) run += s_wave[i];
+        int splits = 0, tsum = 0;
+        for (int j = cb; j < ce; ++j) {
+          const int v = tA[j];
+          if (size + run < N) {
             ++splits;
+            tsum += v + 1;
           }
+          tA[j] = run;
+          run += v;
         }
         splits = wave_sum_dpp(splits);
-        if (lane == 0) s_wave[32 + wv] = splits;
+        tsum = wave_sum_dpp(tsum);
+        if (lane == 0) {
+          s_wave[32 + wv] = splits;
+          s_wave[64 + wv] = tsum;
+        }
         lds_sync();
 #pragma unroll
-        for (int i = 0; i < NW; ++i) m += s_wave[32 + i];
-        // children block size: sum over the split ranks of their children
-        if (m > 0) T = tA[m - 1] + nonempty(cA[ord[m - 1]]) - 1 + m;
+        for (int i = 0; i < NW; ++i) {
+          m += s_wave[32 + i];
+          T += s_wave[64 + i];  // children block: the split ranks' children
+        }
         ph(4);
         // tie-straddle exposure (generic path)
-        if (m > 0 && m < ncand && (s_sort[m - 1] >> 40) == (s_sort[m] >> 40)) {
-          const unsigned long long sz = s_sort[m - 1] >> 40;
+        if (m > 0 && m < ncand && (s_key[s_pos[m - 1]] >> 16) == (s_key[s_pos[m]] >> 16)) {
+          const uint32_t sz = s_key[s_pos[m - 1]] >> 16;
           for (int j = tid; j < ncand; j += kQtThreads) {
-            const unsigned long long key = s_sort[j];
-            if ((key >> 40) == sz) {
+            const int n = s_pos[j];
+            if ((s_key[n] >> 16) == sz) {
               atomicAdd(&s_var[7], 1);
-              atomicAdd(&s_var[8], j < m ? nonempty(cA[(int)(key & 0xFFFF)]) : 1);
+              atomicAdd(&s_var[8], j < m ? nonempty(cA[n]) : 1);
             }
           }
           if (tid == 0) s_var[6] += 1;
         }
-        for (int n = tid; n < size; n += kQtThreads) tB[n] = rank[n] < 0 ? 1 : 0;
+        // kept nodes keep their list order after the children block
+        int kept = 0;
+        for (int n = nb; n < ne; ++n) kept += (rank[n] >= 0 && rank[n] < m) ? 0 : 1;
+        const int kx = wave_incl_scan_dpp(kept);
+        if (lane == 63) s_wave[80 + wv] = kx;
         lds_sync();
-        block_scan_excl<kQtThreads, true>(tB, size, s_tmp);  // kept nodes keep their order after the children
+        int kpos = T + kx - kept;
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+          if (i < wv) kpos += s_wave[80 + i];
         for (int n = nb; n < ne; ++n) {
           const int j = rank[n];
-          if (j < 0) place_kept(n, T + tB[n]);
-          else place_split(n, j, T - (tA[j] + j + nonempty(cA[n])));
+          if (j >= 0 && j < m) place_split(n, j, T - (tA[j] + j + nonempty(cA[n])));
+          else place_kept(n, kpos++);
         }
       }
       expand = wave_sum_dpp(expand);
@@ -503,6 +528,8 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
       }
       // the breadth phase ends once one more full round would overshoot N (:1015)
       if (!finish && !sorted_phase && newSize + 3 * nExp > N) sorted_phase = true;
+      if (!finish && sorted_phase)  // the next round's sort keys (the new list is kB, qB)
+        for (int i = tid; i < newSize; i += kQtThreads) s_key[i] = kB[i] > 1 ? ((uint32_t)kB[i] << 16) | (uint32_t)qB[i] : 0u;
       size = newSize;
       {
         QNode* t0 = nA; nA = nB; nB = t0;
@@ -525,8 +552,11 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
       atomicMax(&s_sort[knode[k] >> 2],
                 ((unsigned long long)key_score(keys[k]) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)k));
     lds_sync();
-    for (int n = tid; n < size && n < g.kcap; n += kQtThreads)
-      out[n] = keys[0xFFFFFFFFu - (uint32_t)(s_sort[n] & 0xFFFFFFFFull)];
+    for (int n = tid; n < size && n < g.kcap; n += kQtThreads) {
+      const unsigned long long b = s_sort[n];
+      if (b) out[n] = keys[0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull)];
+      else atomicOr(err, 8);  // a node without keys: a broken list, reported instead of read past the keys
+    }
     write_tail(size, t_rounds);
     return;
   }
@@ -809,8 +839,11 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
     atomicMax(&s_sort[knode[k]], v);
   }
   __syncthreads();
-  for (int n = tid; n < size && n < g.kcap; n += kQtThreads)
-    out[n] = keys[0xFFFFFFFFu - (uint32_t)(s_sort[n] & 0xFFFFFFFFull)];
+  for (int n = tid; n < size && n < g.kcap; n += kQtThreads) {
+    const unsigned long long b = s_sort[n];
+    if (b) out[n] = keys[0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull)];
+    else atomicOr(err, 8);  // a node without keys: a broken list, reported instead of read past the keys
+  }
   write_tail(size, t_rounds);
 }
 
@@ -818,7 +851,7 @@ size_t quadtree_lds_bytes(const ExtractParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t MN = P.maxnodes, SN = P.sortn;
   return r16(8 * SN) + 2 * r16(sizeof(QNode) * MN) + 4 * r16(4 * MN) + r16(16 * MN) + 2 * r16(4 * (MN + 1)) +
-         2 * r16(4 * MN) + 2 * r16(4 * (P.max_cells_level + 1)) + r16(8 * MN) + r16(16 * MN) + r16(8 * MN) + 256 +
+         2 * r16(4 * MN) + 2 * r16(4 * (P.max_cells_level + 1)) + r16(8 * MN) + r16(16 * MN) + r16(8 * MN) + 512 +
          2 * r16(64) +
          r16(4ull * P.kcap_lds) + r16(2ull * P.kcap_lds);
 }
