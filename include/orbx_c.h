@@ -170,7 +170,8 @@ int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out,
  * that come from that group. Synchronous (waits for the device). */
 int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out);
 /* Device status word of the handle's kernels since the last call (0 = ok;
- * bit 1: quadtree round limit, bit 2: quadtree output over capacity).
+ * bit 1: quadtree round limit, bit 2: quadtree output over capacity, bit 3:
+ * a quadtree node without keys, an internal invariant, never expected).
  * Waits for the device; `reset` != 0 clears it. orbx_extract checks and clears
  * it itself; batch callers (orbx_extract_batch) poll it here. */
 int orbx_get_status(orbx_handle h, int reset, int* status);
