@@ -9,7 +9,7 @@
 // stopping as soon as the list reaches N. Each node finally keeps its
 // max-response key (first in key order on ties).
 //
-// Data-parallel restatement (one 256-thread workgroup per frame x level):
+// Data-parallel restatement (one 512-thread workgroup per frame x level):
 // the list is a node table indexed by list position; keys never move, each
 // key carries its node index. A round is "split a prefix of the candidate
 // sequence": candidates = nodes with > 1 key, taken in list order (breadth
@@ -19,6 +19,12 @@
 // The new list is [children of the split nodes, last split first, each as
 // n4 n3 n2 n1] followed by the untouched nodes in their old order, which is
 // exactly what the reference's push_front/erase sequence produces.
+//
+// Two implementations of the rounds share the key gather and the output:
+// the lean rounds (every plan whose node table fits 16-bit packing and
+// levels with < 65536 keys) and the generic rounds (the fallback, and the
+// round-1 form, ORBX_QT_GENERIC=1 forces it for tests). DESIGN.md section 6
+// has the barrier counts and timings of both.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
