@@ -459,8 +459,11 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   }
   {
     // keep the LDS footprint at 80 KiB so two quadtree blocks fit one CU
+#ifndef ORBX_QT_LDS_KB
+#define ORBX_QT_LDS_KB 80
+#endif
     const size_t base = quadtree_lds_bytes(P);
-    const size_t budget = 80 * 1024;
+    const size_t budget = ORBX_QT_LDS_KB * 1024;
     P.kcap_lds = base < budget ? (int)((budget - base) / 6) & ~15 : 0;
   }
   pl.P = P;
