@@ -86,14 +86,17 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
 #pragma unroll
   for (int k = 0; k < kIcPer; ++k) ic_v[k] = c_ic_coef[min(tid + k * kObThreads, 16 * 24 - 1)];
 
-  // level of this half-wave's slot (kbase is uniform: scalar compares)
-  int l = 0;
+  // levels of the wave's two half-wave slots, in scalar code: the slots are
+  // uniform per half (slot = bx * kObKps + 2 * wave + half)
+  const int slotA = bx * kObKps + 2 * __builtin_amdgcn_readfirstlane(tid >> 6), slotB = slotA + 1;
+  int lA = 0, lB = 0;
 #pragma unroll
-  for (int i = 1; i < kMaxLevels; ++i)
-    if (i < P.L && slot >= P.lv[i].kbase) l = i;
-  // the level fields of both half-waves by uniform index, selected per half
-  const int lA = __builtin_amdgcn_readlane(l, 0), lB = __builtin_amdgcn_readlane(l, 32);
+  for (int i = 1; i < kMaxLevels; ++i) {
+    if (i < P.L && slotA >= P.lv[i].kbase) lA = i;
+    if (i < P.L && slotB >= P.lv[i].kbase) lB = i;
+  }
   const bool hiHalf = (tid & 32) != 0;
+  const int l = hiHalf ? lB : lA;
   const LevelGeom& gA = P.lv[lA];
   const LevelGeom& gB = P.lv[lB];
 #define OB_PICK(a, b) (hiHalf ? (b) : (a))
@@ -106,14 +109,18 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   const uint8_t* lbase = OB_PICK(lp.base[lA], lp.base[lB]);
   const long long lfstride = OB_PICK(lp.fstride[lA], lp.fstride[lB]);
 #undef OB_PICK
-  int cnt_l = 0, before = 0, tot = 0;
+  // keypoints of the levels before each half's level, its own count, the total (scalar)
+  int cntA = 0, cntB = 0, beforeA = 0, beforeB = 0, tot = 0;
 #pragma unroll
   for (int i = 0; i < kMaxLevels; ++i) {
     const int ci = i < P.L ? c[i] : 0;
-    if (i == l) cnt_l = ci;
-    if (i < l) before += ci;
+    if (i == lA) cntA = ci;
+    if (i == lB) cntB = ci;
+    if (i < lA) beforeA += ci;
+    if (i < lB) beforeB += ci;
     tot += ci;
   }
+  const int cnt_l = hiHalf ? cntB : cntA, before = hiHalf ? beforeB : beforeA;
   if (bx == 0 && tid == 0) out_counts[f] = tot;
 
   // ---- the keypoint of this half-wave
