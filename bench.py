@@ -67,11 +67,8 @@ MFMA_FP4_PEAK_TFLOPS = 10066.3
 # VALU lane-op peak: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (the top-2 update costs 2 lane-ops per pair)
 VALU_PEAK_TOPS = 78.6
 STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_top2", "search_init"]
-# the fused path (orbx_front_path): event pairs 0-1 bracket the pyramid, 1-2 nothing, 2-3
-# front_tile_kernel (blur + FAST + NMS + per-cell threshold choice per tile)
-FRONT_STAGES = ["pyramid", None, "blur_fast", "quadtree", "orient_brief", "hamming_top2", "search_init"]
 KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
-           "blur_fast": "front_tile_kernel", "bow_match": "search_bow_kernel<256>",
+           "bow_match": "search_bow_kernel<256>",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
            "hamming_top2": "hamming_top2_mfma_kernel", "search_init": "search_init_kernel"}
 KP, DS = 28, 32  # bytes of one orbx_kp (cv::KeyPoint) and one descriptor
@@ -110,8 +107,6 @@ def algorithmic_bytes(W, H, nkp):
         "fast_grid": sum(P),                                           # read every level once
         "pyr_fast_pass": P[0] + sum(P[:7]) + sum(P[1:]) + sum(P),      # BASELINE.md B_pf
         "orient_brief": nkp * (2 * 31 * 31 + 60),                      # patch gathers + outputs
-        # fused blur + FAST tiles: read every level once, write its blur
-        "blur_fast": 2 * sum(P),
     }
 
 
@@ -151,8 +146,44 @@ def parse_args(argv=None):
     ap.add_argument("--no-host-stream", action="store_true", help="skip the host-streamed throughput leg")
     ap.add_argument("--host-steps", type=int, default=30, help="timed steps of the host-streamed leg")
     ap.add_argument("--spawn", action="store_true", help="use the worker launcher even for --gpus 1")
+    ap.add_argument("--allow-diag", action="store_true",
+                    help="run even with diagnostic ORBX_* variables set (phase clocks, library variants); "
+                         "the line then carries them and is not a valid measurement")
     ap.add_argument("--stub-worker", action="store_true", help=argparse.SUPPRESS)  # launcher tests (CPU)
     return ap.parse_args(argv)
+
+
+# ORBX_* variables the library reads (INTEGRATION.md "Environment variables").
+# Tuning: select among bit-exact code paths; allowed, and stamped into the line.
+ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_PYR_PLAN", "ORBX_QT_GENERIC",
+              "ORBX_INIT_LDS_KB", "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS"}
+# Diagnostics: phase clocks synchronise after every launch, *_STOP / FAST_TWICE
+# skip or repeat work (they only act in -DORBX_DIAG builds), ORBX_LIB_VARIANT
+# loads an A/B build of the library. A timed region under any of them is not
+# the product's: refused unless --allow-diag.
+ENV_DIAG = {"ORBX_LIB_VARIANT", "ORBX_FAST_TWICE", "ORBX_INIT_STOP", "ORBX_STEREO_STOP", "ORBX_VOC_STOP",
+            "ORBX_FAST_PROF", "ORBX_PYR_PROF", "ORBX_QT_PROF", "ORBX_INIT_PROF", "ORBX_BOW_PROF", "ORBX_PROJ_PROF",
+            }
+
+
+def audit_env(allow_diag: bool, environ=None) -> dict:
+    """The ORBX_* variables set for this run (stamped into the JSON line as
+    "orbx_env"). Diagnostic or unknown ones end the run unless allow_diag."""
+    environ = os.environ if environ is None else environ
+    env = {k: v for k, v in sorted(environ.items()) if k.startswith("ORBX_")}
+    bad = sorted(k for k in env if k not in ENV_TUNING)
+    if bad and not allow_diag:
+        raise SystemExit("bench.py: refusing to measure with diagnostic or unknown ORBX_* variables set: "
+                         + ", ".join(f"{k}={env[k]}" for k in bad) + " (pass --allow-diag to run anyway; "
+                         "the line is then stamped and is not a measurement of the product)")
+    return env
+
+
+def library_audit(L) -> dict:
+    """The loaded liborbx build: a -DORBX_DIAG build (orbx_version says 'diag') may skip work."""
+    v = L.orbx_version()
+    v = v.decode() if isinstance(v, bytes) else str(v)
+    return {"version": v, "diag_build": "diag" in v}
 
 
 # --------------------------------------------------------------------------- launcher
@@ -165,10 +196,15 @@ def _free_port() -> int:
 
 
 def visible_gpus() -> int:
-    """GPUs this node exposes, counted without initialising HIP in this process
-    (torch.cuda.device_count() does not initialise the runtime on this image)."""
-    import torch
-    return int(torch.cuda.device_count())
+    """GPUs this node exposes, counted in a short-lived child process so that
+    this (launcher) process never loads the HIP runtime before it spawns the
+    workers (tests/test_bench_launcher.py checks its memory map)."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        raise SystemExit(f"bench.py: could not count GPUs: {r.stderr[-500:]}")
+    return int(r.stdout.strip().splitlines()[-1])
 
 
 def _worker_entry(argv, rank, world, port):
@@ -207,6 +243,7 @@ def main(argv=None):
     args = parse_args(argv)
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
+    audit_env(args.allow_diag)  # before any worker starts
     if "RANK" not in os.environ and (args.gpus > 1 or args.spawn):
         code = launch(args, argv)
         if code:
@@ -239,6 +276,11 @@ def worker(args):
             return run_stub(args, rank, world, dist)
         from orb_slam_cuda_amd import _lib
         L = _lib.lib()
+        lib_info = library_audit(L)
+        if lib_info["diag_build"] and not args.allow_diag:
+            raise SystemExit(f"bench.py: refusing to measure a diagnostics build of liborbx ({lib_info['version']}); "
+                             "rebuild without -DORBX_DIAG or pass --allow-diag")
+        args.audit = {"orbx_env": audit_env(args.allow_diag), "library": lib_info}
         ndev = _lib.device_count()
         if local >= ndev:
             raise SystemExit(f"bench.py: rank {rank} needs device {local}, only {ndev} visible")
@@ -267,7 +309,8 @@ def run_stub(args, rank, world, dist):
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(agg["value"], 2), "unit": "frames/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "per_rank_frames_per_s": agg["per_rank"],
-                          "frames_total": agg["frames"], "data": "stub (no GPU work)"}), flush=True)
+                          "frames_total": agg["frames"], "data": "stub (no GPU work)",
+                          "orbx_env": audit_env(args.allow_diag)}), flush=True)
 
 
 # --------------------------------------------------------------------------- mono pipeline
@@ -562,9 +605,8 @@ def run_mono(args, cfg, rank, world, local, dist):
     BS, S, cap = pipe.BS, pipe.S, pipe.cap
     timed = pipe.evsets[args.warmup * SUB:]
     ev_ms = timed[0][0].elapsed_ms(timed[-1][8])
-    front = pipe.exts[0].front_path
-    names = FRONT_STAGES if front else STAGES
-    ext_stages = [n for n in names[:5] if n]
+    names = STAGES
+    ext_stages = names[:5]
     STAGES_RUN = ext_stages + (["hamming_top2", "search_init"] if not args.no_match else []) \
         + (["bow_transform"] if (args.bow or args.bow_match) else []) + (["bow_match"] if args.bow_match else [])
     # per-stage average durations over the timed steps (ms per launch-group, BS frames),
@@ -572,8 +614,7 @@ def run_mono(args, cfg, rank, world, local, dist):
     st = {s: 0.0 for s in STAGES_RUN}
     for evs in timed:
         for i, s in enumerate(names[:5]):
-            if s:
-                st[s] += evs[i].elapsed_ms(evs[i + 1])
+            st[s] += evs[i].elapsed_ms(evs[i + 1])
         if args.bow or args.bow_match:
             st["bow_transform"] += evs[9].elapsed_ms(evs[10])
         if args.bow_match:
@@ -597,14 +638,13 @@ def run_mono(args, cfg, rank, world, local, dist):
     extract_ms = sum(st[s] for s in ext_stages)
     dominant = max(STAGES_RUN, key=lambda s: st[s])
     # roofline of the pyramid+FAST pass: the kernels that run it
-    pf_ms = st["pyramid"] + (st["blur_fast"] if front else st["fast_grid"])
+    pf_ms = st["pyramid"] + st["fast_grid"]
     pf_gbs = ab["pyr_fast_pass"] * BS / (pf_ms * 1e-3) / 1e9
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
-                  "orient_brief": ab["orient_brief"], "blur_fast": ab["blur_fast"]}
-    # the roofline kernel: the fused blur + FAST tiles (the longest extraction
-    # kernel), or FAST on the per-stage path (the longest one alone, whose
-    # event time in the pipelined run matches its rocprofv3 average)
-    rk = "blur_fast" if front else "fast_grid"
+                  "orient_brief": ab["orient_brief"]}
+    # the roofline kernel: FAST, the longest extraction kernel alone (its event
+    # time in the pipelined run matches its rocprofv3 average)
+    rk = "fast_grid"
     traffic = pmc_bytes(KERNELS[rk])
     ach = hbm_stages[rk] * BS / (st[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -685,6 +725,7 @@ def run_mono(args, cfg, rank, world, local, dist):
             "keypoints_per_frame": round(nkp_mean, 1),
             "init_matches_per_pair": round(float(nm.mean()), 1),
             "bow_matches_per_pair": bow_nm,
+            **args.audit,
         }
         print(json.dumps(out), flush=True)
 
@@ -922,14 +963,12 @@ def run_stereo(args, cfg, rank, world, local, dist):
         if st["m"].status():
             raise RuntimeError("matcher device status word set")
     timed = evs[args.warmup:]
-    front = sets[0]["eL"].front_path
-    names = FRONT_STAGES if front else STAGES
-    stages = [n for n in names[:5] if n] + ["stereo"]
+    names = STAGES
+    stages = names[:5] + ["stereo"]
     sm = {s: 0.0 for s in stages}
     for ev in timed:
         for i, s in enumerate(names[:5]):
-            if s:
-                sm[s] += ev[i].elapsed_ms(ev[i + 1])
+            sm[s] += ev[i].elapsed_ms(ev[i + 1])
         sm["stereo"] += ev[6].elapsed_ms(ev[7])
     sm = {s: v / args.steps for s, v in sm.items()}
     last = sets[(total - 1) % NSET]
@@ -937,8 +976,8 @@ def run_stereo(args, cfg, rank, world, local, dist):
     nkp = last["n"].download(2 * B, np.int32)
     ab = algorithmic_bytes(W, H, float(nkp.mean()))
     hbm_stages = {"pyramid": ab["pyramid"], "blur": ab["blur"], "fast_grid": ab["fast_grid"],
-                  "orient_brief": ab["orient_brief"], "blur_fast": ab["blur_fast"]}
-    rk = "blur_fast" if front else "fast_grid"
+                  "orient_brief": ab["orient_brief"]}
+    rk = "fast_grid"
     ach = hbm_stages[rk] * B / (sm[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_bytes(KERNELS[rk]),
@@ -963,6 +1002,7 @@ def run_stereo(args, cfg, rank, world, local, dist):
             "stage_ms_per_step": {s: round(v, 4) for s, v in sm.items()},
             "keypoints_per_image": round(float(nkp.mean()), 1),
             "stereo_matches_per_pair": round(float(kept.mean()), 1),
+            **args.audit,
         }
         print(json.dumps(out), flush=True)
 

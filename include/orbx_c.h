@@ -175,12 +175,6 @@ int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out);
  * Waits for the device; `reset` != 0 clears it. orbx_extract checks and clears
  * it itself; batch callers (orbx_extract_batch) poll it here. */
 int orbx_get_status(orbx_handle h, int reset, int* status);
-/* 1 if the handle's plan runs the fused blur + FAST tiles (one pass per
- * (level, FAST cell row, chunk of cells): GaussianBlur, FAST, NMS and the
- * per-cell threshold choice), 0 for the separate blur and per-cell FAST
- * kernels (ORBX_FRONT=0 in the environment, or tiles that do not fit LDS).
- * Both produce identical outputs. */
-int orbx_front_path(orbx_handle h);
 /* The rBRIEF test table the kernels use (bit_pattern_31_,
  * src/ORBextractor.cc:236-494): 1024 ints in the reference's flat order
  * (test i = entries 4i..4i+3 = x0, y0, x1, y1), for pattern_mode
@@ -220,7 +214,12 @@ int orbm_destroy(orbm_handle m);
 /* Device status word of the matcher's batched kernels since the last call
  * (0 = ok; bit 8: SearchForInitialization candidate overflow, that pair got
  * no matches; bit 16: orbm_hamming_top2 input over its limits, nA[p] > a_cap
- * or nB[p] > 65535, the excess rows / candidates were not searched). Waits
+ * or nB[p] > 65535, the excess rows / candidates were not searched; bit 32:
+ * orbm_search_by_bow_batch saw a count above kp_pitch or a FeatureVector
+ * index outside [0, n), which was skipped). SearchForInitialization's
+ * candidate lists hold every keypoint of each query's window cells (before
+ * the |dx|, |dy| < r test): up to min(max_kps^2, 4M) entries per pair in the
+ * global fallback, past which bit 8 is set. Waits
  * for the device; `reset` != 0 clears it. The synchronous entry points check
  * and clear it themselves.
  *

@@ -105,7 +105,6 @@ def lib() -> C.CDLL:
         L.orbx_get_tie_stats.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         L.orbx_get_status.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
         L.orbx_get_pattern.argtypes = [C.c_int, C.c_void_p]
-        L.orbx_front_path.argtypes = [C.c_void_p]
         L.orbm_get_status.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
         L.orbm_create.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
         L.orbm_destroy.argtypes = [C.c_void_p]

@@ -121,8 +121,6 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
 int launch_quadtree(const ExtractParams& P, const ExtractBuffers& X, int batch, hipStream_t s);
 int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const ExtractBuffers& X, orbx_kp* kps,
                         uint8_t* desc, int* counts, int batch, hipStream_t s);
-int launch_front_tiles(const ExtractParams& P, const LevelPtrs& lp, const ExtractBuffers& X, int batch,
-                       hipStream_t s);
 size_t quadtree_lds_bytes(const ExtractParams& P);
 size_t pyr_band_lds_bytes(const ExtractParams& P);
 const void* pyr_band_kernel_ptr();

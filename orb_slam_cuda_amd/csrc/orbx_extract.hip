@@ -2,10 +2,6 @@
 //
 // For a batch of B frames, all on one stream, no host round trip:
 //   launch_pyramid       (1, or L-1 launches) ComputePyramid        orbx_pyramid.hip
-//   fused path (default when the tiles fit LDS, P.front):
-//   launch_front_tiles   (1)  GaussianBlur 7x7 + per-cell FAST +    orbx_front.hip
-//                             NMS + threshold choice, per tile
-//   per-stage path (ORBX_FRONT=0):
 //   launch_blur          (1)  GaussianBlur 7x7 s=2                  orbx_blur.hip
 //   launch_fast          (1)  per-cell FAST + NMS                   orbx_fast.hip
 //   launch_quadtree      (1)  DistributeOctTree                     orbx_quadtree.hip
@@ -41,14 +37,9 @@ int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_
   rec(0);
   if ((rc = launch_pyramid(Q, lp, X.rtab, batch, stream))) return rc;
   rec(1);
-  if (P.front) {
-    rec(2);
-    if ((rc = launch_front_tiles(Q, lp, X, batch, stream))) return rc;
-  } else {
-    if ((rc = launch_blur(Q, lp, X.blur, batch, stream))) return rc;
-    rec(2);
-    if ((rc = launch_fast(Q, lp, X.cells, X.slots, X.cell_counts, batch, stream))) return rc;
-  }
+  if ((rc = launch_blur(Q, lp, X.blur, batch, stream))) return rc;
+  rec(2);
+  if ((rc = launch_fast(Q, lp, X.cells, X.slots, X.cell_counts, batch, stream))) return rc;
   rec(3);
   if ((rc = launch_quadtree(Q, X, batch, stream))) return rc;
   rec(4);

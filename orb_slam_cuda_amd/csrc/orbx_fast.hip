@@ -22,6 +22,9 @@
 // unless it is empty, and writes the keys in row-major order (the order
 // cv::FAST emits them) into the cell's fixed slot range. Every compaction is
 // an ordered ballot compaction, so row-major order is preserved throughout.
+#if (defined(ORBX_FAST_SAMEROI) || defined(ORBX_FAST_NOLOAD)) && !defined(ORBX_DIAG)
+#error "result-changing diagnostic switches need -DORBX_DIAG"
+#endif
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -454,7 +457,11 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
   if (prof) (void)hipMemsetAsync(dbg, 0, (size_t)nwg * 32, s);
   // diagnostics: ORBX_FAST_TWICE=1 runs the (idempotent) kernel twice, so the
   // second run's phase clocks show FAST on cache-warm levels
+#ifdef ORBX_DIAG  // diagnostics builds only (tools/variant.sh)
   static const int reps = getenv("ORBX_FAST_TWICE") && getenv("ORBX_FAST_TWICE")[0] == '1' ? 2 : 1;
+#else
+  constexpr int reps = 1;
+#endif
   for (int rep = 0; rep < reps; ++rep) {
     if (fast_tight(P))
       hipLaunchKernelGGL(fast_cells_kernel<kRoiTight>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,

@@ -28,8 +28,6 @@ size_t quadtree_lds_bytes(const ExtractParams& P);
 extern const void* quadtree_kernel_ptr();
 size_t pyr_band_lds_bytes(const ExtractParams& P);
 extern const void* pyr_band_kernel_ptr();
-int plan_tiles(ExtractParams& P, std::vector<int4>& tl, int target_px);
-extern const void* front_tile_kernel_ptr();
 }  // namespace orbx
 
 using namespace orbx;
@@ -76,8 +74,7 @@ struct Plan {
   ExtractParams P{};
   std::vector<CellGeom> cells;
   std::vector<int2> rtab;
-  std::vector<int4> tiles;
-  DeviceBuf pyr, blur, tiles_d, rtab_d, cells_d, umax_d, slots, cell_counts, qkeys, qcounts, qties, qscratch, qnscratch,
+  DeviceBuf pyr, blur, rtab_d, cells_d, umax_d, slots, cell_counts, qkeys, qcounts, qties, qscratch, qnscratch,
       err;
 };
 
@@ -312,7 +309,6 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   pl.rtab.clear();
   long long lvl_off = 0;  // level planes [l][B][h][pitch], same offsets in pyramid and blur
   int slot = 0, kbase = 0, maxnodes = 0, maxcells = 0;
-  bool front_geom_ok = true;
   for (int l = 0; l < L; ++l) {
     LevelGeom& g = P.lv[l];
     const float inv = h->inv_scale[l];
@@ -371,21 +367,6 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     }
     g.ncells = (int)pl.cells.size() - g.cell0;
     g.nslots = slot - g.slot0;
-    // detection rectangle = union of the cell bands (empty bands only at the
-    // far edges); cell (i, j)'s band is [dx0 + j wCell, ..) x [dy0 + i hCell, ..)
-    g.dx0 = g.minBX + 3;
-    g.dy0 = g.minBY + 3;
-    g.dx1 = std::min(g.minBX + g.nCols * g.wCell + 3, g.maxBX - 3);
-    g.dy1 = std::min(g.minBY + g.nRows * g.hCell + 3, g.maxBY - 3);
-    for (int c = 0; c < g.ncells; ++c) {  // the fused tiles rely on this band geometry
-      const CellGeom& cg = pl.cells[g.cell0 + c];
-      if (!cg.cap) continue;
-      const int i = c / g.nCols, j = c % g.nCols;
-      const int bx0 = g.dx0 + j * g.wCell, by0 = g.dy0 + i * g.hCell;
-      if (cg.c0 + 3 != bx0 || cg.r0 + 3 != by0 || cg.c1 - 3 != std::min(bx0 + g.wCell, g.dx1) ||
-          cg.r1 - 3 != std::min(by0 + g.hCell, g.dy1))
-        front_geom_ok = false;
-    }
     maxcells = std::max(maxcells, g.ncells);
     // DistributeOctTree (src/ORBextractor.cc:894-898)
     g.N = h->nfeat[l];
@@ -435,14 +416,6 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     }
   }
   plan_band_pyramid(P, pl.rtab);
-  {
-    // the fused blur + FAST tiles are opt-in (ORBX_FRONT=1): identical
-    // outputs, but measured slower than the separate blur and per-cell FAST
-    // kernels (barrier-bound phases at 12-24 waves per CU)
-    const char* e = getenv("ORBX_FRONT");
-    const char* px = getenv("ORBX_TILE_PX");  // tile width experiments
-    P.front = e && e[0] == '1' && front_geom_ok && plan_tiles(P, pl.tiles, px ? atoi(px) : 256) > 0;
-  }
   if (maxnodes > 65000) return fail(ORBX_EINVAL, "nfeatures too large for the quadtree node table");
   P.slots_per_frame = slot;
   P.ncells_total = (int)pl.cells.size();
@@ -474,7 +447,6 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   int rc;
   if ((rc = pl.pyr.alloc((size_t)lvl_off))) return rc;
   if ((rc = pl.blur.alloc((size_t)lvl_off))) return rc;
-  if ((rc = pl.tiles_d.alloc(P.front ? pl.tiles.size() * sizeof(int4) : 0))) return rc;
   if ((rc = pl.rtab_d.alloc(std::max<size_t>(pl.rtab.size(), 1) * sizeof(int2)))) return rc;
   if ((rc = pl.cells_d.alloc(pl.cells.size() * sizeof(CellGeom)))) return rc;
   if ((rc = pl.umax_d.alloc(16 * sizeof(int)))) return rc;
@@ -504,11 +476,6 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     if (raise_lds_limit(pyr_band_kernel_ptr(), mx))
       return fail(ORBX_EDEVICE, "LDS limit of pyr_band_kernel: %s", hipGetErrorString(hipGetLastError()));
   }
-  if (P.front) {
-    HIP_OK(hipMemcpy(pl.tiles_d.p, pl.tiles.data(), pl.tiles.size() * sizeof(int4), hipMemcpyHostToDevice));
-    if (raise_lds_limit(front_tile_kernel_ptr(), (size_t)P.tl_lds))
-      return fail(ORBX_EDEVICE, "LDS limit of front_tile_kernel: %s", hipGetErrorString(hipGetLastError()));
-  }
   if (raise_lds_limit(quadtree_kernel_ptr(), quadtree_lds_bytes(P)))
     return fail(ORBX_EDEVICE, "LDS limit of quadtree_kernel: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
@@ -518,7 +485,6 @@ static ExtractBuffers buffers_of(const Plan& pl) {
   ExtractBuffers X;
   X.pyr = pl.pyr.as<uint8_t>();
   X.blur = pl.blur.as<uint8_t>();
-  X.tiles = pl.tiles_d.as<int4>();
   X.rtab = pl.rtab_d.as<int2>();
   X.cells = pl.cells_d.as<CellGeom>();
   X.umax = pl.umax_d.as<int>();
@@ -592,7 +558,11 @@ int orbx::raise_lds_limit(const void* fn, size_t bytes) {
 extern "C" {
 
 const char* orbx_last_error(void) { return g_err.c_str(); }
-const char* orbx_version(void) { return "orbx 0.1 (gfx950)"; }
+#ifdef ORBX_DIAG
+const char* orbx_version(void) { return "orbx 0.3 (gfx950, diag)"; }
+#else
+const char* orbx_version(void) { return "orbx 0.3 (gfx950)"; }
+#endif
 
 int orbx_create(const orbx_config* cfg, orbx_handle* out) {
   if (!cfg || !out) return fail(ORBX_EINVAL, "null argument");
@@ -791,7 +761,12 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   const int* head = (const int*)h->h_out;
   const int cnt = head[0], err = head[1];
   if (err) {
-    HIP_OK(hipMemset(h->plan.err.p, 0, 16));  // reported once, not on every later call
+    // reported once, not on every later call: cleared in the handle's stream
+    // order (after any batch call still using the plan, before the next one)
+    if (h->ws.before(h->stream)) return fail(ORBX_EDEVICE, "stream wait on the handle's last use failed");
+    HIP_OK(hipMemsetAsync(h->plan.err.p, 0, 16, h->stream));
+    if (h->ws.after(h->stream)) return fail(ORBX_EDEVICE, "event record failed");
+    HIP_OK(hipStreamSynchronize(h->stream));
     return fail(ORBX_ECAPACITY, "device error word 0x%x", err);
   }
   *n = cnt;
@@ -890,7 +865,6 @@ int orbx_get_status(orbx_handle h, int reset, int* status) {
   return ORBX_OK;
 }
 
-int orbx_front_path(orbx_handle h) { return h && h->plan.P.front ? 1 : 0; }
 
 int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out) {
   if (!h || !out) return fail(ORBX_EINVAL, "null argument");

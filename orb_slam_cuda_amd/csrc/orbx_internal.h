@@ -49,8 +49,6 @@ struct LevelGeom {
   float scale;           // mvScaleFactor[l]
   float size;            // (float)(int)(PATCH_SIZE * mvScaleFactor[l])
   int xtab2;             // band pyramid column table: {sx, a0 | a1 << 16}, replicate folded in
-  // fused blur + FAST tiles (orbx_front.hip)
-  int dx0, dx1, dy0, dy1;  // detection rectangle: the union of the FAST cell bands
 };
 
 struct CellGeom {
@@ -84,12 +82,6 @@ struct ExtractParams {
     int cost;  // largest per-band pixel count over the levels (level 0 staged + computed rows)
   } pyr_plan[6];
   int pyr_nplans;
-  // fused blur + FAST path (orbx_front.hip): one workgroup per (frame, level,
-  // FAST cell row, chunk of cells) blurs its tile and runs FAST, NMS and the
-  // per-cell threshold choice from one LDS copy of it
-  int front;                   // 1 = fused tiles planned (else the blur and per-cell FAST kernels)
-  int tl_per_frame;            // tiles per frame
-  int tl_lds;                  // LDS bytes of the largest tile
   int gauss[7];                // 7-tap Gaussian fixed-point kernel (sum 257)
   LevelGeom lv[kMaxLevels];
 };
@@ -151,7 +143,6 @@ struct ExtractBuffers {
   uint16_t* qnode_scratch;
   long long qscratch_per_fl;  // entries per (frame, level)
   int* err;            // device error word
-  const int4* tiles;   // fused path: 2 int4 per tile ({level, cell row, j0, j1}, {owned blur rect})
 };
 
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames,

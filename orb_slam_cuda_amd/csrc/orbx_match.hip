@@ -15,6 +15,9 @@
 // a sequential wavefront as the fallback), SearchByBoW's per-node greedy
 // loops run one wavefront per node with the best/second reduction across
 // lanes.
+#if (defined(ORBX_M_NOMFMA)) && !defined(ORBX_DIAG)
+#error "result-changing diagnostic switches need -DORBX_DIAG"
+#endif
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -525,7 +528,7 @@ template <int NT>
 __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, float nnratio, int check_ori,
                                                         int kf_vs_kf, int G, int* __restrict__ out_all,
                                                         long long out_pitch, int* __restrict__ bin_all,
-                                                        int* __restrict__ hist_all, int* dbg) {
+                                                        int* __restrict__ hist_all, int* __restrict__ err, int* dbg) {
   constexpr int kWaves = NT / 64;
   const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
   auto stamp = [&](int k, int v) {  // diagnostics only (ORBX_BOW_PROF=1): per-workgroup phase cycles
@@ -555,6 +558,29 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
   int* binOf = bin_all + p * out_pitch;
   int* hist = hist_all + p * 32;
   if (nk <= 0) return;
+  // feature indices come from device CSR arrays the host cannot check: an
+  // index outside [0, min(n, kp_pitch)) is not a candidate and sets status
+  // bit 32 (it would address the next pair's rows or past the buffers)
+  // (a side's pitch is 0 for the single-pair host entry; out rows are indexed by
+  // the A feature for KF-KF and by the B feature for KF-F)
+  auto extent = [&](const BowSide& X, bool out_side) {
+    long long e = X.n[p];
+    if (X.kp_pitch > 0) e = min(e, X.kp_pitch);
+    if (out_side) e = min(e, out_pitch);
+    return (int)e;
+  };
+  const int nAp = extent(A, kf_vs_kf), nBp = extent(B, !kf_vs_kf);
+  if (tid == 0 && g == 0 && (A.n[p] > nAp || B.n[p] > nBp)) atomicOr(err, 32);
+  auto in_a = [&](int i) {
+    const bool ok = (unsigned)i < (unsigned)nAp;
+    if (!ok) atomicOr(err, 32);
+    return ok;
+  };
+  auto in_b = [&](int i) {
+    const bool ok = (unsigned)i < (unsigned)nBp;
+    if (!ok) atomicOr(err, 32);
+    return ok;
+  };
   const float factor = 1.0f / kHistoLength;
   // an accepted match: output, the pair's count and rotation histogram
   auto accept = [&](int idx1, int bestIdx2, int* h) {
@@ -632,8 +658,10 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
         if (S.t.boff[mid] <= i) lo = mid;
         else hi = mid;
       }
-      const int i2 = idxB[S.t.bsrc[lo] + (i - S.t.boff[lo])];
-      const bool ok = !kf_vs_kf || !mpB || mpB[i2] != 0;
+      int i2 = idxB[S.t.bsrc[lo] + (i - S.t.boff[lo])];
+      bool ok = in_b(i2);
+      if (!ok) i2 = 0;
+      ok = ok && (!kf_vs_kf || !mpB || mpB[i2] != 0);
       const uint4* d2 = (const uint4*)(descB + (long long)i2 * 32);
       const uint4 v0 = d2[0], v1 = d2[1];
       *(uint4*)&S.t.bdesc[i][0] = v0;
@@ -654,7 +682,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
       uint32_t t0 = kBowNone, t1 = kBowNone, t2 = kBowNone, t3 = kBowNone;
       uint32_t t4 = kBowNone, t5 = kBowNone, t6 = kBowNone, t7 = kBowNone;
       int nv = -1;
-      if (!mpA || mpA[i1]) {  // (:191-197)
+      if (in_a(i1) && (!mpA || mpA[i1])) {  // (:191-197)
         nv = 0;
         const uint4* d1 = (const uint4*)(descA + (long long)i1 * 32);
         const uint4 a0 = d1[0], a1 = d1[1];
@@ -904,21 +932,25 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
         bok[c] = false;
         q0[c] = q1[c] = make_uint4(0, 0, 0, 0);
         if (pos < nbn) {
-          const int i2 = idxB[b0 + pos];
+          int i2 = idxB[b0 + pos];
+          if (!in_b(i2)) i2 = -1;
           bidx[c] = i2;
-          bok[c] = !kf_vs_kf || !mpB || mpB[i2] != 0;
+          bok[c] = i2 >= 0 && (!kf_vs_kf || !mpB || mpB[i2] != 0);
+          if (i2 < 0) i2 = 0;
           const uint4* d2 = (const uint4*)(descB + (long long)i2 * 32);
           q0[c] = d2[0];
           q1[c] = d2[1];
-          S.f.bidx[wv][pos] = i2;
+          S.f.bidx[wv][pos] = bidx[c];
         }
       }
       for (int ac = a0i; ac < a1i; ac += 64) {
         const int nan_ = min(64, a1i - ac);
         __builtin_amdgcn_wave_barrier();
         if (lane < nan_) {
-          const int i1 = idxA[ac + lane];
-          const bool ok = !mpA || mpA[i1];
+          int i1 = idxA[ac + lane];
+          const bool in = in_a(i1);
+          if (!in) i1 = 0;
+          const bool ok = in && (!mpA || mpA[i1]);
           const uint4* d1 = (const uint4*)(descA + (long long)i1 * 32);
           const uint4 v0 = d1[0], v1 = d1[1];
           uint32_t* w = S.f.adesc[wv][lane];
@@ -970,7 +1002,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
     // very large nodes: candidates streamed from global memory 64 at a time
     for (int pa = a0i; pa < a1i; ++pa) {
       const int idx1 = idxA[pa];
-      if (mpA && !mpA[idx1]) continue;
+      if (!in_a(idx1) || (mpA && !mpA[idx1])) continue;
       const uint4* d1 = (const uint4*)(descA + (long long)idx1 * 32);
       const uint4 a0 = d1[0], a1 = d1[1];
       Top2 acc{256, -1, 256};
@@ -978,7 +1010,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
         const int q = q0 + lane;
         bool valid = false;
         int dist = 0, idx2 = -1;
-        if (q < b1) {
+        if (q < b1 && in_b(idxB[q])) {
           idx2 = idxB[q];
           const bool taken = (s_taken[idx2 >> 5] >> (idx2 & 31)) & 1u;
           valid = !taken && (!kf_vs_kf || !mpB || mpB[idx2] != 0);
@@ -1018,7 +1050,7 @@ __global__ __launch_bounds__(256) void search_bow_finalize_kernel(const int* __r
   __shared__ int s_var[4];
   const int p = blockIdx.x, tid = threadIdx.x;
   int* hist = hist_all + p * 32;
-  const int nout = kf_vs_kf ? nA[p] : min(nB[p], 65536);
+  const int nout = min(kf_vs_kf ? nA[p] : nB[p], (int)min(out_pitch, 65536ll));  // the row's extent
   if (check_ori) {
     if (tid == 0) {
       int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
@@ -1066,7 +1098,8 @@ __global__ __launch_bounds__(256) void search_bow_finalize_kernel(const int* __r
 }
 
 int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnratio, int check_ori, int kf_vs_kf,
-                      int* out, long long out_pitch, int* nmatches, int* bin_scratch, int* hist_scratch, void* stream) {
+                      int* out, long long out_pitch, int* nmatches, int* bin_scratch, int* hist_scratch, int* err,
+                      void* stream) {
   hipStream_t s = (hipStream_t)stream;
   // outputs and bins start at -1 (0xFF bytes), histograms and counts at 0
   if (hipMemsetAsync(out, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
@@ -1079,7 +1112,8 @@ int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnrat
   if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)65536 * 32);
   if (prof) (void)hipMemsetAsync(dbg, 0, (size_t)nwg * 32, s);
   hipLaunchKernelGGL(search_bow_kernel<kBowThreads>, dim3(nwg), dim3(kBowThreads), 0, s, A, B, nnratio,
-                     check_ori, kf_vs_kf, kBowGroups, out, out_pitch, bin_scratch, hist_scratch, prof ? dbg : nullptr);
+                     check_ori, kf_vs_kf, kBowGroups, out, out_pitch, bin_scratch, hist_scratch, err,
+                     prof ? dbg : nullptr);
   if (prof) {
     std::vector<int> h((size_t)nwg * 8);
     (void)hipStreamSynchronize(s);
@@ -1264,10 +1298,10 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
   P.check_ori = check_ori;
   P.kp_pitch = kp_pitch;
   P.cand_cap = m->cand_cap;
-  {
-    const char* st = getenv("ORBX_INIT_STOP");  // diagnostics only
-    P.stop = st ? atoi(st) : 0;
-  }
+  P.stop = 0;
+#ifdef ORBX_DIAG  // diagnostics builds only (tools/variant.sh): stop after a phase, results incomplete
+  if (const char* st = getenv("ORBX_INIT_STOP")) P.stop = atoi(st);
+#endif
   static long long* prof = nullptr;  // ORBX_INIT_PROF: phase clocks of every pair, averaged after the call
   const bool do_prof = getenv("ORBX_INIT_PROF") != nullptr;
   if (do_prof) {
@@ -1417,7 +1451,7 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
   BowSide B{(const uint8_t*)d[6], (const float*)d[7], 1, mpB ? (const uint8_t*)d[8] : nullptr, dn + 1,
             (const uint32_t*)d[9], (const int*)d[10], (const int*)d[11], dn + 3, 0, 0};
   if ((rc = launch_search_bow(A, B, 1, nnratio, check_ori, kf_vs_kf, (int*)d[12], std::max(nout, 1), (int*)d[14],
-                              (int*)d[13], (int*)d[16], st)))
+                              (int*)d[13], (int*)d[16], m->err, st)))
     return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
   int nm = 0;
   MHIP(hipMemcpyAsync(&nm, d[14], 4, hipMemcpyDeviceToHost, st));
@@ -1447,7 +1481,7 @@ int orbm_search_by_bow_batch(orbm_handle m, int pairs, int kp_pitch, int node_pi
   hipStream_t s = (hipStream_t)stream;
   if (m->ws.before(s)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
   const int rc = launch_search_bow(A, B, pairs, nnratio, check_ori, kf_vs_kf, d_out, kp_pitch, d_nmatches,
-                                   m->stereo_sad, m->bow_hist, stream);
+                                   m->stereo_sad, m->bow_hist, m->err, stream);
   if (rc) return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
   if (m->ws.after(s)) return mfail(ORBX_EDEVICE, "event record failed");
   return ORBX_OK;
@@ -1483,7 +1517,9 @@ int orbm_compute_stereo_matches_batch(orbm_handle m, orbx_handle left, int left_
   P.groups = std::max(1, std::min(8, (256 + pairs - 1) / pairs));
   if (const char* e = getenv("ORBX_STEREO_GROUPS")) P.groups = std::max(1, atoi(e));  // tuning experiments
   P.stop = 0;
+#ifdef ORBX_DIAG  // diagnostics builds only: stop after a phase, results incomplete
   if (const char* e = getenv("ORBX_STEREO_STOP")) P.stop = atoi(e);
+#endif
   // workgroup g takes left keypoints iL = g + groups * m: at most this many
   P.jobs_cap = (kp_pitch + P.groups - 1) / P.groups;
   if (stereo_lds_bytes(P.nrows, kp_pitch, P.jobs_cap) > 156 * 1024)

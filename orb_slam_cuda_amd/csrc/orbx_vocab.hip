@@ -561,8 +561,11 @@ int orbv_transform_batch(orbv_handle v, const uint8_t* d_desc, size_t desc_pitch
     }
     VHIP(hipGetLastError());
   }
-  if (const char* e = getenv("ORBX_VOC_STOP"))  // diagnostics: 1 = descend only
-    if (atoi(e) == 1) return ORBX_OK;
+  int voc_stop = 0;
+#ifdef ORBX_DIAG  // diagnostics builds only: 1 = descend only, 2 = FeatureVector only, 3 = no normalisation
+  if (const char* e = getenv("ORBX_VOC_STOP")) voc_stop = atoi(e);
+#endif
+  if (voc_stop == 1) return ORBX_OK;
   int S = 1;
   while (S < cap) S <<= 1;
   const size_t lds = (size_t)S * 12;
@@ -574,7 +577,7 @@ int orbv_transform_batch(orbv_handle v, const uint8_t* d_desc, size_t desc_pitch
   hipLaunchKernelGGL(voc_assemble_kernel, dim3(frames, 2), dim3(kAsThreads), lds, st, cap, S, d_n, d_word_ids, d_node_ids,
                      d_weights, tf, must, !l1, v->n_words, d_bow_words, d_bow_values, d_bow_n, d_fv_nodes, d_fv_off,
                      d_fv_idx, d_fv_n,
-                     getenv("ORBX_VOC_STOP") ? atoi(getenv("ORBX_VOC_STOP")) : 0);
+                     voc_stop);
   VHIP(hipGetLastError());
   return ORBX_OK;
 }

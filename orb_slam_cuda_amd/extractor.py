@@ -157,11 +157,6 @@ class ORBextractor:
         check(lib().orbx_get_tie_stats(self._h, frame0, nframes, ptr(out)))
         return out
 
-    @property
-    def front_path(self) -> bool:
-        """True if the plan runs the fused front kernel (orbx_front_path)."""
-        return bool(lib().orbx_front_path(self._h))
-
     def status(self, reset: bool = True) -> int:
         """Device status word of the handle's kernels (orbx_get_status); 0 = ok."""
         st = C.c_int(0)

@@ -58,3 +58,48 @@ def test_parse_defaults():
     import bench
     a = bench.parse_args([])
     assert a.gpus == 1 and a.batch == 64 and a.pool % a.batch == 0 and a.pool * 1280 * 376 > 256 * 2 ** 20
+
+
+def test_launcher_parent_never_loads_hip():
+    """visible_gpus() counts devices in a child: the launcher process, which
+    spawns the per-GPU workers, must not have the HIP runtime or liborbx mapped."""
+    pytest.importorskip("torch")
+    code = ("import sys; sys.path.insert(0, %r); import bench; n = bench.visible_gpus(); "
+            "m = open('/proc/self/maps').read(); "
+            "print(n, 'libamdhip64' in m, 'liborbx' in m)") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n, hip, orbx = r.stdout.split()
+    assert int(n) >= 0 and hip == "False" and orbx == "False"
+
+
+@pytest.mark.parametrize("var", ["ORBX_INIT_STOP", "ORBX_FAST_TWICE", "ORBX_FAST_PROF", "ORBX_LIB_VARIANT",
+                                 "ORBX_SOMETHING_NEW"])
+def test_bench_refuses_diagnostic_env(var):
+    """A timed region under a switch that skips, repeats or clocks work (or an
+    A/B library variant, or an undocumented variable) is refused..."""
+    pytest.importorskip("torch")
+    r = _run(["--gpus", "1", "--spawn", "--steps", "1", "--warmup", "0", "--stub-worker"], {var: "1"})
+    assert r.returncode != 0 and "refusing" in (r.stderr + r.stdout) and var in r.stderr
+    # ...unless asked for, and then the line names it
+    r = _run(["--gpus", "1", "--spawn", "--steps", "1", "--warmup", "0", "--stub-worker", "--allow-diag"], {var: "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["orbx_env"] == {var: "1"}
+
+
+def test_bench_allows_and_stamps_tuning_env():
+    pytest.importorskip("torch")
+    r = _run(["--gpus", "1", "--spawn", "--steps", "1", "--warmup", "0", "--stub-worker"], {"ORBX_PYR_PLAN": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["orbx_env"] == {"ORBX_PYR_PLAN": "1"}
+
+
+def test_env_audit_unit():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.audit_env(False, {"PATH": "/bin", "ORBX_TOP2_VALU": "1"}) == {"ORBX_TOP2_VALU": "1"}
+    with pytest.raises(SystemExit):
+        bench.audit_env(False, {"ORBX_VOC_STOP": "1"})
+    assert bench.audit_env(True, {"ORBX_VOC_STOP": "1"}) == {"ORBX_VOC_STOP": "1"}

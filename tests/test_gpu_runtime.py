@@ -47,16 +47,6 @@ def test_tie_stats_batch(pkg, O):
     assert ext.status() == 0
 
 
-def test_front_path_is_planned_for_the_bench_shapes(pkg):
-    """The fused blur + FAST tiles (opt-in, ORBX_FRONT=1) hold KITTI (nF 2000
-    and the 4000 init extractor) and EuRoC plans; by default the separate
-    blur and per-cell FAST kernels run."""
-    import os
-    want = os.environ.get("ORBX_FRONT", "0") == "1"
-    for nf, W, H, B in ((2000, 1241, 376, 32), (4000, 1241, 376, 1), (1000, 752, 480, 32), (500, 640, 240, 1)):
-        assert pkg.ORBextractor(nf, 1.2, 8, 20, 7, W, H, max_batch=B).front_path == want
-
-
 def test_small_handle_does_not_shrink_lds_limit(pkg, O):
     """A handle with a small plan created after a large one must not lower the
     per-kernel LDS limit the large one launches with."""
@@ -155,25 +145,3 @@ def test_stereo_batches_on_two_streams_share_one_matcher(pkg, O):
                 O.pyramid(cfg, R["pairs"][i][0]), O.pyramid(cfg, R["pairs"][i][1]),
                 O.level_info(cfg)["scale"], O.level_info(cfg)["inv_scale"], MB, MBF)
             assert kept[i] == rk and np.array_equal(u[i, :nl], ru)
-
-
-@pytest.mark.parametrize("seed,W,H,nf,px", [(0, 1241, 376, 2000, "256"), (3, 752, 480, 1000, "128"),
-                                            (8, 640, 240, 500, "96")])
-def test_fused_blur_fast_tiles_parity(pkg, O, monkeypatch, seed, W, H, nf, px):
-    """The opt-in fused path (ORBX_FRONT=1: GaussianBlur + FAST + NMS + the
-    per-cell threshold choice in one tile kernel) is bit-exact too: keypoints,
-    descriptors, every blurred level and the per-cell FAST candidates."""
-    from orb_slam_cuda_amd.synth import synth_frame
-    monkeypatch.setenv("ORBX_FRONT", "1")
-    monkeypatch.setenv("ORBX_TILE_PX", px)
-    img = synth_frame(seed, W, H)
-    ext = pkg.ORBextractor(nf, 1.2, 8, 20, 7, W, H)
-    assert ext.front_path
-    kp, desc = ext(img)
-    cfg = O.config(nfeatures=nf, width=W, height=H)
-    rkp, rdesc = O.extract(cfg, img)
-    assert np.array_equal(kp.view(np.uint8), rkp.view(np.uint8)) and np.array_equal(desc, rdesc)
-    for l in range(8):
-        assert np.array_equal(ext.level_image(l, blurred=True), O.blur_level(cfg, img, l)), f"blur {l}"
-        c, rc = ext.fast_candidates(l), O.fast_level(cfg, img, l)
-        assert np.array_equal(c.view(np.uint8), rc.view(np.uint8)), f"FAST {l}"

@@ -99,3 +99,24 @@ def test_tie_stats_invariants_on_synthetic_frame(O):
             assert 2 <= st["nodes"][l] <= st["kps"][l] <= per_level[l]
         else:
             assert st["nodes"][l] == st["kps"][l] == 0
+
+
+def test_scale_mode_pinned_by_reference_map(O):
+    """The reference's own map (Examples/Monocular/map.yml, written by
+    MapPoint::write, src/MapPoint.cc:489-490) pins the extractor's top-level
+    scale factor: MapPoint::UpdateNormalAndDepth sets
+    mfMinDistance = mfMaxDistance / mvScaleFactors[nLevels-1]
+    (src/MapPoint.cc:68-69, 372-373) in float. All 775 stored pairs satisfy it
+    with the upstream 1.2^7 table (scale mode U, the default here) and none
+    with the fork's buildGraph override (mode F, src/ORBextractor.cc:674-680)
+    at the KITTI width, so the run that wrote the reference's map used mode U.
+    Values extracted by tests/golden/make_mapyml.py."""
+    d = np.load(os.path.join(GOLDEN, "mapyml_distances.npy"))
+    assert d.shape == (775, 2) and d.dtype == np.float32
+    mx, mn = d[:, 0], d[:, 1]
+    sU = O.level_info(O.config(scale_mode=0))["scale"]
+    assert np.float32(sU[7]) == np.float32(3.5831816)  # iterative float product 1.2^7 (:505-509)
+    assert np.array_equal(mx / np.float32(sU[7]), mn)
+    for w, h in ((1241, 376), (752, 480), (640, 480)):
+        sF = O.level_info(O.config(scale_mode=1, width=w, height=h))["scale"]
+        assert not np.any(mx / np.float32(sF[7]) == mn), (w, h, sF[7])

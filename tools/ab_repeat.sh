@@ -6,7 +6,7 @@ N=$1; shift
 for r in $(seq $N); do
   for v in "$@"; do
     if [ $v = base ]; then unset ORBX_LIB_VARIANT; else export ORBX_LIB_VARIANT=$v; fi
-    timeout -k 10 120 python3 bench.py --steps 100 --warmup 20 --cpu-sample 0 > /tmp/ab.log 2>&1 || exit 1
+    timeout -k 10 120 python3 bench.py --allow-diag --steps 100 --warmup 20 --cpu-sample 0 > /tmp/ab.log 2>&1 || exit 1
     python3 -c "import json;d=json.loads(open('/tmp/ab.log').read().strip().splitlines()[-1]);print('$v', d['value'])" | tee -a /tmp/ab_all.txt
   done
 done

@@ -7,6 +7,6 @@ for v in "$@"; do
   t=$(timeout -k 10 200 python -u -m pytest tests/test_gpu_match.py -x -q -k hamming --timeout 120 --timeout-method thread 2>&1 | tail -n 1)
   echo -n "$v [$t] top2-alone: "
   WHICH=top2 timeout -k 10 60 python3 tools/init_timing.py 64 | grep -o "ms_per_call=[0-9.]*" || exit 1
-  timeout -k 10 120 python3 bench.py --steps 100 --warmup 20 --cpu-sample 0 > /tmp/bv.log 2>&1 || exit 1
+  timeout -k 10 120 python3 bench.py --allow-diag --steps 100 --warmup 20 --cpu-sample 0 > /tmp/bv.log 2>&1 || exit 1
   python3 -c "import json;d=json.loads(open('/tmp/bv.log').read().strip().splitlines()[-1]);print('   bench',d['value'],d['ms_per_step'],'ham',d['stage_ms_per_batch']['hamming_top2'])"
 done
