@@ -678,7 +678,7 @@ def run_mono(args, cfg, rank, world, local, dist):
     del pipe, timed
     import gc
     gc.collect()
-    lat = host = cpu = cpu1 = None
+    lat = host = cpu = cpu1 = tie_rule = None
     solo = world == 1
     if rank == 0 and solo and not args.no_latency:
         lat = latency_leg(cfg, local, frames[:32], args.no_match)
@@ -691,6 +691,7 @@ def run_mono(args, cfg, rank, world, local, dist):
         cpu = cpu_baseline(sample, cfg, args.cpu_sample, args.no_match, nt) if nt > 1 else cpu1
         if lat is not None:
             lat["cpu_oracle"] = cpu_latency(frames[:220], cfg, args.no_match)
+        tie_rule = cpu_tie_rule_study(frames[:8], cfg)
 
     if rank == 0:
         workload = (cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only")
@@ -717,6 +718,7 @@ def run_mono(args, cfg, rank, world, local, dist):
             "latency": lat,
             "host_stream": host,
             "quadtree_tie_straddle": tie,
+            "tie_rule_disagreement": tie_rule,
             "pyr_fast_pass_hbm_gbs": round(pf_gbs, 1),
             "dominant_kernel": KERNELS[dominant],
             "stage_ms_per_batch": {s: round(v, 4) for s, v in st.items()},
@@ -828,6 +830,27 @@ def latency_leg(cfg, local, frames, no_match, n=200, warm=20):
         out["search_init_ms"] = {"median": round(float(np.median(ts)), 4),
                                  "p99": round(float(np.percentile(ts, 99)), 4), "calls": n}
     return out
+
+
+def cpu_tie_rule_study(frames, cfg):
+    """How far the product's quadtree tie rule (node creation order) is from
+    the reference's (heap address, src/ORBextractor.cc:1041), measured on the
+    CPU with the oracle's layout-identical pointer-order quadtree
+    (orc_tie_sequence), and how far the pointer order is
+    from itself under another heap history. Runs with the CPU baseline, after
+    the timed region; the oracle is the checker here, not the product."""
+    from oracle import oracle as O
+    oc = O.config(nfeatures=cfg["nfeatures"], width=cfg["W"], height=cfg["H"])
+    d01, k01 = O.tie_sequence(oc, frames, O.TIE_LATER_FIRST, O.TIE_POINTER)
+    d11, k11 = O.tie_sequence(oc, frames, O.TIE_POINTER, O.TIE_POINTER)
+    return {"frames": int(len(frames)),
+            "creation_vs_pointer": {"levels_list_differs_frac": round(float(d01.mean()), 3),
+                                    "levels_kept_set_differs_frac": round(float((k01 > 0).mean()), 3),
+                                    "keypoints_kept_by_one_rule_per_frame": round(float(k01.sum(1).mean()), 2)},
+            "pointer_vs_pointer_other_heap_history": {"levels_list_differs_frac": round(float(d11.mean()), 3),
+                                                      "levels_kept_set_differs_frac": round(float((k11 > 0).mean()), 3),
+                                                      "keypoints_kept_by_one_run_per_frame": round(float(k11.sum(1).mean()), 2)},
+            "source": "oracle tie-rule study on the host CPU (checker), consecutive frames of the timed sequence"}
 
 
 def cpu_model():

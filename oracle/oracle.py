@@ -138,6 +138,37 @@ def tie_stats(cfg: OrcConfig, img: np.ndarray) -> dict:
     return dict(events=ev, nodes=nd, kps=kp)
 
 
+TIE_LATER_FIRST, TIE_POINTER, TIE_EARLIER_FIRST = 0, 1, 2
+
+
+def extract_rule(cfg: OrcConfig, img: np.ndarray, tie_rule: int):
+    """orc_extract with the quadtree's size ties broken by `tie_rule`
+    (0 creation order later-first = the product's, 1 real heap address as the
+    reference, 2 creation order earlier-first)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    cap = max(16 * cfg.nfeatures, 4096)
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int(0)
+    rc = lib().orc_extract_rule(C.byref(cfg), tie_rule, _p(img), img.shape[1], img.shape[0],
+                                C.c_size_t(img.strides[0]), _p(kps), cap, _p(desc), C.byref(n))
+    assert rc == 0, rc
+    return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def tie_sequence(cfg: OrcConfig, frames: np.ndarray, rule_a: int, rule_b: int):
+    """orc_tie_sequence: per (frame, level) whether rule_a and rule_b keep
+    different keypoint lists, and how many positions only one of them kept."""
+    frames = np.ascontiguousarray(frames, np.uint8)
+    F, H, W = frames.shape
+    L = cfg.nlevels
+    differs = np.zeros((F, L), np.int32)
+    kept = np.zeros((F, L), np.int32)
+    lib().orc_tie_sequence(C.byref(cfg), _p(frames), F, W, H, C.c_size_t(W), C.c_size_t(H * W), rule_a, rule_b,
+                           _p(differs), _p(kept))
+    return differs.astype(bool), kept
+
+
 def distribute_ties(keys: np.ndarray, minX: int, maxX: int, minY: int, maxY: int, N: int):
     keys = np.ascontiguousarray(keys, KP_DTYPE)
     ev, nd, kp = C.c_int(0), C.c_int(0), C.c_int(0)

@@ -17,6 +17,7 @@
 #include "orb_pattern_tbl.h"
 
 #include <algorithm>
+#include <iterator>
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -467,6 +468,7 @@ struct Extractor {
 
   void extract(const Mat8& image, std::vector<KeyPoint>& out, std::vector<uint8_t>& desc,
                std::vector<TieStats>* ties = nullptr);
+  int tie_rule = 0;  // TieRule of the quadtree's sorted rounds (0 = the product's)
 };
 
 // --------------------------------------------------------------- quadtree
@@ -530,9 +532,15 @@ struct SizeSeqNode {
   }
 };
 
+// Tie rules of the sorted rounds (orc_config-independent; tie-rule study in
+// orc_tie_sequence): 0 = creation order, later-created split first (the
+// default shared with the HIP kernel); 1 = the reference's real heap address
+// (distribute_oct_tree_ptr below); 2 = creation order, earlier-created first.
+enum TieRule { kTieLaterFirst = 0, kTiePointer = 1, kTieEarlierFirst = 2 };
+
 std::vector<KeyPoint> distribute_oct_tree(const std::vector<KeyPoint>& vToDistributeKeys,
                                           int minX, int maxX, int minY, int maxY, int N,
-                                          TieStats* ties = nullptr) {
+                                          TieStats* ties = nullptr, int tie_rule = kTieLaterFirst) {
   const int nIni = round(static_cast<float>(maxX - minX) / (maxY - minY));
   const float hX = static_cast<float>(maxX - minX) / nIni;
   long seq = 0;
@@ -610,6 +618,15 @@ std::vector<KeyPoint> distribute_oct_tree(const std::vector<KeyPoint>& vToDistri
         std::vector<SizeSeqNode> vPrevSizeAndPointerToNode = vSizeAndPointerToNode;
         vSizeAndPointerToNode.clear();
         std::sort(vPrevSizeAndPointerToNode.begin(), vPrevSizeAndPointerToNode.end());
+        if (tie_rule == kTieEarlierFirst)  // reverse every run of equal sizes
+          for (size_t a = 0; a < vPrevSizeAndPointerToNode.size();) {
+            size_t b = a;
+            while (b < vPrevSizeAndPointerToNode.size() &&
+                   vPrevSizeAndPointerToNode[b].size == vPrevSizeAndPointerToNode[a].size)
+              ++b;
+            std::reverse(vPrevSizeAndPointerToNode.begin() + a, vPrevSizeAndPointerToNode.begin() + b);
+            a = b;
+          }
         std::vector<int> children(vPrevSizeAndPointerToNode.size(), 0);
         for (int j = vPrevSizeAndPointerToNode.size() - 1; j >= 0; j--) {
           ExtractorNode n1, n2, n3, n4;
@@ -641,6 +658,207 @@ std::vector<KeyPoint> distribute_oct_tree(const std::vector<KeyPoint>& vToDistri
   }
   std::vector<KeyPoint> vResultKeys;
   vResultKeys.reserve(lNodes.size());
+  for (auto it = lNodes.begin(); it != lNodes.end(); it++) {
+    std::vector<KeyPoint>& vNodeKeys = it->vKeys;
+    KeyPoint* pKP = &vNodeKeys[0];
+    float maxResponse = pKP->response;
+    for (size_t k = 1; k < vNodeKeys.size(); k++) {
+      if (vNodeKeys[k].response > maxResponse) {
+        pKP = &vNodeKeys[k];
+        maxResponse = vNodeKeys[k].response;
+      }
+    }
+    vResultKeys.push_back(*pKP);
+  }
+  return vResultKeys;
+}
+
+// ------------------------------------------- quadtree with heap-address ties
+// The reference's own tie-break, for the tie-rule study:
+// DistributeOctTree with an ExtractorNode laid out exactly as
+// include/ORBextractor.h:62-73 (std::vector<cv::KeyPoint> of 28-B keypoints,
+// four cv::Point2i, a std::list iterator, a bool: 72 bytes, so a list node is
+// an 88-byte malloc as in the reference), the reference's sequence of
+// reserve / push_front / copy / erase / temporary destruction
+// (src/ORBextractor.cc:831-1120), and the sorted rounds ordering
+// pair<int, ExtractorNode*> by the real heap address (:1041). Only the heap
+// state on entry differs from the reference process (OpenCV's own allocations
+// before the call are not reproduced).
+struct RefPoint2i {
+  int x, y;
+};
+struct RefExtractorNode {
+  std::vector<KeyPoint> vKeys;
+  RefPoint2i UL, UR, BL, BR;
+  std::list<RefExtractorNode>::iterator lit;
+  bool bNoMore = false;
+  void DivideNode(RefExtractorNode& n1, RefExtractorNode& n2, RefExtractorNode& n3, RefExtractorNode& n4) {
+    const int halfX = ceil(static_cast<float>(UR.x - UL.x) / 2);
+    const int halfY = ceil(static_cast<float>(BR.y - UL.y) / 2);
+    n1.UL = UL;
+    n1.UR = {UL.x + halfX, UL.y};
+    n1.BL = {UL.x, UL.y + halfY};
+    n1.BR = {UL.x + halfX, UL.y + halfY};
+    n1.vKeys.reserve(vKeys.size());
+    n2.UL = n1.UR;
+    n2.UR = UR;
+    n2.BL = n1.BR;
+    n2.BR = {UR.x, UL.y + halfY};
+    n2.vKeys.reserve(vKeys.size());
+    n3.UL = n1.BL;
+    n3.UR = n1.BR;
+    n3.BL = BL;
+    n3.BR = {n1.BR.x, BL.y};
+    n3.vKeys.reserve(vKeys.size());
+    n4.UL = n3.UR;
+    n4.UR = n2.BR;
+    n4.BL = n3.BR;
+    n4.BR = BR;
+    n4.vKeys.reserve(vKeys.size());
+    for (const KeyPoint& kp : vKeys) {
+      if (kp.x < n1.UR.x)
+        (kp.y < n1.BR.y ? n1 : n3).vKeys.push_back(kp);
+      else
+        (kp.y < n1.BR.y ? n2 : n4).vKeys.push_back(kp);
+    }
+    for (RefExtractorNode* n : {&n1, &n2, &n3, &n4})
+      if (n->vKeys.size() == 1) n->bNoMore = true;
+  }
+};
+static_assert(sizeof(KeyPoint) == 28, "cv::KeyPoint is 28 bytes");
+static_assert(sizeof(RefExtractorNode) == 72, "layout of the reference's ExtractorNode");
+
+// Creation sequence of the pointer variant's nodes, kept beside the heap
+// (fixed static table, no allocation during the call) so the study can see
+// how address order relates to creation order: per sorted round, adjacent
+// equal-size entries in address order counted as "later-created at the
+// higher address" (concordant with rule 0) or not.
+struct PtrSeqTable {
+  static constexpr int kCap = 1 << 17;
+  const void* key[kCap];
+  long seq[kCap];
+  long next = 0;
+  long concordant = 0, discordant = 0;
+  void clear() {
+    std::memset(key, 0, sizeof(key));
+    next = 0;
+  }
+  static size_t slot(const void* p) { return ((uintptr_t)p >> 4) * 0x9E3779B97F4A7C15ull >> (64 - 17); }
+  void put(const void* p) {
+    size_t i = slot(p);
+    while (key[i] && key[i] != p) i = (i + 1) & (kCap - 1);
+    key[i] = p;
+    seq[i] = next++;
+  }
+  long get(const void* p) const {
+    size_t i = slot(p);
+    while (key[i] && key[i] != p) i = (i + 1) & (kCap - 1);
+    return key[i] ? seq[i] : -1;
+  }
+};
+PtrSeqTable* g_ptr_seq = nullptr;  // set by orc_tie_address_order (study only)
+
+std::vector<KeyPoint> distribute_oct_tree_ptr(const std::vector<KeyPoint>& vToDistributeKeys, int minX, int maxX,
+                                              int minY, int maxY, int N, int nfeatures) {
+  if (g_ptr_seq) g_ptr_seq->clear();
+  const int nIni = round(static_cast<float>(maxX - minX) / (maxY - minY));
+  const float hX = static_cast<float>(maxX - minX) / nIni;
+  std::list<RefExtractorNode> lNodes;
+  std::vector<RefExtractorNode*> vpIniNodes;
+  vpIniNodes.resize(nIni);
+  for (int i = 0; i < nIni; i++) {
+    RefExtractorNode ni;
+    ni.UL = {(int)(hX * static_cast<float>(i)), 0};
+    ni.UR = {(int)(hX * static_cast<float>(i + 1)), 0};
+    ni.BL = {ni.UL.x, maxY - minY};
+    ni.BR = {ni.UR.x, maxY - minY};
+    ni.vKeys.reserve(vToDistributeKeys.size());
+    lNodes.push_back(ni);  // copies an empty vector: the list node's vKeys starts with no buffer
+    vpIniNodes[i] = &lNodes.back();
+  }
+  for (size_t i = 0; i < vToDistributeKeys.size(); i++) {
+    const KeyPoint& kp = vToDistributeKeys[i];
+    vpIniNodes[(size_t)(kp.x / hX)]->vKeys.push_back(kp);
+  }
+  auto lit = lNodes.begin();
+  while (lit != lNodes.end()) {
+    if (lit->vKeys.size() == 1) {
+      lit->bNoMore = true;
+      lit++;
+    } else if (lit->vKeys.empty()) {
+      lit = lNodes.erase(lit);
+    } else {
+      lit++;
+    }
+  }
+  bool bFinish = false;
+  std::vector<std::pair<int, RefExtractorNode*>> vSizeAndPointerToNode;
+  vSizeAndPointerToNode.reserve(lNodes.size() * 4);
+  // the reference's "add childs if they contain points" block, per child
+  auto add_child = [&](RefExtractorNode& n, int* nToExpand) {
+    if (n.vKeys.size() > 0) {
+      lNodes.push_front(n);
+      if (g_ptr_seq) g_ptr_seq->put(&lNodes.front());
+      if (n.vKeys.size() > 1) {
+        if (nToExpand) (*nToExpand)++;
+        vSizeAndPointerToNode.push_back(std::make_pair((int)n.vKeys.size(), &lNodes.front()));
+        lNodes.front().lit = lNodes.begin();
+      }
+    }
+  };
+  while (!bFinish) {
+    int prevSize = lNodes.size();
+    lit = lNodes.begin();
+    int nToExpand = 0;
+    vSizeAndPointerToNode.clear();
+    while (lit != lNodes.end()) {
+      if ((int)lNodes.size() >= N) {
+        bFinish = true;
+        break;
+      }
+      if (lit->bNoMore) {
+        lit++;
+        continue;
+      }
+      RefExtractorNode n1, n2, n3, n4;
+      lit->DivideNode(n1, n2, n3, n4);
+      add_child(n1, &nToExpand);
+      add_child(n2, &nToExpand);
+      add_child(n3, &nToExpand);
+      add_child(n4, &nToExpand);
+      lit = lNodes.erase(lit);
+    }
+    if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) {
+      bFinish = true;
+    } else if (((int)lNodes.size() + nToExpand * 3) > N) {
+      while (!bFinish) {
+        prevSize = lNodes.size();
+        std::vector<std::pair<int, RefExtractorNode*>> vPrevSizeAndPointerToNode = vSizeAndPointerToNode;
+        vSizeAndPointerToNode.clear();
+        std::sort(vPrevSizeAndPointerToNode.begin(), vPrevSizeAndPointerToNode.end());  // ties: heap address
+        if (g_ptr_seq)
+          for (size_t a = 1; a < vPrevSizeAndPointerToNode.size(); ++a)
+            if (vPrevSizeAndPointerToNode[a].first == vPrevSizeAndPointerToNode[a - 1].first) {
+              const bool later_higher = g_ptr_seq->get(vPrevSizeAndPointerToNode[a].second) >
+                                        g_ptr_seq->get(vPrevSizeAndPointerToNode[a - 1].second);
+              (later_higher ? g_ptr_seq->concordant : g_ptr_seq->discordant)++;
+            }
+        for (int j = vPrevSizeAndPointerToNode.size() - 1; j >= 0; j--) {
+          RefExtractorNode n1, n2, n3, n4;
+          vPrevSizeAndPointerToNode[j].second->DivideNode(n1, n2, n3, n4);
+          add_child(n1, nullptr);
+          add_child(n2, nullptr);
+          add_child(n3, nullptr);
+          add_child(n4, nullptr);
+          lNodes.erase(vPrevSizeAndPointerToNode[j].second->lit);
+          if ((int)lNodes.size() >= N) break;
+        }
+        if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) bFinish = true;
+      }
+    }
+  }
+  std::vector<KeyPoint> vResultKeys;
+  vResultKeys.reserve(nfeatures);
   for (auto it = lNodes.begin(); it != lNodes.end(); it++) {
     std::vector<KeyPoint>& vNodeKeys = it->vKeys;
     KeyPoint* pKP = &vNodeKeys[0];
@@ -711,8 +929,11 @@ void Extractor::extract(const Mat8& image, std::vector<KeyPoint>& out, std::vect
     int bx[4];
     fast_level(level, cand, bx);
     std::vector<KeyPoint>& keypoints = allKeypoints[level];
-    keypoints = distribute_oct_tree(cand, bx[0], bx[1], bx[2], bx[3], mnFeaturesPerLevel[level],
-                                    ties ? &(*ties)[level] : nullptr);
+    if (tie_rule == kTiePointer)
+      keypoints = distribute_oct_tree_ptr(cand, bx[0], bx[1], bx[2], bx[3], mnFeaturesPerLevel[level], cfg.nfeatures);
+    else
+      keypoints = distribute_oct_tree(cand, bx[0], bx[1], bx[2], bx[3], mnFeaturesPerLevel[level],
+                                      ties ? &(*ties)[level] : nullptr, tie_rule);
     const int scaledPatchSize = PATCH_SIZE * mvScaleFactor[level];
     for (auto& kp : keypoints) {
       kp.x += bx[0];
@@ -940,6 +1161,76 @@ int orc_extract_tie_stats(const orc_config* cfg, const uint8_t* img, int w, int 
     if (nodes) nodes[l] = z.nodes;
     if (kps) kps[l] = z.kps;
   }
+  return 0;
+}
+
+int orc_extract_rule(const orc_config* cfg, int tie_rule, const uint8_t* img, int w, int h, size_t stride,
+                     orc_kp* kps, int cap, uint8_t* desc, int* n) {
+  Extractor ex(*cfg);
+  ex.tie_rule = tie_rule;
+  std::vector<KeyPoint> out;
+  std::vector<uint8_t> d;
+  ex.extract(wrap_image(img, w, h, stride), out, d);
+  *n = (int)out.size();
+  if ((int)out.size() > cap) return -1;
+  std::memcpy(kps, out.data(), out.size() * sizeof(KeyPoint));
+  if (desc) std::memcpy(desc, d.data(), d.size());
+  return 0;
+}
+
+int orc_tie_sequence(const orc_config* cfg, const uint8_t* frames, int nframes, int w, int h, size_t stride,
+                     size_t frame_bytes, int rule_a, int rule_b, int* differs, int* kept_diff) {
+  // pass 1: every frame with rule_a in sequence, as the reference's Tracking
+  // thread extracts them (one extractor, one heap history); pass 2: rule_b
+  const int L = cfg->nlevels;
+  std::vector<std::vector<std::vector<KeyPoint>>> res[2];
+  for (int r = 0; r < 2; ++r) {
+    Extractor ex(*cfg);
+    ex.tie_rule = r ? rule_b : rule_a;
+    res[r].resize(nframes);
+    for (int f = 0; f < nframes; ++f) {
+      std::vector<KeyPoint> out;
+      std::vector<uint8_t> d;
+      ex.extract(wrap_image(frames + (size_t)f * frame_bytes, w, h, stride), out, d);
+      res[r][f].assign(L, {});
+      for (const KeyPoint& k : out) res[r][f][k.octave].push_back(k);
+    }
+  }
+  auto key = [](const KeyPoint& k) { return std::make_pair(k.y, k.x); };
+  for (int f = 0; f < nframes; ++f)
+    for (int l = 0; l < L; ++l) {
+      const auto& a = res[0][f][l];
+      const auto& b = res[1][f][l];
+      bool same = a.size() == b.size();
+      for (size_t i = 0; same && i < a.size(); ++i) same = std::memcmp(&a[i], &b[i], sizeof(KeyPoint)) == 0;
+      differs[f * L + l] = !same;
+      // keypoints kept by one rule and not the other (by position)
+      std::vector<std::pair<float, float>> ka, kb, only;
+      for (const auto& k : a) ka.push_back(key(k));
+      for (const auto& k : b) kb.push_back(key(k));
+      std::sort(ka.begin(), ka.end());
+      std::sort(kb.begin(), kb.end());
+      std::set_symmetric_difference(ka.begin(), ka.end(), kb.begin(), kb.end(), std::back_inserter(only));
+      kept_diff[f * L + l] = (int)only.size();
+    }
+  return 0;
+}
+
+int orc_tie_address_order(const orc_config* cfg, const uint8_t* frames, int nframes, int w, int h, size_t stride,
+                          size_t frame_bytes, long* concordant, long* discordant) {
+  static PtrSeqTable table;  // static storage: the study allocates nothing on the heap per node
+  g_ptr_seq = &table;
+  table.concordant = table.discordant = 0;
+  Extractor ex(*cfg);
+  ex.tie_rule = kTiePointer;
+  for (int f = 0; f < nframes; ++f) {
+    std::vector<KeyPoint> out;
+    std::vector<uint8_t> d;
+    ex.extract(wrap_image(frames + (size_t)f * frame_bytes, w, h, stride), out, d);
+  }
+  *concordant = table.concordant;
+  *discordant = table.discordant;
+  g_ptr_seq = nullptr;
   return 0;
 }
 

@@ -72,6 +72,20 @@ int orc_extract_tie_stats(const orc_config* cfg, const uint8_t* img, int w, int 
                           size_t stride, int* events, int* nodes, int* kps);
 int orc_distribute_ties(const orc_kp* keys, int nkeys, int minX, int maxX, int minY,
                         int maxY, int N, int* events, int* nodes, int* kps);
+/* Quadtree tie-rule study: orc_extract with the sorted
+ * rounds' size ties broken by rule 0 = node creation order, later-created
+ * first (the product's rule), 1 = the reference's real heap address with a
+ * layout-identical ExtractorNode and its allocation sequence, 2 = creation
+ * order, earlier-created first. */
+int orc_extract_rule(const orc_config* cfg, int tie_rule, const uint8_t* img, int w,
+                     int h, size_t stride, orc_kp* kps, int cap, uint8_t* desc, int* n);
+/* Extracts nframes frames in sequence with rule_a (one extractor, as the
+ * reference's Tracking thread does), then with rule_b, and reports per
+ * (frame, level) whether the kept keypoint lists differ and how many
+ * keypoint positions only one of them kept. */
+int orc_tie_sequence(const orc_config* cfg, const uint8_t* frames, int nframes, int w,
+                     int h, size_t stride, size_t frame_bytes, int rule_a, int rule_b,
+                     int* differs, int* kept_diff);
 /* The rBRIEF test table (bit_pattern_31_, src/ORBextractor.cc:236-494) the
  * oracle uses: 1024 entries, fork (0) or upstream (1) variant. */
 void orc_pattern(int pattern_mode, signed char* out1024);

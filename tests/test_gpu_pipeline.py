@@ -72,23 +72,25 @@ def _check_batches(O, cfg, frames, pipe, batches, check):
     W, H = cfg["W"], cfg["H"]
     # frame of slot j of batch k: the pool slot k % nb; slot 0 = the previous batch's last frame
     fidx = lambda k, j: ((k % nb) * B + j - 1) if j > 0 else (((k - 1) % nb) * B + B - 1)
-    need = sorted({fidx(k, j) for k in check for j in range(B + 1)})
+    # the last batch's carry (step batches - 1) already wrote slot 0 of set batches % 3, i.e.
+    # of batch batches - 3: after the run that slot holds the next batch's t-1 frame
+    held = lambda k, j: fidx(batches, 0) if (j == 0 and k == batches - 3) else fidx(k, j)
+    need = sorted({fidx(k, j) for k in check for j in range(B + 1)} | {held(k, 0) for k in check})
     ref = _oracle_frames(O, cfg, frames, need)
     pairs = []
     for k in check:
         n, kps, desc, (bi, bd, sd), m12, nm = _download_set(pipe, k)
         for j in range(B + 1):
-            rk, rd = ref[fidx(k, j)]
+            rk, rd = ref[held(k, j)]
             assert n[j] == len(rk), (k, j)
             assert np.array_equal(kps[j, :n[j]].view(np.uint8), rk.view(np.uint8)), ("keypoints", k, j)
             assert np.array_equal(desc[j, :n[j]], rd), ("descriptors", k, j)
         for p in range(B):
-            pairs.append((k, p, n, kps, desc, bi, bd, sd, m12, nm))
+            pairs.append((k, p, ref[fidx(k, p)], ref[fidx(k, p + 1)], bi, bd, sd, m12, nm))
 
     def one(t):
-        k, p, n, kps, desc, bi, bd, sd, m12, nm = t
-        k1, d1 = kps[p, :n[p]], desc[p, :n[p]]              # frame t-1 (slot p)
-        k2, d2 = kps[p + 1, :n[p + 1]], desc[p + 1, :n[p + 1]]  # frame t (slot p + 1)
+        # inputs = the oracle's frames t-1 and t (equal to the device's, checked above)
+        k, p, (k1, d1), (k2, d2), bi, bd, sd, m12, nm = t
         ri, rd, rs = O.hamming_top2(d2, d1)
         r12, rnm, _ = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), np.stack([k1["x"], k1["y"]], 1),
                                                   100, 0.9, True)

@@ -120,3 +120,30 @@ def test_scale_mode_pinned_by_reference_map(O):
     for w, h in ((1241, 376), (752, 480), (640, 480)):
         sF = O.level_info(O.config(scale_mode=1, width=w, height=h))["scale"]
         assert not np.any(mx / np.float32(sF[7]) == mn), (w, h, sF[7])
+
+
+def test_tie_rule_study_pointer_order_is_heap_history(O):
+    """The reference breaks the quadtree's size ties by heap address
+    (src/ORBextractor.cc:1041). The oracle's rule 1 runs a layout-identical
+    ExtractorNode with the reference's allocation sequence on the real glibc
+    heap. Measured on committed-seed C3 frames:
+    * the product's creation-order rule is deterministic (rule 0 twice: equal);
+    * the pointer rule is NOT reproducible by the reference itself: the same
+      frames through it a second time (another heap history) keep a different
+      keypoint list order at most levels and some different keypoints;
+    * creation order differs from the pointer order by about as much as the
+      pointer order differs from itself, in a small fraction of the kept keypoints."""
+    from orb_slam_cuda_amd.synth import SynthSequence
+    fr = SynthSequence(1000, 1241, 376).frames(6)  # the bench's rank-0 C3 sequence
+    cfg = O.config()
+    d00, k00 = O.tie_sequence(cfg, fr, 0, 0)
+    assert not d00.any() and not k00.any()
+    d01, k01 = O.tie_sequence(cfg, fr, 0, 1)
+    d11, k11 = O.tie_sequence(cfg, fr, 1, 1)
+    kept = 2000 * len(fr)
+    assert d01.mean() > 0.5 and d11.mean() > 0.5        # list order: heap-dependent at most levels
+    assert 0 < k01.sum() < 0.05 * kept and 0 < k11.sum() < 0.05 * kept
+    # which node the cut-off split also moves a level's count within the reference's overshoot (N .. N + 2)
+    a = O.extract_rule(cfg, fr[0], 0)[0]
+    b = O.extract_rule(cfg, fr[0], 1)[0]
+    assert np.abs(np.bincount(a["octave"], minlength=8) - np.bincount(b["octave"], minlength=8)).max() <= 2
