@@ -156,7 +156,9 @@ def parse_args(argv=None):
 # ORBX_* variables the library reads (INTEGRATION.md "Environment variables").
 # Tuning: select among bit-exact code paths; allowed, and stamped into the line.
 ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_PYR_PLAN", "ORBX_QT_GENERIC",
-              "ORBX_INIT_LDS_KB", "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS"}
+              "ORBX_INIT_LDS_KB", "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS",
+              # the C++ shim's configuration (shim/src/ORBextractor.cc); bench.py does not read them
+              "ORBX_DEVICE", "ORBX_SCALE_MODE", "ORBX_PATTERN"}
 # Diagnostics: phase clocks synchronise after every launch, *_STOP / FAST_TWICE
 # skip or repeat work (they only act in -DORBX_DIAG builds), ORBX_LIB_VARIANT
 # loads an A/B build of the library. A timed region under any of them is not

@@ -36,7 +36,20 @@ constexpr int kObThreads = ORBX_OB_THREADS;  // 256: 4 waves, 8 keypoints
 constexpr int kObKps = kObThreads / 32;
 constexpr int kObRadius = 19;                // |rotated pattern offset| <= 18.4, rounded
 constexpr int kObRows = 2 * kObRadius + 1;   // 39
-constexpr int kObStride = 64;                // 4 x 16-byte chunks per staged row
+// staged row stride: the 4 x 16-byte chunks of a row, padded so that the
+// rotated pattern's byte gathers spread over the banks (bank = dword mod 32:
+// 64-byte rows put every other row on the same 16 banks)
+#ifndef ORBX_OB_STRIDE
+#define ORBX_OB_STRIDE 64
+#endif
+constexpr int kObStride = ORBX_OB_STRIDE;
+static_assert(kObStride >= 64 && kObStride % 8 == 0, "rows hold 4 chunks, 8-byte aligned");
+// IC coefficient rows in LDS: 24 dwords each, padded to an odd stride so the
+// 16 |v| rows a wave reads at once fall in distinct banks
+#ifndef ORBX_OB_ICSTRIDE
+#define ORBX_OB_ICSTRIDE 24
+#endif
+constexpr int kIcStride = ORBX_OB_ICSTRIDE;
 
 // IC_Angle coefficient dwords per |v| (0..15): byte j of dword k is column
 // u = 4k + j - 15; {u if 0 < u <= umax[|v|]}, {-u if -umax <= u < 0}, {1 if |u| <= umax}
@@ -63,7 +76,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
                                                                   int* __restrict__ out_counts) {
   __shared__ __attribute__((aligned(16))) uint8_t s_patch[kObKps][kObRows * kObStride];
   __shared__ float4 s_tests[256];
-  __shared__ uint32_t s_ictab[16 * 24];
+  __shared__ uint32_t s_ictab[16 * kIcStride];
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
   const int bx = wg % gridDim.x, f = wg / gridDim.x, tid = threadIdx.x;
   const int lane = tid & 31, hk = tid >> 5;  // keypoint of this half-wave within the workgroup
@@ -160,7 +173,10 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
     if (tid + k * kObThreads < 256) s_tests[tid + k * kObThreads] = test_v[k];
 #pragma unroll
   for (int k = 0; k < kIcPer; ++k)
-    if (tid + k * kObThreads < 16 * 24) s_ictab[tid + k * kObThreads] = ic_v[k];
+    if (tid + k * kObThreads < 16 * 24) {
+      const int i = tid + k * kObThreads;
+      s_ictab[(i / 24) * kIcStride + i % 24] = ic_v[k];
+    }
   // unpredicated stores (an empty slot writes its own unused patch, lanes past
   // the last chunk rewrite it with the same bytes), so no load waits in a branch
   {
@@ -168,7 +184,12 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
 #pragma unroll
     for (int k = 0; k < kPerLane; ++k) {
       const int i = min(lane + 32 * k, kChunks - 1), r = i >> 2, ch = i & 3;
-      *(uint4*)(dst + r * kObStride + ch * 16) = pv[k];
+      if constexpr (kObStride % 16 == 0) {
+        *(uint4*)(dst + r * kObStride + ch * 16) = pv[k];
+      } else {  // 8-byte aligned rows: two b64 stores (a misaligned b128 store replays)
+        *(uint2*)(dst + r * kObStride + ch * 16) = make_uint2(pv[k].x, pv[k].y);
+        *(uint2*)(dst + r * kObStride + ch * 16 + 8) = make_uint2(pv[k].z, pv[k].w);
+      }
     }
   }
   __syncthreads();  // staged patch, test table, IC coefficient table
@@ -179,7 +200,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   int m10 = 0, m01 = 0;
   if (valid && lane < kPatchSize) {
     const int v = lane - kHalfPatch, av = v < 0 ? -v : v;
-    const uint32_t* tp = s_ictab + av * 24;
+    const uint32_t* tp = s_ictab + av * kIcStride;
     uint32_t pos = 0, neg = 0, sum = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {

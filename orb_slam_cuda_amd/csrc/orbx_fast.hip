@@ -22,7 +22,7 @@
 // unless it is empty, and writes the keys in row-major order (the order
 // cv::FAST emits them) into the cell's fixed slot range. Every compaction is
 // an ordered ballot compaction, so row-major order is preserved throughout.
-#if (defined(ORBX_FAST_SAMEROI) || defined(ORBX_FAST_NOLOAD)) && !defined(ORBX_DIAG)
+#if (defined(ORBX_FAST_SAMEROI) || defined(ORBX_FAST_NOLOAD) || defined(ORBX_FAST_LCAP)) && !defined(ORBX_DIAG)
 #error "result-changing diagnostic switches need -DORBX_DIAG"
 #endif
 #include <algorithm>
@@ -150,10 +150,16 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
     const uint64_t m2 = __ballot(any[0].y != 0) & colm[2] & rowm, m3 = __ballot(any[1].y != 0) & colm[3] & rowm;
     int pos = n1 + mbcnt64(m0) + mbcnt64(m1) + mbcnt64(m2) + mbcnt64(m3);
     const uint16_t e = (uint16_t)((by << 8) | x);
-    if ((m0 >> lane) & 1) list[pos++] = e;
-    if ((m1 >> lane) & 1) list[pos++] = (uint16_t)(e + 1);
-    if ((m2 >> lane) & 1) list[pos++] = (uint16_t)(e + 2);
-    if ((m3 >> lane) & 1) list[pos] = (uint16_t)(e + 3);
+#ifdef ORBX_FAST_LCAP  // timing experiment (diagnostics builds): a capped list, results incomplete
+#define LIST_AT(i) list[min((i), ORBX_FAST_LCAP - 1)]
+#else
+#define LIST_AT(i) list[i]
+#endif
+    if ((m0 >> lane) & 1) LIST_AT(pos++) = e;
+    if ((m1 >> lane) & 1) LIST_AT(pos++) = (uint16_t)(e + 1);
+    if ((m2 >> lane) & 1) LIST_AT(pos++) = (uint16_t)(e + 2);
+    if ((m3 >> lane) & 1) LIST_AT(pos) = (uint16_t)(e + 3);
+#undef LIST_AT
     n1 += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
   }
   return n1;
@@ -302,6 +308,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
       case 2: n1 = compass4<2>(roi, list, bw, bh, t, lane); break;
       default: n1 = compass4<3>(roi, list, bw, bh, t, lane); break;
     }
+#ifdef ORBX_FAST_LCAP
+    n1 = min(n1, ORBX_FAST_LCAP);
+#endif
   } else {
     // four row groups per step so their LDS reads are in flight together
     for (int by0 = 0; by0 < bh; by0 += 4 * rstep) {
@@ -444,8 +453,13 @@ size_t fast_lds_bytes(const ExtractParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t band = (size_t)P.fast_bw_max * P.fast_bh_max;
   const int stride = fast_tight(P) ? kRoiTight : kRoiWide;
+#ifdef ORBX_FAST_LCAP
+  const size_t list = std::min(band, (size_t)ORBX_FAST_LCAP);
+#else
+  const size_t list = band;
+#endif
   return r16(std::max((size_t)P.fast_rh_max * stride, 16 * ((band + 63) / 64))) +
-         r16((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1) + r16(2 * band);
+         r16((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1) + r16(2 * list);
 }
 
 int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cells, uint32_t* slots,

@@ -8,6 +8,8 @@
 //
 //   orbx_shim_driver --version
 //   orbx_shim_driver FRAMES.u8 NFRAMES W H VOC.txt|- OUTDIR
+//   orbx_shim_driver --scene SCENE.bin OUT.bin   (one ORBmatcher method on a test scene, scene.cc)
+//   orbx_shim_driver --stereo LEFT.u8 RIGHT.u8 W H BF OUTDIR   (stereo Frame + ComputeStereoMatches)
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -39,10 +41,51 @@ static std::vector<int> ids(const std::vector<MapPoint*>& v) {
   return r;
 }
 
+int run_scene(const std::string& in, const std::string& out);  // scene.cc
+
+// The stereo Frame constructor (src/Frame.cc:60-128): two extractors, left
+// and right extraction, ComputeStereoMatches; writes the left keypoints,
+// descriptors, mvuRight and mvDepth.
+static int run_stereo(const char* left, const char* right, int W, int H, float bf, const std::string& out) {
+  std::vector<uint8_t> L((size_t)W * H), R((size_t)W * H);
+  for (auto& lr : {std::make_pair(left, &L), std::make_pair(right, &R)}) {
+    FILE* f = fopen(lr.first, "rb");
+    if (!f || fread(lr.second->data(), 1, lr.second->size(), f) != lr.second->size()) {
+      fprintf(stderr, "cannot read %s\n", lr.first);
+      return 2;
+    }
+    fclose(f);
+  }
+  ORBextractor left_ext(2000, 1.2f, 8, 20, 7, W, H), right_ext(2000, 1.2f, 8, 20, 7, W, H);
+  // Frame::fx from K (src/Frame.cc:103-108): the KITTI calibration
+  Frame::fx = 718.856f;
+  Frame::fy = 718.856f;
+  Frame::cx = 607.1928f;
+  Frame::cy = 185.2157f;
+  Frame::invfx = 1.0f / Frame::fx;
+  Frame::invfy = 1.0f / Frame::fy;
+  Frame F(cv::Mat(H, W, CV_8U, L.data(), W), cv::Mat(H, W, CV_8U, R.data(), W), &left_ext, &right_ext, nullptr, bf);
+  write_file(out + "/kpL.bin", F.mvKeys.data(), F.mvKeys.size() * sizeof(cv::KeyPoint));
+  write_file(out + "/kpR.bin", F.mvKeysRight.data(), F.mvKeysRight.size() * sizeof(cv::KeyPoint));
+  write_file(out + "/uright.bin", F.mvuRight.data(), F.mvuRight.size() * 4);
+  write_file(out + "/depth.bin", F.mvDepth.data(), F.mvDepth.size() * 4);
+  const float mb = F.mb;
+  write_file(out + "/mb.bin", &mb, 4);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc == 2 && std::string(argv[1]) == "--version") {
     printf("%s\n", orbx_version());
     return 0;
+  }
+  try {
+    if (argc == 4 && std::string(argv[1]) == "--scene") return run_scene(argv[2], argv[3]);
+    if (argc == 8 && std::string(argv[1]) == "--stereo")
+      return run_stereo(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), (float)atof(argv[6]), argv[7]);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "error: %s\n", e.what());
+    return 4;
   }
   if (argc != 7) {
     fprintf(stderr, "usage: %s FRAMES.u8 NFRAMES W H VOC.txt|- OUTDIR\n", argv[0]);

@@ -41,6 +41,10 @@ class ORBextractor {
   // GetTime records ("Pyramid/Resize", "FAST+Grid", ...).
   int GetStageTimes(std::vector<float>& ms, std::vector<const char*>& names);
 
+  // The liborbx handle (its device pyramid of the last call is what
+  // Frame::ComputeStereoMatches reads through orbm_compute_stereo_matches).
+  orbx_handle handle() const { return h_; }
+
  protected:
   int nfeatures;
   double scaleFactor;

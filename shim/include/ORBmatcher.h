@@ -1,9 +1,13 @@
 // Source-compatible replacement for the reference's include/ORBmatcher.h
-// (:36-110). Every public member is declared as in the reference; this shim
-// implements DescriptorDistance, SearchForInitialization and both SearchByBoW
-// overloads over liborbx (src/ORBmatcher.cc here). The projection, fusion,
-// Sim3 and triangulation members follow INTEGRATION.md §3 over the same
-// C-ABI and need the reference's MapPoint/KeyFrame, so they are declared only.
+// (:36-110). Every public member is declared as in the reference and defined
+// over liborbx in src/ORBmatcher.cc here: DescriptorDistance,
+// SearchForInitialization, both SearchByBoW overloads, the four
+// SearchByProjection overloads, SearchForTriangulation, SearchBySim3 and both
+// Fuse overloads (whose map mutations run in the reference's order on the
+// host). Additions, none of which changes a caller: Handle() (the calling
+// thread's device workspace, also used by Frame::ComputeStereoMatches) and a
+// private record builder that reads MapPoint::mfMinDistance / mfMaxDistance
+// (a real build adds `friend class ORBmatcher;` to MapPoint).
 #ifndef ORBMATCHER_H
 #define ORBMATCHER_H
 
@@ -13,6 +17,8 @@
 
 #include <opencv2/core/core.hpp>
 #include <opencv2/features2d/features2d.hpp>
+
+#include "orbx_c.h"
 
 #include "Frame.h"
 #include "KeyFrame.h"
@@ -53,9 +59,18 @@ class ORBmatcher {
   static const int TH_HIGH;
   static const int HISTO_LENGTH;
 
+  // liborbx matcher workspace of the calling thread (Tracking, LocalMapping
+  // and LoopClosing each run their own); the device is ORBX_DEVICE (default 0)
+  static orbm_handle Handle();
+
  protected:
   float mfNNratio;
   bool mbCheckOrientation;
+
+ private:
+  // orbm_map_point_world of a MapPoint (GetWorldPos, GetNormal, mfMinDistance,
+  // mfMaxDistance, Observations() > 0) for the pose-projection searches
+  static orbm_map_point_world MapPointRecord(MapPoint* pMP, float angle, int octave, bool valid);
 };
 
 }  // namespace ORB_SLAM2

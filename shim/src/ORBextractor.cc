@@ -2,6 +2,7 @@
 // (constructor :496-560, operator() :1538-1548 / CPU branch :1710-1808).
 #include "ORBextractor.h"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -25,10 +26,25 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
   c.min_th_fast = _minThFAST;
   c.width = width;
   c.height = height;
-  c.device = 0;
+  // Device and parity modes, read once per extractor (environment table):
+  //   ORBX_DEVICE      HIP device (default 0)
+  //   ORBX_SCALE_MODE  U = the 1.2^l geometry (default; the reference's own map.yml was
+  //                    written with it, tests/test_pins.py) or F = the fork's buildGraph
+  //                    override of the scale tables (src/ORBextractor.cc:674-680)
+  //   ORBX_PATTERN     fork = bit_pattern_31_ with the fork's entry 96 (default) or upstream
+  const char* dev = getenv("ORBX_DEVICE");
+  const char* sm = getenv("ORBX_SCALE_MODE");
+  const char* pm = getenv("ORBX_PATTERN");
+  c.device = dev ? atoi(dev) : 0;
   c.max_batch = 1;
   c.scale_mode = ORBX_SCALE_U;
+  if (sm && (sm[0] == 'F' || sm[0] == 'f' || sm[0] == '1')) c.scale_mode = ORBX_SCALE_F;
+  else if (sm && !(sm[0] == 'U' || sm[0] == 'u' || sm[0] == '0'))
+    throw std::runtime_error(std::string("ORBX_SCALE_MODE must be U or F, not ") + sm);
   c.pattern_mode = ORBX_PATTERN_FORK;
+  if (pm && std::string(pm) == "upstream") c.pattern_mode = ORBX_PATTERN_UPSTREAM;
+  else if (pm && std::string(pm) != "fork")
+    throw std::runtime_error(std::string("ORBX_PATTERN must be fork or upstream, not ") + pm);
   orbx_check(orbx_create(&c, &h_));
   mvScaleFactor.resize(nlevels);
   mvInvScaleFactor.resize(nlevels);

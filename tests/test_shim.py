@@ -99,3 +99,118 @@ def test_shim_host_matches_oracle(pkg, O, tmp_path):
     rout, rnm = O.search_by_bow(d1, k1["angle"], good(k1), fv[0], d2, k2["angle"], good(k2), fv[1], 0.75, True, True)
     got = np.fromfile(out / "bow_kf_kf.bin", dtype=np.int32)
     assert got[0] == rnm > 20 and np.array_equal(got[1:], rout)
+
+
+# ------------------------------------------------------------ scene mode
+SCENES = [("local_map", dict(seed=1)), ("local_map", dict(seed=2, th=1.0, ratio=0.9, stereo=False)),
+          ("last_frame", dict(seed=1)), ("last_frame", dict(seed=2, stereo=False, motion="none")),
+          ("keyframe", dict(seed=1)), ("keyframe", dict(seed=2, th=3.0, orb_dist=64)),
+          ("sim3", dict(seed=1)), ("sim3", dict(seed=2, th=5, s=0.7)),
+          ("fuse", dict(seed=1)), ("fuse", dict(seed=2, th=5.0)),
+          ("fuse_sim3", dict(seed=1)), ("sim3_match", dict(seed=1)), ("sim3_match", dict(seed=2, s12=1.08)),
+          ("triangulation", dict(seed=1)), ("triangulation", dict(seed=2, only_stereo=True))]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("op,kw", SCENES, ids=[f"{o}-{i}" for i, (o, _) in enumerate(SCENES)])
+def test_shim_matcher_methods_match_oracle(pkg, O, tmp_path, op, kw):
+    """Every ORBmatcher method through the compiled drop-in shim, called on
+    reference-typed Frames / KeyFrames / MapPoints as Tracking, LocalMapping
+    and LoopClosing call it (shim/host/scene.cc), against the oracle's result
+    translated into the pointer state the reference leaves (tests/shimscene.py)."""
+    import shimscene
+    assert os.path.exists(DRIVER), "build the shim first (make -C shim / __graft_entry__.build())"
+    recs, want = getattr(shimscene, op)(O, **kw)
+    scene, out = tmp_path / "scene.bin", tmp_path / "out.bin"
+    shimscene.write_scene(scene, recs)
+    r = subprocess.run([DRIVER, "--scene", str(scene), str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(out, dtype=np.int32)
+    assert got[0] == want[0], (op, got[0], want[0])
+    assert np.array_equal(got, want), (op, np.nonzero(got[:len(want)] != want[:len(got)])[0][:10])
+    assert want[0] > 20  # the scene exercises the method
+
+
+@pytest.mark.gpu
+def test_shim_stereo_frame_matches_oracle(pkg, O, tmp_path):
+    """The stereo Frame constructor through the shim: two ORBextractors, then
+    Frame::ComputeStereoMatches (src/Frame.cc:60-128, 465-639) over
+    orbm_compute_stereo_matches, against the oracle's extraction + stereo matching."""
+    from orb_slam_cuda_amd.synth import stereo_pair
+    assert os.path.exists(DRIVER)
+    W, H, bf = 1241, 376, 0.54 * 718.856
+    L, R = stereo_pair(21, W, H)
+    lp, rp = tmp_path / "l.u8", tmp_path / "r.u8"
+    np.ascontiguousarray(L).tofile(lp)
+    np.ascontiguousarray(R).tofile(rp)
+    r = subprocess.run([DRIVER, "--stereo", str(lp), str(rp), str(W), str(H), repr(bf), str(tmp_path)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    cfg = O.config(nfeatures=2000, width=W, height=H)
+    kl, dl = O.extract(cfg, L)
+    kr, dr = O.extract(cfg, R)
+    assert np.array_equal(np.fromfile(tmp_path / "kpL.bin", dtype=kl.dtype).view(np.uint8), kl.view(np.uint8))
+    assert np.array_equal(np.fromfile(tmp_path / "kpR.bin", dtype=kr.dtype).view(np.uint8), kr.view(np.uint8))
+    mb = np.fromfile(tmp_path / "mb.bin", dtype=np.float32)[0]
+    assert mb == np.float32(bf) / np.float32(718.856)
+    info = O.level_info(cfg)
+    ru, rd, rk = O.compute_stereo_matches(kl, dl, kr, dr, O.pyramid(cfg, L), O.pyramid(cfg, R), info["scale"],
+                                          info["inv_scale"], mb, np.float32(bf))
+    u = np.fromfile(tmp_path / "uright.bin", dtype=np.float32)
+    d = np.fromfile(tmp_path / "depth.bin", dtype=np.float32)
+    assert np.array_equal(u, ru) and np.array_equal(d, rd) and rk > 100
+
+
+def test_shim_defines_every_reference_method():
+    """No ORBmatcher method of the reference header is declared without a
+    definition in the shim (each appears as ORBmatcher::Name in src/ORBmatcher.cc)."""
+    text = open(os.path.join(SHIM, "include", "ORBmatcher.h")).read()
+    body = open(os.path.join(SHIM, "src", "ORBmatcher.cc")).read()
+    declared = set(re.findall(r"\b(Search\w+|Fuse|DescriptorDistance)\s*\(", text))
+    for name in declared:
+        assert f"ORBmatcher::{name}(" in body, name
+    # overload counts: 4 SearchByProjection, 2 SearchByBoW, 2 Fuse
+    for name, k in (("SearchByProjection", 4), ("SearchByBoW", 2), ("Fuse", 2)):
+        assert body.count(f"int ORBmatcher::{name}(") == k, name
+    assert "void Frame::ComputeStereoMatches()" in open(os.path.join(SHIM, "src", "Frame.cc")).read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,pattern", [("F", "fork"), ("U", "upstream")])
+def test_shim_extractor_modes_from_environment(pkg, O, tmp_path, mode, pattern):
+    """The shim's ORBextractor reads ORBX_SCALE_MODE / ORBX_PATTERN / ORBX_DEVICE
+    once in its constructor (shim/src/ORBextractor.cc): mode F (the fork's
+    buildGraph scale override, src/ORBextractor.cc:674-680) and the upstream
+    pattern through operator() against the oracle in the same modes."""
+    from orb_slam_cuda_amd.synth import SynthSequence
+    W, H, n = 1241, 376, 1
+    frames = SynthSequence(9, W, H).frames(n)
+    fpath = tmp_path / "frames.u8"
+    frames.tofile(fpath)
+    out = tmp_path / "out"
+    out.mkdir()
+    env = dict(os.environ, ORBX_SCALE_MODE=mode, ORBX_PATTERN=pattern, ORBX_DEVICE="0")
+    r = subprocess.run([DRIVER, str(fpath), str(n), str(W), str(H), "-", str(out)], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    cfg = O.config(nfeatures=2000, width=W, height=H, scale_mode=1 if mode == "F" else 0,
+                   pattern_mode=1 if pattern == "upstream" else 0)
+    rkp, rdesc = O.extract(cfg, frames[0])
+    kp = np.fromfile(out / "kp0.bin", dtype=rkp.dtype)
+    desc = np.fromfile(out / "desc0.bin", dtype=np.uint8).reshape(-1, 32)
+    assert len(kp) == len(rkp) > 1000
+    assert np.array_equal(kp.view(np.uint8), rkp.view(np.uint8)) and np.array_equal(desc, rdesc)
+    if mode == "F":  # level sizes differ from mode U: the override really took effect
+        lvl = O.pyramid_level(cfg, frames[0], 1)
+        assert lvl.shape != O.pyramid_level(O.config(), frames[0], 1).shape
+
+
+def test_shim_rejects_unknown_scale_mode(tmp_path):
+    _build()
+    frames = np.zeros((1, 64, 64), np.uint8)
+    fpath = tmp_path / "f.u8"
+    frames.tofile(fpath)
+    env = dict(os.environ, ORBX_SCALE_MODE="Q")
+    r = subprocess.run([DRIVER, str(fpath), "1", "64", "64", "-", str(tmp_path)], capture_output=True, text=True,
+                       timeout=60, env=env)
+    assert r.returncode != 0 and "ORBX_SCALE_MODE" in r.stderr
