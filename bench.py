@@ -146,6 +146,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-host-stream", action="store_true", help="skip the host-streamed throughput leg")
     ap.add_argument("--host-steps", type=int, default=30, help="timed steps of the host-streamed leg")
     ap.add_argument("--spawn", action="store_true", help="use the worker launcher even for --gpus 1")
+    ap.add_argument("--split-sequence", action="store_true",
+                    help="split ONE synthetic sequence (pool x N frames) into contiguous blocks, one per GPU; "
+                         "each rank extracts the frame before its block itself for the boundary pair (SURVEY §8(e))")
+    ap.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)  # tests: every rank on device 0
+    ap.add_argument("--dump-pairs", default=None, help=argparse.SUPPRESS)  # tests: rank r saves batch 0's outputs
     ap.add_argument("--allow-diag", action="store_true",
                     help="run even with diagnostic ORBX_* variables set (phase clocks, library variants); "
                          "the line then carries them and is not a valid measurement")
@@ -220,7 +225,7 @@ def launch(args, argv) -> int:
     call); returns the first non-zero worker exit code, or 0."""
     import multiprocessing as mp
     N = args.gpus
-    if not args.stub_worker:
+    if not args.stub_worker and not args.share_device:
         n = visible_gpus()
         if N > n:
             raise SystemExit(f"bench.py: --gpus {N} but only {n} GPU(s) visible; refusing to oversubscribe")
@@ -284,6 +289,8 @@ def worker(args):
                              "rebuild without -DORBX_DIAG or pass --allow-diag")
         args.audit = {"orbx_env": audit_env(args.allow_diag), "library": lib_info}
         ndev = _lib.device_count()
+        if args.share_device:
+            local = 0  # tests only: several ranks on one device
         if local >= ndev:
             raise SystemExit(f"bench.py: rank {rank} needs device {local}, only {ndev} visible")
         # the device is selected before ANY allocation, stream or event of this process
@@ -325,7 +332,7 @@ class MonoPipeline:
 
     NS = 3  # output sets: batch k writes set k % 3
 
-    def __init__(self, args, cfg, local, frames_pool, host=False, need_events=True):
+    def __init__(self, args, cfg, local, frames_pool, host=False, need_events=True, boundary=False, halo=None):
         import orb_slam_cuda_amd as pkg
         from orb_slam_cuda_amd import _lib
         self.args, self.cfg, self.host = args, cfg, host
@@ -402,6 +409,21 @@ class MonoPipeline:
                 self.d_bow_out, self.d_bow_nm = DA(B * cap * 4), DA(B * 4)
         self.need_events = need_events
         self.ev = {}
+        # --split-sequence: the first batch of every pass over the pool gets its
+        # slot 0 (frame t-1 of the block's first frame) by extracting the frame
+        # before the block (`halo`) on the matching stream, or an empty frame for
+        # the sequence's first block, instead of the carry of the pool's last frame
+        self.boundary = boundary and not host
+        if self.boundary:
+            self.halo_ext = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=1)
+            self.d_halo = None
+            if halo is not None:
+                hb = np.zeros((H, pitch), np.uint8)
+                hb[:, :W] = halo
+                self.d_halo = DA(self.fbytes)
+                self.d_halo.upload(hb)
+            self.d_zero = DA(16)
+            self.d_zero.zero()
 
     def _event(self, name, k):
         e = self.ev.get((name, k))
@@ -473,7 +495,11 @@ class MonoPipeline:
             check(L.orbx_memcpy_dtod_async(vp(self.d_counts[nb].ptr), vp(self.d_counts[b].ptr + B * 4), 4, st.s))
 
         s_match, s_init = self.s_match, self.s_init
-        if a.carry == "ext" or a.serial:
+        if self.boundary and k == 0:
+            self.first_slot(0, s_match)  # batch 0's slot 0, ahead of its matching on this stream
+        if self.boundary and (k + 1) % self.nbatches == 0:
+            pass  # the next batch starts a pass over the pool: its slot 0 is the boundary frame (below)
+        elif a.carry == "ext" or a.serial:
             # slot 0 of set (k+1) % 3 was last read by matching k-2
             if k >= 2 and not a.serial:
                 self.s_ext.wait(self.ev_done[k - 2])
@@ -481,7 +507,12 @@ class MonoPipeline:
         self.ev_ext[k].record(self.s_ext)
         if not a.serial:
             s_match.wait(self.ev_ext[k])
-        if a.carry == "match" and not a.serial:
+        if self.boundary and (k + 1) % self.nbatches == 0:
+            if self.two_match and k >= 2:
+                s_match.wait(self.ev_done2[k - 2])
+            self.first_slot(nb, s_match)  # in order after matching k-2, the last reader of set (k+1) % 3
+            self.ev_carry[k].record(s_match)
+        elif a.carry == "match" and not a.serial:
             if self.two_match and k >= 2:
                 s_match.wait(self.ev_done2[k - 2])  # SearchForInitialization k-2 also read set (k+1) % 3
             carry(s_match)  # in order after matching k-2, the last reader of set (k+1) % 3
@@ -551,6 +582,17 @@ class MonoPipeline:
                 cp(self.h_nm[b].ptr, self.d_nm[b].ptr, B * 4)
             self.ev_out[k].record(d2h)
 
+    def first_slot(self, b, st):
+        """Slot 0 of output set b for a block's first batch: the boundary frame's
+        keypoints, descriptors and count (extracted here), or count 0."""
+        vp = C.c_void_p
+        if self.d_halo is None:
+            self.check(self.L.orbx_memcpy_dtod_async(vp(self.d_counts[b].ptr), vp(self.d_zero.ptr), 4, st.s))
+            return
+        self.check(self.L.orbx_extract_batch(self.halo_ext.handle, vp(self.d_halo.ptr), 1, self.fbytes, self.pitch,
+                                             vp(self.d_kps[b].ptr), vp(self.d_desc[b].ptr), vp(self.d_counts[b].ptr),
+                                             st.s))
+
     def sync_all(self):
         for se in self.s_exts:
             se.synchronize()
@@ -595,15 +637,25 @@ class MonoPipeline:
 
 def run_mono(args, cfg, rank, world, local, dist):
     from orb_slam_cuda_amd import sharding
-    from orb_slam_cuda_amd.synth import SynthSequence
+    from orb_slam_cuda_amd.synth import SynthSequence, SynthStream
     W, H, NF, B = cfg["W"], cfg["H"], cfg["nfeatures"], args.batch
     pool = max(B, (args.pool // B) * B)
-    frames = SynthSequence(sharding.sequence_seed(rank), W, H).frames(pool)
-    pipe = MonoPipeline(args, cfg, local, frames)
+    halo = None
+    if args.split_sequence:
+        # ONE sequence of pool x world frames; this rank's pool is its block
+        stream = SynthStream(sharding.sequence_seed(0), W, H)
+        block, prev = sharding.split_sequence(pool * world, rank, world)
+        frames = stream.frames(block)
+        halo = stream.frame(prev) if prev is not None else None
+    else:
+        frames = SynthSequence(sharding.sequence_seed(rank), W, H).frames(pool)
+    pipe = MonoPipeline(args, cfg, local, frames, boundary=args.split_sequence, halo=halo)
     SUB = max(1, args.batches_per_step)
     wall_rank, issue = pipe.run(args.warmup * SUB, args.steps * SUB, dist)
     agg = aggregate(B * SUB * args.steps, wall_rank, dist, world)
     pipe.check_status()
+    if args.dump_pairs:
+        dump_batch0(args, pipe, rank, block if args.split_sequence else None, prev if args.split_sequence else None)
     BS, S, cap = pipe.BS, pipe.S, pipe.cap
     timed = pipe.evsets[args.warmup * SUB:]
     ev_ms = timed[0][0].elapsed_ms(timed[-1][8])
@@ -697,6 +749,8 @@ def run_mono(args, cfg, rank, world, local, dist):
 
     if rank == 0:
         workload = (cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only")
+        if args.split_sequence:
+            workload += f"; ONE sequence of {pool * world} frames split into {world} contiguous blocks"
         out = {
             "metric": METRIC, "value": round(agg["value"], 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(agg["wall"] / args.steps * 1e3, 4),
@@ -708,7 +762,8 @@ def run_mono(args, cfg, rank, world, local, dist):
                        "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
                        "frames_per_step_per_gpu": B * SUB, "batches_per_step": SUB, "frames_per_batch": B,
                        "resident_pool_frames": pool,
-                       "parallelism": f"frame-sharded x{world}, one process per GPU, no collectives",
+                       "parallelism": (f"sequence split x{world} (contiguous blocks, boundary frame re-extracted per rank)"
+                                       if args.split_sequence else f"frame-sharded x{world}") + ", one process per GPU, no collectives",
                        "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS,
                        "match_stream_priority": ("low" if args.priority else "high" if args.match_priority
                                                  else "normal")},
@@ -732,6 +787,25 @@ def run_mono(args, cfg, rank, world, local, dist):
             **args.audit,
         }
         print(json.dumps(out), flush=True)
+
+
+def dump_batch0(args, pipe, rank, block, prev):
+    """Tests only (--dump-pairs DIR): batch 0's outputs of this rank (the run
+    must be one batch long so that output set 0 still holds them)."""
+    import orb_slam_cuda_amd as pkg
+    B, cap = pipe.B, pipe.cap
+    if pipe.total != 1:
+        raise SystemExit("--dump-pairs needs exactly one batch (--steps 1 --warmup 0 --batches-per-step 1)")
+    os.makedirs(args.dump_pairs, exist_ok=True)
+    np.savez(os.path.join(args.dump_pairs, f"rank{rank}.npz"),
+             counts=pipe.d_counts[0].download(B + 1, np.int32),
+             kps=pipe.d_kps[0].download((B + 1) * cap, pkg.KP_DTYPE).reshape(B + 1, cap),
+             desc=pipe.d_desc[0].download((B + 1, cap, 32), np.uint8),
+             m12=pipe.d_m12[0].download((B, cap), np.int32), nm=pipe.d_nm[0].download(B, np.int32),
+             bi=pipe.d_bi[0].download((B, cap), np.int32), bd=pipe.d_bd[0].download((B, cap), np.int32),
+             sd=pipe.d_sd[0].download((B, cap), np.int32),
+             block=np.array([block.start, block.stop] if block is not None else [-1, -1]),
+             prev=np.array([-1 if prev is None else prev]))
 
 
 SQ_LAUNCH_FRAMES = 32   # frames per extraction launch of the committed SQ counter run

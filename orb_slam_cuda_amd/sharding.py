@@ -30,6 +30,17 @@ def boundary_frame(block: range) -> int | None:
     return block.start - 1 if block.start > 0 else None
 
 
+def split_sequence(n_frames: int, rank: int, world: int) -> tuple[range, int | None]:
+    """ONE sequence of n_frames split over `world` ranks (bench.py
+    --split-sequence): the rank's contiguous block and the
+    frame t-1 its first pair needs from the block before (None for rank 0).
+    One process per GPU holds no other rank's device memory, so the rank
+    extracts that boundary frame itself (one extra frame per block) instead of
+    receiving its descriptors from rank - 1: no data-path exchange."""
+    block = shard_frames(n_frames, rank, world)
+    return block, boundary_frame(block)
+
+
 def sequence_seed(rank: int, base: int = 1000) -> int:
     """Seed of the synthetic sequence a rank streams in the benchmark (one per GPU, C5)."""
     return base + rank

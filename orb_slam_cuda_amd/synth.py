@@ -108,6 +108,49 @@ class SynthSequence:
         return out
 
 
+class SynthStream:
+    """A random-access synthetic sequence for splitting ONE sequence across
+    ranks (bench.py --split-sequence): frame t is the window of the walk at t
+    over one canvas with its own noise, so any rank renders its block (and the
+    t-1 frame before it) without rendering the frames of the ranks before it.
+    The walk (integer shifts in [-8, 8], reflected at the canvas edge, as
+    SynthSequence) comes from its own generator, two draws per frame; the
+    noise of frame t from default_rng((seed, t))."""
+
+    MARGIN = SynthSequence.MARGIN
+
+    def __init__(self, seed: int, W: int = KITTI_WH[0], H: int = KITTI_WH[1]):
+        self.seed, self.W, self.H = seed, W, H
+        self.canvas = _paint_canvas(np.random.default_rng(seed), W + 2 * self.MARGIN, H + 2 * self.MARGIN)
+        self._walk = [(self.MARGIN, self.MARGIN)]
+        self._wrng = np.random.default_rng((seed, 1 << 30))
+
+    def origin(self, t: int) -> tuple[int, int]:
+        M = self.MARGIN
+        while len(self._walk) <= t:
+            ox, oy = self._walk[-1]
+            dx, dy = (int(v) for v in self._wrng.integers(-8, 9, size=2))
+            if not 0 <= ox + dx <= 2 * M:
+                dx = -dx
+            if not 0 <= oy + dy <= 2 * M:
+                dy = -dy
+            self._walk.append((ox + dx, oy + dy))
+        return self._walk[t]
+
+    def frame(self, t: int) -> np.ndarray:
+        ox, oy = self.origin(t)
+        win = self.canvas[oy:oy + self.H, ox:ox + self.W]
+        noisy = win + np.random.default_rng((self.seed, t)).integers(-6, 7, size=win.shape)
+        return np.clip(np.rint(noisy), 0, 255).astype(np.uint8)
+
+    def frames(self, idx) -> np.ndarray:
+        idx = list(idx)
+        out = np.empty((len(idx), self.H, self.W), np.uint8)
+        for i, t in enumerate(idx):
+            out[i] = self.frame(t)
+        return out
+
+
 def stereo_pair(seed: int, W: int = KITTI_WH[0], H: int = KITTI_WH[1]) -> tuple[np.ndarray, np.ndarray]:
     """Rectified left/right pair: the right image sees the scene shifted left
     by a disparity d in [5, 40] (a point at column u in the left image is at

@@ -51,3 +51,39 @@ def test_bench_euroc_and_extract_only():
 def test_bench_stereo():
     out = _bench(["--config", "stereo", "--steps", "3", "--warmup", "1", "--batch", "16", "--cpu-sample", "0"])
     assert out["unit"] == "stereo pairs/s" and out["stereo_matches_per_pair"] > 100
+
+
+def test_split_sequence_boundary_pair_two_ranks(O, tmp_path):
+    """bench.py --split-sequence with two ranks (both on device 0, a test-only
+    flag) through the spawned-worker launcher: ONE sequence of 128 frames,
+    rank 1's block starts at frame 64, and its first pair (frame 63 -> 64), whose
+    t-1 frame rank 1 extracts itself, must match the oracle exactly: keypoints,
+    descriptors, dense top-2 and SearchForInitialization (src/ORBmatcher.cc:405-520).
+    Rank 0's first frame has no predecessor (count 0, no matches)."""
+    import numpy as np
+    from orb_slam_cuda_amd.synth import SynthStream
+    out = _bench(["--gpus", "2", "--spawn", "--share-device", "--split-sequence", "--steps", "1", "--warmup", "0",
+                  "--batches-per-step", "1", "--pool", "64", "--dump-pairs", str(tmp_path), "--cpu-sample", "0",
+                  "--no-latency", "--no-host-stream"])
+    assert out["n_gpus"] == 2 and "split" in out["config"]["parallelism"]
+    W, H = 1241, 376
+    stream = SynthStream(1000, W, H)
+    cfg = O.config(nfeatures=2000, width=W, height=H)
+    r0 = np.load(tmp_path / "rank0.npz")
+    r1 = np.load(tmp_path / "rank1.npz")
+    assert list(r0["block"]) == [0, 64] and list(r1["block"]) == [64, 128] and int(r1["prev"][0]) == 63
+    assert r0["counts"][0] == 0 and r0["nm"][0] == 0
+    for pair in (0, 1, 37):  # the boundary pair and two interior ones of rank 1
+        fa, fb = 63 + pair, 64 + pair
+        k1, d1 = O.extract(cfg, stream.frame(fa))
+        k2, d2 = O.extract(cfg, stream.frame(fb))
+        n1, n2 = r1["counts"][pair], r1["counts"][pair + 1]
+        assert n1 == len(k1) and n2 == len(k2)
+        assert np.array_equal(r1["kps"][pair, :n1].view(np.uint8), k1.view(np.uint8))
+        assert np.array_equal(r1["desc"][pair + 1, :n2], d2)
+        ri, rd, rs = O.hamming_top2(d2, d1)
+        assert np.array_equal(r1["bi"][pair, :n2], ri) and np.array_equal(r1["bd"][pair, :n2], rd)
+        assert np.array_equal(r1["sd"][pair, :n2], rs)
+        r12, rnm, _ = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), np.stack([k1["x"], k1["y"]], 1),
+                                                  100, 0.9, True)
+        assert r1["nm"][pair] == rnm > 20 and np.array_equal(r1["m12"][pair, :n1], r12)

@@ -60,3 +60,53 @@ def test_shard_frames_partition():
             assert np.array_equal(cat, np.arange(n))
             sizes = [len(b) for b in blocks]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _split_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import hashlib
+    from orb_slam_cuda_amd import sharding
+    from orb_slam_cuda_amd.synth import SynthStream
+    dist = sharding.init_control_plane()
+    r, w, _ = sharding.rank_info()
+    block, prev = sharding.split_sequence(12, r, w)  # bench.py --split-sequence: pool x world frames
+    s = SynthStream(sharding.sequence_seed(0), 160, 120)
+    h = lambda a: hashlib.sha1(np.ascontiguousarray(a).tobytes()).hexdigest()
+    mine = [h(f) for f in s.frames(block)]
+    halo = h(s.frame(prev)) if prev is not None else None
+    everyone = [None] * w
+    dist.all_gather_object(everyone, (r, block.start, block.stop, prev, mine, halo))
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put(everyone)
+
+
+def test_split_sequence_blocks_and_boundary_frames():
+    """--split-sequence bookkeeping with world_size 2 on gloo: the ranks' blocks
+    tile ONE sequence, and the boundary frame rank 1 renders for its first pair
+    is byte-identical to the last frame of rank 0's block (frames from
+    SynthStream are random-access and rank-independent)."""
+    pytest.importorskip("torch")
+    import multiprocessing as mp
+    from orb_slam_cuda_amd.synth import SynthStream
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_split_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    (r0, a0, b0, p0, m0, h0), (r1, a1, b1, p1, m1, h1) = res[0]
+    assert (a0, b0, p0) == (0, 6, None) and (a1, b1, p1) == (6, 12, 5)
+    assert h0 is None and h1 == m0[-1]
+    assert len(set(m0 + m1)) == 12
+    # the stream is the same sequence whoever renders it, in any order
+    s = SynthStream(1000, 160, 120)
+    later_first = s.frames([7, 2])
+    fresh = SynthStream(1000, 160, 120)
+    assert np.array_equal(later_first[1], fresh.frame(2)) and np.array_equal(later_first[0], fresh.frame(7))
