@@ -5,7 +5,7 @@
 // the oracle:
 //   op 1 SearchByProjection(F, vpMapPoints, th)           Tracking.cc:1277
 //   op 2 SearchByProjection(CurrentFrame, LastFrame, ...)  Tracking.cc:962, 968
-//   op 3 SearchByProjection(CurrentFrame, pKF, found, ...) Tracking.cc:1515
+//   op 3 SearchByProjection(CurrentFrame, pKF, found, ...) Tracking.cc:1540, 1554
 //   op 4 SearchByProjection(pKF, Scw, vpPoints, vpMatched) LoopClosing.cc:414
 //   op 5 Fuse(pKF, vpMapPoints, th)                       LocalMapping.cc:525, 550
 //   op 6 Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)     LoopClosing.cc:654

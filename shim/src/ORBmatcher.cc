@@ -195,7 +195,7 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
   return n;
 }
 
-// SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (:1472-1599): Tracking::Relocalization (Tracking.cc:1515)
+// SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (:1472-1599): Tracking::Relocalization (Tracking.cc:1540, 1554)
 int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
                                    const float th, const int ORBdist) {
   const std::vector<MapPoint*> vpMPs = pKF->GetMapPointMatches();
