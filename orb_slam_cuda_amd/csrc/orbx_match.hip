@@ -486,6 +486,9 @@ struct BowSide {
 #ifndef ORBX_BOW_GROUPS
 #define ORBX_BOW_GROUPS 8
 #endif
+#ifndef ORBX_BOW_BALANCE
+#define ORBX_BOW_BALANCE 1  // node ranges of equal estimated work (0: equal node counts)
+#endif
 constexpr int kBowGroups = ORBX_BOW_GROUPS;  // workgroups per pair (node ranges)
 constexpr int kBowThreads = 256;
 constexpr int kBowK = 8;         // smallest keys kept per A row
@@ -541,7 +544,65 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
   const int p = blockIdx.x / G, g = blockIdx.x - p * G;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nnA = A.nn[p], nnB = B.nn[p];
+  const int* offA0 = A.off + p * (A.node_pitch + 1);
+#if ORBX_BOW_BALANCE
+  // The pair's nodes split into G contiguous ranges of equal estimated work
+  // rather than equal node counts (node sizes are skewed: a few nodes hold
+  // hundreds of features, and a range's time follows its largest nodes). A
+  // node of n A rows costs about n x (n + 4) (B's node sizes follow A's in
+  // consecutive frames; no B lookup needed here): node j goes to workgroup
+  // floor(excl_j x G / total), which is non-decreasing in j.
+  int k0, k1;
+  {
+    auto work = [&](int j) {
+      const int n = offA0[j + 1] - offA0[j];
+      return n * (n + 4);
+    };
+    int tot = 0;
+    for (int j = tid; j < nnA; j += NT) tot += work(j);
+    tot = wave_sum_dpp(tot);
+    if (lane == 0) s_scan[wv] = tot;
+    __syncthreads();
+    long long W = 0;
+    for (int w = 0; w < kWaves; ++w) W += s_scan[w];
+    __syncthreads();
+    int lt = 0, le = 0;
+    long long carry = 0;
+    for (int j0 = 0; j0 < nnA; j0 += NT) {
+      const int j = j0 + tid;
+      const int wj = j < nnA ? work(j) : 0;
+      const int incl = wave_incl_scan_dpp(wj);
+      if (lane == 63) s_scan[wv] = incl;
+      __syncthreads();
+      long long before = carry;
+      for (int w = 0; w < wv; ++w) before += s_scan[w];
+      const long long excl = before + incl - wj;
+      if (j < nnA) {
+        const int owner = W > 0 ? (int)min((long long)(G - 1), excl * G / W) : 0;
+        lt += owner < g;
+        le += owner <= g;
+      }
+      for (int w = 0; w < kWaves; ++w) carry += s_scan[w];
+      __syncthreads();
+    }
+    lt = wave_sum_dpp(lt);
+    le = wave_sum_dpp(le);
+    if (lane == 0) {
+      s_scan[wv] = lt;
+      s_hist[wv] = le;
+    }
+    __syncthreads();
+    k0 = k1 = 0;
+    for (int w = 0; w < kWaves; ++w) {
+      k0 += s_scan[w];
+      k1 += s_hist[w];
+    }
+    __syncthreads();
+  }
+  const int nk = k1 - k0;
+#else
   const int k0 = (int)((long long)g * nnA / G), k1 = (int)((long long)(g + 1) * nnA / G), nk = k1 - k0;
+#endif
   const uint8_t* descA = A.desc + p * A.kp_pitch * 32;
   const uint8_t* descB = B.desc + p * B.kp_pitch * 32;
   const float* angA = A.angle + p * A.kp_pitch * A.angle_stride;
