@@ -13,11 +13,12 @@
 //   (a) every band pixel: centre + 4 compass ring pixels; a 9-arc always
 //       covers two compass points, so pixels without two agreeing compass
 //       points cannot be corners at t_low = min(iniTh, minTh);
-//   (b) survivors: full 16-pixel ring test (9 contiguous darker/brighter);
-//   (c) detected pixels: OpenCV's cornerScore<16> (the largest threshold at
-//       which the pixel is still detected, minus 1), written to a score map.
-// One score map serves both thresholds because a pixel is detected at t iff
-// its score is >= t. NMS then visits only detected pixels, records the
+//   (b) survivors: OpenCV's cornerScore<16> (the largest threshold at which
+//       the pixel is still detected, minus 1), two pixels per lane in packed
+//       i16x2 arithmetic; a pixel is detected at t iff its score is >= t, so
+//       the score is the detection test (no separate 16-pixel ring test) and
+//       detected pixels write it to a score map.
+// One score map serves both thresholds. NMS then visits only detected pixels, records the
 // survivors at iniThFAST and minThFAST as ballots, keeps the iniThFAST set
 // unless it is empty, and writes the keys in row-major order (the order
 // cv::FAST emits them) into the cell's fixed slot range. Every compaction is
@@ -167,6 +168,9 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
 
 #ifndef ORBX_FAST_PK
 #define ORBX_FAST_PK 1  // packed-u16 compass pre-test (0: the scalar form, for A/B)
+#endif
+#ifndef ORBX_FAST_PKSCORE
+#define ORBX_FAST_PKSCORE 1  // packed two-pixel cornerScore as the detection test (0: ring test + score pass)
 #endif
 #ifndef ORBX_FAST_WAVES
 #define ORBX_FAST_WAVES 8  // VGPR budget: 8 waves per SIMD (<= 64 VGPRs; 41 used)
@@ -365,8 +369,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     }
   }
   stamp(1);
-  // (b) full ring test, compacted in place (reads of a chunk precede its writes)
   int n2 = 0;
+#if ORBX_FAST_PKSCORE
+  // (b+c) cornerScore<16> of every compass survivor, two per lane as packed
+  // i16x2 (entries i and i + 64 of a 128-entry chunk): detected iff score >= t,
+  // so the score replaces the ring test. Detected pixels keep their score in
+  // the map and are compacted in place, row-major (chunk reads precede writes).
+  for (int i0 = 0; i0 < n1; i0 += 128) {
+    const int iA = i0 + lane, iB = iA + 64;
+    const int eA = list[min(iA, n1 - 1)], eB = list[min(iB, n1 - 1)];
+    const LDSP uint8_t* cA = band + u24mul(eA >> 8, kRoiStride) + (eA & 255);
+    const LDSP uint8_t* cB = band + u24mul(eB >> 8, kRoiStride) + (eB & 255);
+    const i16x2 v = {(short)cA[0], (short)cB[0]};
+    i16x2 D[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const i16x2 p = {(short)cA[ring_off<kRoiStride>(k)], (short)cB[ring_off<kRoiStride>(k)]};
+      D[k] = v - p;
+    }
+    const i16x2 s = corner_score16_x2(D, t);
+    const bool dA = iA < n1 && s.x >= t, dB = iB < n1 && s.y >= t;
+    const uint64_t mA = __ballot(dA), mB = __ballot(dB);
+    if (dA) {
+      list[n2 + mbcnt64(mA)] = (uint16_t)eA;
+      sc[u24mul((eA >> 8) + 1, sw) + (eA & 255) + 1] = (uint8_t)s.x;
+    }
+    n2 += __popcll(mA);
+    if (dB) {
+      list[n2 + mbcnt64(mB)] = (uint16_t)eB;
+      sc[u24mul((eB >> 8) + 1, sw) + (eB & 255) + 1] = (uint8_t)s.y;
+    }
+    n2 += __popcll(mB);
+  }
+  stamp(2);
+#else
+  // (b) full ring test, compacted in place (reads of a chunk precede its writes)
   for (int i0 = 0; i0 < n1; i0 += 64) {
     const int i = i0 + lane;
     const int e = i < n1 ? list[i] : 0;
@@ -393,6 +430,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     for (int k = 0; k < 16; ++k) d[k] = v - c[ring_off<kRoiStride>(k)];
     sc[u24mul((e >> 8) + 1, sw) + (e & 255) + 1] = (uint8_t)corner_score16(d, t);
   }
+#endif
   __syncthreads();
   stamp(3);
   // (d) 3x3 NMS at both thresholds (neighbours below a threshold count as 0)

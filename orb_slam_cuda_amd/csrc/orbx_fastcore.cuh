@@ -46,6 +46,48 @@ __device__ __forceinline__ int corner_score16(const int (&d)[16], int threshold)
   return -b0 - 1;
 }
 
+// The same score for two pixels at once, packed i16x2 (one pixel per half).
+// Branch-free restatement: cornerScore<16>'s early `continue`s skip only
+// updates that cannot change a0 / b0 (the partial arc minimum already bounds
+// the full one), so
+//   a0 = max(t, max over the 16 arcs of 9 of min(d)),
+//   b0 = min(-a0, min over the 16 arcs of 9 of max(d)),  score = -b0 - 1.
+// The 9-arcs starting at k and k+1 (k even) share the 8-run starting at k+1,
+// so the run minima come from a min tree over the odd starts only. A pixel
+// is FAST-detected at t iff its score is >= t.
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ i16x2 corner_score16_x2(const i16x2 (&D)[16], int threshold) {
+  i16x2 lo[8], hi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {  // runs of 2 from odd start s = 2j + 1
+    lo[j] = __builtin_elementwise_min(D[2 * j + 1], D[(2 * j + 2) & 15]);
+    hi[j] = __builtin_elementwise_max(D[2 * j + 1], D[(2 * j + 2) & 15]);
+  }
+  i16x2 lo4[8], hi4[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {  // runs of 4
+    lo4[j] = __builtin_elementwise_min(lo[j], lo[(j + 1) & 7]);
+    hi4[j] = __builtin_elementwise_max(hi[j], hi[(j + 1) & 7]);
+  }
+  const short t = (short)threshold;
+  i16x2 a0 = {t, t};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {  // runs of 8 from s, extended to the 9-arcs from s - 1 and s
+    const i16x2 a = __builtin_elementwise_min(lo4[j], lo4[(j + 2) & 7]);
+    a0 = __builtin_elementwise_max(a0, __builtin_elementwise_min(a, D[2 * j]));
+    a0 = __builtin_elementwise_max(a0, __builtin_elementwise_min(a, D[(2 * j + 9) & 15]));
+  }
+  i16x2 b0 = -a0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const i16x2 b = __builtin_elementwise_max(hi4[j], hi4[(j + 2) & 7]);
+    b0 = __builtin_elementwise_min(b0, __builtin_elementwise_max(b, D[2 * j]));
+    b0 = __builtin_elementwise_min(b0, __builtin_elementwise_max(b, D[(2 * j + 9) & 15]));
+  }
+  const i16x2 one = {1, 1};
+  return -b0 - one;
+}
+
 // 9 contiguous set bits in a circular 16-bit mask
 __device__ __forceinline__ bool has_arc9(uint32_t m) {
   const uint32_t x = m | (m << 16);
