@@ -60,37 +60,6 @@ __device__ __forceinline__ int ring_off(int k) {
   return ry[k] * kRoiStride + rx[k];
 }
 
-// 16-bit dark / bright masks of the ring (bit k: ring pixel k < lo / > hi),
-// two ring pixels (k, k + 8) per packed u16x2 register: saturating subtract,
-// min with 1, shift into bit k of each half (v_pk_sub_u16 clamp, v_pk_min_u16,
-// v_lshl_or_b32 per pair instead of a compare + select + shift per pixel)
-// packed u16x2 ops as written: the compiler turns min(sub_sat(a, b), 1) back
-// into a compare + select per half
-__device__ __forceinline__ uint32_t pk_sub_sat_u16(uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-template <int kRoiStride>
-__device__ __forceinline__ void ring_masks(const LDSP uint8_t* c, int lo, int hi, uint32_t* dark, uint32_t* bright) {
-  const uint32_t l16 = (uint32_t)max(lo, 0), h16 = (uint32_t)hi;  // lo < 0: nothing is darker
-  const uint32_t vl = l16 | (l16 << 16), vh = h16 | (h16 << 16), one = 0x00010001u;
-  uint32_t dk = 0, br = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t x = (uint32_t)c[ring_off<kRoiStride>(k)] | ((uint32_t)c[ring_off<kRoiStride>(k + 8)] << 16);
-    dk |= pk_min_u16(pk_sub_sat_u16(vl, x), one) << k;
-    br |= pk_min_u16(pk_sub_sat_u16(x, vh), one) << k;
-  }
-  *dark = (dk & 0xFFu) | ((dk >> 8) & 0xFF00u);
-  *bright = (br & 0xFFu) | ((br >> 8) & 0xFF00u);
-}
-
 // (a) of the tight-stride kernel on dword LDS reads: a lane tests 4
 // horizontally adjacent band pixels (G = ceil(bw / 4) lanes per band row,
 // 64 / G rows per pass). Band pixel (y, x) is ROI byte (y + 3) * 44 + OX + 3 + x
@@ -105,10 +74,6 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
   typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
   // byte offsets, from the group's first dword, of the group's centres, +3 and -3 neighbours
   constexpr int kC = OX + 3, kN4 = OX + 6, kN12 = OX;
-  auto ext = [](const uint32_t* d, int o) -> uint32_t {
-    return (o & 3) == 0 ? d[o >> 2] : __builtin_amdgcn_alignbyte(d[(o >> 2) + 1], d[o >> 2], o & 3);
-  };
-  auto bits = [](uint32_t x) { return __builtin_bit_cast(u16x2, x); };
   const int G = (bw + 3) >> 2, RP = 64 / G;
   const int r = lane / G, g = lane - r * G, x = 4 * g;
   const bool lane_ok = r < RP;
@@ -131,15 +96,18 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
       du[k] = (kC >> 2) + k <= ((kC + 3) >> 2) ? ru[(kC >> 2) + k] : 0u;
       dd[k] = (kC >> 2) + k <= ((kC + 3) >> 2) ? rd[(kC >> 2) + k] : 0u;
     }
-    const uint32_t v4 = ext(dc, kC), n4 = ext(dc, kN4), n12 = ext(dc, kN12);
-    const uint32_t n8 = ext(du, kC & 3), n0 = ext(dd, kC & 3);
     u16x2 any[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // h = 0: pixels 0 and 2, h = 1: pixels 1 and 3
-      const uint32_t sh = 8 * h;
-      const u16x2 v = bits((v4 >> sh) & 0x00FF00FFu);
-      const u16x2 a0 = bits((n0 >> sh) & 0x00FF00FFu), a4 = bits((n4 >> sh) & 0x00FF00FFu);
-      const u16x2 a8 = bits((n8 >> sh) & 0x00FF00FFu), a12 = bits((n12 >> sh) & 0x00FF00FFu);
+      // bytes o + h and o + h + 2 of a staged run as a u16x2 pair: one v_perm_b32
+      auto pair = [h](const uint32_t* d, int o) -> u16x2 {
+        const int b = (o & 3) + h;
+        const uint32_t sel = (uint32_t)b | 0x0C00u | ((uint32_t)(b + 2) << 16) | 0x0C000000u;
+        return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(d[(o >> 2) + 1], d[o >> 2], sel));
+      };
+      const u16x2 v = pair(dc, kC);
+      const u16x2 a0 = pair(dd, kC & 3), a4 = pair(dc, kN4);
+      const u16x2 a8 = pair(du, kC & 3), a12 = pair(dc, kN12);
       const u16x2 s1 = __builtin_elementwise_min(a0, a4), l1 = __builtin_elementwise_max(a0, a4);
       const u16x2 s2 = __builtin_elementwise_min(a8, a12), l2 = __builtin_elementwise_max(a8, a12);
       const u16x2 a = __builtin_elementwise_max(s1, s2), b = __builtin_elementwise_min(l1, l2);
@@ -168,9 +136,6 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
 
 #ifndef ORBX_FAST_PK
 #define ORBX_FAST_PK 1  // packed-u16 compass pre-test (0: the scalar form, for A/B)
-#endif
-#ifndef ORBX_FAST_PKSCORE
-#define ORBX_FAST_PKSCORE 1  // packed two-pixel cornerScore as the detection test (0: ring test + score pass)
 #endif
 #ifndef ORBX_FAST_WAVES
 #define ORBX_FAST_WAVES 8  // VGPR budget: 8 waves per SIMD (<= 64 VGPRs; 41 used)
@@ -370,8 +335,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   }
   stamp(1);
   int n2 = 0;
-#if ORBX_FAST_PKSCORE
-  // (b+c) cornerScore<16> of every compass survivor, two per lane as packed
+  // (b) cornerScore<16> of every compass survivor, two per lane as packed
   // i16x2 (entries i and i + 64 of a 128-entry chunk): detected iff score >= t,
   // so the score replaces the ring test. Detected pixels keep their score in
   // the map and are compacted in place, row-major (chunk reads precede writes).
@@ -402,35 +366,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     n2 += __popcll(mB);
   }
   stamp(2);
-#else
-  // (b) full ring test, compacted in place (reads of a chunk precede its writes)
-  for (int i0 = 0; i0 < n1; i0 += 64) {
-    const int i = i0 + lane;
-    const int e = i < n1 ? list[i] : 0;
-    bool det = false;
-    if (i < n1) {
-      const LDSP uint8_t* c = band + u24mul(e >> 8, kRoiStride) + (e & 255);
-      const int v = c[0];
-      uint32_t dk, br;
-      ring_masks<kRoiStride>(c, v - t, v + t, &dk, &br);
-      det = has_arc9(dk) || has_arc9(br);
-    }
-    const uint64_t m = __ballot(det);
-    if (det) list[n2 + mbcnt64(m)] = (uint16_t)e;
-    n2 += __popcll(m);
-  }
-  stamp(2);
-  // (c) FAST scores of the detected pixels
-  for (int i = lane; i < n2; i += 64) {
-    const int e = list[i];
-    const LDSP uint8_t* c = band + u24mul(e >> 8, kRoiStride) + (e & 255);
-    const int v = c[0];
-    int d[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) d[k] = v - c[ring_off<kRoiStride>(k)];
-    sc[u24mul((e >> 8) + 1, sw) + (e & 255) + 1] = (uint8_t)corner_score16(d, t);
-  }
-#endif
   __syncthreads();
   stamp(3);
   // (d) 3x3 NMS at both thresholds (neighbours below a threshold count as 0)
@@ -496,8 +431,11 @@ size_t fast_lds_bytes(const ExtractParams& P) {
 #else
   const size_t list = band;
 #endif
+#ifndef ORBX_FAST_LDS_PAD
+#define ORBX_FAST_LDS_PAD 0  // residency experiments (tools/variant.sh): extra LDS per wave
+#endif
   return r16(std::max((size_t)P.fast_rh_max * stride, 16 * ((band + 63) / 64))) +
-         r16((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1) + r16(2 * list);
+         r16((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1) + r16(2 * list) + ORBX_FAST_LDS_PAD;
 }
 
 int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cells, uint32_t* slots,
@@ -534,7 +472,7 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
       for (int k = 0; k < 7; ++k) t[k] += h[w * 8 + k];
     }
     n = n ? n : 1;
-    fprintf(stderr, "fast: %d cells; avg cycles at stage end: staged %.0f compass %.0f ring %.0f score %.0f done %.0f; avg n1 %.1f n2 %.1f\n",
+    fprintf(stderr, "fast: %d cells; avg cycles at stage end: staged %.0f compass %.0f score %.0f synced %.0f done %.0f; avg n1 %.1f n2 %.1f\n",
             n, t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6] / n);
   }
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
