@@ -344,6 +344,11 @@ static int launch_band(const ExtractParams& P, const LevelPtrs& lp, const int2* 
         avg[k] += h[w * 16 + k];
         mx[k] = std::max(mx[k], h[w * 16 + k]);
       }
+    fprintf(stderr, "pyr_band plans (bands/cost/lds):");
+    for (int i = 0; i < P.pyr_nplans; ++i)
+      fprintf(stderr, " %d/%d/%d", P.pyr_plan[i].nbands, P.pyr_plan[i].cost,
+              P.pyr_plan[i].lds_a + P.pyr_plan[i].lds_b + P.pyr_plan[i].lds_y + 16);
+    fprintf(stderr, "\n");
     fprintf(stderr, "pyr_band: %d WGs (%d bands); phase cycles avg/max:", nwg, P.pyr_nbands);
     for (int k = 0; k < P.L; ++k) fprintf(stderr, " [%d] %.0f/%d", k, avg[k] / nwg, mx[k]);
     fprintf(stderr, "\n");
