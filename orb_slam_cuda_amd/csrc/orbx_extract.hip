@@ -7,8 +7,7 @@
 //   launch_quadtree      (1)  DistributeOctTree                     orbx_quadtree.hip
 //   launch_orient_brief  (1)  IC_Angle + rBRIEF + scale/assemble    orbx_brief.hip
 // Optional events (caller-owned or the handle's ORBX_TIMING ones) bracket
-// every stage on the launch stream (fused path: ev[1..2] is empty and
-// ev[2..3] brackets the blur + FAST tiles).
+// every stage on the launch stream (ev[i], ev[i+1] around stage i).
 #include "orbx_device.cuh"
 
 namespace orbx {

@@ -484,19 +484,35 @@ struct BowSide {
 };
 
 #ifndef ORBX_BOW_GROUPS
-#define ORBX_BOW_GROUPS 8
+#define ORBX_BOW_GROUPS 24
 #endif
 #ifndef ORBX_BOW_BALANCE
 #define ORBX_BOW_BALANCE 1  // node ranges of equal estimated work (0: equal node counts)
 #endif
+// Workgroup shape (C3 + BoW bench, 64 KITTI pairs): alone, 8 ranges of <= 768
+// rows on 512 threads are fastest (34.9 us; 256 threads 40.8 us), but in the
+// pipelined step those 71 KB-LDS workgroups wait for CUs the extraction
+// kernels hold (0.24 ms of event time per batch); 24 ranges of <= 256 rows
+// (~26 KB) on 256 threads fit beside them: 0.135 ms, 106 k -> 118 k frames/s.
+// Ranges past the caps take the per-wave fallback.
 constexpr int kBowGroups = ORBX_BOW_GROUPS;  // workgroups per pair (node ranges)
-constexpr int kBowThreads = 256;
+#ifndef ORBX_BOW_THREADS
+#define ORBX_BOW_THREADS 256
+#endif
+constexpr int kBowThreads = ORBX_BOW_THREADS;
 constexpr int kBowK = 8;         // smallest keys kept per A row
-constexpr int kBowCapB = 768;    // B rows staged per workgroup
-constexpr int kBowCapA = 768;    // A rows per workgroup
-constexpr int kBowCapN = 256;    // nodes per workgroup
+#ifndef ORBX_BOW_CAP
+#define ORBX_BOW_CAP 256
+#endif
+constexpr int kBowCapB = ORBX_BOW_CAP;      // B rows staged per workgroup
+constexpr int kBowCapA = ORBX_BOW_CAP;      // A rows per workgroup
+constexpr int kBowCapN = ORBX_BOW_CAP / 3;  // nodes per workgroup
 constexpr int kBowMaxB = 256;    // fallback: B features of a node held in registers (4 chunks of 64 lanes)
 constexpr uint32_t kBowNone = 0xFFFFFFFFu;
+#ifndef ORBX_BOW_ROWCOST
+#define ORBX_BOW_ROWCOST 64
+#endif
+constexpr int kBowRowCost = ORBX_BOW_ROWCOST;  // a row's fixed cost in candidate scans (range balance)
 #ifndef ORBX_BOW_ROUNDS
 #define ORBX_BOW_ROUNDS 16
 #endif
@@ -514,6 +530,9 @@ struct BowTables {  // the two-pass layout
   int boff[kBowCapN + 1];       // node j's B rows at [boff[j], boff[j+1])
   int aoff[kBowCapN + 1];       // node j's A rows at [aoff[j], aoff[j+1]) (relative to the range)
   int bsrc[kBowCapN];           // node j's B CSR start
+  int sstart[kBowCapN + 1];     // phase (1) lane slots: the k-th node in slot order starts at sstart[k]
+  int snode[kBowCapN];          // ... and is node snode[k]
+  int rescan[kBowCapA];         // greedy rounds: rows whose list ran out, rescanned by whole waves
   uint32_t taken[kBowCapB / 32];  // by staged position
 };
 struct BowFallback {  // the per-wave layout
@@ -549,14 +568,17 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
   // The pair's nodes split into G contiguous ranges of equal estimated work
   // rather than equal node counts (node sizes are skewed: a few nodes hold
   // hundreds of features, and a range's time follows its largest nodes). A
-  // node of n A rows costs about n x (n + 4) (B's node sizes follow A's in
-  // consecutive frames; no B lookup needed here): node j goes to workgroup
-  // floor(excl_j x G / total), which is non-decreasing in j.
+  // node of n A rows costs about n x (n + kBowRowCost): the candidate scans
+  // plus each row's fixed part (its node lookup and two dependent global
+  // loads, worth ~64 candidates; with n x (n + 4) the first range of a pair
+  // took ~540 rows, two passes of the workgroup's lanes). B's node sizes
+  // follow A's in consecutive frames, so no B lookup is needed here: node j
+  // goes to workgroup floor(excl_j x G / total), non-decreasing in j.
   int k0, k1;
   {
     auto work = [&](int j) {
       const int n = offA0[j + 1] - offA0[j];
-      return n * (n + 4);
+      return n * (n + kBowRowCost);
     };
     int tot = 0;
     for (int j = tid; j < nnA; j += NT) tot += work(j);
@@ -679,12 +701,29 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
   // ---- node table: B node per A node, staged B offsets (block scan of counts)
   bool fits = nk <= kBowCapN && na <= kBowCapA;
   if (fits) {
+    // B's node list in LDS (the claim table is free until the greedy rounds):
+    // the per-node lower_bound then waits on LDS, not on ~7 dependent global loads
+    const bool nodes_lds = nnB <= kBowCapB;
+    uint32_t* const snb = (uint32_t*)S.t.claim;
+    if (nodes_lds)
+      for (int i = tid; i < nnB; i += NT) snb[i] = nodesB[i];
+    __syncthreads();
+    auto find_b_lds = [&](uint32_t id) {
+      int lo = 0, hi = nnB;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (snb[mid] < id) lo = mid + 1;
+        else hi = mid;
+      }
+      return (lo < nnB && snb[lo] == id) ? lo : -1;
+    };
     int carry = 0;
     for (int j0 = 0; j0 < nk; j0 += NT) {
       const int j = j0 + tid;
       int cnt = 0, src = 0;
       if (j < nk) {
-        const int kb = find_b(nodesA[k0 + j]);
+        const uint32_t id = nodesA[k0 + j];
+        const int kb = nodes_lds ? find_b_lds(id) : find_b(id);
         if (kb >= 0) {
           src = offB[kb];
           cnt = offB[kb + 1] - src;
@@ -711,6 +750,8 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
     __syncthreads();
     const int nb = S.t.boff[nk];
     for (int i = tid; i < kBowCapB / 32; i += NT) S.t.taken[i] = 0;
+    // the range's A feature indices (phase (1) then needs one dependent global load, not two)
+    for (int i = tid; i < na; i += NT) S.t.match[i] = idxA[a_base + i];
     // ---- stage the range's B rows in node order (static filter: KF-KF needs a good MapPoint)
     for (int i = tid; i < nb; i += NT) {
       int lo = 0, hi = nk;  // node j with boff[j] <= i < boff[j+1]
@@ -731,23 +772,72 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
     }
     __syncthreads();
     stamp(2, -1);
-    // ---- (1) per A row, its kBowK smallest keys over the node's candidates
-    for (int ia = tid; ia < na; ia += NT) {
-      int lo = 0, hi = nk;  // node j with aoff[j] <= ia < aoff[j+1]
+    // ---- (1) per A row, its kBowK smallest keys over the node's candidates.
+    // A row of a node with nb B rows gets L = 1, 2, 4 or 8 adjacent lanes
+    // (nb > 48, 96, 192), each scanning every L-th candidate; the L sorted
+    // lists then merge by xor shuffles. Without the split one lane walks all
+    // nb candidates and the largest node sets the workgroup's time. Lane
+    // slots: nodes ordered by L descending (node order within), each row's L
+    // slots contiguous and L-aligned (every block before has a multiple of
+    // L slots).
+    auto lanes_of = [](int nbn) { return nbn > 192 ? 8 : nbn > 96 ? 4 : nbn > 48 ? 2 : 1; };
+    int nslots = 0;
+    {
+      int base = 0, rank0 = 0;  // slots and nodes of the classes before
+      for (int Lc = 8; Lc >= 1; Lc >>= 1) {
+        int carry = 0;
+        for (int j0 = 0; j0 < nk; j0 += NT) {
+          const int j = j0 + tid;
+          const bool mine = j < nk && lanes_of(S.t.boff[j + 1] - S.t.boff[j]) == Lc;
+          const int sz = mine ? (S.t.aoff[j + 1] - S.t.aoff[j]) * Lc : 0;
+          const uint64_t bm = __ballot(mine);
+          const int incl = wave_incl_scan_dpp(sz);
+          if (lane == 63) s_scan[wv] = incl;
+          if (lane == 0) s_hist[wv] = __popcll(bm);
+          __syncthreads();
+          int before = carry, rb = rank0;
+          for (int w = 0; w < wv; ++w) {
+            before += s_scan[w];
+            rb += s_hist[w];
+          }
+          if (mine) {
+            const int k = rb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+            S.t.sstart[k] = base + before + incl - sz;
+            S.t.snode[k] = j;
+          }
+          for (int w = 0; w < kWaves; ++w) {
+            carry += s_scan[w];
+            rank0 += s_hist[w];
+          }
+          __syncthreads();
+        }
+        base += carry;
+      }
+      nslots = base;
+      if (tid == 0) S.t.sstart[nk] = nslots;
+    }
+    __syncthreads();
+    for (int s0 = 0; s0 < nslots; s0 += NT) {  // uniform trip count: the shuffles below see every lane
+      const int sl = s0 + tid;
+      const bool act = sl < nslots;
+      int lo = 0, hi = nk;  // slot-order node k with sstart[k] <= sl < sstart[k+1]
       while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
-        if (S.t.aoff[mid] <= ia) lo = mid;
+        if (S.t.sstart[mid] <= min(sl, nslots - 1)) lo = mid;
         else hi = mid;
       }
-      const int i1 = idxA[a_base + ia];
+      const int j = min(max(S.t.snode[lo], 0), nk - 1);  // (every rank is written; the clamp guards the indexing)
+      const int q0 = S.t.boff[j], q1 = S.t.boff[j + 1];
+      const int L = lanes_of(q1 - q0), rel = min(sl, nslots - 1) - S.t.sstart[lo];
+      const int ia = S.t.aoff[j] + rel / L, sub = rel & (L - 1);
+      const int i1 = S.t.match[ia];  // idxA[a_base + ia], staged
       uint32_t t0 = kBowNone, t1 = kBowNone, t2 = kBowNone, t3 = kBowNone;
       uint32_t t4 = kBowNone, t5 = kBowNone, t6 = kBowNone, t7 = kBowNone;
       int nv = -1;
-      if (in_a(i1) && (!mpA || mpA[i1])) {  // (:191-197)
+      if (act && in_a(i1) && (!mpA || mpA[i1])) {  // (:191-197)
         nv = 0;
         const uint4* d1 = (const uint4*)(descA + (long long)i1 * 32);
         const uint4 a0 = d1[0], a1 = d1[1];
-        const int q0 = S.t.boff[lo], q1 = S.t.boff[lo + 1];
         auto insert = [&](uint32_t key) {  // into the ascending t0..t7
           uint32_t m;
           m = min(t0, key); key = max(t0, key); t0 = m;
@@ -760,13 +850,13 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
           t7 = min(t7, key);
         };
         // two candidates per step: their LDS reads are in flight together
-        int q = q0;
-        for (; q + 1 < q1; q += 2) {
-          const int okA = S.t.bidx[q], okB = S.t.bidx[q + 1];
+        int q = q0 + sub;
+        for (; q + L < q1; q += 2 * L) {
+          const int okA = S.t.bidx[q], okB = S.t.bidx[q + L];
           const uint4 b0 = *(const uint4*)&S.t.bdesc[q][0], b1 = *(const uint4*)&S.t.bdesc[q][4];
-          const uint4 c0 = *(const uint4*)&S.t.bdesc[q + 1][0], c1 = *(const uint4*)&S.t.bdesc[q + 1][4];
+          const uint4 c0 = *(const uint4*)&S.t.bdesc[q + L][0], c1 = *(const uint4*)&S.t.bdesc[q + L][4];
           const uint32_t kA = ((uint32_t)hamming256(a0, a1, b0, b1) << 16) | (uint32_t)(q - q0);
-          const uint32_t kB = ((uint32_t)hamming256(a0, a1, c0, c1) << 16) | (uint32_t)(q + 1 - q0);
+          const uint32_t kB = ((uint32_t)hamming256(a0, a1, c0, c1) << 16) | (uint32_t)(q + L - q0);
           if (okA >= 0) insert(kA), ++nv;
           if (okB >= 0) insert(kB), ++nv;
         }
@@ -776,10 +866,38 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
                  (uint32_t)(q - q0));
         }
       }
-      S.t.top[ia][0] = make_uint4(t0, t1, t2, t3);
-      S.t.top[ia][1] = make_uint4(t4, t5, t6, t7);
-      S.t.nv[ia] = nv;
-      S.t.rq[ia] = S.t.boff[lo] | (S.t.boff[lo + 1] << 16);
+      // merge the row's L lists: with the partner's list reversed, the
+      // elementwise minima are the 8 smallest of the union as a bitonic
+      // sequence, sorted by three half-cleaner stages (both partners end with
+      // the same list; keys are unique, so the merge is exact)
+      for (int st = 1; st < 8; st <<= 1) {
+        if (!__ballot(act && L > st)) break;  // wave-uniform
+        const uint32_t u0 = __shfl_xor(t0, st), u1 = __shfl_xor(t1, st), u2 = __shfl_xor(t2, st);
+        const uint32_t u3 = __shfl_xor(t3, st), u4 = __shfl_xor(t4, st), u5 = __shfl_xor(t5, st);
+        const uint32_t u6 = __shfl_xor(t6, st), u7 = __shfl_xor(t7, st);
+        const int unv = __shfl_xor(nv, st);
+        if (L > st) {
+          uint32_t m[8] = {min(t0, u7), min(t1, u6), min(t2, u5), min(t3, u4),
+                           min(t4, u3), min(t5, u2), min(t6, u1), min(t7, u0)};
+#pragma unroll
+          for (int h = 4; h >= 1; h >>= 1)
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+              if ((i & h) == 0) {
+                const uint32_t x = m[i], y = m[i + h];
+                m[i] = min(x, y);
+                m[i + h] = max(x, y);
+              }
+          t0 = m[0]; t1 = m[1]; t2 = m[2]; t3 = m[3]; t4 = m[4]; t5 = m[5]; t6 = m[6]; t7 = m[7];
+          nv = (nv < 0 || unv < 0) ? -1 : nv + unv;  // the row's lanes agree on validity
+        }
+      }
+      if (act && sub == 0) {
+        S.t.top[ia][0] = make_uint4(t0, t1, t2, t3);
+        S.t.top[ia][1] = make_uint4(t4, t5, t6, t7);
+        S.t.nv[ia] = nv;
+        S.t.rq[ia] = q0 | (q1 << 16);
+      }
     }
     __syncthreads();
     stamp(3, -1);
@@ -792,7 +910,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
     // unique fixed point = the sequential result, so the rounds stop there.
     // Rows with a decision changing after kBowRounds rounds fall back to the
     // sequential pass below.
-    auto decide = [&](int ia, auto&& taken) -> int {  // staged position or -1
+    auto decide = [&](int ia, auto&& taken, bool defer = false) -> int {  // staged position, -1, or -2 = deferred rescan
       const int nv = S.t.nv[ia];
       if (nv < 0) return -1;
       const int rq = S.t.rq[ia], q0 = rq & 0xFFFF, q1 = rq >> 16;
@@ -813,6 +931,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
         ++found;
       }
       if (found < 2 && nv > kBowK) {
+        if (defer) return -2;
         // the list ran out under taken rows: rescan the node (strict < of :211-226)
         const int i1 = idxA[a_base + ia];
         const uint4* da = (const uint4*)(descA + (long long)i1 * 32);
@@ -839,8 +958,11 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
     const int nb_ = S.t.boff[nk];
     for (int ia = tid; ia < na; ia += NT) S.t.match[ia] = decide(ia, [](int, int) { return false; });
     bool settled = false;
+    int rounds = 0;
     for (int round = 0; round < kBowRounds && !settled; ++round) {
+      ++rounds;
       for (int q = tid; q < nb_; q += NT) S.t.claim[q] = INT_MAX;
+      if (tid == 0) s_queue = 0;
       __syncthreads();
       for (int ia = tid; ia < na; ia += NT) {
         const int q = S.t.match[ia];
@@ -849,8 +971,39 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
       __syncthreads();
       int changed = 0;
       for (int ia = tid; ia < na; ia += NT) {
-        const int m = decide(ia, [&](int row, int q) { return S.t.claim[q] < row; });
-        if (m != S.t.match[ia]) {
+        const int m = decide(ia, [&](int row, int q) { return S.t.claim[q] < row; }, true);
+        if (m == -2) {
+          S.t.rescan[atomicAdd(&s_queue, 1)] = ia;
+        } else if (m != S.t.match[ia]) {
+          S.t.match[ia] = m;
+          changed = 1;
+        }
+      }
+      __syncthreads();
+      // rows whose list ran out: a wave per row, lanes over the node's
+      // candidates (taken = claimed by an earlier row), two wave minima
+      const int nq = s_queue;
+      for (int qi = wv; qi < nq; qi += kWaves) {
+        const int ia = S.t.rescan[qi];
+        const int rq = S.t.rq[ia], q0 = rq & 0xFFFF, q1 = rq >> 16;
+        const int i1 = idxA[a_base + ia];
+        const uint4* da = (const uint4*)(descA + (long long)i1 * 32);
+        const uint4 a0 = da[0], a1 = da[1];
+        uint32_t b1k = 0x7FFFFFFFu, b2k = 0x7FFFFFFFu;
+        for (int q = q0 + lane; q < q1; q += 64) {
+          if (S.t.bidx[q] < 0 || S.t.claim[q] < ia) continue;
+          const uint32_t k = ((uint32_t)hamming256(a0, a1, *(const uint4*)&S.t.bdesc[q][0],
+                                                   *(const uint4*)&S.t.bdesc[q][4]) << 16) | (uint32_t)(q - q0);
+          b2k = min(b2k, max(b1k, k));
+          b1k = min(b1k, k);
+        }
+        const uint32_t m1 = (uint32_t)wave_min((int)b1k);  // keys < 2^25
+        const uint32_t m2 = (uint32_t)wave_min((int)(b1k == m1 ? b2k : b1k));
+        const int d1 = m1 == 0x7FFFFFFFu ? 256 : (int)(m1 >> 16);
+        const int d2 = m2 == 0x7FFFFFFFu ? 256 : (int)(m2 >> 16);
+        const bool pass = kf_vs_kf ? (d1 < kThLow) : (d1 <= kThLow);
+        const int m = (pass && (float)d1 < __fmul_rn(nnratio, (float)min(d2, 256))) ? q0 + (int)(m1 & 0xFFFF) : -1;
+        if (lane == 0 && m != S.t.match[ia]) {
           S.t.match[ia] = m;
           changed = 1;
         }
@@ -860,82 +1013,89 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
     if (settled) {
       for (int ia = tid; ia < na; ia += NT) S.t.nv[ia] = S.t.match[ia];
     } else {
-      // sequential: one lane per node, A rows in node order, taken sets in registers
-      for (int j = tid; j < nk; j += NT) {
+      // sequential: a wave per node, A rows in node order. The node's taken
+      // set is wave-uniform: four 64-bit masks (positions < 256 in the node;
+      // larger nodes use the LDS bits for the rest). Lane k < 8 checks key k
+      // of the row's list, a ballot gives the first two untaken keys, and the
+      // next row's key is read while the current one is decided. A row whose
+      // list ran out (fewer than two untaken keys left while it saw more than
+      // kBowK candidates) rescans its node: lanes over the candidates, two
+      // wave minima.
+      for (int j = wv; j < nk; j += kWaves) {
         const int q0 = S.t.boff[j], q1 = S.t.boff[j + 1];
+        const int r0 = S.t.aoff[j], r1 = S.t.aoff[j + 1];
         if (q0 == q1) {  // node absent from B (or empty)
-          for (int ia = S.t.aoff[j]; ia < S.t.aoff[j + 1]; ++ia) S.t.nv[ia] = -1;
+          for (int ia = r0 + lane; ia < r1; ia += 64) S.t.nv[ia] = -1;
           continue;
         }
-        const bool reg = q1 - q0 <= 128;
-        uint64_t tk0 = 0, tk1 = 0;  // taken positions 0..63, 64..127 (reg)
-        auto taken = [&](int r) -> bool {  // r: position in the node
-          if (reg) return ((((r & 64) ? tk1 : tk0) >> (r & 63)) & 1ull) != 0;
+        uint64_t tk[4] = {0, 0, 0, 0};  // taken node positions 0..255 (uniform)
+        auto is_taken = [&](int r) -> bool {  // r: position in the node (per lane)
+          if (r < 256) {
+            const uint64_t m = r < 128 ? (r < 64 ? tk[0] : tk[1]) : (r < 192 ? tk[2] : tk[3]);
+            return (m >> (r & 63)) & 1ull;
+          }
           const int q = q0 + r;
           return (S.t.taken[q >> 5] >> (q & 31)) & 1u;
         };
-        const int r0 = S.t.aoff[j], r1 = S.t.aoff[j + 1];
-        uint4 nxA = S.t.top[r0][0], nxB = S.t.top[r0][1];
-        int nxt_nv = S.t.nv[r0];
+        uint32_t key_n = lane < kBowK ? ((const uint32_t*)S.t.top[r0])[lane] : kBowNone;
+        int nv_n = S.t.nv[r0];
         for (int ia = r0; ia < r1; ++ia) {
-          const uint4 tA = nxA, tB = nxB;
-          const int nv = nxt_nv;
+          const uint32_t key = key_n;
+          const int nv = nv_n;  // uniform
           if (ia + 1 < r1) {
-            nxA = S.t.top[ia + 1][0];
-            nxB = S.t.top[ia + 1][1];
-            nxt_nv = S.t.nv[ia + 1];
+            key_n = lane < kBowK ? ((const uint32_t*)S.t.top[ia + 1])[lane] : kBowNone;
+            nv_n = S.t.nv[ia + 1];
           }
           int res = -1;
           if (nv >= 0) {
-            int d1 = 256, d2 = 256, r1st = -1, found = 0;
-            const uint32_t keys[kBowK] = {tA.x, tA.y, tA.z, tA.w, tB.x, tB.y, tB.z, tB.w};
-  #pragma unroll
-            for (int k = 0; k < kBowK; ++k) {
-              const uint32_t key = keys[k];
-              if (key == kBowNone || found == 2 || taken((int)(key & 0xFFFF))) continue;
-              if (found == 0) {
-                d1 = (int)(key >> 16);
-                r1st = (int)(key & 0xFFFF);
-              } else {
-                d2 = (int)(key >> 16);
-              }
-              ++found;
+            const bool ok = key != kBowNone && !is_taken((int)(key & 0xFFFF));
+            const uint64_t bm = __ballot(ok);
+            int d1 = 256, d2 = 256, r1st = -1;
+            if (bm) {
+              const uint32_t k1 = (uint32_t)__builtin_amdgcn_readlane((int)key, __ffsll((long long)bm) - 1);
+              d1 = (int)(k1 >> 16);
+              r1st = (int)(k1 & 0xFFFF);
+              const uint64_t bm2 = bm & (bm - 1);
+              if (bm2) d2 = (int)((uint32_t)__builtin_amdgcn_readlane((int)key, __ffsll((long long)bm2) - 1) >> 16);
             }
-            if (found < 2 && nv > kBowK) {
+            if (__popcll(bm) < 2 && nv > kBowK) {
               // the list ran out under taken rows: rescan the node (strict < of :211-226)
               const int i1 = idxA[a_base + ia];
               const uint4* da = (const uint4*)(descA + (long long)i1 * 32);
               const uint4 a0 = da[0], a1 = da[1];
-              d1 = 256;
-              d2 = 256;
-              r1st = -1;
-              for (int r = 0; r < q1 - q0; ++r) {
-                if (S.t.bidx[q0 + r] < 0 || taken(r)) continue;
-                const int dist = hamming256(a0, a1, *(const uint4*)&S.t.bdesc[q0 + r][0],
-                                            *(const uint4*)&S.t.bdesc[q0 + r][4]);
-                if (dist < d1) {
-                  d2 = d1;
-                  d1 = dist;
-                  r1st = r;
-                } else if (dist < d2) {
-                  d2 = dist;
-                }
+              uint32_t b1k = 0x7FFFFFFFu, b2k = 0x7FFFFFFFu;  // the lane's two smallest keys
+              for (int r = lane; r < q1 - q0; r += 64) {
+                if (S.t.bidx[q0 + r] < 0 || is_taken(r)) continue;
+                const uint32_t k = ((uint32_t)hamming256(a0, a1, *(const uint4*)&S.t.bdesc[q0 + r][0],
+                                                         *(const uint4*)&S.t.bdesc[q0 + r][4]) << 16) | (uint32_t)r;
+                b2k = min(b2k, max(b1k, k));
+                b1k = min(b1k, k);
               }
+              // keys < 2^25: the signed DPP minimum orders them
+              const uint32_t m1 = (uint32_t)wave_min((int)b1k);
+              const uint32_t m2 = (uint32_t)wave_min((int)(b1k == m1 ? b2k : b1k));
+              d1 = m1 == 0x7FFFFFFFu ? 256 : (int)(m1 >> 16);
+              d2 = m2 == 0x7FFFFFFFu ? 256 : (int)(m2 >> 16);
+              r1st = m1 == 0x7FFFFFFFu ? -1 : (int)(m1 & 0xFFFF);
             }
             // d1 = 256 never passes; with d1 < 256 the reference's bestIdx is set
             const bool pass = kf_vs_kf ? (d1 < kThLow) : (d1 <= kThLow);
             if (pass && (float)d1 < __fmul_rn(nnratio, (float)min(d2, 256))) {
               res = q0 + r1st;
-              if (reg) {
+              if (r1st < 256) {
                 const uint64_t bit = 1ull << (r1st & 63);
-                tk0 |= (r1st & 64) ? 0ull : bit;
-                tk1 |= (r1st & 64) ? bit : 0ull;
-              } else {
-                atomicOr(&S.t.taken[res >> 5], 1u << (res & 31));
+                tk[0] |= r1st < 64 ? bit : 0ull;
+                tk[1] |= (r1st >> 6) == 1 ? bit : 0ull;
+                tk[2] |= (r1st >> 6) == 2 ? bit : 0ull;
+                tk[3] |= (r1st >> 6) == 3 ? bit : 0ull;
+              } else if (lane == 0) {
+                atomicOr(&S.t.taken[res >> 5], 1u << (res & 31));  // words shared with other waves' nodes
               }
             }
           }
-          S.t.nv[ia] = res;
+          if (lane == 0) S.t.nv[ia] = res;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
         }
       }
     }
@@ -954,7 +1114,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
     if (dbg) {
       __syncthreads();
       stamp(0, -1);
-      stamp(5, nk);
+      stamp(5, nk + 1000 * (settled ? rounds : 99));  // diagnostics: nodes + 1000 x rounds (99: sequential)
       stamp(6, na);
       stamp(7, S.t.boff[nk]);
     }
@@ -1180,13 +1340,31 @@ int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnrat
     (void)hipStreamSynchronize(s);
     (void)hipMemcpy(h.data(), dbg, h.size() * 4, hipMemcpyDeviceToHost);
     double t[8] = {0}, mx[8] = {0};
-    int nfb = 0;
+    int nfb = 0, nseq = 0, rsum = 0;
     for (int w = 0; w < nwg; ++w) {
       if (h[w * 8 + 5] < 0) ++nfb;
+      if (h[w * 8 + 5] >= 0) {  // nodes + 1000 x rounds
+        const int rd = h[w * 8 + 5] / 1000;
+        nseq += rd == 99;
+        rsum += rd == 99 ? 0 : rd;
+        h[w * 8 + 5] %= 1000;
+      }
       for (int k = 0; k < 8; ++k) t[k] += h[w * 8 + k], mx[k] = std::max(mx[k], (double)h[w * 8 + k]);
     }
+    fprintf(stderr, "bow: %d WGs sequential greedy, the others settled in %.1f rounds on average\n", nseq,
+            nwg > nseq ? (double)rsum / (nwg - nseq) : 0.0);
     fprintf(stderr, "bow: %d WGs (%d fallback); avg/max cycles at: table %.0f/%.0f staged %.0f/%.0f top %.0f/%.0f greedy %.0f/%.0f end %.0f/%.0f; avg nodes %.1f rows A %.1f B %.1f\n",
             nwg, nfb, t[1] / nwg, mx[1], t[2] / nwg, mx[2], t[3] / nwg, mx[3], t[4] / nwg, mx[4], t[0] / nwg, mx[0], t[5] / nwg, t[6] / nwg, t[7] / nwg);
+    // the slowest workgroups: phase ends, nodes, A rows, B rows, and the pair's group index
+    std::vector<int> order(nwg);
+    for (int w = 0; w < nwg; ++w) order[w] = w;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return h[a * 8] > h[b * 8]; });
+    for (int r = 0; r < std::min(nwg, 8); ++r) {
+      const int w = order[r];
+      fprintf(stderr, "bow slow[%d]: wg %d (pair %d group %d) table %d staged %d top %d greedy %d end %d; nodes %d A %d B %d\n",
+              r, w, w / kBowGroups, w % kBowGroups, h[w * 8 + 1], h[w * 8 + 2], h[w * 8 + 3], h[w * 8 + 4], h[w * 8], h[w * 8 + 5],
+              h[w * 8 + 6], h[w * 8 + 7]);
+    }
   }
   hipLaunchKernelGGL(search_bow_finalize_kernel, dim3(pairs), dim3(256), 0, s, A.n, B.n, kf_vs_kf, check_ori, out,
                      out_pitch, bin_scratch, hist_scratch, nmatches);
