@@ -860,7 +860,11 @@ int orbx_get_status(orbx_handle h, int reset, int* status) {
   if (h->ws.ev) HIP_OK(hipEventSynchronize(h->ws.ev));
   int e = 0;
   HIP_OK(hipMemcpy(&e, h->plan.err.p, 4, hipMemcpyDeviceToHost));
-  if (reset && e) HIP_OK(hipMemset(h->plan.err.p, 0, 16));
+  // cleared on the handle's stream, ordered after the batches that set it
+  if (reset && e) {
+    HIP_OK(hipMemsetAsync(h->plan.err.p, 0, 16, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  }
   *status = e;
   return ORBX_OK;
 }
