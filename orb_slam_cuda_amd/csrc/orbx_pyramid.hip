@@ -143,10 +143,22 @@ constexpr int kPyrBandThreads = ORBX_PYR_THREADS;
 
 // Rows of one level for one thread: all 32 source bytes of a row pair are
 // read before any is used, so one LDS wait covers them.
+// A thread's 8 output columns are kPyrRuns runs of 8 / kPyrRuns: run k starts
+// at column (8 / kPyrRuns) * (gi + k * G), G = ceil(w / 8). With runs of 2
+// (default) the 32 lanes of an LDS half-wave read source bytes within ~77
+// bytes (20 dwords, distinct banks of ds_read_u8); runs of 4 spread them over
+// ~154 bytes (39 dwords on 32 banks: 2-way conflicts).
+#ifndef ORBX_PYR_RUN
+#define ORBX_PYR_RUN 2
+#endif
+constexpr int kPyrRun = ORBX_PYR_RUN, kPyrRuns = 8 / kPyrRun;
+static_assert(kPyrRun == 2 || kPyrRun == 4, "runs of 2 or 4 columns");
+__device__ __forceinline__ int pyr_col(int gi, int G, int q) { return kPyrRun * (gi + (q / kPyrRun) * G) + q % kPyrRun; }
+
 template <bool AREA2X>
 __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtrs& lp, int l, int f,
                                           const uint8_t* src, uint8_t* dst, const int2* yt_rows, int src_lo,
-                                          int2 cd, int2 own, int r0, int rstep, int xa, int xb, const int (&sx)[8],
+                                          int2 cd, int2 own, int r0, int rstep, int gi, int G, const int (&sx)[8],
                                           const int (&a0v)[8], const int (&a1v)[8]) {
   const LevelGeom& g = P.lv[l];
   const int spitch = P.lv[l - 1].lpitch, w = g.w;
@@ -178,17 +190,32 @@ __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtr
         v[q] = sat_u8((__mul24(D0, b0) + __mul24(D1, b1) + (1 << 21)) >> 22);
       }
     }
-    const uint32_t pa = pack4_u8(v[0], v[1], v[2], v[3]), pb = pack4_u8(v[4], v[5], v[6], v[7]);
     uint8_t* lrow = dst + __mul24(r - cd.x, g.lpitch);
-    *(uint32_t*)(lrow + xa) = pa;
-    *(uint32_t*)(lrow + xb) = pb;
-    if (r >= own.x && r <= own.y) {
-      uint8_t* drow = G0 + (long long)r * lp.pitch[l];
-      // level pitch and xa, xb are multiples of 4
-      if (xa + 4 <= w) *(uint32_t*)(drow + xa) = pa;
-      else for (int q = 0; xa + q < w; ++q) drow[xa + q] = (uint8_t)(pa >> (8 * q));
-      if (xb + 4 <= w) *(uint32_t*)(drow + xb) = pb;
-      else for (int q = 0; xb + q < w; ++q) drow[xb + q] = (uint8_t)(pb >> (8 * q));
+    const bool owned = r >= own.x && r <= own.y;
+    uint8_t* drow = G0 + (long long)r * lp.pitch[l];
+    if constexpr (kPyrRun == 4) {
+      const int xa = pyr_col(gi, G, 0), xb = pyr_col(gi, G, 4);
+      const uint32_t pa = pack4_u8(v[0], v[1], v[2], v[3]), pb = pack4_u8(v[4], v[5], v[6], v[7]);
+      *(uint32_t*)(lrow + xa) = pa;
+      *(uint32_t*)(lrow + xb) = pb;
+      if (owned) {
+        // level pitch and xa, xb are multiples of 4
+        if (xa + 4 <= w) *(uint32_t*)(drow + xa) = pa;
+        else for (int q = 0; xa + q < w; ++q) drow[xa + q] = (uint8_t)(pa >> (8 * q));
+        if (xb + 4 <= w) *(uint32_t*)(drow + xb) = pb;
+        else for (int q = 0; xb + q < w; ++q) drow[xb + q] = (uint8_t)(pb >> (8 * q));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPyrRuns; ++k) {
+        const int xk = pyr_col(gi, G, 2 * k);
+        const uint16_t pk = (uint16_t)(sat_u8(v[2 * k]) | (sat_u8(v[2 * k + 1]) << 8));
+        *(uint16_t*)(lrow + xk) = pk;  // the LDS row holds the run even past w (pitch >= w + 8)
+        if (owned) {
+          if (xk + 2 <= w) *(uint16_t*)(drow + xk) = pk;
+          else if (xk < w) drow[xk] = (uint8_t)pk;
+        }
+      }
     }
   }
 }
@@ -275,14 +302,13 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams
 
   // column coefficients: level l+1's are fetched while level l is computed
   int2 nxt[8];
-  // a thread's 8 columns are two runs of 4, [4g, 4g+4) and [4(g+G), 4(g+G)+4)
-  // with G = ceil(w/8): neighbouring lanes then read source bytes ~5 apart,
-  // which keeps each LDS byte read within few dwords per bank group
+  // a thread's 8 columns are kPyrRuns runs (pyr_col) with G = ceil(w/8):
+  // neighbouring lanes read source bytes a run's width x 1.2 apart
   auto fetch_cols = [&](int l) {
     const LevelGeom& g = P.lv[l];
     const int G = (g.w + 7) >> 3, gi = tid % G;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) nxt[q] = rtab[g.xtab2 + min(4 * (gi + (q >> 2) * G) + (q & 3), g.w - 1)];
+    for (int q = 0; q < 8; ++q) nxt[q] = rtab[g.xtab2 + min(pyr_col(gi, G, q), g.w - 1)];
   };
   fetch_cols(1);
   lds_sync();  // LDS only: the owned rows written to HBM are not read back here
@@ -297,7 +323,6 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams
     const int2 cs = bt[2 * (l - 1)], cd = bt[2 * l], own = bt[2 * l + 1];
     const int G = (g.w + 7) >> 3, rstep = kPyrBandThreads / G;
     const int gi = tid % G, r0 = tid / G;
-    const int xa = 4 * gi, xb = 4 * (gi + G);
     int sx[8], a0v[8], a1v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -308,9 +333,9 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams
     if (l + 1 < L) fetch_cols(l + 1);
     if (r0 < rstep) {
       if (g.area2x)
-        band_rows<true>(P, lp, l, f, src, dst, s_yt + yoff, cs.x, cd, own, r0, rstep, xa, xb, sx, a0v, a1v);
+        band_rows<true>(P, lp, l, f, src, dst, s_yt + yoff, cs.x, cd, own, r0, rstep, gi, G, sx, a0v, a1v);
       else
-        band_rows<false>(P, lp, l, f, src, dst, s_yt + yoff, cs.x, cd, own, r0, rstep, xa, xb, sx, a0v, a1v);
+        band_rows<false>(P, lp, l, f, src, dst, s_yt + yoff, cs.x, cd, own, r0, rstep, gi, G, sx, a0v, a1v);
     }
     yoff += cd.y - cd.x + 1;
     lds_sync();
