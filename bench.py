@@ -748,7 +748,9 @@ def run_mono(args, cfg, rank, world, local, dist):
         tie_rule = cpu_tie_rule_study(frames[:8], cfg)
 
     if rank == 0:
-        workload = (cfg["workload"] if not args.no_match else cfg["workload"].split(", extract")[0] + ", extract only")
+        workload = (cfg["workload"] if not args.no_match
+                    else "C2" + cfg["workload"].split(", extract")[0][2:] + ", extract only"
+                    if cfg["workload"].startswith("C3") else cfg["workload"].split(", extract")[0] + ", extract only")
         if args.split_sequence:
             workload += f"; ONE sequence of {pool * world} frames split into {world} contiguous blocks"
         out = {
