@@ -124,10 +124,11 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
 #else
 #define LIST_AT(i) list[i]
 #endif
-    if ((m0 >> lane) & 1) LIST_AT(pos++) = e;
-    if ((m1 >> lane) & 1) LIST_AT(pos++) = (uint16_t)(e + 1);
-    if ((m2 >> lane) & 1) LIST_AT(pos++) = (uint16_t)(e + 2);
-    if ((m3 >> lane) & 1) LIST_AT(pos) = (uint16_t)(e + 3);
+    // the masks themselves predicate the stores (inverse ballot: no per-lane bit test)
+    if (__builtin_amdgcn_inverse_ballot_w64(m0)) LIST_AT(pos++) = e;
+    if (__builtin_amdgcn_inverse_ballot_w64(m1)) LIST_AT(pos++) = (uint16_t)(e + 1);
+    if (__builtin_amdgcn_inverse_ballot_w64(m2)) LIST_AT(pos++) = (uint16_t)(e + 2);
+    if (__builtin_amdgcn_inverse_ballot_w64(m3)) LIST_AT(pos) = (uint16_t)(e + 3);
 #undef LIST_AT
     n1 += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
   }
@@ -401,46 +402,56 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   // (d) 3x3 NMS at both thresholds (neighbours below a threshold count as 0)
   const int ti = P.t_ini, tm = P.t_min;
   const int nch2 = (n2 + 63) >> 6;
-  int n_ini = 0;
-  for (int ch = 0; ch < nch2; ++ch) {
-    const int i = ch * 64 + lane;
-    bool ki = false, km = false;
-    if (i < n2) {
-      const int e = list[i];
-      const LDSP uint8_t* q = sc + u24mul((e >> 8) + 1, sw) + (e & 255) + 1;
-      const int s = q[0];
-      bool gi = s >= ti && s > 0, gm = s >= tm && s > 0;
-      const int nbv[8] = {q[-1], q[1], q[-sw - 1], q[-sw], q[-sw + 1], q[sw - 1], q[sw], q[sw + 1]};
+  auto nms = [&](int i, bool* ki, bool* km) {  // detected entry i kept at iniThFAST / minThFAST
+    const int e = list[i];
+    const LDSP uint8_t* q = sc + u24mul((e >> 8) + 1, sw) + (e & 255) + 1;
+    const int s = q[0];
+    bool gi = s >= ti && s > 0, gm = s >= tm && s > 0;
+    const int nbv[8] = {q[-1], q[1], q[-sw - 1], q[-sw], q[-sw + 1], q[sw - 1], q[sw], q[sw + 1]};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int x = nbv[j];
-        if (x >= ti && x >= s) gi = false;
-        if (x >= tm && x >= s) gm = false;
-      }
-      ki = gi;
-      km = gm;
+    for (int j = 0; j < 8; ++j) {
+      const int x = nbv[j];
+      if (x >= ti && x >= s) gi = false;
+      if (x >= tm && x >= s) gm = false;
     }
-    const uint64_t bi = __ballot(ki), bm = __ballot(km);
-    if (lane == 0) {
-      ball[2 * ch] = bi;
-      ball[2 * ch + 1] = bm;
-    }
-    n_ini += __popcll(bi);
-  }
-  __syncthreads();
-  const int which = n_ini > 0 ? 0 : 1;
+    *ki = gi;
+    *km = gm;
+  };
   uint32_t* out = slots + (long long)f * P.slots_per_frame + cg.slot_off;
+  auto emit = [&](int e, int pos) {  // the kept pixel's key, row-major position pos in the cell's slots
+    const int by = e >> 8, bx = e & 255;
+    const int x = cg.c0 + 3 + bx - g.minBX, y = cg.r0 + 3 + by - g.minBY;
+    if (pos < cg.cap) out[pos] = pack_key(x, y, sc[(by + 1) * sw + bx + 1]);
+  };
   int base = 0;
-  for (int ch = 0; ch < nch2; ++ch) {
-    const uint64_t m = ball[2 * ch + which];
-    if ((m >> lane) & 1ull) {
-      const int e = list[ch * 64 + lane];
-      const int by = e >> 8, bx = e & 255;
-      const int pos = base + mbcnt64(m);
-      const int x = cg.c0 + 3 + bx - g.minBX, y = cg.r0 + 3 + by - g.minBY;
-      if (pos < cg.cap) out[pos] = pack_key(x, y, sc[(by + 1) * sw + bx + 1]);
+  if (nch2 <= 1) {
+    // at most 64 detected pixels (the common case): the ballots stay in registers
+    bool ki = false, km = false;
+    if (lane < n2) nms(lane, &ki, &km);
+    const uint64_t bi = __ballot(ki), bm = __ballot(km);
+    const uint64_t m = bi ? bi : bm;
+    if (__builtin_amdgcn_inverse_ballot_w64(m)) emit(list[lane], mbcnt64(m));
+    base = __popcll(m);
+  } else {
+    int n_ini = 0;
+    for (int ch = 0; ch < nch2; ++ch) {
+      const int i = ch * 64 + lane;
+      bool ki = false, km = false;
+      if (i < n2) nms(i, &ki, &km);
+      const uint64_t bi = __ballot(ki), bm = __ballot(km);
+      if (lane == 0) {
+        ball[2 * ch] = bi;
+        ball[2 * ch + 1] = bm;
+      }
+      n_ini += __popcll(bi);
     }
-    base += __popcll(m);
+    __syncthreads();
+    const int which = n_ini > 0 ? 0 : 1;
+    for (int ch = 0; ch < nch2; ++ch) {
+      const uint64_t m = ball[2 * ch + which];
+      if (__builtin_amdgcn_inverse_ballot_w64(m)) emit(list[ch * 64 + lane], base + mbcnt64(m));
+      base += __popcll(m);
+    }
   }
   if (lane == 0) *cnt = min(base, (int)cg.cap);
   stamp(4);
