@@ -368,14 +368,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     const int eA = list[min(iA, n1 - 1)], eB = list[min(iB, n1 - 1)];
     const LDSP uint8_t* cA = band + u24mul(eA >> 8, kRoiStride) + (eA & 255);
     const LDSP uint8_t* cB = band + u24mul(eB >> 8, kRoiStride) + (eB & 255);
-    const i16x2 v = {(short)cA[0], (short)cB[0]};
-    i16x2 D[16];
+    const u16x2_t v = {(unsigned short)cA[0], (unsigned short)cB[0]};
+    u16x2_t R[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const i16x2 p = {(short)cA[ring_off<kRoiStride>(k)], (short)cB[ring_off<kRoiStride>(k)]};
-      D[k] = v - p;
-    }
-    const i16x2 s = corner_score16_x2(D, t);
+    for (int k = 0; k < 16; ++k) R[k] = (u16x2_t){(unsigned short)cA[ring_off<kRoiStride>(k)], (unsigned short)cB[ring_off<kRoiStride>(k)]};
+    const i16x2 s = corner_score16_x2_ring(R, v, t);
     if (kOverlay) {  // score rows up to the chunk's last band row + 1: dead for every later chunk
       const int yhi = list[min(i0 + 127, n1 - 1)] >> 8;
       for (int i = zrow * (kRoiStride / 4) + lane; i < (yhi + 2) * (kRoiStride / 4); i += 64) ((LDSP uint32_t*)sc)[i] = 0;

@@ -23,34 +23,42 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 // so the run minima come from a min tree over the odd starts only. A pixel
 // is FAST-detected at t iff its score is >= t.
 typedef short i16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ i16x2 corner_score16_x2(const i16x2 (&D)[16], int threshold) {
-  i16x2 lo[8], hi[8];
+// Computed from the ring pixels p[k] themselves (u16x2, one pixel per half)
+// and the centre v: min over an arc of (v - p) = v - max over the arc of p
+// (exact in integers), so the trees run on p and v enters once:
+//   a0 = max(t, v - min over arcs of (max of p)),
+//   b0 = min(-a0, v - max over arcs of (min of p)),  score = -b0 - 1
+// (no per-pixel d = v - p subtractions).
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ i16x2 corner_score16_x2_ring(const u16x2_t (&P)[16], u16x2_t v, int threshold) {
+  u16x2_t hi[8], lo[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {  // runs of 2 from odd start s = 2j + 1
-    lo[j] = __builtin_elementwise_min(D[2 * j + 1], D[(2 * j + 2) & 15]);
-    hi[j] = __builtin_elementwise_max(D[2 * j + 1], D[(2 * j + 2) & 15]);
+    hi[j] = __builtin_elementwise_max(P[2 * j + 1], P[(2 * j + 2) & 15]);
+    lo[j] = __builtin_elementwise_min(P[2 * j + 1], P[(2 * j + 2) & 15]);
   }
-  i16x2 lo4[8], hi4[8];
+  u16x2_t hi4[8], lo4[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {  // runs of 4
-    lo4[j] = __builtin_elementwise_min(lo[j], lo[(j + 1) & 7]);
     hi4[j] = __builtin_elementwise_max(hi[j], hi[(j + 1) & 7]);
+    lo4[j] = __builtin_elementwise_min(lo[j], lo[(j + 1) & 7]);
   }
-  const short t = (short)threshold;
-  i16x2 a0 = {t, t};
+  const u16x2_t big = {0xFFFF, 0xFFFF}, zero = {0, 0};
+  u16x2_t A = big, B = zero;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {  // runs of 8 from s, extended to the 9-arcs from s - 1 and s
-    const i16x2 a = __builtin_elementwise_min(lo4[j], lo4[(j + 2) & 7]);
-    a0 = __builtin_elementwise_max(a0, __builtin_elementwise_min(a, D[2 * j]));
-    a0 = __builtin_elementwise_max(a0, __builtin_elementwise_min(a, D[(2 * j + 9) & 15]));
+    const u16x2_t a = __builtin_elementwise_max(hi4[j], hi4[(j + 2) & 7]);
+    A = __builtin_elementwise_min(A, __builtin_elementwise_max(a, P[2 * j]));
+    A = __builtin_elementwise_min(A, __builtin_elementwise_max(a, P[(2 * j + 9) & 15]));
+    const u16x2_t b = __builtin_elementwise_min(lo4[j], lo4[(j + 2) & 7]);
+    B = __builtin_elementwise_max(B, __builtin_elementwise_min(b, P[2 * j]));
+    B = __builtin_elementwise_max(B, __builtin_elementwise_min(b, P[(2 * j + 9) & 15]));
   }
-  i16x2 b0 = -a0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const i16x2 b = __builtin_elementwise_max(hi4[j], hi4[(j + 2) & 7]);
-    b0 = __builtin_elementwise_min(b0, __builtin_elementwise_max(b, D[2 * j]));
-    b0 = __builtin_elementwise_min(b0, __builtin_elementwise_max(b, D[(2 * j + 9) & 15]));
-  }
+  const i16x2 vs = __builtin_bit_cast(i16x2, v);
+  const short t = (short)threshold;
+  const i16x2 tt = {t, t};
+  const i16x2 a0 = __builtin_elementwise_max(tt, vs - __builtin_bit_cast(i16x2, A));
+  const i16x2 b0 = __builtin_elementwise_min(-a0, vs - __builtin_bit_cast(i16x2, B));
   const i16x2 one = {1, 1};
   return -b0 - one;
 }
