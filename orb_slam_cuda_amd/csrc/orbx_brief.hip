@@ -24,13 +24,10 @@
 
 namespace orbx {
 
-// test t: {x0, y0, x1, y1} as four signed bytes (fork and upstream tables),
-// ordered lane-major: lane l's tests l + 32k (k = 0..7) are dwords 8l .. 8l+7,
-// two 16-byte loads per lane issued with the patch loads. Read from the
-// constant buffer instead of a per-workgroup LDS copy: 4 KB less LDS per
-// workgroup (7 instead of 6 resident per CU) for 8 VALU per test
-// (byte extract + int->float, exact).
-__constant__ uint32_t c_brief_tests[2][256];
+// test t: {x0, y0, x1, y1} as floats (fork and upstream tables), converted once
+// on the host so a test costs one 16-byte LDS read instead of 4 byte
+// extracts + 4 int->float conversions per lane
+__constant__ float4 c_brief_tests[2][256];
 
 #ifndef ORBX_OB_THREADS
 #define ORBX_OB_THREADS 256
@@ -78,6 +75,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
                                                                   uint8_t* __restrict__ out_desc,
                                                                   int* __restrict__ out_counts) {
   __shared__ __attribute__((aligned(16))) uint8_t s_patch[kObKps][kObRows * kObStride];
+  __shared__ float4 s_tests[256];
   __shared__ uint32_t s_ictab[16 * kIcStride];
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
   const int bx = wg % gridDim.x, f = wg / gridDim.x, tid = threadIdx.x;
@@ -93,11 +91,11 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   int c[kMaxLevels];
 #pragma unroll
   for (int i = 0; i < kMaxLevels; ++i) c[i] = cnt[i];
-  constexpr int kIcPer = (16 * 24 + kObThreads - 1) / kObThreads;
+  constexpr int kTestsPer = (256 + kObThreads - 1) / kObThreads, kIcPer = (16 * 24 + kObThreads - 1) / kObThreads;
+  float4 test_v[kTestsPer];
   uint32_t ic_v[kIcPer];
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4* tl = (const u32x4*)&c_brief_tests[P.pattern_upstream ? 1 : 0][8 * lane];
-  const u32x4 tq0 = tl[0], tq1 = tl[1];
+#pragma unroll
+  for (int k = 0; k < kTestsPer; ++k) test_v[k] = c_brief_tests[P.pattern_upstream ? 1 : 0][min(tid + k * kObThreads, 255)];
 #pragma unroll
   for (int k = 0; k < kIcPer; ++k) ic_v[k] = c_ic_coef[min(tid + k * kObThreads, 16 * 24 - 1)];
 
@@ -171,6 +169,9 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
 #pragma unroll
   for (int k = 0; k < 9; ++k) w[k] = q[k];
 #pragma unroll
+  for (int k = 0; k < kTestsPer; ++k)
+    if (tid + k * kObThreads < 256) s_tests[tid + k * kObThreads] = test_v[k];
+#pragma unroll
   for (int k = 0; k < kIcPer; ++k)
     if (tid + k * kObThreads < 16 * 24) {
       const int i = tid + k * kObThreads;
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
       }
     }
   }
-  __syncthreads();  // staged patch, IC coefficient table
+  __syncthreads();  // staged patch, test table, IC coefficient table
 
   // ---- IC_Angle (:164-191): per row, the pixels weighted with v_dot4_u32_u8
   // against coefficient dwords (u for u > 0 / -u for u < 0 / 1, inside the
@@ -223,12 +224,10 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   // GET_VALUE(idx): center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)]
   const uint8_t* pc = s_patch[hk] + kObRadius * kObStride + (x - c0);
   uint32_t dword[8];
-  const uint32_t tw[8] = {tq0.x, tq0.y, tq0.z, tq0.w, tq1.x, tq1.y, tq1.z, tq1.w};
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const uint32_t t = tw[k];
-    const float px0 = (float)(int8_t)(t & 0xFF), py0 = (float)(int8_t)((t >> 8) & 0xFF);
-    const float px1 = (float)(int8_t)((t >> 16) & 0xFF), py1 = (float)((int32_t)t >> 24);
+    const float4 t = s_tests[lane + 32 * k];
+    const float px0 = t.x, py0 = t.y, px1 = t.z, py1 = t.w;
     const int ry0 = __float2int_rn(__fadd_rn(__fmul_rn(px0, b), __fmul_rn(py0, a)));
     const int rx0 = __float2int_rn(__fsub_rn(__fmul_rn(px0, a), __fmul_rn(py0, b)));
     const int ry1 = __float2int_rn(__fadd_rn(__fmul_rn(px1, b), __fmul_rn(py1, a)));
@@ -278,13 +277,12 @@ int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const Extra
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return ORBX_EDEVICE;
   if (!g_pattern_uploaded[dev]) {
-    uint32_t t[2][256];
+    float4 t[2][256];
     for (int m = 0; m < 2; ++m)
-      for (int i = 0; i < 256; ++i) {  // test i at lane i % 32, slot i / 32
+      for (int i = 0; i < 256; ++i) {
         int q[4];
         brief_test(m, i, q);
-        t[m][8 * (i % 32) + i / 32] = (uint32_t)(uint8_t)(int8_t)q[0] | ((uint32_t)(uint8_t)(int8_t)q[1] << 8) |
-                                      ((uint32_t)(uint8_t)(int8_t)q[2] << 16) | ((uint32_t)(uint8_t)(int8_t)q[3] << 24);
+        t[m][i] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
       }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_tests), t, sizeof(t)) != hipSuccess) return ORBX_EDEVICE;
     // umax of the r = 15 circle (ORBextractor ctor :540-555; PATCH_SIZE is fixed at 31)
