@@ -162,6 +162,7 @@ def parse_args(argv=None):
 # Tuning: select among bit-exact code paths; allowed, and stamped into the line.
 ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_PYR_PLAN", "ORBX_QT_GENERIC",
               "ORBX_INIT_LDS_KB", "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS",
+              "ORBX_BOW_ROUNDS",
               # the C++ shim's configuration (shim/src/ORBextractor.cc); bench.py does not read them
               "ORBX_DEVICE", "ORBX_SCALE_MODE", "ORBX_PATTERN"}
 # Diagnostics: phase clocks synchronise after every launch, *_STOP / FAST_TWICE

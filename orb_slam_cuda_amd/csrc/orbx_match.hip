@@ -516,7 +516,8 @@ constexpr int kBowRowCost = ORBX_BOW_ROWCOST;  // a row's fixed cost in candidat
 #ifndef ORBX_BOW_ROUNDS
 #define ORBX_BOW_ROUNDS 16
 #endif
-constexpr int kBowRounds = ORBX_BOW_ROUNDS;  // greedy fixed-point rounds before the sequential pass (0: sequential only)
+constexpr int kBowRounds = ORBX_BOW_ROUNDS;  // default greedy fixed-point rounds before the sequential pass
+// (ORBX_BOW_ROUNDS=<n> in the environment overrides it per call; 0: the sequential pass only; results are the same)
 
 struct BowTables {  // the two-pass layout
   uint32_t bdesc[kBowCapB][8];  // the range's B rows, node by node
@@ -548,7 +549,7 @@ union BowLds {
 
 template <int NT>
 __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, float nnratio, int check_ori,
-                                                        int kf_vs_kf, int G, int* __restrict__ out_all,
+                                                        int kf_vs_kf, int G, int max_rounds, int* __restrict__ out_all,
                                                         long long out_pitch, int* __restrict__ bin_all,
                                                         int* __restrict__ hist_all, int* __restrict__ err, int* dbg) {
   constexpr int kWaves = NT / 64;
@@ -908,7 +909,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
     // i chose it: claim = the first such row). Row 1 of a node is right in
     // round 0 and row i by round i - 1, and a round without changes is the
     // unique fixed point = the sequential result, so the rounds stop there.
-    // Rows with a decision changing after kBowRounds rounds fall back to the
+    // Rows with a decision changing after max_rounds rounds fall back to the
     // sequential pass below.
     auto decide = [&](int ia, auto&& taken, bool defer = false) -> int {  // staged position, -1, or -2 = deferred rescan
       const int nv = S.t.nv[ia];
@@ -959,7 +960,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
     for (int ia = tid; ia < na; ia += NT) S.t.match[ia] = decide(ia, [](int, int) { return false; });
     bool settled = false;
     int rounds = 0;
-    for (int round = 0; round < kBowRounds && !settled; ++round) {
+    for (int round = 0; round < max_rounds && !settled; ++round) {
       ++rounds;
       for (int q = tid; q < nb_; q += NT) S.t.claim[q] = INT_MAX;
       if (tid == 0) s_queue = 0;
@@ -1330,10 +1331,12 @@ int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnrat
   static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_BOW_PROF=1)
   static const bool prof = getenv("ORBX_BOW_PROF") && getenv("ORBX_BOW_PROF")[0] == '1';
   const int nwg = pairs * kBowGroups;
+  const char* rs = getenv("ORBX_BOW_ROUNDS");  // read per call (tests force the sequential pass with 0)
+  const int rounds = rs ? std::max(0, std::min(atoi(rs), 1 << 16)) : kBowRounds;
   if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)65536 * 32);
   if (prof) (void)hipMemsetAsync(dbg, 0, (size_t)nwg * 32, s);
   hipLaunchKernelGGL(search_bow_kernel<kBowThreads>, dim3(nwg), dim3(kBowThreads), 0, s, A, B, nnratio,
-                     check_ori, kf_vs_kf, kBowGroups, out, out_pitch, bin_scratch, hist_scratch, err,
+                     check_ori, kf_vs_kf, kBowGroups, rounds, out, out_pitch, bin_scratch, hist_scratch, err,
                      prof ? dbg : nullptr);
   if (prof) {
     std::vector<int> h((size_t)nwg * 8);

@@ -11,12 +11,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=[(10, 6), (4, 5), (2, 4)], ids=["k10L6", "k4L5", "k2L4"])
+@pytest.fixture(scope="module", params=[(10, 6), (16, 5), (10, 5), (4, 5), (2, 4)],
+                ids=["k10L6", "k16L5", "k10L5", "k4L5", "k2L4"])
 def voc(pkg, request):
     """k10 L6: ~100 FeatureVector nodes of ~20 features (the two-pass path);
-    k4 L5: 4 nodes of ~500 (long greedy chains, top-list rescans); k2 L4: the
-    root only, one node of ~2000 (over the LDS tables: the per-wave fallback
-    with candidates streamed from global memory)."""
+    k16 L5 / k10 L5: 16 nodes of ~125 / 10 of ~200 (a row's candidates split
+    over 4 / 8 lanes, long greedy chains, rescans by whole waves); k4 L5: 4
+    nodes of ~500 (over a range's 256 rows: the per-wave fallback); k2 L4: the
+    root only, one node of ~2000 (candidates streamed from global memory)."""
     from orb_slam_cuda_amd.synth import synthetic_vocabulary
     k, L = request.param
     v = synthetic_vocabulary(k, L, seed=1)
@@ -50,8 +52,13 @@ def _extract_and_bow(pkg, v, frames):
     return ext, cap, D, host, s
 
 
-@pytest.mark.parametrize("kf_vs_kf,ratio,ori", [(0, 0.7, 1), (1, 0.75, 1), (0, 0.75, 0)])
-def test_search_by_bow_batch_parity(pkg, O, voc, kf_vs_kf, ratio, ori):
+@pytest.mark.parametrize("kf_vs_kf,ratio,ori,rounds", [(0, 0.7, 1, None), (1, 0.75, 1, None), (0, 0.75, 0, None),
+                                                      (0, 0.7, 1, "0"), (1, 0.75, 1, "1")])
+def test_search_by_bow_batch_parity(pkg, O, voc, kf_vs_kf, ratio, ori, rounds, monkeypatch):
+    """ORBX_BOW_ROUNDS=0 / 1: the greedy resolved by the wave-per-node
+    sequential pass (after 0 / 1 fixed-point rounds), the same answers."""
+    if rounds is not None:
+        monkeypatch.setenv("ORBX_BOW_ROUNDS", rounds)
     from orb_slam_cuda_amd import _lib
     from orb_slam_cuda_amd.synth import SynthSequence
     v, V = voc
