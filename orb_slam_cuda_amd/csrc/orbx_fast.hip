@@ -39,14 +39,13 @@ namespace orbx {
 #define LDSP __attribute__((address_space(3)))
 
 // ROI row stride in LDS: 44 when every cell ROI fits 3 + rw <= 44 bytes (cells
-// of <= 35 px, KITTI and EuRoC: staged with dword loads from the dword below
-// the ROI), else 80 (>= 65-px ROI + 15 bytes of 16-B alignment slack, 16-byte
-// staging). The tight stride cuts a wave's LDS from ~8.0 KB to ~6.3 KB.
-#ifndef ORBX_FAST_TIGHT_E
-#define ORBX_FAST_TIGHT_E 4   // staging element of the tight stride: 4 -> stride 44, 8 -> stride 48
-#endif
-constexpr int kTightE = ORBX_FAST_TIGHT_E;
-constexpr int kRoiTight = kTightE == 4 ? 44 : 48, kRoiWide = 80;
+// of <= 35 px: KITTI), 48 when it fits 48 (cells of <= 39 px: EuRoC, whose
+// top level has 36-px cells), staged with dword loads from the dword below
+// the ROI; else 80 (>= 65-px ROI + 15 bytes of 16-B alignment slack, 16-byte
+// staging, the scalar compass). The tight strides keep a wave's LDS near
+// 6 KB instead of ~8 KB and run the dword compass (compass4).
+constexpr int kTightE = 4;  // staging element of the tight strides
+constexpr int kRoiTight = 44, kRoiTight2 = 48, kRoiWide = 80;
 
 // 24-bit multiply (full-rate v_mul_u32_u24; the compiler cannot prove the
 // operand ranges and otherwise picks the quarter-rate 32/64-bit forms)
@@ -62,15 +61,14 @@ __device__ __forceinline__ int ring_off(int k) {
 
 // (a) of the tight-stride kernel on dword LDS reads: a lane tests 4
 // horizontally adjacent band pixels (G = ceil(bw / 4) lanes per band row,
-// 64 / G rows per pass). Band pixel (y, x) is ROI byte (y + 3) * 44 + OX + 3 + x
+// 64 / G rows per pass). Band pixel (y, x) is ROI byte (y + 3) * S + OX + 3 + x
 // (OX = the cell's byte offset in its first staged dword, a template
 // parameter so every byte extraction is one v_alignbyte_b32 with a constant
 // shift). Pixels split into even / odd u16x2 pairs for the packed compass
 // network; per-pixel ballots give the row-major ordered compaction.
-template <int OX>
+template <int S, int OX>
 __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* list, int bw, int bh, int t,
                                         int lane) {
-  constexpr int S = kRoiTight;
   typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
   // byte offsets, from the group's first dword, of the group's centres, +3 and -3 neighbours
   constexpr int kC = OX + 3, kN4 = OX + 6, kN12 = OX;
@@ -213,15 +211,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
 #else
   const uint8_t* rows = lp.base[l] + f * lp.fstride[l] + (long long)cg.r0 * pitch;
 #endif
-  constexpr bool kTight = kRoiStride == kRoiTight;
+  constexpr bool kTight = kRoiStride != kRoiWide;
   const int a0 = kTight ? (cg.c0 & ~(kTightE - 1)) : (cg.c0 & ~15), ox = cg.c0 - a0;
   // unpredicated staging: lanes past the last piece load and store it again
   // (same bytes), so all of a lane's loads stay in registers and in flight
   if (lp.aligned16[l] && kTight) {
-    // kTightE-byte pieces from the piece at or below c0 (<= 11 dwords or 6
-    // qwords per row), kK per lane in flight
+    // dwords from the one at or below c0 (<= kRoiStride / 4 per row), kK per
+    // lane in flight
     typedef unsigned int piece_t __attribute__((ext_vector_type(kTightE / 4)));
-    constexpr int kK = kTightE == 4 ? 8 : 5;
+    constexpr int kK = 8;
     // a fixed kPR pieces per staged row, so the lane -> (row, piece) split is
     // a division by a constant; pieces past the ROI's last one (nd) and rows
     // past the last (rh) reload that piece / row (same bytes, same LDS slot)
@@ -294,12 +292,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
 
   // (a) compass pre-test over all band pixels, row-major ordered compaction
   int n1 = 0;
-  if constexpr (kTight && kTightE == 4) {
+  if constexpr (kTight) {
     switch (ox) {
-      case 0: n1 = compass4<0>(roi, list, bw, bh, t, lane); break;
-      case 1: n1 = compass4<1>(roi, list, bw, bh, t, lane); break;
-      case 2: n1 = compass4<2>(roi, list, bw, bh, t, lane); break;
-      default: n1 = compass4<3>(roi, list, bw, bh, t, lane); break;
+      case 0: n1 = compass4<kRoiStride, 0>(roi, list, bw, bh, t, lane); break;
+      case 1: n1 = compass4<kRoiStride, 1>(roi, list, bw, bh, t, lane); break;
+      case 2: n1 = compass4<kRoiStride, 2>(roi, list, bw, bh, t, lane); break;
+      default: n1 = compass4<kRoiStride, 3>(roi, list, bw, bh, t, lane); break;
     }
 #ifdef ORBX_FAST_LCAP
     n1 = min(n1, ORBX_FAST_LCAP);
@@ -458,12 +456,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   }
 }
 
-static bool fast_tight(const ExtractParams& P) { return P.fast_bw_max + 6 + kTightE - 1 <= kRoiTight; }
+// the ROI row stride of a plan's launch: the tightest that holds every cell ROI
+// (+ the 3 bytes of its first staged dword below c0)
+static int fast_stride(const ExtractParams& P) {
+  const int need = P.fast_bw_max + 6 + kTightE - 1;
+  return need <= kRoiTight ? kRoiTight : need <= kRoiTight2 ? kRoiTight2 : kRoiWide;
+}
 
 size_t fast_lds_bytes(const ExtractParams& P) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t band = (size_t)P.fast_bw_max * P.fast_bh_max;
-  const int stride = fast_tight(P) ? kRoiTight : kRoiWide;
+  const int stride = fast_stride(P);
 #ifdef ORBX_FAST_LCAP
   const size_t list = std::min(band, (size_t)ORBX_FAST_LCAP);
 #else
@@ -494,8 +497,12 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
   constexpr int reps = 1;
 #endif
   for (int rep = 0; rep < reps; ++rep) {
-    if (fast_tight(P))
+    const int stride = fast_stride(P);
+    if (stride == kRoiTight)
       hipLaunchKernelGGL(fast_cells_kernel<kRoiTight>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
+                         lp, cells, slots, cell_counts, prof ? dbg : nullptr);
+    else if (stride == kRoiTight2)
+      hipLaunchKernelGGL(fast_cells_kernel<kRoiTight2>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
                          lp, cells, slots, cell_counts, prof ? dbg : nullptr);
     else
       hipLaunchKernelGGL(fast_cells_kernel<kRoiWide>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,

@@ -97,7 +97,8 @@ def test_golden_vectors(pkg, name):
     dict(nf=2000, ini=30, mn=10),
     dict(nf=2000, ini=5, mn=12),                    # iniTh < minTh
     dict(nf=0),                                     # no features requested
-    dict(nf=600, W=369, H=300),                     # 37-px cells at level 4: FAST's 80-byte ROI stride path
+    dict(nf=600, W=369, H=300),                     # 39-px cells at level 5: FAST's 48-byte ROI stride, full
+    dict(nf=600, W=420, H=300),                     # 43-px cells at level 7: FAST's 80-byte ROI stride path
 ])
 def test_config_parity(pkg, O, kw):
     from orb_slam_cuda_amd.synth import synth_frame
