@@ -140,6 +140,8 @@ def parse_args(argv=None):
                     help="also SearchByBoW of every frame against its predecessor as reference keyframe (implies --bow)")
     ap.add_argument("--match-streams", type=int, choices=[1, 2], default=1,
                     help="2: SearchForInitialization on its own stream, beside the dense top-2")
+    ap.add_argument("--match-order", choices=["bow-first", "top2-first"], default="top2-first",
+                    help="with --bow/--bow-match: order of the vocabulary stages and the dense top-2 on the matching stream")
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
                     help="stream that copies a batch's last frame for the next batch's first pair")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency leg")
@@ -518,42 +520,48 @@ class MonoPipeline:
                 s_match.wait(self.ev_done2[k - 2])  # SearchForInitialization k-2 also read set (k+1) % 3
             carry(s_match)  # in order after matching k-2, the last reader of set (k+1) % 3
             self.ev_carry[k].record(s_match)
-        if self.voc is not None:
-            evs[9].record(s_match)
-            # Frame::ComputeBoW (src/Frame.cc:394-401, levelsup 4) of the batch's frames
-            # (slots 1..B; with --bow-match also slot 0, the reference keyframe of slot 1)
-            s0 = 0 if self.bow_match else 1
-            check(L.orbv_transform_batch(self.voc.handle, vp(self.d_desc[b].ptr + s0 * cap * DS), cap * DS,
-                                         vp(self.d_counts[b].ptr + 4 * s0), B + 1 - s0, cap, 4, vp(self.d_bw.ptr),
-                                         vp(self.d_bv.ptr), vp(self.d_bn.ptr), vp(self.d_fn.ptr), vp(self.d_fo.ptr),
-                                         vp(self.d_fi.ptr), vp(self.d_fnn.ptr), vp(self.d_vw[0].ptr),
-                                         vp(self.d_vw[1].ptr), vp(self.d_vw[2].ptr), s_match.s), vocabulary=True)
-            evs[10].record(s_match)
-            if self.bow_match:
-                # SearchByBoW(KF, F) of frame t against frame t-1 as the reference keyframe, every
-                # keyframe feature with a MapPoint (Tracking::TrackReferenceKeyFrame, ratio 0.7,
-                # src/Tracking.cc:839-842), all B pairs in one launch
-                ofs = lambda d, k, pitch, size: vp(d.ptr + k * pitch * size)
-                sides = []
-                for side in (0, 1):
-                    sides += [ofs(self.d_kps[b], side, cap, KP), ofs(self.d_desc[b], side, cap, DS),
-                              ofs(self.d_counts[b], side, 1, 4), None, ofs(self.d_fn, side, cap, 4),
-                              ofs(self.d_fo, side, cap + 1, 4), ofs(self.d_fi, side, cap, 4),
-                              ofs(self.d_fnn, side, 1, 4)]
-                check(L.orbm_search_by_bow_batch(self.bow_matcher.handle, B, cap, cap, *sides, C.c_float(0.7), 1, 0,
-                                                 vp(self.d_bow_out.ptr), vp(self.d_bow_nm.ptr), s_match.s),
-                      matcher=True)
-                evs[12].record(s_match)
-        if evs is not None:
-            evs[6].record(s_match)
-        if not a.no_match:
-            # query = frame t (slots 1..B), candidates = frame t-1 (slots 0..B-1)
-            check(L.orbm_hamming_top2(self.matcher.handle, vp(self.d_desc[b].ptr + cap * DS), cap * DS,
-                                      vp(self.d_counts[b].ptr + 4), cap, vp(self.d_desc[b].ptr), cap * DS,
-                                      vp(self.d_counts[b].ptr), B, vp(self.d_bi[b].ptr), vp(self.d_bd[b].ptr),
-                                      vp(self.d_sd[b].ptr), s_match.s), matcher=True)
+        def bow():
+            if self.voc is not None:
+                evs[9].record(s_match)
+                # Frame::ComputeBoW (src/Frame.cc:394-401, levelsup 4) of the batch's frames
+                # (slots 1..B; with --bow-match also slot 0, the reference keyframe of slot 1)
+                s0 = 0 if self.bow_match else 1
+                check(L.orbv_transform_batch(self.voc.handle, vp(self.d_desc[b].ptr + s0 * cap * DS), cap * DS,
+                                             vp(self.d_counts[b].ptr + 4 * s0), B + 1 - s0, cap, 4, vp(self.d_bw.ptr),
+                                             vp(self.d_bv.ptr), vp(self.d_bn.ptr), vp(self.d_fn.ptr), vp(self.d_fo.ptr),
+                                             vp(self.d_fi.ptr), vp(self.d_fnn.ptr), vp(self.d_vw[0].ptr),
+                                             vp(self.d_vw[1].ptr), vp(self.d_vw[2].ptr), s_match.s), vocabulary=True)
+                evs[10].record(s_match)
+                if self.bow_match:
+                    # SearchByBoW(KF, F) of frame t against frame t-1 as the reference keyframe, every
+                    # keyframe feature with a MapPoint (Tracking::TrackReferenceKeyFrame, ratio 0.7,
+                    # src/Tracking.cc:839-842), all B pairs in one launch
+                    ofs = lambda d, k, pitch, size: vp(d.ptr + k * pitch * size)
+                    sides = []
+                    for side in (0, 1):
+                        sides += [ofs(self.d_kps[b], side, cap, KP), ofs(self.d_desc[b], side, cap, DS),
+                                  ofs(self.d_counts[b], side, 1, 4), None, ofs(self.d_fn, side, cap, 4),
+                                  ofs(self.d_fo, side, cap + 1, 4), ofs(self.d_fi, side, cap, 4),
+                                  ofs(self.d_fnn, side, 1, 4)]
+                    check(L.orbm_search_by_bow_batch(self.bow_matcher.handle, B, cap, cap, *sides, C.c_float(0.7), 1, 0,
+                                                     vp(self.d_bow_out.ptr), vp(self.d_bow_nm.ptr), s_match.s),
+                          matcher=True)
+                    evs[12].record(s_match)
+        def top2():
             if evs is not None:
-                evs[7].record(s_match)
+                evs[6].record(s_match)
+            if not a.no_match:
+                # query = frame t (slots 1..B), candidates = frame t-1 (slots 0..B-1)
+                check(L.orbm_hamming_top2(self.matcher.handle, vp(self.d_desc[b].ptr + cap * DS), cap * DS,
+                                          vp(self.d_counts[b].ptr + 4), cap, vp(self.d_desc[b].ptr), cap * DS,
+                                          vp(self.d_counts[b].ptr), B, vp(self.d_bi[b].ptr), vp(self.d_bd[b].ptr),
+                                          vp(self.d_sd[b].ptr), s_match.s), matcher=True)
+                if evs is not None:
+                    evs[7].record(s_match)
+        order = (bow, top2) if a.match_order == "bow-first" else (top2, bow)
+        for stage in order:
+            stage()
+        if not a.no_match:
             if self.two_match:  # after batch k's extraction and the carry into its slot 0 (step k-1)
                 s_init.wait(self.ev_ext[k])
                 if k >= 1:
@@ -769,7 +777,8 @@ def run_mono(args, cfg, rank, world, local, dist):
                                        if args.split_sequence else f"frame-sharded x{world}") + ", one process per GPU, no collectives",
                        "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS,
                        "match_stream_priority": ("low" if args.priority else "high" if args.match_priority
-                                                 else "normal")},
+                                                 else "normal"),
+                       **({"match_order": args.match_order} if (args.bow or args.bow_match) else {})},
             "per_rank_frames_per_s": agg["per_rank"],
             "roofline": roof,
             "match_roofline": match_roof,

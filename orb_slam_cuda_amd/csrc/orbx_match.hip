@@ -454,7 +454,10 @@ __device__ __forceinline__ Top2 wave_top2(bool valid, int dist, int pos) {
 // that node's A features only, the taken bits of a workgroup's nodes are
 // private to it, and only the rotation histogram and the match count are the
 // pair's (global atomics: hist[0..29] bins, hist[30] count;
-// search_bow_finalize_kernel applies ComputeThreeMaxima after).
+// search_bow_finalize_kernel applies ComputeThreeMaxima after). An accepted
+// match goes to the pair's row record, bin << 16 | matched index, in a
+// scratch that is all -1 between calls (finalize writes `out` from it and
+// resets it and the histogram, so no fill launches precede the kernel).
 //
 // Inside a node the reference is greedy (src/ORBmatcher.cc:186-262): A rows in
 // node order, each taking the best untaken B row. The workgroup splits that
@@ -549,9 +552,9 @@ union BowLds {
 
 template <int NT>
 __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, float nnratio, int check_ori,
-                                                        int kf_vs_kf, int G, int max_rounds, int* __restrict__ out_all,
-                                                        long long out_pitch, int* __restrict__ bin_all,
-                                                        int* __restrict__ hist_all, int* __restrict__ err, int* dbg) {
+                                                        int kf_vs_kf, int G, int max_rounds, long long out_pitch,
+                                                        int* __restrict__ rec_all, int* __restrict__ hist_all,
+                                                        int* __restrict__ err, int* dbg) {
   constexpr int kWaves = NT / 64;
   const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
   auto stamp = [&](int k, int v) {  // diagnostics only (ORBX_BOW_PROF=1): per-workgroup phase cycles
@@ -638,8 +641,7 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
   const int* offB = B.off + p * (B.node_pitch + 1);
   const int* idxA = A.idx + p * A.node_pitch;
   const int* idxB = B.idx + p * B.node_pitch;
-  int* out = out_all + p * out_pitch;
-  int* binOf = bin_all + p * out_pitch;
+  int* rec = rec_all + p * out_pitch;
   int* hist = hist_all + p * 32;
   if (nk <= 0) return;
   // feature indices come from device CSR arrays the host cannot check: an
@@ -668,23 +670,17 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
   const float factor = 1.0f / kHistoLength;
   // an accepted match: output, the pair's count and rotation histogram
   auto accept = [&](int idx1, int bestIdx2, int* h) {
-    int histIdx;
-    if (kf_vs_kf) {
-      out[idx1] = bestIdx2;
-      histIdx = idx1;
-    } else {
-      out[bestIdx2] = idx1;
-      histIdx = bestIdx2;
-    }
+    int bin = 0;
     atomicAdd(&h[30], 1);
     if (check_ori) {
       float rot = __fsub_rn(angA[(long long)idx1 * A.angle_stride], angB[(long long)bestIdx2 * B.angle_stride]);
       if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-      int bin = (int)roundf(__fmul_rn(rot, factor));
+      bin = (int)roundf(__fmul_rn(rot, factor));
       if (bin == kHistoLength) bin = 0;
-      binOf[histIdx] = bin;
       atomicAdd(&h[bin], 1);
     }
+    if (kf_vs_kf) rec[idx1] = bin << 16 | bestIdx2;
+    else rec[bestIdx2] = bin << 16 | idx1;
   };
   // lower_bound of a node id in B's node list (the lock-step walk of :180-264
   // meets exactly the shared ids); -1 when B lacks it
@@ -1264,18 +1260,21 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
 }
 
 // Rotation consistency (src/ORBmatcher.cc:267-285, ComputeThreeMaxima :1601-1642)
-// and the final count, one workgroup per pair.
-__global__ __launch_bounds__(256) void search_bow_finalize_kernel(const int* __restrict__ nA, const int* __restrict__ nB,
-                                                                  int kf_vs_kf, int check_ori, int* __restrict__ out_all,
-                                                                  long long out_pitch, const int* __restrict__ bin_all,
+// and the final count, one workgroup per pair: `out` rows from the row
+// records (-1 for rows without a match, past the pair's extent, or whose bin
+// is not one of the three maxima), then the records and the histogram go back
+// to -1 / 0 for the next call.
+__global__ __launch_bounds__(256) void search_bow_finalize_kernel(int check_ori, int* __restrict__ out_all,
+                                                                  long long out_pitch, int* __restrict__ rec_all,
                                                                   int* __restrict__ hist_all, int* __restrict__ nmatches) {
   __shared__ int s_var[4];
   const int p = blockIdx.x, tid = threadIdx.x;
   int* hist = hist_all + p * 32;
-  const int nout = min(kf_vs_kf ? nA[p] : nB[p], (int)min(out_pitch, 65536ll));  // the row's extent
-  if (check_ori) {
-    if (tid == 0) {
-      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+  int count = 0;
+  if (tid == 0) {
+    count = hist[30];
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    if (check_ori) {
       for (int i = 0; i < kHistoLength; i++) {
         const int s = hist[i];
         if (s > max1) {
@@ -1295,39 +1294,51 @@ __global__ __launch_bounds__(256) void search_bow_finalize_kernel(const int* __r
       } else if (max3 < __fmul_rn(0.1f, (float)max1)) {
         ind3 = -1;
       }
-      s_var[0] = ind1;
-      s_var[1] = ind2;
-      s_var[2] = ind3;
-      s_var[3] = 0;
     }
-    __syncthreads();
-    const int ind1 = s_var[0], ind2 = s_var[1], ind3 = s_var[2];
-    int* out = out_all + p * out_pitch;
-    const int* binOf = bin_all + p * out_pitch;
-    int removed = 0;
-    for (int i = tid; i < nout; i += 256) {
-      const int b = binOf[i];
-      if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
-      out[i] = -1;
-      ++removed;
-    }
-    if (removed) atomicAdd(&s_var[3], removed);
-    __syncthreads();
-    if (tid == 0) nmatches[p] = hist[30] - s_var[3];
-  } else if (tid == 0) {
-    nmatches[p] = hist[30];
+    s_var[0] = ind1;
+    s_var[1] = ind2;
+    s_var[2] = ind3;
+    s_var[3] = 0;
   }
+  __syncthreads();
+  if (tid < 32) hist[tid] = 0;
+  const int ind1 = s_var[0], ind2 = s_var[1], ind3 = s_var[2];
+  int* out = out_all + p * out_pitch;
+  int* rec = rec_all + p * out_pitch;
+  int removed = 0;
+  for (long long i = tid; i < out_pitch; i += 256) {
+    const int v = rec[i];
+    int o = -1;
+    if (v >= 0) {
+      rec[i] = -1;
+      const int b = v >> 16;
+      if (!check_ori || b == ind1 || b == ind2 || b == ind3) o = v & 0xFFFF;
+      else ++removed;
+    }
+    out[i] = o;
+  }
+  if (removed) atomicAdd(&s_var[3], removed);
+  __syncthreads();
+  if (tid == 0) nmatches[p] = count - s_var[3];
 }
 
+// rec_scratch / hist_scratch: the row records (all -1) and histograms (all 0)
+// between calls when *clean; otherwise they are filled first. *clean is false
+// from the search launch until its finalize is queued.
 int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnratio, int check_ori, int kf_vs_kf,
-                      int* out, long long out_pitch, int* nmatches, int* bin_scratch, int* hist_scratch, int* err,
-                      void* stream) {
+                      int* out, long long out_pitch, int* nmatches, int* rec_scratch, int* hist_scratch, bool* clean,
+                      int* err, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  // outputs and bins start at -1 (0xFF bytes), histograms and counts at 0
-  if (hipMemsetAsync(out, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
-      hipMemsetAsync(bin_scratch, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
-      hipMemsetAsync(hist_scratch, 0, (size_t)pairs * 32 * 4, s) != hipSuccess)
+  if (!*clean && (hipMemsetAsync(rec_scratch, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
+                  hipMemsetAsync(hist_scratch, 0, (size_t)pairs * 32 * 4, s) != hipSuccess))
     return ORBX_EDEVICE;
+#ifdef ORBX_BOW_FILLS  // diagnostics (tools/variant.sh): the three fill launches of the previous scheme, harmless here
+  if (*clean && (hipMemsetAsync(out, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
+                 hipMemsetAsync(rec_scratch, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
+                 hipMemsetAsync(hist_scratch, 0, (size_t)pairs * 32 * 4, s) != hipSuccess))
+    return ORBX_EDEVICE;
+#endif
+  *clean = false;
   static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_BOW_PROF=1)
   static const bool prof = getenv("ORBX_BOW_PROF") && getenv("ORBX_BOW_PROF")[0] == '1';
   const int nwg = pairs * kBowGroups;
@@ -1336,7 +1347,7 @@ int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnrat
   if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)65536 * 32);
   if (prof) (void)hipMemsetAsync(dbg, 0, (size_t)nwg * 32, s);
   hipLaunchKernelGGL(search_bow_kernel<kBowThreads>, dim3(nwg), dim3(kBowThreads), 0, s, A, B, nnratio,
-                     check_ori, kf_vs_kf, kBowGroups, rounds, out, out_pitch, bin_scratch, hist_scratch, err,
+                     check_ori, kf_vs_kf, kBowGroups, rounds, out_pitch, rec_scratch, hist_scratch, err,
                      prof ? dbg : nullptr);
   if (prof) {
     std::vector<int> h((size_t)nwg * 8);
@@ -1369,9 +1380,11 @@ int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnrat
               h[w * 8 + 6], h[w * 8 + 7]);
     }
   }
-  hipLaunchKernelGGL(search_bow_finalize_kernel, dim3(pairs), dim3(256), 0, s, A.n, B.n, kf_vs_kf, check_ori, out,
-                     out_pitch, bin_scratch, hist_scratch, nmatches);
-  return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+  hipLaunchKernelGGL(search_bow_finalize_kernel, dim3(pairs), dim3(256), 0, s, check_ori, out, out_pitch, rec_scratch,
+                     hist_scratch, nmatches);
+  if (hipGetLastError() != hipSuccess) return ORBX_EDEVICE;
+  *clean = true;
+  return ORBX_OK;
 }
 
 // ------------------------------------------------------------ launchers
@@ -1427,12 +1440,14 @@ struct orbx_matcher {
   long long cand_cap = 0;
   uint32_t* cand = nullptr;
   int* err = nullptr;
-  int* stereo_sad = nullptr;  // [max_pairs][max_kps] SAD per left keypoint (-1 = none); SearchByBoW bins
-  int* bow_hist = nullptr;    // [max_pairs][32] SearchByBoW rotation histogram (+ match count)
+  int* stereo_sad = nullptr;  // [max_pairs][max_kps] SAD per left keypoint (-1 = none)
+  int* bow_hist = nullptr;    // [max_pairs][32] SearchByBoW rotation histogram (+ match count), 0 between calls
+  int* bow_rec = nullptr;     // [max_pairs][max_kps] SearchByBoW row records, -1 between calls
+  bool bow_clean = false;     // bow_hist / bow_rec hold their between-calls values
   int* pose_picks = nullptr;  // pose-projection picks per point (frames x mp_pitch)
   size_t pose_picks_cap = 0;
   hipStream_t stream = nullptr;
-  WsOrder ws;  // stream order of cand / stereo_sad / pose_picks across caller streams
+  WsOrder ws;  // stream order of cand / stereo_sad / pose_picks / bow_* across caller streams
   // staging for the synchronous entry points
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -1465,7 +1480,8 @@ int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out) {
   if (hipMalloc(&m->cand, (size_t)max_pairs * m->cand_cap * 4) != hipSuccess ||
       hipMalloc(&m->err, 16) != hipSuccess ||
       hipMalloc(&m->stereo_sad, (size_t)max_pairs * max_kps * 4) != hipSuccess ||
-      hipMalloc(&m->bow_hist, (size_t)max_pairs * 32 * 4) != hipSuccess) {
+      hipMalloc(&m->bow_hist, (size_t)max_pairs * 32 * 4) != hipSuccess ||
+      hipMalloc(&m->bow_rec, (size_t)max_pairs * max_kps * 4) != hipSuccess) {
     orbm_destroy(m);
     return mfail(ORBX_ENOMEM, "matcher workspace allocation failed");
   }
@@ -1484,6 +1500,7 @@ int orbm_destroy(orbm_handle m) {
   if (m->err) (void)hipFree(m->err);
   if (m->stereo_sad) (void)hipFree(m->stereo_sad);
   if (m->bow_hist) (void)hipFree(m->bow_hist);
+  if (m->bow_rec) (void)hipFree(m->bow_rec);
   if (m->pose_picks) (void)hipFree(m->pose_picks);
   if (m->stage) (void)hipFree(m->stage);
   if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -1692,8 +1709,9 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
             (const uint32_t*)d[3], (const int*)d[4], (const int*)d[5], dn + 2, 0, 0};
   BowSide B{(const uint8_t*)d[6], (const float*)d[7], 1, mpB ? (const uint8_t*)d[8] : nullptr, dn + 1,
             (const uint32_t*)d[9], (const int*)d[10], (const int*)d[11], dn + 3, 0, 0};
+  bool clean = false;  // staging memory: records and histogram filled first
   if ((rc = launch_search_bow(A, B, 1, nnratio, check_ori, kf_vs_kf, (int*)d[12], std::max(nout, 1), (int*)d[14],
-                              (int*)d[13], (int*)d[16], m->err, st)))
+                              (int*)d[13], (int*)d[16], &clean, m->err, st)))
     return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
   int nm = 0;
   MHIP(hipMemcpyAsync(&nm, d[14], 4, hipMemcpyDeviceToHost, st));
@@ -1723,7 +1741,7 @@ int orbm_search_by_bow_batch(orbm_handle m, int pairs, int kp_pitch, int node_pi
   hipStream_t s = (hipStream_t)stream;
   if (m->ws.before(s)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
   const int rc = launch_search_bow(A, B, pairs, nnratio, check_ori, kf_vs_kf, d_out, kp_pitch, d_nmatches,
-                                   m->stereo_sad, m->bow_hist, m->err, stream);
+                                   m->bow_rec, m->bow_hist, &m->bow_clean, m->err, stream);
   if (rc) return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
   if (m->ws.after(s)) return mfail(ORBX_EDEVICE, "event record failed");
   return ORBX_OK;

@@ -69,27 +69,42 @@ __global__ __launch_bounds__(256) void voc_descend_kernel(VocDev V, const uint8_
   int node = 0, level = 0;
   uint32_t nid = 0;
   bool nid_set = nid_level <= 0;
-  while (true) {
-    const int2 cf = V.child[node];
-    if (cf.y == 0) break;  // isLeaf(): no children
-    ++level;
-    int best = INT_MAX;
-    for (int c = sub; c < cf.y; c += GL) {
-      const uint4 a = V.desc[2 * (cf.x + c)], b = V.desc[2 * (cf.x + c) + 1];
-      const int d = __popc(a.x ^ q0.x) + __popc(a.y ^ q0.y) + __popc(a.z ^ q0.z) + __popc(a.w ^ q0.w) +
-                    __popc(b.x ^ q1.x) + __popc(b.y ^ q1.y) + __popc(b.z ^ q1.z) + __popc(b.w ^ q1.w);
-      best = min(best, (d << 16) | c);
-    }
-    if (GL <= 16) {  // group minimum on DPP (quad, half-row, row), no LDS round trip
-      best = min(best, dpp_i<kDppQuad1032>(INT_MAX, best));
-      best = min(best, dpp_i<kDppQuad2301>(INT_MAX, best));
-      if (GL > 4) best = min(best, dpp_i<kDppHalfMirror>(INT_MAX, best));
-      if (GL > 8) best = min(best, dpp_i<kDppMirror>(INT_MAX, best));
+  // group minimum on DPP (quad, half-row, row) for GL <= 16, no LDS round trip
+  auto group_min = [](int v) {
+    if (GL <= 16) {
+      v = min(v, dpp_i<kDppQuad1032>(INT_MAX, v));
+      v = min(v, dpp_i<kDppQuad2301>(INT_MAX, v));
+      if (GL > 4) v = min(v, dpp_i<kDppHalfMirror>(INT_MAX, v));
+      if (GL > 8) v = min(v, dpp_i<kDppMirror>(INT_MAX, v));
     } else {
 #pragma unroll
-      for (int o = GL / 2; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, GL));
+      for (int o = GL / 2; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, GL));
     }
+    return v;
+  };
+  // each candidate's own {first child, count} is loaded beside its descriptor,
+  // and the winner's handed over by two more group minima, so a level costs
+  // one dependent global round trip instead of two
+  int2 cf = V.child[0];
+  while (cf.y != 0) {  // isLeaf(): no children
+    ++level;
+    int mine = INT_MAX;
+    int2 mcf = make_int2(0, 0);
+    for (int c = sub; c < cf.y; c += GL) {
+      const uint4 a = V.desc[2 * (cf.x + c)], b = V.desc[2 * (cf.x + c) + 1];
+      const int2 nc = V.child[cf.x + c];
+      const int d = __popc(a.x ^ q0.x) + __popc(a.y ^ q0.y) + __popc(a.z ^ q0.z) + __popc(a.w ^ q0.w) +
+                    __popc(b.x ^ q1.x) + __popc(b.y ^ q1.y) + __popc(b.z ^ q1.z) + __popc(b.w ^ q1.w);
+      const int key = (d << 16) | c;
+      if (key < mine) {
+        mine = key;
+        mcf = nc;
+      }
+    }
+    const int best = group_min(mine);  // keys are distinct: exactly one lane holds the winner
     node = cf.x + (best & 0xFFFF);
+    const bool win = mine == best;
+    cf = make_int2(group_min(win ? mcf.x : INT_MAX), group_min(win ? mcf.y : INT_MAX));
     if (level == nid_level) {
       nid = V.orig[node];
       nid_set = true;
