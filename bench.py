@@ -140,8 +140,10 @@ def parse_args(argv=None):
                     help="also SearchByBoW of every frame against its predecessor as reference keyframe (implies --bow)")
     ap.add_argument("--match-streams", type=int, choices=[1, 2], default=1,
                     help="2: SearchForInitialization on its own stream, beside the dense top-2")
-    ap.add_argument("--match-order", choices=["bow-first", "top2-first"], default="top2-first",
-                    help="with --bow/--bow-match: order of the vocabulary stages and the dense top-2 on the matching stream")
+    ap.add_argument("--match-order", type=match_order, default="top2,bow,init",
+                    help="order of the matching stages on the matching stream: a permutation of top2 (dense "
+                         "Hamming top-2), bow (ComputeBoW [+ SearchByBoW], with --bow/--bow-match), init "
+                         "(SearchForInitialization)")
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
                     help="stream that copies a batch's last frame for the next batch's first pair")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency leg")
@@ -246,6 +248,13 @@ def launch(args, argv) -> int:
                 if q.is_alive():
                     q.terminate()
     return code
+
+
+def match_order(v):
+    names = v.split(",")
+    if sorted(names) != ["bow", "init", "top2"]:
+        raise argparse.ArgumentTypeError("a permutation of top2,bow,init")
+    return v
 
 
 def main(argv=None):
@@ -558,23 +567,24 @@ class MonoPipeline:
                                           vp(self.d_sd[b].ptr), s_match.s), matcher=True)
                 if evs is not None:
                     evs[7].record(s_match)
-        order = (bow, top2) if a.match_order == "bow-first" else (top2, bow)
-        for stage in order:
-            stage()
-        if not a.no_match:
-            if self.two_match:  # after batch k's extraction and the carry into its slot 0 (step k-1)
-                s_init.wait(self.ev_ext[k])
-                if k >= 1:
-                    s_init.wait(self.ev_carry[k - 1])
+        def init():
+            if not a.no_match:
+                if self.two_match:  # after batch k's extraction and the carry into its slot 0 (step k-1)
+                    s_init.wait(self.ev_ext[k])
+                    if k >= 1:
+                        s_init.wait(self.ev_carry[k - 1])
+                if evs is not None:
+                    evs[11].record(s_init)
+                check(L.orbm_search_for_initialization_batch(
+                    self.matcher.handle, vp(self.d_kps[b].ptr), vp(self.d_desc[b].ptr), vp(self.d_counts[b].ptr),
+                    vp(self.d_kps[b].ptr + cap * KP), vp(self.d_desc[b].ptr + cap * DS), vp(self.d_counts[b].ptr + 4),
+                    cap, B, self.bounds, None, 100, C.c_float(0.9), 1, vp(self.d_m12[b].ptr), vp(self.d_nm[b].ptr),
+                    s_init.s), matcher=True)
             if evs is not None:
-                evs[11].record(s_init)
-            check(L.orbm_search_for_initialization_batch(
-                self.matcher.handle, vp(self.d_kps[b].ptr), vp(self.d_desc[b].ptr), vp(self.d_counts[b].ptr),
-                vp(self.d_kps[b].ptr + cap * KP), vp(self.d_desc[b].ptr + cap * DS), vp(self.d_counts[b].ptr + 4),
-                cap, B, self.bounds, None, 100, C.c_float(0.9), 1, vp(self.d_m12[b].ptr), vp(self.d_nm[b].ptr),
-                s_init.s), matcher=True)
-        if evs is not None:
-            evs[8].record(s_init)
+                evs[8].record(s_init)
+        stages = {"bow": bow, "top2": top2, "init": init}
+        for name in a.match_order.split(","):
+            stages[name]()
         self.ev_done[k].record(s_match)
         if self.two_match:
             self.ev_done2[k].record(s_init)
@@ -778,7 +788,7 @@ def run_mono(args, cfg, rank, world, local, dist):
                        "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS,
                        "match_stream_priority": ("low" if args.priority else "high" if args.match_priority
                                                  else "normal"),
-                       **({"match_order": args.match_order} if (args.bow or args.bow_match) else {})},
+                       "match_order": args.match_order},
             "per_rank_frames_per_s": agg["per_rank"],
             "roofline": roof,
             "match_roofline": match_roof,
