@@ -223,7 +223,8 @@ int orbm_destroy(orbm_handle m);
  * for the device; `reset` != 0 clears it. The synchronous entry points check
  * and clear it themselves.
  *
- * Device workspaces (candidate lists, stereo SAD, pose picks) belong to the
+ * Device workspaces (candidate lists, stereo SAD, pose picks, SearchByBoW row
+ * records and histograms) belong to the
  * handle: batched calls on different streams are ordered by the library
  * (each waits for the previous user of the workspace), so they never
  * overlap on it. The same holds for an extractor handle's plan buffers, and

@@ -124,6 +124,28 @@ def test_dense_noise_uses_global_quadtree_path(pkg, O):
     assert_same(kp, desc, rkp, rdesc)
 
 
+@pytest.mark.parametrize("W,H", [(1241, 376), (752, 480)])
+def test_fast_noise_ramp(pkg, O, W, H):
+    # noise of rising amplitude across the frame: cells from a handful of
+    # compass survivors to nearly every band pixel listed, from no corners to
+    # hundreds detected (the multi-chunk NMS path), per-cell FAST candidates
+    # and the full extraction
+    rng = np.random.default_rng(6)
+    amp = np.repeat(np.linspace(2, 128, 16), -(-W // 16))[:W][None, :]
+    base = np.linspace(60, 190, H)[:, None]
+    img = np.clip(base + rng.uniform(-1, 1, size=(H, W)) * amp, 0, 255).astype(np.uint8)
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H)
+    kp, desc = ext(img)
+    cfg = oracle_cfg(O, 2000, W, H)
+    for l in range(8):
+        g, r = ext.fast_candidates(l), O.fast_level(cfg, img, l)
+        assert len(g) == len(r), (l, len(g), len(r))
+        for f in ("x", "y", "response"):
+            assert np.array_equal(g[f], r[f]), f"fast {l} {f}"
+    rkp, rdesc = O.extract(cfg, img)
+    assert_same(kp, desc, rkp, rdesc)
+
+
 def test_generic_quadtree_rounds(pkg, O, monkeypatch):
     # the generic quadtree rounds (plans whose node table does not fit the lean
     # rounds' 16-bit packing) on a normal frame and on dense noise
