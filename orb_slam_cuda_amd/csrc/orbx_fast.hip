@@ -133,16 +133,6 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
   return n1;
 }
 
-#ifndef ORBX_FAST_OVERLAY
-#define ORBX_FAST_OVERLAY 0  // 1: score map overlaid on the dead ROI rows (see the kernel's LDS carve)
-#endif
-// bytes of the overlaid ROI + score map + NMS ballot region
-__host__ __device__ constexpr int fast_region_bytes(int rh_max, int bw_max, int bh_max, int stride) {
-  return (rh_max + 2) * stride > (((bh_max + 2) * stride + 15) & ~15) + 16 * ((bw_max * bh_max + 63) / 64)
-             ? (rh_max + 2) * stride
-             : (((bh_max + 2) * stride + 15) & ~15) + 16 * ((bw_max * bh_max + 63) / 64);
-}
-
 #ifndef ORBX_FAST_PK
 #define ORBX_FAST_PK 1  // packed-u16 compass pre-test (0: the scalar form, for A/B)
 #endif
@@ -185,23 +175,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   // LDS-typed pointers: 32-bit offsets in every address computation
   LDSP unsigned char* sp = (LDSP unsigned char*)smem;
   auto take = [&](size_t bytes) { LDSP unsigned char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
-  // ORBX_FAST_OVERLAY: the score map lives in the ROI region instead: score
-  // row r at region row r (stride kRoiStride), the ROI two rows below, so the
-  // score of band row y lands in ROI row y - 1, which no pixel of band row >= y
-  // reads; phase (b) zeroes the score rows behind its row-major frontier
-  // (fewer LDS bytes per wave, more zeroing work inside the phase)
-  constexpr bool kOverlay = ORBX_FAST_OVERLAY;
-  LDSP uint8_t* reg = kOverlay ? (LDSP uint8_t*)take(fast_region_bytes(P.fast_rh_max, P.fast_bw_max, P.fast_bh_max,
-                                                                       kRoiStride))
-                               : nullptr;
-  LDSP uint8_t* roi = kOverlay ? reg + 2 * kRoiStride : (LDSP uint8_t*)take((size_t)P.fast_rh_max * kRoiStride);
+  LDSP uint8_t* roi = (LDSP uint8_t*)take((size_t)P.fast_rh_max * kRoiStride);
   // score map with a zero ring, row stride bw + 1: the right border of a row
   // is the left border of the next, which no score is ever written to
-  LDSP uint8_t* sc = kOverlay ? reg : (LDSP uint8_t*)take((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1);
+  LDSP uint8_t* sc = (LDSP uint8_t*)take((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1);
   LDSP uint16_t* list = (LDSP uint16_t*)take(2ull * P.fast_bw_max * P.fast_bh_max);
   // the NMS ballots live in the ROI's LDS: the ROI is dead once the scores are
   // written (phase (d) reads only the list and the score map)
-  LDSP uint64_t* ball = kOverlay ? (LDSP uint64_t*)(reg + (((bh + 2) * kRoiStride + 15) & ~15)) : (LDSP uint64_t*)roi;
+  LDSP uint64_t* ball = (LDSP uint64_t*)roi;
 
   const int l = cg.level;
   const LevelGeom& g = P.lv[l];
@@ -275,12 +256,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     for (int r = 0; r < rh; ++r)
       for (int c = lane; c < rw; c += 64) roi[r * kRoiStride + ox + c] = rows[(long long)r * pitch + cg.c0 + c];
   }
-  const int sw = kOverlay ? kRoiStride : bw + 1;
-  if (kOverlay) {  // score rows 0 and 1 (above the ROI); the others behind phase (b)'s frontier
-    if (lane < kRoiStride / 2) ((LDSP uint32_t*)sc)[lane] = 0;
-  } else {
-    for (int i = lane; i < (sw * (bh + 2) + 1 + 3) >> 2; i += 64) ((LDSP uint32_t*)sc)[i] = 0;
-  }
+  const int sw = bw + 1;
+  for (int i = lane; i < (sw * (bh + 2) + 1 + 3) >> 2; i += 64) ((LDSP uint32_t*)sc)[i] = 0;
   __syncthreads();
   stamp(0);
 
@@ -356,7 +333,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     }
   }
   stamp(1);
-  int n2 = 0, zrow = 2;  // overlay: score rows [0, zrow) are zero or hold scores
+  int n2 = 0;
   // (b) cornerScore<16> of every compass survivor, two per lane as packed
   // i16x2 (entries i and i + 64 of a 128-entry chunk): detected iff score >= t,
   // so the score replaces the ring test. Detected pixels keep their score in
@@ -371,11 +348,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
 #pragma unroll
     for (int k = 0; k < 16; ++k) R[k] = (u16x2_t){(unsigned short)cA[ring_off<kRoiStride>(k)], (unsigned short)cB[ring_off<kRoiStride>(k)]};
     const i16x2 s = corner_score16_x2_ring(R, v, t);
-    if (kOverlay) {  // score rows up to the chunk's last band row + 1: dead for every later chunk
-      const int yhi = list[min(i0 + 127, n1 - 1)] >> 8;
-      for (int i = zrow * (kRoiStride / 4) + lane; i < (yhi + 2) * (kRoiStride / 4); i += 64) ((LDSP uint32_t*)sc)[i] = 0;
-      zrow = max(zrow, yhi + 2);
-    }
     const bool dA = iA < n1 && s.x >= t, dB = iB < n1 && s.y >= t;
     const uint64_t mA = __ballot(dA), mB = __ballot(dB);
     if (dA) {
@@ -389,8 +361,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     }
     n2 += __popcll(mB);
   }
-  if (kOverlay)
-    for (int i = zrow * (kRoiStride / 4) + lane; i < (bh + 2) * (kRoiStride / 4); i += 64) ((LDSP uint32_t*)sc)[i] = 0;
   stamp(2);
   __syncthreads();
   stamp(3);
@@ -475,9 +445,6 @@ size_t fast_lds_bytes(const ExtractParams& P) {
 #ifndef ORBX_FAST_LDS_PAD
 #define ORBX_FAST_LDS_PAD 0  // residency experiments (tools/variant.sh): extra LDS per wave
 #endif
-  if (ORBX_FAST_OVERLAY)
-    return r16(fast_region_bytes(P.fast_rh_max, P.fast_bw_max, P.fast_bh_max, stride)) + r16(2 * list) +
-           ORBX_FAST_LDS_PAD;
   return r16(std::max((size_t)P.fast_rh_max * stride, 16 * ((band + 63) / 64))) +
          r16((size_t)(P.fast_bw_max + 1) * (P.fast_bh_max + 2) + 1) + r16(2 * list) + ORBX_FAST_LDS_PAD;
 }

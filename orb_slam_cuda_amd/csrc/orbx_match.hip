@@ -1332,12 +1332,6 @@ int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnrat
   if (!*clean && (hipMemsetAsync(rec_scratch, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
                   hipMemsetAsync(hist_scratch, 0, (size_t)pairs * 32 * 4, s) != hipSuccess))
     return ORBX_EDEVICE;
-#ifdef ORBX_BOW_FILLS  // diagnostics (tools/variant.sh): the three fill launches of the previous scheme, harmless here
-  if (*clean && (hipMemsetAsync(out, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
-                 hipMemsetAsync(rec_scratch, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
-                 hipMemsetAsync(hist_scratch, 0, (size_t)pairs * 32 * 4, s) != hipSuccess))
-    return ORBX_EDEVICE;
-#endif
   *clean = false;
   static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_BOW_PROF=1)
   static const bool prof = getenv("ORBX_BOW_PROF") && getenv("ORBX_BOW_PROF")[0] == '1';
