@@ -152,10 +152,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   };
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
   const int cell = wg % P.ncells_total, f = wg / P.ncells_total, lane = threadIdx.x;
-  // the whole 16-byte cell record in one scalar load (int16 fields unpacked
-  // from it, so no 16-bit vector load sits on the critical path)
   CellGeom cg;
   {
+    // the whole 16-byte cell record in one scalar load (int16 fields unpacked
+    // from it, so no 16-bit vector load sits on the critical path)
     const int4 raw = ((const int4*)cells)[cell];
     cg.c0 = (int16_t)(raw.x & 0xFFFF);
     cg.r0 = (int16_t)(raw.x >> 16);
@@ -164,6 +164,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     cg.slot_off = raw.z;
     cg.cap = (int16_t)(raw.w & 0xFFFF);
     cg.level = (int16_t)(raw.w >> 16);
+    // diagnostics: clock at which the cell record arrived (the test waits for it)
+    if (dbg && threadIdx.x == 0 && raw.w != -1)
+      dbg[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + 7] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
   }
   int* cnt = cell_counts + (long long)f * P.ncells_total + cell;
   const int rw = cg.c1 - cg.c0, rh = cg.r1 - cg.r0;
@@ -484,11 +487,11 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
     for (int w = 0; w < nwg; ++w) {
       if (h[w * 8 + 4] == 0) continue;  // skipped cell
       ++n;
-      for (int k = 0; k < 7; ++k) t[k] += h[w * 8 + k];
+      for (int k = 0; k < 8; ++k) t[k] += h[w * 8 + k];
     }
     n = n ? n : 1;
-    fprintf(stderr, "fast: %d cells; avg cycles at stage end: staged %.0f compass %.0f score %.0f synced %.0f done %.0f; avg n1 %.1f n2 %.1f\n",
-            n, t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6] / n);
+    fprintf(stderr, "fast: %d cells; avg cycles at stage end: record %.0f staged %.0f compass %.0f score %.0f synced %.0f done %.0f; avg n1 %.1f n2 %.1f\n",
+            n, t[7] / n, t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6] / n);
   }
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
