@@ -58,6 +58,19 @@ def test_parse_defaults():
     import bench
     a = bench.parse_args([])
     assert a.gpus == 1 and a.batch == 64 and a.pool % a.batch == 0 and a.pool * 1280 * 376 > 256 * 2 ** 20
+    assert a.match_order == "top2,bow,init"
+
+
+@pytest.mark.parametrize("order,ok", [("init,top2,bow", True), ("bow,top2,init", True), ("top2,bow", False),
+                                      ("top2,top2,init", False), ("top2,bow,init,x", False)])
+def test_parse_match_order(order, ok):
+    sys.path.insert(0, ROOT)
+    import bench
+    if ok:
+        assert bench.parse_args(["--match-order", order]).match_order == order
+    else:
+        with pytest.raises(SystemExit):
+            bench.parse_args(["--match-order", order])
 
 
 def test_launcher_parent_never_loads_hip():
