@@ -1323,14 +1323,17 @@ __global__ __launch_bounds__(256) void search_bow_finalize_kernel(int check_ori,
 }
 
 // rec_scratch / hist_scratch: the row records (all -1) and histograms (all 0)
-// between calls when *clean; otherwise they are filled first. *clean is false
-// from the search launch until its finalize is queued.
+// between calls when *clean; otherwise their first rec_ints / hist_ints (the
+// whole buffers, so that a later call with more pairs or a wider pitch also
+// finds them clean) are filled first. *clean is false from the search launch
+// until its finalize is queued.
 int launch_search_bow(const BowSide& A, const BowSide& B, int pairs, float nnratio, int check_ori, int kf_vs_kf,
-                      int* out, long long out_pitch, int* nmatches, int* rec_scratch, int* hist_scratch, bool* clean,
-                      int* err, void* stream) {
+                      int* out, long long out_pitch, int* nmatches, int* rec_scratch, size_t rec_ints,
+                      int* hist_scratch, size_t hist_ints, bool* clean, int* err, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (!*clean && (hipMemsetAsync(rec_scratch, 0xFF, (size_t)pairs * out_pitch * 4, s) != hipSuccess ||
-                  hipMemsetAsync(hist_scratch, 0, (size_t)pairs * 32 * 4, s) != hipSuccess))
+  if ((size_t)pairs * out_pitch > rec_ints || (size_t)pairs * 32 > hist_ints) return ORBX_ECAPACITY;
+  if (!*clean && (hipMemsetAsync(rec_scratch, 0xFF, rec_ints * 4, s) != hipSuccess ||
+                  hipMemsetAsync(hist_scratch, 0, hist_ints * 4, s) != hipSuccess))
     return ORBX_EDEVICE;
   *clean = false;
   static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_BOW_PROF=1)
@@ -1671,8 +1674,8 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
   const size_t sz[] = {r16((size_t)nA * 32), r16((size_t)nA * 4), r16((size_t)nA), r16((size_t)fvA.n_nodes * 4),
                        r16((size_t)(fvA.n_nodes + 1) * 4), r16((size_t)ia * 4), r16((size_t)nB * 32),
                        r16((size_t)nB * 4), r16((size_t)nB), r16((size_t)fvB.n_nodes * 4),
-                       r16((size_t)(fvB.n_nodes + 1) * 4), r16((size_t)ib * 4), r16((size_t)nout * 4),
-                       r16((size_t)nout * 4), 16, 16, 128};
+                       r16((size_t)(fvB.n_nodes + 1) * 4), r16((size_t)ib * 4), r16((size_t)std::max(nout, 1) * 4),
+                       r16((size_t)std::max(nout, 1) * 4), 16, 16, 128};  // out / records: the launch's pitch
   size_t tot = 0;
   for (size_t v : sz) tot += v;
   int rc;
@@ -1705,7 +1708,7 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
             (const uint32_t*)d[9], (const int*)d[10], (const int*)d[11], dn + 3, 0, 0};
   bool clean = false;  // staging memory: records and histogram filled first
   if ((rc = launch_search_bow(A, B, 1, nnratio, check_ori, kf_vs_kf, (int*)d[12], std::max(nout, 1), (int*)d[14],
-                              (int*)d[13], (int*)d[16], &clean, m->err, st)))
+                              (int*)d[13], (size_t)std::max(nout, 1), (int*)d[16], 32, &clean, m->err, st)))
     return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
   int nm = 0;
   MHIP(hipMemcpyAsync(&nm, d[14], 4, hipMemcpyDeviceToHost, st));
@@ -1734,8 +1737,9 @@ int orbm_search_by_bow_batch(orbm_handle m, int pairs, int kp_pitch, int node_pi
   BowSide B{d_descB, (const float*)d_kpB + 3, 7, d_mpB, d_nB, d_nodesB, d_offB, d_idxB, d_nnB, kp_pitch, node_pitch};
   hipStream_t s = (hipStream_t)stream;
   if (m->ws.before(s)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
-  const int rc = launch_search_bow(A, B, pairs, nnratio, check_ori, kf_vs_kf, d_out, kp_pitch, d_nmatches,
-                                   m->bow_rec, m->bow_hist, &m->bow_clean, m->err, stream);
+  const int rc = launch_search_bow(A, B, pairs, nnratio, check_ori, kf_vs_kf, d_out, kp_pitch, d_nmatches, m->bow_rec,
+                                   (size_t)m->max_pairs * m->max_kps, m->bow_hist, (size_t)m->max_pairs * 32,
+                                   &m->bow_clean, m->err, stream);
   if (rc) return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
   if (m->ws.after(s)) return mfail(ORBX_EDEVICE, "event record failed");
   return ORBX_OK;

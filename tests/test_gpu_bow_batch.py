@@ -94,3 +94,44 @@ def test_search_by_bow_batch_parity(pkg, O, voc, kf_vs_kf, ratio, ori, rounds, m
         nout = na if kf_vs_kf else nb
         assert nm[p] == rnm and np.array_equal(out[p, :nout], rout), p
         assert rnm > 20
+
+
+def test_search_by_bow_batch_reuse(pkg, O, voc):
+    """One matcher over calls of growing size: the row-record scratch the
+    finalize kernel restores must be clean for pairs a previous call never
+    touched (2 pairs, then 6 twice)."""
+    from orb_slam_cuda_amd import _lib
+    from orb_slam_cuda_amd.synth import SynthSequence
+    v, V = voc
+    P = 6
+    frames = SynthSequence(32, 1241, 376).frames(P + 1)
+    ext, cap, D, h, s = _extract_and_bow(pkg, V, frames)
+    mp = np.ones((P + 1, cap), np.uint8)
+    d_mp = _lib.DeviceArray(mp.nbytes)
+    d_mp.upload(mp)
+    m = pkg.ORBmatcher(0.7, True, max_pairs=P, max_kps=cap)
+    off = lambda arr, k, pitch, size: C.c_void_p(arr.ptr + k * pitch * size)
+    args = []
+    for side in (0, 1):
+        args += [off(D["kp"], side, cap, 28), off(D["desc"], side, cap, 32), off(D["n"], side, 1, 4),
+                 off(d_mp, side, cap, 1) if side == 0 else None,
+                 off(D["fn"], side, cap, 4), off(D["fo"], side, cap + 1, 4), off(D["fi"], side, cap, 4),
+                 off(D["fnn"], side, 1, 4)]
+    csr = lambda f: (h["fn"][f, :h["fnn"][f]], h["fo"][f, :h["fnn"][f] + 1], h["fi"][f, :h["fo"][f, h["fnn"][f]]])
+    ref = [O.search_by_bow(h["desc"][p, :h["n"][p]], h["kp"][p, :h["n"][p]]["angle"], mp[p, :h["n"][p]], csr(p),
+                           h["desc"][p + 1, :h["n"][p + 1]], h["kp"][p + 1, :h["n"][p + 1]]["angle"],
+                           np.ones(h["n"][p + 1], np.uint8), csr(p + 1), 0.7, 1, 0) for p in range(P)]
+    for pairs in (2, P, P):
+        d_out, d_nm = _lib.DeviceArray(P * cap * 4), _lib.DeviceArray(P * 4)
+        _lib.check(_lib.lib().orbm_search_by_bow_batch(m.handle, pairs, cap, cap, *args, C.c_float(0.7), 1, 0,
+                                                       C.c_void_p(d_out.ptr), C.c_void_p(d_nm.ptr), s.s),
+                   matcher=True)
+        s.synchronize()
+        out = d_out.download(P * cap, np.int32).reshape(P, cap)
+        nm = d_nm.download(P, np.int32)
+        assert m.status() == 0
+        for p in range(pairs):
+            rout, rnm = ref[p]
+            nb = h["n"][p + 1]
+            assert nm[p] == rnm and np.array_equal(out[p, :nb], rout), (pairs, p)
+            assert (out[p, nb:] == -1).all()
