@@ -240,6 +240,9 @@ __device__ __forceinline__ uint32_t top2_ukey(uint32_t kb, int base) {
   const int v = (int)k - 1;
   return ((uint32_t)(v >> 15) << 16) | (uint32_t)((v & (kMBlock - 1)) + base);
 }
+#ifndef ORBX_M_PAIRS
+#define ORBX_M_PAIRS 1  // top-2 update on pairs of results (0: one result per step, for A/B)
+#endif
 __device__ __forceinline__ void top2_merge(uint32_t& u1, uint32_t& u2, uint32_t x1, uint32_t x2) {
   u2 = min(min(max(u1, x1), u2), x2);
   u1 = min(u1, x1);
@@ -319,6 +322,25 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(ORBX_
 #if defined(ORBX_M_NOTOP2)  // timing experiment only: MFMA without the top-2 update
       const float x0 = acc[0];
       k1[q] = min(__float_as_uint(x0), k1[q]);
+#elif ORBX_M_PAIRS
+      // results in pairs: with k1 <= k2, the second smallest of
+      // {k1, k2, x0, x1} is min(med3(k1, x0, x1), k2) and the smallest
+      // min3(k1, x0, x1); two pairs share one min3 into k2, so four values
+      // cost 5 integer VALU instead of 8 (positive floats order as their bit
+      // patterns)
+#pragma unroll
+      for (int r = 0; r < 16; r += 4) {
+        const float xf0 = acc[r], xf1 = acc[r + 1], xf2 = acc[r + 2], xf3 = acc[r + 3];
+        const uint32_t x0 = __float_as_uint(xf0), x1 = __float_as_uint(xf1);
+        const uint32_t x2 = __float_as_uint(xf2), x3 = __float_as_uint(xf3);
+        // (the medians as v_med3_f32, so no integer min is shared with the
+        // new minimum's and each folds into one v_min3_u32)
+        const uint32_t t0 = __float_as_uint(__builtin_amdgcn_fmed3f(xf0, xf1, __uint_as_float(k1[q])));
+        const uint32_t m = min(min(k1[q], x0), x1);
+        const uint32_t t1 = __float_as_uint(__builtin_amdgcn_fmed3f(xf2, xf3, __uint_as_float(m)));
+        k1[q] = min(min(m, x2), x3);
+        k2[q] = min(min(t0, t1), k2[q]);
+      }
 #else
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -365,13 +387,28 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(ORBX_
       rk_reset();
     }
     const int nval = min(kMChunk, je - c0);
+#ifdef ORBX_M_PREF
+    // the next tile's candidate fragments are read while this tile computes
+    const int ntile = (nval + 31) >> 5;
+    i32x4_t nx[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) nx[s] = sC[buf][hf][0][s][lane];
+#endif
     for (int t = 0; t * 32 < nval; ++t) {
       i32x8_t af[4];
+#ifdef ORBX_M_PREF
+#pragma unroll
+      for (int s = 0; s < 4; ++s) af[s] = (i32x8_t){nx[s][0], nx[s][1], nx[s][2], nx[s][3], 0, 0, 0, 0};
+      const int tn = min(t + 1, ntile - 1);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) nx[s] = sC[buf][hf][tn][s][lane];
+#else
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const i32x4_t v = sC[buf][hf][t][s][lane];
         af[s] = (i32x8_t){v[0], v[1], v[2], v[3], 0, 0, 0, 0};
       }
+#endif
       const int nrow = nval - 32 * t;  // valid rows of this tile
       if (nrow >= 32) {
         top2_tile(af, rk);
