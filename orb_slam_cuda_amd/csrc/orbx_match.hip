@@ -240,6 +240,9 @@ __device__ __forceinline__ uint32_t top2_ukey(uint32_t kb, int base) {
   const int v = (int)k - 1;
   return ((uint32_t)(v >> 15) << 16) | (uint32_t)((v & (kMBlock - 1)) + base);
 }
+#ifndef ORBX_M_ILV
+#define ORBX_M_ILV 1  // MFMA chains of the query tiles interleaved (0: tile-major, for A/B and the timing experiments)
+#endif
 #ifndef ORBX_M_PAIRS
 #define ORBX_M_PAIRS 1  // top-2 update on pairs of results (0: one result per step, for A/B)
 #endif
@@ -306,7 +309,45 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(ORBX_
   uint4 pre[kRep];
 #pragma unroll
   for (int i = 0; i < kRep; ++i) pre[i] = jb < je ? Bp[2 * min(jb + sr + kMRowsPerPass * i, je - 1) + spart] : make_uint4(0, 0, 0, 0);
+  // top-2 update of query tile q with one tile's 16 results per lane: results
+  // in pairs; with k1 <= k2, the second smallest of {k1, k2, x0, x1} is
+  // min(med3(k1, x0, x1), k2) and the smallest min3(k1, x0, x1); two pairs
+  // share one min3 into k2, so four values cost 5 integer VALU instead of 8
+  // (positive floats order as their bit patterns; the medians as v_med3_f32,
+  // so no integer min is shared with the new minimum's and each folds into
+  // one v_min3_u32)
+  auto top2_update = [&](int q, const f32x16_t& acc) {
+#pragma unroll
+    for (int r = 0; r < 16; r += 4) {
+      const float xf0 = acc[r], xf1 = acc[r + 1], xf2 = acc[r + 2], xf3 = acc[r + 3];
+      const uint32_t x0 = __float_as_uint(xf0), x1 = __float_as_uint(xf1);
+      const uint32_t x2 = __float_as_uint(xf2), x3 = __float_as_uint(xf3);
+      const uint32_t t0 = __float_as_uint(__builtin_amdgcn_fmed3f(xf0, xf1, __uint_as_float(k1[q])));
+      const uint32_t m = min(min(k1[q], x0), x1);
+      const uint32_t t1 = __float_as_uint(__builtin_amdgcn_fmed3f(xf2, xf3, __uint_as_float(m)));
+      k1[q] = min(min(m, x2), x3);
+      k2[q] = min(min(t0, t1), k2[q]);
+    }
+  };
   auto top2_tile = [&](const i32x8_t (&af)[4], const f32x16_t& rkt) {
+#if ORBX_M_ILV && !defined(ORBX_M_NOMFMA) && !defined(ORBX_M_NOTOP2)
+    // step-major: the four query tiles' accumulation chains interleaved
+    // (34.3 -> 33.1 us per 64 pairs alone against tile-major chains)
+    f32x16_t accs[kMqTiles];
+#pragma unroll
+    for (int q = 0; q < kMqTiles; ++q) accs[q] = rkt;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int q = 0; q < kMqTiles; ++q) {
+        const i32x8_t bf = (i32x8_t){qf[q][s][0], qf[q][s][1], qf[q][s][2], qf[q][s][3], 0, 0, 0, 0};
+        accs[q] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[s], bf, accs[q], 4, 4, 0, 141, 0, 127);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kMqTiles; ++q) top2_update(q, accs[q]);
+    return;
+#endif
 #pragma unroll
     for (int q = 0; q < kMqTiles; ++q) {
       f32x16_t acc = rkt;
@@ -323,24 +364,7 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(ORBX_
       const float x0 = acc[0];
       k1[q] = min(__float_as_uint(x0), k1[q]);
 #elif ORBX_M_PAIRS
-      // results in pairs: with k1 <= k2, the second smallest of
-      // {k1, k2, x0, x1} is min(med3(k1, x0, x1), k2) and the smallest
-      // min3(k1, x0, x1); two pairs share one min3 into k2, so four values
-      // cost 5 integer VALU instead of 8 (positive floats order as their bit
-      // patterns)
-#pragma unroll
-      for (int r = 0; r < 16; r += 4) {
-        const float xf0 = acc[r], xf1 = acc[r + 1], xf2 = acc[r + 2], xf3 = acc[r + 3];
-        const uint32_t x0 = __float_as_uint(xf0), x1 = __float_as_uint(xf1);
-        const uint32_t x2 = __float_as_uint(xf2), x3 = __float_as_uint(xf3);
-        // (the medians as v_med3_f32, so no integer min is shared with the
-        // new minimum's and each folds into one v_min3_u32)
-        const uint32_t t0 = __float_as_uint(__builtin_amdgcn_fmed3f(xf0, xf1, __uint_as_float(k1[q])));
-        const uint32_t m = min(min(k1[q], x0), x1);
-        const uint32_t t1 = __float_as_uint(__builtin_amdgcn_fmed3f(xf2, xf3, __uint_as_float(m)));
-        k1[q] = min(min(m, x2), x3);
-        k2[q] = min(min(t0, t1), k2[q]);
-      }
+      top2_update(q, acc);
 #else
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
