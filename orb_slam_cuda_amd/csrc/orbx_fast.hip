@@ -45,7 +45,15 @@ namespace orbx {
 // staging, the scalar compass). The tight strides keep a wave's LDS near
 // 6 KB instead of ~8 KB and run the dword compass (compass4).
 constexpr int kTightE = 4;  // staging element of the tight strides
-constexpr int kRoiTight = 44, kRoiTight2 = 48, kRoiWide = 80;
+#ifndef ORBX_FAST_T1
+#define ORBX_FAST_T1 44  // tight strides (bank-conflict experiments: tools/variant.sh)
+#endif
+#ifndef ORBX_FAST_T2
+#define ORBX_FAST_T2 48
+#endif
+constexpr int kRoiTight = ORBX_FAST_T1, kRoiTight2 = ORBX_FAST_T2, kRoiWide = 80;
+static_assert(kRoiTight < kRoiTight2 && kRoiTight2 < kRoiWide && kRoiTight % 4 == 0 && kRoiTight2 % 4 == 0,
+              "tight strides in increasing order, whole dwords");
 
 // 24-bit multiply (full-rate v_mul_u32_u24; the compiler cannot prove the
 // operand ranges and otherwise picks the quarter-rate 32/64-bit forms)
@@ -203,11 +211,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     // dwords from the one at or below c0 (<= kRoiStride / 4 per row), kK per
     // lane in flight
     typedef unsigned int piece_t __attribute__((ext_vector_type(kTightE / 4)));
-    constexpr int kK = 8;
     // a fixed kPR pieces per staged row, so the lane -> (row, piece) split is
     // a division by a constant; pieces past the ROI's last one (nd) and rows
     // past the last (rh) reload that piece / row (same bytes, same LDS slot)
     constexpr int kPR = kRoiStride / kTightE;
+    constexpr int kK = (41 * kPR + 63) / 64 > 8 ? (41 * kPR + 63) / 64 : 8;  // a 41-row ROI in one burst
     const int nd = (cg.c1 - a0 + kTightE - 1) / kTightE, total = rh * kPR;
     piece_t v[kK];
     int ro[kK], lo[kK];
