@@ -149,6 +149,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency leg")
     ap.add_argument("--no-host-stream", action="store_true", help="skip the host-streamed throughput leg")
     ap.add_argument("--host-steps", type=int, default=30, help="timed steps of the host-streamed leg")
+    ap.add_argument("--h2d-split", type=int, default=2,
+                    help="host-streamed leg: the batch upload in this many parts, each on a copy stream of its own "
+                         "(a multiple of the extraction halves; an extraction half waits for its own parts only)")
     ap.add_argument("--spawn", action="store_true", help="use the worker launcher even for --gpus 1")
     ap.add_argument("--split-sequence", action="store_true",
                     help="split ONE synthetic sequence (pool x N frames) into contiguous blocks, one per GPU; "
@@ -391,6 +394,11 @@ class MonoPipeline:
             self.h_m12 = [HA(B * cap, np.int32) for _ in range(NS)]
             self.h_nm = [HA(B, np.int32) for _ in range(NS)]
             self.s_h2d, self.s_d2h = _lib.Stream(), _lib.Stream()
+            # --h2d-split N: the upload in N parts on N copy streams (half h waits for its own parts)
+            nparts = args.h2d_split if not args.serial else 1
+            if nparts < 1 or (nparts > 1 and (nparts % S or B % nparts)):
+                raise SystemExit(f"bench.py: --h2d-split {nparts} must divide the batch and be a multiple of --split")
+            self.s_h2ds = [self.s_h2d] + [_lib.Stream() for _ in range(nparts - 1)]
         prio = 1 if args.priority else None
         self.s_exts = [_lib.Stream(prio) for _ in range(S)]
         self.s_ext = self.s_exts[0]
@@ -453,7 +461,7 @@ class MonoPipeline:
         self.ev_carry = [E() for _ in range(total)]
         self.ev_part = [[E() for _ in range(self.S)] for _ in range(total)]
         if self.host:
-            self.ev_in = [E() for _ in range(total)]
+            self.ev_in = [[E() for _ in self.s_h2ds] for _ in range(total)]
             self.ev_out = [E() for _ in range(total)]
 
     def frames_ptr(self, k):
@@ -473,11 +481,15 @@ class MonoPipeline:
         evs = self.evsets[k] if self.evsets is not None else None
         if self.host:
             # H2D of batch k into input slot k % 3, after extraction k-3 read it
-            if k >= NS:
-                self.s_h2d.wait(self.ev_ext[k - NS])
             src = self.h_pool.ptr + (k % self.nbatches) * B * self.fbytes
-            check(L.orbx_memcpy_htod_async(vp(self.d_in[k % NS].ptr), vp(src), B * self.fbytes, self.s_h2d.s))
-            self.ev_in[k].record(self.s_h2d)
+            parts = len(self.s_h2ds)
+            for i, sh in enumerate(self.s_h2ds):
+                if k >= NS:
+                    sh.wait(self.ev_ext[k - NS])
+                lo, hi = i * B // parts, (i + 1) * B // parts
+                check(L.orbx_memcpy_htod_async(vp(self.d_in[k % NS].ptr + lo * self.fbytes),
+                                               vp(src + lo * self.fbytes), (hi - lo) * self.fbytes, sh.s))
+                self.ev_in[k][i].record(sh)
         fp = self.frames_ptr(k)
         for h, (ex, se) in enumerate(zip(self.exts, self.s_exts)):
             if h == 0 and evs is not None:
@@ -485,7 +497,10 @@ class MonoPipeline:
                 check(L.orbx_set_stage_events(ex.handle, arr))
             sv = se if not a.serial else self.s_ext
             if self.host:
-                sv.wait(self.ev_in[k])
+                nparts = len(self.s_h2ds)
+                per = nparts // self.S
+                for i in range(h * per, (h + 1) * per) if nparts > 1 else (0,):
+                    sv.wait(self.ev_in[k][i])  # the parts holding half h's frames
             if not a.serial and k >= NS:
                 sv.wait(self.ev_done[k - NS])  # matching k-3 was the last reader of set k % 3
                 if self.two_match:
@@ -618,7 +633,8 @@ class MonoPipeline:
         self.s_match.synchronize()
         self.s_init.synchronize()
         if self.host:
-            self.s_h2d.synchronize()
+            for sh in self.s_h2ds:
+                sh.synchronize()
             self.s_d2h.synchronize()
 
     def run(self, warmup, steps, dist):
