@@ -30,7 +30,7 @@ pytestmark = pytest.mark.gpu
 KP, DS = 28, 32
 
 
-def _run_pipeline(argv, batches):
+def _run_pipeline(argv, batches, host=False):
     import bench
     from orb_slam_cuda_amd import _lib, sharding
     from orb_slam_cuda_amd.synth import SynthSequence
@@ -38,7 +38,7 @@ def _run_pipeline(argv, batches):
     cfg = bench.CONFIGS[args.config]
     W, H, B = cfg["W"], cfg["H"], args.batch
     frames = SynthSequence(sharding.sequence_seed(0), W, H).frames(args.pool)
-    pipe = bench.MonoPipeline(args, cfg, 0, frames)
+    pipe = bench.MonoPipeline(args, cfg, 0, frames, host=host)
     assert pipe.S == 2 and pipe.NS == 3 and not args.serial and args.carry == "match" and args.match_priority
     assert pipe.nbatches > 1  # the pool cycles: level 0 streams from a different slot every batch
     pipe.run(0, batches, None)  # the timed region's issue order, without the warmup split
@@ -143,3 +143,23 @@ def test_timed_pipeline_bow_match_matches_oracle(pkg, O):
                                     0.7, True, False)
         assert nm[p] == rnm and np.array_equal(out[p, :n[b]], rout), p
     assert nm.mean() > 20
+
+
+@pytest.mark.parametrize("parts", [1, 2, 4])
+def test_host_streamed_pipeline_matches_oracle(pkg, O, parts):
+    """The host-streamed leg (bench.py host_stream_leg): every batch uploaded
+    from pinned host memory in `parts` pieces on their own copy streams, each
+    extraction half waiting for its own pieces; outputs read back on a copy
+    stream. A missing upload edge would extract stale or partial frames."""
+    batches = 4
+    args, cfg, frames, pipe, _ = _run_pipeline(["--pool", str(3 * 64), "--h2d-split", str(parts)], batches, host=True)
+    assert len(pipe.s_h2ds) == parts
+    _check_batches(O, cfg, frames, pipe, batches, [batches - 2, batches - 1])
+    # the read-back of the last batch equals the device outputs
+    k = batches - 1
+    B, cap, s = pipe.B, pipe.cap, k % pipe.NS
+    n, kps, desc, _, m12, nm = _download_set(pipe, k)
+    assert np.array_equal(pipe.h_counts[s].a, n[1:])
+    assert np.array_equal(pipe.h_kps[s].a.reshape(B, cap * KP), kps[1:].view(np.uint8).reshape(B, cap * KP))
+    assert np.array_equal(pipe.h_desc[s].a.reshape(B, cap, 32), desc[1:])
+    assert np.array_equal(pipe.h_nm[s].a, nm)
