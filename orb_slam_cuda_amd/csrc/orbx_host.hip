@@ -89,9 +89,11 @@ struct orbx_extractor {
   hipStream_t stream = nullptr;
   // staging for the synchronous API: device buffers, pinned host staging and
   // the captured H2D -> 5 kernels -> D2H chain of a one-frame call
-  DeviceBuf d_in, d_kps, d_desc, d_counts;
+  // orbx_extract's device output block, laid out as h_out so that one copy
+  // brings back the count, the keypoints and the descriptors (out_desc_off)
+  DeviceBuf d_in, d_out;
   void* h_in = nullptr;   // pinned: the image, rows at the device pitch
-  void* h_out = nullptr;  // pinned: {count, status, -, -} + cap keypoints + cap descriptors
+  void* h_out = nullptr;  // pinned: {count, status, -, -} + cap keypoints + (16-B aligned) cap descriptors
   size_t h_in_bytes = 0, h_out_bytes = 0;
   hipGraphExec_t graph = nullptr;
   int graph_w = 0, graph_h = 0;
@@ -655,19 +657,23 @@ static int host_reserve(void** p, size_t* have, size_t need) {
   return ORBX_OK;
 }
 
+// offset of the descriptors in orbx_extract's output block (16-byte aligned
+// for orient_brief's 16-byte stores)
+static size_t out_desc_off(int cap_frame) { return (16 + (size_t)cap_frame * sizeof(orbx_kp) + 15) & ~(size_t)15; }
+
 static int issue_one_frame(orbx_extractor* h, size_t pitch, int hh, int cap_frame) {
   hipStream_t s = h->stream;
   HIP_OK(hipMemcpyAsync(h->d_in.p, h->h_in, pitch * hh, hipMemcpyHostToDevice, s));
+  uint8_t* d = h->d_out.as<uint8_t>();
+  const size_t doff = out_desc_off(cap_frame);
   const int rc = launch_extract(h->plan.P, buffers_of(h->plan), h->d_in.as<uint8_t>(), 1, pitch * hh, pitch,
-                                h->d_kps.as<orbx_kp>(), h->d_desc.as<uint8_t>(), h->d_counts.as<int>(), s,
-                                h->timing ? (void**)h->ev : nullptr);
+                                (orbx_kp*)(d + 16), d + doff, (int*)d, s, h->timing ? (void**)h->ev : nullptr);
   if (rc) return fail(rc, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+  // count, keypoints and descriptors in one copy, then the status word over
+  // bytes 4..7 of the block's header (same stream: in this order)
   uint8_t* o = (uint8_t*)h->h_out;
-  HIP_OK(hipMemcpyAsync(o, h->d_counts.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(o, d, doff + (size_t)cap_frame * 32, hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(o + 4, h->plan.err.p, 4, hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(o + 16, h->d_kps.p, (size_t)cap_frame * sizeof(orbx_kp), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(o + 16 + (size_t)cap_frame * sizeof(orbx_kp), h->d_desc.p, (size_t)cap_frame * 32,
-                        hipMemcpyDeviceToHost, s));
   return ORBX_OK;
 }
 
@@ -691,7 +697,7 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   }
   const int cap_frame = h->plan.P.kp_per_frame;
   const size_t pitch = ((size_t)w + 63) & ~(size_t)63;
-  const size_t out_bytes = 16 + (size_t)cap_frame * (sizeof(orbx_kp) + 32);
+  const size_t out_bytes = out_desc_off(cap_frame) + (size_t)cap_frame * 32;
   int rc;
   auto drop_graph = [&]() {
     if (h->graph) (void)hipGraphExecDestroy(h->graph);
@@ -701,17 +707,9 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
     drop_graph();
     if ((rc = h->d_in.alloc(pitch * hh))) return rc;
   }
-  if (h->d_kps.n < (size_t)cap_frame * sizeof(orbx_kp)) {
+  if (h->d_out.n < out_bytes) {
     drop_graph();
-    if ((rc = h->d_kps.alloc((size_t)cap_frame * sizeof(orbx_kp)))) return rc;
-  }
-  if (h->d_desc.n < (size_t)cap_frame * 32) {
-    drop_graph();
-    if ((rc = h->d_desc.alloc((size_t)cap_frame * 32))) return rc;
-  }
-  if (h->d_counts.n < 16) {
-    drop_graph();
-    if ((rc = h->d_counts.alloc(16))) return rc;
+    if ((rc = h->d_out.alloc(out_bytes))) return rc;
   }
   if (h->h_in_bytes < pitch * hh || h->h_out_bytes < out_bytes) drop_graph();
   if ((rc = host_reserve(&h->h_in, &h->h_in_bytes, pitch * hh)) ||
@@ -773,7 +771,7 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   if (cnt > cap) return fail(ORBX_ECAPACITY, "%d keypoints do not fit cap %d", cnt, cap);
   const uint8_t* o = (const uint8_t*)h->h_out + 16;
   if (kps) memcpy(kps, o, (size_t)cnt * sizeof(orbx_kp));
-  if (desc) memcpy(desc, o + (size_t)cap_frame * sizeof(orbx_kp), (size_t)cnt * 32);
+  if (desc) memcpy(desc, (const uint8_t*)h->h_out + out_desc_off(cap_frame), (size_t)cnt * 32);
   return ORBX_OK;
 }
 
