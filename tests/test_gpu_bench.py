@@ -87,3 +87,25 @@ def test_split_sequence_boundary_pair_two_ranks(O, tmp_path):
         r12, rnm, _ = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), np.stack([k1["x"], k1["y"]], 1),
                                                   100, 0.9, True)
         assert r1["nm"][pair] == rnm > 20 and np.array_equal(r1["m12"][pair, :n1], r12)
+
+
+def test_bench_torchrun_two_ranks_one_device():
+    """The driver's multi-GPU launch command (python -m torch.distributed.run
+    --nproc-per-node N ... bench.py --gpus N) with two ranks, both on device 0
+    (--share-device, test only): every rank runs its own pipeline, the
+    barrier + max-over-ranks timing holds, rank 0 prints the one line."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29517", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--share-device", "--steps", "3", "--warmup", "1", "--pool", "128", "--cpu-sample", "0",
+           "--no-latency", "--no-host-stream"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and len(out["per_rank_frames_per_s"]) == 2
+    assert out["value"] > 0 and out["scaling"] == "weak"
+    assert out["cpu_baseline"] is None  # rank 0 at N = 1 only
