@@ -53,41 +53,75 @@ __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp
   const uint8_t* S = lp.base[l] + f * lp.fstride[l];
   const int pitch = lp.pitch[l];
   // stage rows y0-3 .. y0+TH+2, columns x0-16 .. x0+TW+15
-  // every thread's chunks are loaded at once (unpredicated: a chunk that
-  // leaves the image loads the level start and is rewritten from byte loads
-  // with reflection after the aligned chunks are stored)
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   constexpr int kChunks = kBlurInW / 16, kItems = (kBlurTH + 6) * kChunks, kPer = (kItems + 255) / 256;
-  u32x4 v[kPer];
-  bool direct[kPer];
-  int gys[kPer];
+  if (lp.aligned16[l]) {
+    // every chunk is a 16-byte load from inside its (row-reflected) source
+    // row: chunks left of column 0 or past the pitch load a clamped chunk of
+    // the row instead (a chunk holding a column < W never needs the clamp:
+    // W <= pitch, both multiples of 16 apart from W). The 3 columns each side
+    // of the level that BORDER_REFLECT_101 supplies are written afterwards
+    // from the staged columns, on edge tiles only.
+    u32x4 v[kPer];
 #pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const int i = min(tid + 256 * q, kItems - 1);
-    const int r = i / kChunks, ch = i - r * kChunks;
-    gys[q] = reflect101(min(max(y0 + r - 3, -(H - 1)), 2 * H - 2), H);
-    const int gx = x0 - 16 + ch * 16;
-    const uint8_t* src = S + (long long)gys[q] * pitch + gx;
-    direct[q] = gx >= 0 && gx + 16 <= W && (((uintptr_t)src) & 15) == 0;
-    v[q] = *(const u32x4*)(direct[q] ? src : S);
-  }
+    for (int q = 0; q < kPer; ++q) {
+      const int i = min(tid + 256 * q, kItems - 1);
+      const int r = i / kChunks, ch = i - r * kChunks;
+      const int gy = reflect101(min(max(y0 + r - 3, -(H - 1)), 2 * H - 2), H);
+      const int gx = min(max(x0 - 16 + ch * 16, 0), pitch - 16);
+      v[q] = *(const u32x4*)(S + (long long)gy * pitch + gx);
+    }
 #pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const int i = min(tid + 256 * q, kItems - 1);
-    const int r = i / kChunks, ch = i - r * kChunks;
-    *(u32x4*)&in[r][ch * 16] = v[q];
-  }
+    for (int q = 0; q < kPer; ++q) {
+      const int i = min(tid + 256 * q, kItems - 1);
+      const int r = i / kChunks, ch = i - r * kChunks;
+      *(u32x4*)&in[r][ch * 16] = v[q];
+    }
+    const bool left = x0 == 0, right = x0 + kBlurTW + 3 > W;
+    if (left || right) {
+      __syncthreads();
+      // column x < 0 -> -x, x >= W -> 2W - 2 - x (staged column = x - x0 + 16)
+      for (int i = tid; i < (kBlurTH + 6) * 6; i += 256) {
+        const int r = i / 6, kk = i - r * 6;
+        int x = kk < 3 ? -1 - kk : W + kk - 3;
+        if ((kk < 3 && !left) || (kk >= 3 && !right) || x - x0 + 16 >= kBlurInW) continue;
+        in[r][x - x0 + 16] = in[r][reflect101(x, W) - x0 + 16];
+      }
+    }
+  } else {
+    // unaligned levels: chunks that leave the image are rewritten from byte
+    // loads with reflection after the aligned chunks are stored
+    u32x4 v[kPer];
+    bool direct[kPer];
+    int gys[kPer];
 #pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    if (direct[q]) continue;
-    const int i = min(tid + 256 * q, kItems - 1);
-    const int r = i / kChunks, ch = i - r * kChunks;
-    const int gx = x0 - 16 + ch * 16;
-    const uint8_t* src = S + (long long)gys[q] * pitch;
+    for (int q = 0; q < kPer; ++q) {
+      const int i = min(tid + 256 * q, kItems - 1);
+      const int r = i / kChunks, ch = i - r * kChunks;
+      gys[q] = reflect101(min(max(y0 + r - 3, -(H - 1)), 2 * H - 2), H);
+      const int gx = x0 - 16 + ch * 16;
+      const uint8_t* src = S + (long long)gys[q] * pitch + gx;
+      direct[q] = gx >= 0 && gx + 16 <= W && (((uintptr_t)src) & 15) == 0;
+      v[q] = *(const u32x4*)(direct[q] ? src : S);
+    }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int xx = min(max(gx + k, -(W - 1)), 2 * W - 2);
-      in[r][ch * 16 + k] = src[reflect101(xx, W)];
+    for (int q = 0; q < kPer; ++q) {
+      const int i = min(tid + 256 * q, kItems - 1);
+      const int r = i / kChunks, ch = i - r * kChunks;
+      *(u32x4*)&in[r][ch * 16] = v[q];
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      if (direct[q]) continue;
+      const int i = min(tid + 256 * q, kItems - 1);
+      const int r = i / kChunks, ch = i - r * kChunks;
+      const int gx = x0 - 16 + ch * 16;
+      const uint8_t* src = S + (long long)gys[q] * pitch;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int xx = min(max(gx + k, -(W - 1)), 2 * W - 2);
+        in[r][ch * 16 + k] = src[reflect101(xx, W)];
+      }
     }
   }
   __syncthreads();
