@@ -66,6 +66,9 @@ __device__ __forceinline__ int half_sum(int v) {
   return (threadIdx.x & 32) ? hi : lo;
 }
 
+// kLv: the level loops' unrolled length (8 covers the usual 8-level
+// pyramid in half the scalar bookkeeping of kMaxLevels)
+template <int kLv>
 __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams P, LevelPtrs lp,
                                                                   const uint8_t* __restrict__ blur,
                                                                   const uint32_t* __restrict__ qkeys,
@@ -88,9 +91,9 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   // loads are in flight)
   const uint32_t key_raw = slot < P.kp_per_frame ? qkeys[(long long)f * P.kp_per_frame + slot] : 0u;
   const int* cnt = qcounts + f * P.L;
-  int c[kMaxLevels];
+  int c[kLv];
 #pragma unroll
-  for (int i = 0; i < kMaxLevels; ++i) c[i] = cnt[i];
+  for (int i = 0; i < kLv; ++i) c[i] = cnt[i];
   constexpr int kTestsPer = (256 + kObThreads - 1) / kObThreads, kIcPer = (16 * 24 + kObThreads - 1) / kObThreads;
   float4 test_v[kTestsPer];
   uint32_t ic_v[kIcPer];
@@ -104,7 +107,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   const int slotA = bx * kObKps + 2 * __builtin_amdgcn_readfirstlane(tid >> 6), slotB = slotA + 1;
   int lA = 0, lB = 0;
 #pragma unroll
-  for (int i = 1; i < kMaxLevels; ++i) {
+  for (int i = 1; i < kLv; ++i) {
     if (i < P.L && slotA >= P.lv[i].kbase) lA = i;
     if (i < P.L && slotB >= P.lv[i].kbase) lB = i;
   }
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   // keypoints of the levels before each half's level, its own count, the total (scalar)
   int cntA = 0, cntB = 0, beforeA = 0, beforeB = 0, tot = 0;
 #pragma unroll
-  for (int i = 0; i < kMaxLevels; ++i) {
+  for (int i = 0; i < kLv; ++i) {
     const int ci = i < P.L ? c[i] : 0;
     if (i == lA) cntA = ci;
     if (i == lB) cntB = ci;
@@ -301,8 +304,12 @@ int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const Extra
     g_pattern_uploaded[dev] = true;
   }
   dim3 grid((P.kp_per_frame + kObKps - 1) / kObKps, batch);
-  hipLaunchKernelGGL(orient_brief_kernel, grid, dim3(kObThreads), 0, s, P, lp, X.blur, X.qkeys, X.qcounts, X.umax,
-                     kps, desc, counts);
+  if (P.L <= 8)
+    hipLaunchKernelGGL(orient_brief_kernel<8>, grid, dim3(kObThreads), 0, s, P, lp, X.blur, X.qkeys, X.qcounts,
+                       X.umax, kps, desc, counts);
+  else
+    hipLaunchKernelGGL(orient_brief_kernel<kMaxLevels>, grid, dim3(kObThreads), 0, s, P, lp, X.blur, X.qkeys,
+                       X.qcounts, X.umax, kps, desc, counts);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
