@@ -84,7 +84,26 @@ CONFIGS = {
                   workload="C5: EuRoC-shaped 752x480 mono u8, nFeatures=1000, 8 levels x1.2, "
                            "extract + match vs t-1 (dense Hamming top-2 + SearchForInitialization), "
                            "one sequence per GPU"),
+    # the reference's other shipped camera settings (parity cases, not bench lines)
+    "kitti14": dict(W=1226, H=370, nfeatures=2000, nlevels=10, ini=17, mn=7,
+                    workload="Examples/Monocular/KITTI14.yaml: 1226x370, nFeatures=2000, 10 levels x1.2, 17/7, "
+                             "extract + match vs t-1"),
+    "intcatch1080": dict(W=1920, H=1080, nfeatures=2000, nlevels=3, ini=10, mn=4,
+                         workload="Examples/Monocular/intcatch-1080p.yaml: 1920x1080, nFeatures=2000, 3 levels "
+                                  "x1.2, 10/4, extract + match vs t-1"),
 }
+
+
+def ext_params(cfg):
+    """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) of a config
+    (the yaml's ORBextractor.* keys, src/Tracking.cc:123-141)."""
+    return (cfg["nfeatures"], cfg.get("scale", 1.2), cfg.get("nlevels", 8), cfg.get("ini", 20), cfg.get("mn", 7))
+
+
+def oracle_config(O, cfg):
+    nf, sc, nl, ini, mn = ext_params(cfg)
+    return O.config(nfeatures=nf, width=cfg["W"], height=cfg["H"], scale_factor=sc, nlevels=nl,
+                    ini_th=ini, min_th=mn)
 
 
 def level_sizes(W, H, L=8, s=1.2):
@@ -98,14 +117,14 @@ def level_sizes(W, H, L=8, s=1.2):
     return out
 
 
-def algorithmic_bytes(W, H, nkp):
+def algorithmic_bytes(W, H, nkp, L=8, s=1.2):
     """Per-frame algorithmic HBM bytes of each stage (DESIGN.md "Roofline")."""
-    P = [w * h for w, h in level_sizes(W, H)]
+    P = [w * h for w, h in level_sizes(W, H, L, s)]
     return {
-        "pyramid": sum(P[l - 1] + P[l] for l in range(1, 8)),         # read l-1, write l
+        "pyramid": sum(P[l - 1] + P[l] for l in range(1, L)),         # read l-1, write l
         "blur": 2 * sum(P),                                            # read + write every level
         "fast_grid": sum(P),                                           # read every level once
-        "pyr_fast_pass": P[0] + sum(P[:7]) + sum(P[1:]) + sum(P),      # BASELINE.md B_pf
+        "pyr_fast_pass": P[0] + sum(P[:L - 1]) + sum(P[1:]) + sum(P),  # BASELINE.md B_pf
         "orient_brief": nkp * (2 * 31 * 31 + 60),                      # patch gathers + outputs
     }
 
@@ -374,7 +393,7 @@ class MonoPipeline:
         if S < 1 or B % S:
             raise SystemExit("--split must divide --batch")
         self.S, self.BS = S, B // S
-        self.exts = [pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=self.BS) for _ in range(S)]
+        self.exts = [pkg.ORBextractor(*ext_params(cfg), W, H, device=local, max_batch=self.BS) for _ in range(S)]
         self.cap = cap = self.exts[0].frame_capacity
         NS = self.NS
         DA = _lib.DeviceArray
@@ -435,7 +454,7 @@ class MonoPipeline:
         # the sequence's first block, instead of the carry of the pool's last frame
         self.boundary = boundary and not host
         if self.boundary:
-            self.halo_ext = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=1)
+            self.halo_ext = pkg.ORBextractor(*ext_params(cfg), W, H, device=local, max_batch=1)
             self.d_halo = None
             if halo is not None:
                 hb = np.zeros((H, pitch), np.uint8)
@@ -723,7 +742,7 @@ def run_mono(args, cfg, rank, world, local, dist):
            "fraction_of_kept": round(float(ties[:, :, 2].sum() / max(1, cnt[1:].sum())), 4),
            "levels_with_event_frac": round(float((ties[:, :, 0] > 0).mean()), 3),
            "frames": int(len(ties))}
-    ab = algorithmic_bytes(W, H, nkp_mean)
+    ab = algorithmic_bytes(W, H, nkp_mean, ext_params(cfg)[2], ext_params(cfg)[1])
     extract_ms = sum(st[s] for s in ext_stages)
     dominant = max(STAGES_RUN, key=lambda s: st[s])
     # roofline of the pyramid+FAST pass: the kernels that run it
@@ -796,7 +815,8 @@ def run_mono(args, cfg, rank, world, local, dist):
                     f"{pool} resident frames per GPU cycled batch by batch",
             "config": {"workload": workload + (" + Frame::ComputeBoW (synthetic k10 L6 vocabulary)" if (args.bow or args.bow_match) else "")
                                    + (" + SearchByBoW(KF t-1, F t)" if args.bow_match else ""),
-                       "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": 8, "scale_factor": 1.2,
+                       "frame": f"{W}x{H}", "nfeatures": NF, "nlevels": ext_params(cfg)[2],
+                       "scale_factor": ext_params(cfg)[1], "fast_thresholds": list(ext_params(cfg)[3:]),
                        "frames_per_step_per_gpu": B * SUB, "batches_per_step": SUB, "frames_per_batch": B,
                        "resident_pool_frames": pool,
                        "parallelism": (f"sequence split x{world} (contiguous blocks, boundary frame re-extracted per rank)"
@@ -898,7 +918,7 @@ def latency_leg(cfg, local, frames, no_match, n=200, warm=20):
     from orb_slam_cuda_amd import _lib
     W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
     L = _lib.lib()
-    ext = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local)
+    ext = pkg.ORBextractor(*ext_params(cfg), W, H, device=local)
     cap = ext.frame_capacity
     imgs = [np.ascontiguousarray(f) for f in frames]
     kps = [np.empty(cap, pkg.KP_DTYPE) for _ in imgs]
@@ -954,7 +974,7 @@ def cpu_tie_rule_study(frames, cfg):
     from itself under another heap history. Runs with the CPU baseline, after
     the timed region; the oracle is the checker here, not the product."""
     from oracle import oracle as O
-    oc = O.config(nfeatures=cfg["nfeatures"], width=cfg["W"], height=cfg["H"])
+    oc = oracle_config(O, cfg)
     d01, k01 = O.tie_sequence(oc, frames, O.TIE_LATER_FIRST, O.TIE_POINTER)
     d11, k11 = O.tie_sequence(oc, frames, O.TIE_POINTER, O.TIE_POINTER)
     return {"frames": int(len(frames)),
@@ -983,7 +1003,7 @@ def cpu_latency(frames, cfg, no_match, warm=20):
     frames after `warm` warm-up frames (>= 200 frames)."""
     from oracle import oracle as O
     W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
-    oc = O.config(nfeatures=NF, width=W, height=H)
+    oc = oracle_config(O, cfg)
     te, ts, prev = [], [], None
     for fr in frames:
         t0 = time.perf_counter()
@@ -1037,8 +1057,8 @@ def run_stereo(args, cfg, rank, world, local, dist):
     sets = []
     s_one = _lib.Stream() if args.serial else None  # --serial: every launch on one stream
     for _ in range(NSET):
-        eL = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=B)
-        eR = pkg.ORBextractor(NF, 1.2, 8, 20, 7, W, H, device=local, max_batch=B)
+        eL = pkg.ORBextractor(*ext_params(cfg), W, H, device=local, max_batch=B)
+        eR = pkg.ORBextractor(*ext_params(cfg), W, H, device=local, max_batch=B)
         cap = eL.frame_capacity
         sL = s_one or _lib.Stream()
         sets.append(dict(eL=eL, eR=eR, sL=sL, sR=s_one or _lib.Stream(),
@@ -1128,7 +1148,7 @@ def run_stereo(args, cfg, rank, world, local, dist):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(agg["wall"] / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic rectified pairs (orb_slam_cuda_amd/synth.py stereo_pair)",
-            "config": {"workload": cfg["workload"], "frame": f"2x{W}x{H}", "nfeatures": NF, "nlevels": 8,
+            "config": {"workload": cfg["workload"], "frame": f"2x{W}x{H}", "nfeatures": NF, "nlevels": ext_params(cfg)[2],
                        "scale_factor": 1.2, "pairs_per_step_per_gpu": B,
                        "parallelism": f"pair-sharded x{world}, one process per GPU, no collectives",
                        "streams": 1 if args.serial else 2 * NSET,
@@ -1148,7 +1168,7 @@ def cpu_baseline_stereo(pairs, cfg, n):
     """The CPU oracle on a bounded sample of pairs: extract left + right, pyramids, ComputeStereoMatches."""
     from oracle import oracle as O
     W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
-    oc = O.config(nfeatures=NF, width=W, height=H)
+    oc = oracle_config(O, cfg)
     li = O.level_info(oc)
     t0 = time.perf_counter()
     for i in range(n):
@@ -1199,7 +1219,7 @@ def cpu_baseline(frames, cfg, n, no_match, threads=1):
     """
     from oracle import oracle as O
     W, H, NF = cfg["W"], cfg["H"], cfg["nfeatures"]
-    oc = O.config(nfeatures=NF, width=W, height=H)
+    oc = oracle_config(O, cfg)
     n = min(n, len(frames))
     what = " + dense top-2 + SearchForInitialization vs t-1"
     if threads <= 1:

@@ -139,7 +139,10 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int h_, size_t stride
 /* Batched, device-resident, asynchronous on `stream` (hipStream_t; NULL =
  * the default stream).
  * d_frames: batch frames of (height x width) u8, row stride `row_stride`,
- * frame i at d_frames + i*frame_pitch. Outputs: frame i's keypoints at
+ * frame i at d_frames + i*frame_pitch. The kernels read each row in 16-byte
+ * chunks: every row, the last row of the last frame included, must be
+ * readable up to ceil16(width) bytes from its start (a 64-byte pitch, as
+ * bench.py uses, always is). Outputs: frame i's keypoints at
  * d_kps + i*cap, descriptors at d_desc + i*cap*32, count in d_counts[i],
  * where cap = orbx_frame_capacity(h). Level-major order as the reference. */
 int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch,
@@ -254,7 +257,12 @@ typedef struct orbm_grid_bounds {
 } orbm_grid_bounds;
 
 /* ORBmatcher::SearchForInitialization on host buffers (synchronous).
- * prev_xy: 2*n1 floats, vbPrevMatched, updated in place. matches12: n1. */
+ * prev_xy: 2*n1 floats, vbPrevMatched, updated in place. matches12: n1.
+ * n1 / n2 are not bounded by the matcher's max_kps: only octave-0 keypoints
+ * take part (compacted on the host; at most 65535 per frame, and their
+ * per-keypoint tables must fit the kernel's LDS, ~4,000), and a pair whose
+ * candidate lists exceed the per-pair workspace is re-run in a workspace
+ * grown to its size, so dense inputs return results, not ORBX_ECAPACITY. */
 int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1,
                                    const uint8_t* desc1, int n1,
                                    const orbx_kp* kp2, const uint8_t* desc2,
@@ -268,7 +276,10 @@ int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1,
  * d_prev_xy: pairs x kp_pitch x 2 floats (in/out), or NULL to centre the
  * windows on F1's own keypoints (the initial mvbPrevMatched of
  * Tracking::MonocularInitialization, src/Tracking.cc:645-647; nothing is
- * written back then); d_matches12: pairs x kp_pitch; d_nmatches: pairs. */
+ * written back then); d_matches12: pairs x kp_pitch; d_nmatches: pairs.
+ * A pair whose candidate lists exceed the workspace (more than min(max_kps^2,
+ * 4M) entries; with max_kps <= 2048 that cannot happen) gets no matches and
+ * sets status bit 8 (orbm_get_status); never a truncated result. */
 int orbm_search_for_initialization_batch(
     orbm_handle m, const orbx_kp* d_kp1, const uint8_t* d_desc1,
     const int* d_n1, const orbx_kp* d_kp2, const uint8_t* d_desc2,

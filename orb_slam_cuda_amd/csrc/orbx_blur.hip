@@ -57,18 +57,21 @@ __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp
   constexpr int kChunks = kBlurInW / 16, kItems = (kBlurTH + 6) * kChunks, kPer = (kItems + 255) / 256;
   if (lp.aligned16[l]) {
     // every chunk is a 16-byte load from inside its (row-reflected) source
-    // row: chunks left of column 0 or past the pitch load a clamped chunk of
+    // row: chunks left of column 0 or past ceil16(W) load a clamped chunk of
     // the row instead (a chunk holding a column < W never needs the clamp:
     // W <= pitch, both multiples of 16 apart from W). The 3 columns each side
     // of the level that BORDER_REFLECT_101 supplies are written afterwards
     // from the staged columns, on edge tiles only.
+    // last chunk start: inside ceil16(W) (level 0 is the caller's frame, whose
+    // rows orbx_extract_batch only promises readable that far, orbx_c.h)
+    const int xmax = min(pitch, (W + 15) & ~15) - 16;
     u32x4 v[kPer];
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int i = min(tid + 256 * q, kItems - 1);
       const int r = i / kChunks, ch = i - r * kChunks;
       const int gy = reflect101(min(max(y0 + r - 3, -(H - 1)), 2 * H - 2), H);
-      const int gx = min(max(x0 - 16 + ch * 16, 0), pitch - 16);
+      const int gx = min(max(x0 - 16 + ch * 16, 0), xmax);
       v[q] = *(const u32x4*)(S + (long long)gy * pitch + gx);
     }
 #pragma unroll

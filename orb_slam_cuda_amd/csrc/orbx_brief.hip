@@ -17,6 +17,9 @@
 // evaluated per lane, and 8 tests per lane (test t = lane + 32k) give, by
 // one ballot per k, descriptor dword k of both keypoints at once
 // (bit j of byte i = test 8i + j).
+#include <atomic>
+#include <mutex>
+
 #include "orbx_device.cuh"
 #include "orbx_pattern.h"
 #include "orbx_sincosf.h"
@@ -273,35 +276,43 @@ static void brief_test(int m, int i, int t[4]) {
   t[3] = kBriefPointY[2 * i + 1];
 }
 
-static bool g_pattern_uploaded[64] = {};  // per device: constant memory is per device
+// Per device (constant memory is per device). Two extractor handles may run on
+// two host threads, as the reference's stereo Frame does (src/Frame.cc:77-80):
+// the first launch on a device uploads under the lock, later ones only read the
+// flag (acquire pairs with the release store after the upload).
+static std::atomic<bool> g_pattern_uploaded[64];
+static std::mutex g_pattern_mutex;
 
 int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const ExtractBuffers& X, orbx_kp* kps,
                         uint8_t* desc, int* counts, int batch, hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return ORBX_EDEVICE;
-  if (!g_pattern_uploaded[dev]) {
-    float4 t[2][256];
-    for (int m = 0; m < 2; ++m)
-      for (int i = 0; i < 256; ++i) {
-        int q[4];
-        brief_test(m, i, q);
-        t[m][i] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
-      }
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_tests), t, sizeof(t)) != hipSuccess) return ORBX_EDEVICE;
-    // umax of the r = 15 circle (ORBextractor ctor :540-555; PATCH_SIZE is fixed at 31)
-    constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
-    uint32_t coef[16 * 24] = {};
-    for (int av = 0; av < 16; ++av)
-      for (int b = 0; b < 32; ++b) {
-        const int u = b - kHalfPatch, au = u < 0 ? -u : u;
-        if (au > kUmax[av] || b >= kPatchSize) continue;
-        const int k = b >> 2, sh = 8 * (b & 3);
-        if (u > 0) coef[av * 24 + k] |= (uint32_t)u << sh;
-        if (u < 0) coef[av * 24 + 8 + k] |= (uint32_t)(-u) << sh;
-        coef[av * 24 + 16 + k] |= 1u << sh;
-      }
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_ic_coef), coef, sizeof(coef)) != hipSuccess) return ORBX_EDEVICE;
-    g_pattern_uploaded[dev] = true;
+  if (!g_pattern_uploaded[dev].load(std::memory_order_acquire)) {
+    std::lock_guard<std::mutex> lock(g_pattern_mutex);
+    if (!g_pattern_uploaded[dev].load(std::memory_order_relaxed)) {
+      float4 t[2][256];
+      for (int m = 0; m < 2; ++m)
+        for (int i = 0; i < 256; ++i) {
+          int q[4];
+          brief_test(m, i, q);
+          t[m][i] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+        }
+      if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_tests), t, sizeof(t)) != hipSuccess) return ORBX_EDEVICE;
+      // umax of the r = 15 circle (ORBextractor ctor :540-555; PATCH_SIZE is fixed at 31)
+      constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+      uint32_t coef[16 * 24] = {};
+      for (int av = 0; av < 16; ++av)
+        for (int b = 0; b < 32; ++b) {
+          const int u = b - kHalfPatch, au = u < 0 ? -u : u;
+          if (au > kUmax[av] || b >= kPatchSize) continue;
+          const int k = b >> 2, sh = 8 * (b & 3);
+          if (u > 0) coef[av * 24 + k] |= (uint32_t)u << sh;
+          if (u < 0) coef[av * 24 + 8 + k] |= (uint32_t)(-u) << sh;
+          coef[av * 24 + 16 + k] |= 1u << sh;
+        }
+      if (hipMemcpyToSymbol(HIP_SYMBOL(c_ic_coef), coef, sizeof(coef)) != hipSuccess) return ORBX_EDEVICE;
+      g_pattern_uploaded[dev].store(true, std::memory_order_release);
+    }
   }
   dim3 grid((P.kp_per_frame + kObKps - 1) / kObKps, batch);
   if (P.L <= 8)

@@ -210,7 +210,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
   const int tid = threadIdx.x;
   // ---- phase 2a: candidate lists in reference order: a 16-lane row per
   // query, a lane per window column; column c's entries follow the entries of
-  // columns < c (row prefix sum), each (query slot << 12 | sorted position)
+  // columns < c (row prefix sum), each (query slot << 16 | sorted position)
   for (int g = tid / kWinLanes; g < nq0; g += kInitThreads / kWinLanes) {
     const int l16 = tid & (kWinLanes - 1);
     const int i1 = S.qlist[g];
@@ -237,7 +237,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
       for (int p = pb; p < pe; ++p) {
         const float qx = S.pos[2 * p], qy = S.pos[2 * p + 1];
         cand[o++] = fabsf(__fsub_rn(qx, x)) < P.r && fabsf(__fsub_rn(qy, y)) < P.r
-                        ? ((uint32_t)g << 12) | (uint32_t)p
+                        ? ((uint32_t)g << 16) | (uint32_t)p
                         : kInitVoid;
       }
       base += group_sum<kWinLanes>(own);
@@ -261,7 +261,7 @@ __device__ void init_solve(const InitParams& P, const InitShared& S, CandPtr can
   for (int c = tid; c < total; c += kInitThreads) {
     const uint32_t e = cand[c];
     if (e == kInitVoid) continue;
-    const int g = (int)(e >> 12), p = (int)(e & 0xFFF);
+    const int g = (int)(e >> 16), p = (int)(e & 0xFFFF);
     uint4 a0, a1;
     if (qd_lds) {
       const LDSP uint32_t* w = qd + 8 * g;
@@ -660,11 +660,13 @@ __global__ __launch_bounds__(kInitThreads) void search_init_kernel(
   if (P.prof && tid == 0) P.prof[blockIdx.x * 16 + 13] = total;
   if (P.stop == 2) return;
   if (total > P.cand_lds && total > P.cand_cap) {
-    // overflow is reported (status bit 8), never truncated: the pair gets no
-    // matches rather than stale outputs of an earlier call
+    // overflow is reported (status bit 8, the largest list total in err[1]),
+    // never truncated: the pair gets no matches rather than stale outputs of
+    // an earlier call; the host entry point grows its workspace and re-runs
     for (int i = tid; i < min(n1, K); i += kInitThreads) m12_out[i] = -1;
     if (tid == 0) {
       atomicOr(err, 8);
+      atomicMax(err + 1, total);
       nmatches[pr] = 0;
     }
     return;
@@ -705,8 +707,9 @@ int launch_search_init(const InitParams& P0, const orbx_kp* kp1, const uint8_t* 
                        int* matches12, int* nmatches, int* err, int pairs, void* stream) {
   InitParams P = P0;
   const size_t fixed = init_lds_fixed_bytes(P.kp_pitch);
-  // sorted positions and i2 are 12-bit fields of the candidate entries / keys
-  if (P.kp_pitch > 4096 || fixed + 4096 > kInitLdsBudget) return ORBX_ECAPACITY;
+  // query slots and sorted positions are 16-bit fields of the candidate entries;
+  // the per-keypoint tables must leave LDS room for candidates
+  if (P.kp_pitch > 65535 || fixed + 4096 > kInitLdsBudget) return ORBX_ECAPACITY;
   // LDS request: the whole CU by default; ORBX_INIT_LDS_KB caps it (candidates and
   // F2's descriptors then spill to global memory) so a workgroup can start on a CU
   // that extraction workgroups still partly occupy

@@ -516,7 +516,8 @@ __device__ __forceinline__ Top2 wave_top2(bool valid, int dist, int pos) {
 // private to it, and only the rotation histogram and the match count are the
 // pair's (global atomics: hist[0..29] bins, hist[30] count;
 // search_bow_finalize_kernel applies ComputeThreeMaxima after). An accepted
-// match goes to the pair's row record, bin << 16 | matched index, in a
+// match goes to the pair's row record, bin << 16 | matched index (16 bits: the
+// entry points bound both frames' counts by 65536), in a
 // scratch that is all -1 between calls (finalize writes `out` from it and
 // resets it and the histogram, so no fill launches precede the kernel).
 //
@@ -641,8 +642,10 @@ __global__ __launch_bounds__(NT) void search_bow_kernel(BowSide A, BowSide B, fl
   // goes to workgroup floor(excl_j x G / total), non-decreasing in j.
   int k0, k1;
   {
+    // n clamped at 4096 in the estimate (it only drives the balance): with at
+    // most 65536 rows per frame every sum below then stays far inside 32 bits
     auto work = [&](int j) {
-      const int n = offA0[j + 1] - offA0[j];
+      const int n = min(offA0[j + 1] - offA0[j], 4096);
       return n * (n + kBowRowCost);
     };
     int tot = 0;
@@ -1497,6 +1500,8 @@ struct orbx_matcher {
   int sortn = 1;
   long long cand_cap = 0;
   uint32_t* cand = nullptr;
+  uint32_t* host_cand = nullptr;  // orbm_search_for_initialization's own workspace, grown on demand
+  long long host_cand_cap = 0;
   int* err = nullptr;
   int* stereo_sad = nullptr;  // [max_pairs][max_kps] SAD per left keypoint (-1 = none)
   int* bow_hist = nullptr;    // [max_pairs][32] SearchByBoW rotation histogram (+ match count), 0 between calls
@@ -1518,6 +1523,63 @@ static int stage_reserve(orbx_matcher* m, size_t bytes) {
   m->stage_bytes = 0;
   MHIP(hipMalloc(&m->stage, bytes));
   m->stage_bytes = bytes;
+  return ORBX_OK;
+}
+
+static int search_init_launch(orbx_matcher* m, const orbx_kp* d_kp1, const uint8_t* d_desc1, const int* d_n1,
+                              const orbx_kp* d_kp2, const uint8_t* d_desc2, const int* d_n2, int kp_pitch, int pairs,
+                              orbm_grid_bounds b, float* d_prev_xy, int window, float nnratio, int check_ori,
+                              int* d_matches12, int* d_nmatches, void* stream, uint32_t* cand, long long cand_cap) {
+  InitParams P{};
+  P.minX = b.min_x;
+  P.maxX = b.max_x;
+  P.minY = b.min_y;
+  P.maxY = b.max_y;
+  // mfGridElementWidthInv / HeightInv (src/Frame.cc:154-155)
+  P.invW = static_cast<float>(kGridCols) / static_cast<float>(b.max_x - b.min_x);
+  P.invH = static_cast<float>(kGridRows) / static_cast<float>(b.max_y - b.min_y);
+  P.r = (float)window;
+  P.nnratio = nnratio;
+  P.check_ori = check_ori;
+  P.kp_pitch = kp_pitch;
+  P.cand_cap = cand_cap;
+  P.stop = 0;
+#ifdef ORBX_DIAG  // diagnostics builds only (tools/variant.sh): stop after a phase, results incomplete
+  if (const char* st = getenv("ORBX_INIT_STOP")) P.stop = atoi(st);
+#endif
+  static long long* prof = nullptr;  // ORBX_INIT_PROF: phase clocks of every pair, averaged after the call
+  const bool do_prof = getenv("ORBX_INIT_PROF") != nullptr;
+  if (do_prof) {
+    if (pairs > 4096) return mfail(ORBX_EINVAL, "ORBX_INIT_PROF: at most 4096 pairs");
+    if (!prof) MHIP(hipMalloc(&prof, (size_t)4096 * 16 * 8));
+    MHIP(hipMemset(prof, 0, (size_t)pairs * 16 * 8));
+    P.prof = prof;
+  }
+  if (m->ws.before((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
+  const int rc = launch_search_init(P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, d_prev_xy, cand,
+                                    d_matches12, d_nmatches, m->err, pairs, stream);
+  if (!rc && m->ws.after((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "event record failed");
+  if (do_prof && !rc) {
+    std::vector<long long> h((size_t)pairs * 16);
+    MHIP(hipStreamSynchronize((hipStream_t)stream));
+    MHIP(hipMemcpy(h.data(), prof, h.size() * 8, hipMemcpyDeviceToHost));
+    double ph[9] = {0}, rounds = 0, conv = 0, tot = 0, snap = 0;
+    for (int q = 0; q < pairs; ++q) {
+      for (int k = 1; k < 9; ++k)
+        if (h[q * 16 + k]) ph[k] += (double)(h[q * 16 + k] - h[q * 16]);
+      rounds += h[q * 16 + 11];
+      snap += h[q * 16 + 9];
+      conv += h[q * 16 + 12];
+      tot += h[q * 16 + 13];
+    }
+    fprintf(stderr, "search_init phases (avg clocks from start): sort %.0f qlist %.0f count %.0f walk %.0f dist %.0f "
+            "rounds %.0f end %.0f | rounds %.1f converged %.2f candidates %.0f snapshots %.0f\n", ph[1] / pairs,
+            ph[2] / pairs, ph[3] / pairs, ph[4] / pairs, ph[5] / pairs, ph[7] / pairs, ph[8] / pairs,
+            rounds / pairs, conv / pairs, tot / pairs, snap / pairs);
+  }
+  if (rc == ORBX_ECAPACITY)
+    return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization's LDS grid", kp_pitch);
+  if (rc) return mfail(ORBX_EDEVICE, "search_init launch: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
 }
 
@@ -1555,6 +1617,7 @@ int orbm_destroy(orbm_handle m) {
   if (m->ws.ev) (void)hipEventSynchronize(m->ws.ev);
   m->ws.release();
   if (m->cand) (void)hipFree(m->cand);
+  if (m->host_cand) (void)hipFree(m->host_cand);
   if (m->err) (void)hipFree(m->err);
   if (m->stereo_sad) (void)hipFree(m->stereo_sad);
   if (m->bow_hist) (void)hipFree(m->bow_hist);
@@ -1572,7 +1635,10 @@ int orbm_get_status(orbm_handle m, int reset, int* status) {
   MHIP(hipDeviceSynchronize());  // the matcher's kernels run on caller streams
   int e = 0;
   MHIP(hipMemcpy(&e, m->err, 4, hipMemcpyDeviceToHost));
-  if (reset && e) MHIP(hipMemset(m->err, 0, 16));
+  if (reset && e) {
+    MHIP(hipMemsetAsync(m->err, 0, 16, nullptr));
+    MHIP(hipStreamSynchronize(nullptr));
+  }
   *status = e;
   return ORBX_OK;
 }
@@ -1602,57 +1668,8 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
   if (!m || pairs < 1 || pairs > m->max_pairs || kp_pitch < 1 || kp_pitch > m->max_kps)
     return mfail(ORBX_EINVAL, "pairs/kp_pitch exceed the matcher workspace");
   MHIP(hipSetDevice(m->device));
-  InitParams P{};
-  P.minX = b.min_x;
-  P.maxX = b.max_x;
-  P.minY = b.min_y;
-  P.maxY = b.max_y;
-  // mfGridElementWidthInv / HeightInv (src/Frame.cc:154-155)
-  P.invW = static_cast<float>(kGridCols) / static_cast<float>(b.max_x - b.min_x);
-  P.invH = static_cast<float>(kGridRows) / static_cast<float>(b.max_y - b.min_y);
-  P.r = (float)window;
-  P.nnratio = nnratio;
-  P.check_ori = check_ori;
-  P.kp_pitch = kp_pitch;
-  P.cand_cap = m->cand_cap;
-  P.stop = 0;
-#ifdef ORBX_DIAG  // diagnostics builds only (tools/variant.sh): stop after a phase, results incomplete
-  if (const char* st = getenv("ORBX_INIT_STOP")) P.stop = atoi(st);
-#endif
-  static long long* prof = nullptr;  // ORBX_INIT_PROF: phase clocks of every pair, averaged after the call
-  const bool do_prof = getenv("ORBX_INIT_PROF") != nullptr;
-  if (do_prof) {
-    if (pairs > 4096) return mfail(ORBX_EINVAL, "ORBX_INIT_PROF: at most 4096 pairs");
-    if (!prof) MHIP(hipMalloc(&prof, (size_t)4096 * 16 * 8));
-    MHIP(hipMemset(prof, 0, (size_t)pairs * 16 * 8));
-    P.prof = prof;
-  }
-  if (m->ws.before((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
-  const int rc = launch_search_init(P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, d_prev_xy, m->cand,
-                                    d_matches12, d_nmatches, m->err, pairs, stream);
-  if (!rc && m->ws.after((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "event record failed");
-  if (do_prof && !rc) {
-    std::vector<long long> h((size_t)pairs * 16);
-    MHIP(hipStreamSynchronize((hipStream_t)stream));
-    MHIP(hipMemcpy(h.data(), prof, h.size() * 8, hipMemcpyDeviceToHost));
-    double ph[9] = {0}, rounds = 0, conv = 0, tot = 0, snap = 0;
-    for (int q = 0; q < pairs; ++q) {
-      for (int k = 1; k < 9; ++k)
-        if (h[q * 16 + k]) ph[k] += (double)(h[q * 16 + k] - h[q * 16]);
-      rounds += h[q * 16 + 11];
-      snap += h[q * 16 + 9];
-      conv += h[q * 16 + 12];
-      tot += h[q * 16 + 13];
-    }
-    fprintf(stderr, "search_init phases (avg clocks from start): sort %.0f qlist %.0f count %.0f walk %.0f dist %.0f "
-            "rounds %.0f end %.0f | rounds %.1f converged %.2f candidates %.0f snapshots %.0f\n", ph[1] / pairs,
-            ph[2] / pairs, ph[3] / pairs, ph[4] / pairs, ph[5] / pairs, ph[7] / pairs, ph[8] / pairs,
-            rounds / pairs, conv / pairs, tot / pairs, snap / pairs);
-  }
-  if (rc == ORBX_ECAPACITY)
-    return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization's LDS grid", kp_pitch);
-  if (rc) return mfail(ORBX_EDEVICE, "search_init launch: %s", hipGetErrorString(hipGetLastError()));
-  return ORBX_OK;
+  return search_init_launch(m, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, kp_pitch, pairs, b, d_prev_xy, window,
+                            nnratio, check_ori, d_matches12, d_nmatches, stream, m->cand, m->cand_cap);
 }
 
 int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1, const uint8_t* desc1, int n1,
@@ -1660,9 +1677,44 @@ int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1, const uint
                                    float* prev_xy, int window, float nnratio, int check_ori, int* matches12,
                                    int* nmatches) {
   if (!m || !nmatches || n1 < 0 || n2 < 0) return mfail(ORBX_EINVAL, "bad argument");
-  if (n1 > m->max_kps || n2 > m->max_kps) return mfail(ORBX_ECAPACITY, "more keypoints than max_kps");
+  if ((n1 && (!kp1 || !desc1 || !prev_xy || !matches12)) || (n2 && (!kp2 || !desc2)))
+    return mfail(ORBX_EINVAL, "null array");
   MHIP(hipSetDevice(m->device));
-  const int pitch = std::max(std::max(n1, n2), 1);
+  // Only octave-0 keypoints take part (src/ORBmatcher.cc:424-428: level1 > 0 is
+  // skipped; GetFeaturesInArea(.., level1, level1) returns octave-0 keypoints of
+  // F2, src/Frame.cc:350-352), so both frames are compacted to them in index
+  // order before the upload: the kernel's per-keypoint tables then scale with
+  // the octave-0 counts, not with the frames' sizes, and every result maps back
+  // through the index lists. Other keypoints keep matches12 = -1 and their
+  // vbPrevMatched entry.
+  std::vector<int> q1, q2;
+  q1.reserve(n1);
+  q2.reserve(n2);
+  for (int i = 0; i < n1; ++i)
+    if (kp1[i].octave == 0) q1.push_back(i);
+  for (int i = 0; i < n2; ++i)
+    if (kp2[i].octave == 0) q2.push_back(i);
+  const int c1 = (int)q1.size(), c2 = (int)q2.size();
+  for (int i = 0; i < n1; ++i) matches12[i] = -1;
+  if (c1 == 0 || c2 == 0) {
+    *nmatches = 0;
+    return ORBX_OK;
+  }
+  const int pitch = std::max(c1, c2);
+  if (pitch > 65535) return mfail(ORBX_ECAPACITY, "more than 65535 octave-0 keypoints");
+  std::vector<orbx_kp> hk((size_t)c1 + c2);
+  std::vector<uint8_t> hd(((size_t)c1 + c2) * 32);
+  std::vector<float> hp((size_t)c1 * 2);
+  for (int k = 0; k < c1; ++k) {
+    hk[k] = kp1[q1[k]];
+    memcpy(&hd[(size_t)k * 32], desc1 + (size_t)q1[k] * 32, 32);
+    hp[2 * k] = prev_xy[2 * q1[k]];
+    hp[2 * k + 1] = prev_xy[2 * q1[k] + 1];
+  }
+  for (int k = 0; k < c2; ++k) {
+    hk[c1 + k] = kp2[q2[k]];
+    memcpy(&hd[((size_t)c1 + k) * 32], desc2 + (size_t)q2[k] * 32, 32);
+  }
   const size_t kpb = (size_t)pitch * sizeof(orbx_kp), db = (size_t)pitch * 32;
   const size_t bytes = 2 * kpb + 2 * db + (size_t)pitch * 8 + (size_t)pitch * 4 + 64;
   int rc;
@@ -1677,31 +1729,56 @@ int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1, const uint
   int* dn = dm + pitch;  // n1, n2, nmatches
   if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));  // created on first use
   hipStream_t st = m->stream;
-  const int hn[2] = {n1, n2};
-  if (n1) {
-    MHIP(hipMemcpyAsync(dk1, kp1, (size_t)n1 * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
-    MHIP(hipMemcpyAsync(dd1, desc1, (size_t)n1 * 32, hipMemcpyHostToDevice, st));
-    MHIP(hipMemcpyAsync(dprev, prev_xy, (size_t)n1 * 8, hipMemcpyHostToDevice, st));
-  }
-  if (n2) {
-    MHIP(hipMemcpyAsync(dk2, kp2, (size_t)n2 * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
-    MHIP(hipMemcpyAsync(dd2, desc2, (size_t)n2 * 32, hipMemcpyHostToDevice, st));
-  }
+  const int hn[2] = {c1, c2};
+  MHIP(hipMemcpyAsync(dk1, hk.data(), (size_t)c1 * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
+  MHIP(hipMemcpyAsync(dd1, hd.data(), (size_t)c1 * 32, hipMemcpyHostToDevice, st));
+  MHIP(hipMemcpyAsync(dprev, hp.data(), (size_t)c1 * 8, hipMemcpyHostToDevice, st));
+  MHIP(hipMemcpyAsync(dk2, hk.data() + c1, (size_t)c2 * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
+  MHIP(hipMemcpyAsync(dd2, hd.data() + (size_t)c1 * 32, (size_t)c2 * 32, hipMemcpyHostToDevice, st));
   MHIP(hipMemcpyAsync(dn, hn, 8, hipMemcpyHostToDevice, st));
-  rc = orbm_search_for_initialization_batch(m, dk1, dd1, dn, dk2, dd2, dn + 1, pitch, 1, bounds, dprev, window,
-                                            nnratio, check_ori, dm, dn + 2, st);
-  if (rc) return rc;
-  int err = 0, nm = 0;
-  MHIP(hipMemcpyAsync(&err, m->err, 4, hipMemcpyDeviceToHost, st));
-  MHIP(hipMemcpyAsync(&nm, dn + 2, 4, hipMemcpyDeviceToHost, st));
-  if (n1) {
-    MHIP(hipMemcpyAsync(matches12, dm, (size_t)n1 * 4, hipMemcpyDeviceToHost, st));
-    MHIP(hipMemcpyAsync(prev_xy, dprev, (size_t)n1 * 8, hipMemcpyDeviceToHost, st));
+  // the candidate lists of a dense pair can exceed the matcher's per-pair
+  // workspace: the kernel then reports the total it needs (err[1]) and this
+  // call grows a workspace of its own to that size and runs again, so no input
+  // the reference accepts is refused for want of scratch
+  int err[2] = {0, 0}, nm = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    MHIP(hipMemsetAsync(m->err, 0, 16, st));
+    if (attempt == 0) {
+      rc = search_init_launch(m, dk1, dd1, dn, dk2, dd2, dn + 1, pitch, 1, bounds, dprev, window, nnratio,
+                              check_ori, dm, dn + 2, st, m->cand, m->cand_cap);
+    } else {
+      const long long need = err[1];
+      if (need > m->host_cand_cap) {
+        MHIP(hipStreamSynchronize(st));
+        if (m->host_cand) (void)hipFree(m->host_cand);
+        m->host_cand = nullptr;
+        m->host_cand_cap = 0;
+        MHIP(hipMalloc(&m->host_cand, (size_t)need * 4));
+        m->host_cand_cap = need;
+      }
+      rc = search_init_launch(m, dk1, dd1, dn, dk2, dd2, dn + 1, pitch, 1, bounds, dprev, window, nnratio,
+                              check_ori, dm, dn + 2, st, m->host_cand, m->host_cand_cap);
+    }
+    if (rc) return rc;
+    MHIP(hipMemcpyAsync(err, m->err, 8, hipMemcpyDeviceToHost, st));
+    MHIP(hipStreamSynchronize(st));
+    if (!(err[0] & 8)) break;
   }
+  MHIP(hipMemsetAsync(m->err, 0, 16, st));
+  if (err[0]) {
+    MHIP(hipStreamSynchronize(st));
+    return mfail(ORBX_ECAPACITY, "candidate workspace overflow (err 0x%x, need %d)", err[0], err[1]);
+  }
+  std::vector<int> hm(c1);
+  MHIP(hipMemcpyAsync(&nm, dn + 2, 4, hipMemcpyDeviceToHost, st));
+  MHIP(hipMemcpyAsync(hm.data(), dm, (size_t)c1 * 4, hipMemcpyDeviceToHost, st));
+  MHIP(hipMemcpyAsync(hp.data(), dprev, (size_t)c1 * 8, hipMemcpyDeviceToHost, st));
   MHIP(hipStreamSynchronize(st));
-  if (err) {
-    (void)hipMemset(m->err, 0, 16);
-    return mfail(ORBX_ECAPACITY, "candidate workspace overflow (err 0x%x)", err);
+  for (int k = 0; k < c1; ++k) {
+    const int i1 = q1[k];
+    matches12[i1] = hm[k] >= 0 ? q2[hm[k]] : -1;
+    prev_xy[2 * i1] = hp[2 * k];  // written by the kernel for matched queries, else the uploaded value
+    prev_xy[2 * i1 + 1] = hp[2 * k + 1];
   }
   *nmatches = nm;
   return ORBX_OK;
@@ -1725,7 +1802,10 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
     }
     return true;
   };
+  // the row records keep the matched index in 16 bits (bin << 16 | index):
+  // B's index in KF-KF mode, A's in KF-Frame mode; B's candidates are 16-bit too
   if (nB > 65536) return mfail(ORBX_EINVAL, "nB must be <= 65536");
+  if (!kf_vs_kf && nA > 65536) return mfail(ORBX_EINVAL, "nA must be <= 65536 (KF-Frame row records)");
   if (!check_fv(fvA, nA) || !check_fv(fvB, nB))
     return mfail(ORBX_EINVAL, "FeatureVector must have ascending node ids and disjoint in-range indices");
   MHIP(hipSetDevice(m->device));

@@ -10,6 +10,8 @@
 #ifndef ORBX_SHIM_FRAME_H
 #define ORBX_SHIM_FRAME_H
 #include <cmath>
+#include <exception>
+#include <thread>
 #include <vector>
 
 #include <opencv2/core/core.hpp>
@@ -38,14 +40,33 @@ class Frame {
     image_bounds(imGray);
   }
   // The stereo constructor (src/Frame.cc:60-128): left and right extraction
-  // (the reference runs them on two std::threads, :77-80), then
-  // ComputeStereoMatches(); bf = baseline x fx, mb = bf / fx.
+  // on two std::threads, as the reference does (:77-80, threadLeft /
+  // threadRight over ExtractORB), then ComputeStereoMatches(); bf = baseline
+  // x fx, mb = bf / fx. The two extractor handles are independent; an
+  // exception on either thread is rethrown here after both joined.
   Frame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* extractorLeft, ORBextractor* extractorRight,
         ORBVocabulary* voc, float bf)
       : mpORBvocabulary(voc), mpORBextractorLeft(extractorLeft), mpORBextractorRight(extractorRight), mbf(bf) {
     scale_info();
-    (*mpORBextractorLeft)(imLeft, cv::noArray(), mvKeys, mDescriptors);
-    (*mpORBextractorRight)(imRight, cv::noArray(), mvKeysRight, mDescriptorsRight);
+    std::exception_ptr errL, errR;
+    std::thread threadLeft([&] {
+      try {
+        (*mpORBextractorLeft)(imLeft, cv::noArray(), mvKeys, mDescriptors);
+      } catch (...) {
+        errL = std::current_exception();
+      }
+    });
+    std::thread threadRight([&] {
+      try {
+        (*mpORBextractorRight)(imRight, cv::noArray(), mvKeysRight, mDescriptorsRight);
+      } catch (...) {
+        errR = std::current_exception();
+      }
+    });
+    threadLeft.join();
+    threadRight.join();
+    if (errL) std::rethrow_exception(errL);
+    if (errR) std::rethrow_exception(errR);
     N = (int)mvKeys.size();
     mvKeysUn = mvKeys;
     image_bounds(imLeft);

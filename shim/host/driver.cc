@@ -9,7 +9,8 @@
 //   orbx_shim_driver --version
 //   orbx_shim_driver FRAMES.u8 NFRAMES W H VOC.txt|- OUTDIR
 //   orbx_shim_driver --scene SCENE.bin OUT.bin   (one ORBmatcher method on a test scene, scene.cc)
-//   orbx_shim_driver --stereo LEFT.u8 RIGHT.u8 W H BF OUTDIR   (stereo Frame + ComputeStereoMatches)
+//   orbx_shim_driver --stereo LEFT.u8 RIGHT.u8 NPAIRS W H BF OUTDIR
+//                                 (stereo Frames, two extraction threads each, + ComputeStereoMatches)
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -43,11 +44,14 @@ static std::vector<int> ids(const std::vector<MapPoint*>& v) {
 
 int run_scene(const std::string& in, const std::string& out);  // scene.cc
 
-// The stereo Frame constructor (src/Frame.cc:60-128): two extractors, left
-// and right extraction, ComputeStereoMatches; writes the left keypoints,
-// descriptors, mvuRight and mvDepth.
-static int run_stereo(const char* left, const char* right, int W, int H, float bf, const std::string& out) {
-  std::vector<uint8_t> L((size_t)W * H), R((size_t)W * H);
+// The stereo Frame constructor (src/Frame.cc:60-128) over NPAIRS stereo
+// pairs: two extractors, left and right extraction on two std::threads
+// (Frame.h, as the reference's :77-80), ComputeStereoMatches; writes each
+// pair's left / right keypoints, mvuRight and mvDepth.
+static int run_stereo(const char* left, const char* right, int npairs, int W, int H, float bf,
+                      const std::string& out) {
+  const size_t plane = (size_t)W * H;
+  std::vector<uint8_t> L(plane * npairs), R(plane * npairs);
   for (auto& lr : {std::make_pair(left, &L), std::make_pair(right, &R)}) {
     FILE* f = fopen(lr.first, "rb");
     if (!f || fread(lr.second->data(), 1, lr.second->size(), f) != lr.second->size()) {
@@ -64,13 +68,19 @@ static int run_stereo(const char* left, const char* right, int W, int H, float b
   Frame::cy = 185.2157f;
   Frame::invfx = 1.0f / Frame::fx;
   Frame::invfy = 1.0f / Frame::fy;
-  Frame F(cv::Mat(H, W, CV_8U, L.data(), W), cv::Mat(H, W, CV_8U, R.data(), W), &left_ext, &right_ext, nullptr, bf);
-  write_file(out + "/kpL.bin", F.mvKeys.data(), F.mvKeys.size() * sizeof(cv::KeyPoint));
-  write_file(out + "/kpR.bin", F.mvKeysRight.data(), F.mvKeysRight.size() * sizeof(cv::KeyPoint));
-  write_file(out + "/uright.bin", F.mvuRight.data(), F.mvuRight.size() * 4);
-  write_file(out + "/depth.bin", F.mvDepth.data(), F.mvDepth.size() * 4);
-  const float mb = F.mb;
-  write_file(out + "/mb.bin", &mb, 4);
+  for (int i = 0; i < npairs; ++i) {
+    Frame F(cv::Mat(H, W, CV_8U, L.data() + i * plane, W), cv::Mat(H, W, CV_8U, R.data() + i * plane, W), &left_ext,
+            &right_ext, nullptr, bf);
+    const std::string k = std::to_string(i);
+    write_file(out + "/kpL" + k + ".bin", F.mvKeys.data(), F.mvKeys.size() * sizeof(cv::KeyPoint));
+    write_file(out + "/descL" + k + ".bin", F.mDescriptors.data, (size_t)F.N * 32);
+    write_file(out + "/kpR" + k + ".bin", F.mvKeysRight.data(), F.mvKeysRight.size() * sizeof(cv::KeyPoint));
+    write_file(out + "/descR" + k + ".bin", F.mDescriptorsRight.data, F.mvKeysRight.size() * 32);
+    write_file(out + "/uright" + k + ".bin", F.mvuRight.data(), F.mvuRight.size() * 4);
+    write_file(out + "/depth" + k + ".bin", F.mvDepth.data(), F.mvDepth.size() * 4);
+    const float mb = F.mb;
+    write_file(out + "/mb.bin", &mb, 4);
+  }
   return 0;
 }
 
@@ -81,8 +91,8 @@ int main(int argc, char** argv) {
   }
   try {
     if (argc == 4 && std::string(argv[1]) == "--scene") return run_scene(argv[2], argv[3]);
-    if (argc == 8 && std::string(argv[1]) == "--stereo")
-      return run_stereo(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), (float)atof(argv[6]), argv[7]);
+    if (argc == 9 && std::string(argv[1]) == "--stereo")
+      return run_stereo(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), (float)atof(argv[7]), argv[8]);
   } catch (const std::exception& e) {
     fprintf(stderr, "error: %s\n", e.what());
     return 4;

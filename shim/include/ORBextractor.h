@@ -5,7 +5,9 @@
 #ifndef ORBEXTRACTOR_H
 #define ORBEXTRACTOR_H
 
+#include <chrono>
 #include <list>
+#include <string>
 #include <vector>
 
 #include <opencv2/core/core.hpp>
@@ -14,7 +16,34 @@
 
 namespace ORB_SLAM2 {
 
+class ORBextractor;
+
+// Per-stage time records (include/ORBextractor.h:41-60): Tracking.cc also
+// times its own stages with them (src/Tracking.cc:290-945).
+struct times_t {
+  int frame;
+  std::string name;
+  int level;
+  long long time;
+};
+
+class GetTime {
+ public:
+  GetTime(ORBextractor* o, std::string name, int level);
+  GetTime(std::vector<times_t>& times, int nFrame, std::string name, int level);
+  ~GetTime();
+
+ private:
+  GetTime();
+  ORBextractor* o;
+  times_t t;
+  std::chrono::steady_clock::time_point start;
+  std::vector<times_t>& times;
+};
+
 class ORBextractor {
+  friend class GetTime;
+
  public:
   enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
 
@@ -58,8 +87,16 @@ class ORBextractor {
   std::vector<float> mvLevelSigma2;
   std::vector<float> mvInvLevelSigma2;
 
+  // the reference's per-extractor statistics (:145-148): operator()'s host
+  // time, the frame count, and with ORBX_TIMING=1 the device stage times of
+  // every call, written to times.csv by the destructor (src/ORBextractor.cc:800-820)
+  long long totalTime = 0;
+  unsigned int nFrame = 0;
+  std::vector<times_t> times;
+
   orbx_handle h_ = nullptr;
   int cap_ = 0;
+  bool timing_ = false;
 };
 
 }  // namespace ORB_SLAM2

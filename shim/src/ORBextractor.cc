@@ -2,7 +2,10 @@
 // (constructor :496-560, operator() :1538-1548 / CPU branch :1710-1808).
 #include "ORBextractor.h"
 
+#include <chrono>
 #include <cstdlib>
+#include <fstream>
+#include <iostream>
 #include <stdexcept>
 #include <string>
 
@@ -58,9 +61,25 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
   orbx_check(orbx_get_levels_info(h_, &nl, lw.data(), lh.data(), mnFeaturesPerLevel.data()));
   cap_ = orbx_frame_capacity(h_);
   if (cap_ <= 0) throw std::runtime_error("liborbx: bad frame capacity");
+  // ORBX_TIMING=1: the library records its stage events (orbx_create reads the
+  // same variable) and every call's stage times go to `times`
+  const char* tm = getenv("ORBX_TIMING");
+  timing_ = tm && atoi(tm) != 0;
 }
 
+// The reference's destructor (src/ORBextractor.cc:800-820): average host time
+// per frame on stdout, the time records appended to times.csv in its layout.
 ORBextractor::~ORBextractor() {
+  if (nFrame) std::cout << "Avg computed frame ORB: " << ((double)totalTime / nFrame) / 1000000.0 << "ms" << std::endl;
+  if (!times.empty()) {
+    std::ofstream timesFile;
+    timesFile.open("times.csv", std::ios_base::app);
+    timesFile << "#Frame;Name Processing function;Level;Time spent (ns);Time spent (ms)" << std::endl;
+    for (const times_t& t : times) {
+      timesFile << t.frame << ";" << t.name << ";" << t.level << ";" << t.time << ";" << t.time / 1000000.0 << ";"
+                << std::endl;
+    }
+  }
   if (h_) orbx_destroy(h_);
 }
 
@@ -69,6 +88,9 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask*/, s
   if (_image.empty()) return;  // :1542-1543
   cv::Mat image = _image.getMat();
   assert(image.type() == CV_8UC1);  // :1546
+  const auto start = std::chrono::steady_clock::now();
+  {
+  GetTime total(this, "Total Time ORB extraction", -1);  // :1548 (recorded only with ORBX_TIMING=1)
   _keypoints.resize(cap_);
   cv::Mat desc(cap_, 32, CV_8U);
   int n = 0;
@@ -88,6 +110,40 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask*/, s
     mvImagePyramid[l].create(lh[l], lw[l], CV_8U);
     orbx_check(orbx_get_level(h_, /*frame=*/0, l, /*blurred=*/0, mvImagePyramid[l].data, mvImagePyramid[l].step));
   }
+  if (timing_) {
+    // the device stages under the reference's GetTime names; one launch covers
+    // every pyramid level, so the level field is -1 (as the VX branch's
+    // whole-graph records, :1561-1700)
+    std::vector<float> ms;
+    std::vector<const char*> names;
+    const int n_st = GetStageTimes(ms, names);
+    for (int i = 0; i < n_st; ++i) times.push_back(times_t{(int)nFrame, names[i], -1, (long long)(ms[i] * 1e6)});
+  }
+  }
+  totalTime += std::chrono::duration<long long, std::nano>(std::chrono::steady_clock::now() - start).count();  // :1810-1814
+  nFrame++;
+}
+
+GetTime::GetTime(std::vector<times_t>& times, int nFrame, std::string name, int level) : o(nullptr), times(times) {
+  t.frame = nFrame;
+  t.name = name;
+  t.level = level;
+  start = std::chrono::steady_clock::now();
+}
+
+GetTime::GetTime(ORBextractor* o, std::string name, int level) : o(o), times(o->times) {
+  t.frame = (int)o->nFrame;
+  t.name = name;
+  t.level = level;
+  start = std::chrono::steady_clock::now();
+}
+
+// Records on destruction (src/ORBextractor.cc:1896-1904); an extractor's own
+// records only when its timing is on (ORBX_TIMING=1), Tracking's always.
+GetTime::~GetTime() {
+  if (o && !o->timing_) return;
+  t.time = std::chrono::duration<long long, std::nano>(std::chrono::steady_clock::now() - start).count();
+  times.push_back(t);
 }
 
 int ORBextractor::GetStageTimes(std::vector<float>& ms, std::vector<const char*>& names) {

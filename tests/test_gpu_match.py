@@ -309,21 +309,27 @@ def test_search_for_initialization_contention(pkg, O, seed, ratio):
         assert nm == rnm and np.array_equal(np.array(v12, np.int32), r12) and np.array_equal(p, rprev)
 
 
-def test_search_for_initialization_overflow_then_recovers(pkg, O):
-    """More candidates than the per-pair list area (4 M entries): 2100 x 2100
-    level-0 keypoints in one window. The call reports ECAPACITY rather than
-    truncating; the next call on the same matcher is exact again."""
+def test_search_for_initialization_dense_window_no_capacity_cliff(pkg, O):
+    """2100 x 2100 level-0 keypoints in one window: 4.41 M candidate entries,
+    more than the matcher's per-pair list area (min(max_kps^2, 4M)). The host
+    entry point (the shim's path) grows its workspace and returns the
+    reference's matches instead of ECAPACITY; the next call is exact too."""
     W, H = 1241, 376
     rng = np.random.default_rng(9)
     n = 2100
-    k1 = _kps(pkg, rng.uniform(500, 560, n), rng.uniform(150, 210, n))
-    k2 = _kps(pkg, rng.uniform(500, 560, n), rng.uniform(150, 210, n))
-    d1 = rng.integers(0, 256, (n, 32), np.uint8)
-    d2 = rng.integers(0, 256, (n, 32), np.uint8)
+    k1 = _kps(pkg, rng.uniform(500, 560, n), rng.uniform(150, 210, n), rng.uniform(0, 360, n))
+    k2 = _kps(pkg, rng.uniform(500, 560, n), rng.uniform(150, 210, n), rng.uniform(0, 360, n))
+    base = rng.integers(0, 256, 32, dtype=np.uint8)
+    d1 = np.stack([_flip(rng, base, int(rng.integers(0, 40))) for _ in range(n)])
+    d2 = np.stack([_flip(rng, base, int(rng.integers(0, 40))) for _ in range(n)])
     m = pkg.ORBmatcher(0.9, True, max_kps=n)
-    F1, F2 = pkg.Frame.from_extraction(k1, d1, W, H), pkg.Frame.from_extraction(k2, d2, W, H)
-    with pytest.raises(pkg.OrbxError):
-        m.SearchForInitialization(F1, F2, np.stack([k1["x"], k1["y"]], 1).astype(np.float32), None, 100)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    v12 = []
+    nm = m.SearchForInitialization(pkg.Frame.from_extraction(k1, d1, W, H), pkg.Frame.from_extraction(k2, d2, W, H),
+                                   prev, v12, 100)
+    r12, rnm, rprev = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), np.stack([k1["x"], k1["y"]], 1),
+                                                  100, 0.9, True)
+    assert nm == rnm and np.array_equal(np.array(v12, np.int32), r12) and np.array_equal(prev, rprev)
     (a1, e1), (a2, e2) = _pair(O, 5)
     prev = np.stack([a1["x"], a1["y"]], 1).astype(np.float32)
     v12 = []
@@ -332,3 +338,82 @@ def test_search_for_initialization_overflow_then_recovers(pkg, O):
     r12, rnm, rprev = O.search_for_initialization(a1, e1, a2, e2, (0, W, 0, H), np.stack([a1["x"], a1["y"]], 1),
                                                   100, 0.9, True)
     assert nm == rnm and np.array_equal(np.array(v12, np.int32), r12) and np.array_equal(prev, rprev)
+
+
+def test_search_for_initialization_shim_sized_matcher_dense_level0(pkg, O):
+    """The shim's matcher (max_kps 8192, shim/src/ORBmatcher.cc) on frames of
+    6000 keypoints whose 3000 octave-0 keypoints crowd a 150-px square: frames
+    larger than the kernel's per-keypoint LDS tables and 9 M candidate entries.
+    Octave-0 compaction on the host and the grown workspace give the oracle's
+    matches12 / vbPrevMatched (non-octave-0 queries untouched)."""
+    W, H = 1241, 376
+    rng = np.random.default_rng(21)
+    n, n0 = 6000, 3000
+
+    def frame():
+        oc = np.concatenate([np.zeros(n0, np.int32), rng.integers(1, 8, n - n0).astype(np.int32)])
+        rng.shuffle(oc)
+        x = np.where(oc == 0, rng.uniform(400, 550, n), rng.uniform(20, W - 20, n))
+        y = np.where(oc == 0, rng.uniform(120, 270, n), rng.uniform(20, H - 20, n))
+        k = _kps(pkg, x, y, rng.uniform(0, 360, n))
+        k["octave"] = oc
+        return k
+
+    k1, k2 = frame(), frame()
+    # F2's descriptors: a few bits from a random F1 descriptor (repeats give steals)
+    d1 = rng.integers(0, 256, (n, 32), np.uint8)
+    src = rng.integers(0, n, n)
+    d2 = np.stack([_flip(rng, d1[j], int(rng.integers(0, 12))) for j in src])
+    prev0 = np.stack([k1["x"] + 3.0, k1["y"] - 2.0], 1).astype(np.float32)
+    m = pkg.ORBmatcher(0.9, True, max_kps=8192)
+    prev = prev0.copy()
+    v12 = []
+    nm = m.SearchForInitialization(pkg.Frame.from_extraction(k1, d1, W, H), pkg.Frame.from_extraction(k2, d2, W, H),
+                                   prev, v12, 100)
+    r12, rnm, rprev = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), prev0, 100, 0.9, True)
+    assert rnm > 20
+    assert nm == rnm and np.array_equal(np.array(v12, np.int32), r12) and np.array_equal(prev, rprev)
+
+
+def test_batch_search_init_overflow_is_reported(pkg, O):
+    """The device batch entry cannot grow its workspace inside a stream: a pair
+    whose lists exceed it gets no matches and status bit 8, never truncated
+    results; the other pairs of the launch and the next launch are exact."""
+    import ctypes as C
+
+    from orb_slam_cuda_amd import _lib
+    W, H = 1241, 376
+    rng = np.random.default_rng(9)
+    cap = 2100
+    dense = (_kps(pkg, rng.uniform(500, 560, cap), rng.uniform(150, 210, cap)),
+             rng.integers(0, 256, (cap, 32), np.uint8))
+    dense2 = (_kps(pkg, rng.uniform(500, 560, cap), rng.uniform(150, 210, cap)),
+              rng.integers(0, 256, (cap, 32), np.uint8))
+    pairs = [_pair(O, 40), (dense, dense2)]
+    P = len(pairs)
+    kp = np.zeros((2 * P, cap), pkg.KP_DTYPE)
+    de = np.zeros((2 * P, cap, 32), np.uint8)
+    n = np.zeros(2 * P, np.int32)
+    for p, ((k1, d1), (k2, d2)) in enumerate(pairs):
+        kp[p, :len(k1)], de[p, :len(k1)], n[p] = k1, d1, len(k1)
+        kp[P + p, :len(k2)], de[P + p, :len(k2)], n[P + p] = k2, d2, len(k2)
+    dk, dd, dn = (_lib.DeviceArray(a.nbytes) for a in (kp, de, n))
+    dk.upload(kp), dd.upload(de), dn.upload(n)
+    dm, dnm = _lib.DeviceArray(P * cap * 4), _lib.DeviceArray(P * 4)
+    m = pkg.ORBmatcher(0.9, True, max_pairs=P, max_kps=cap)
+    L = _lib.lib()
+    _lib.check(L.orbm_search_for_initialization_batch(
+        m.handle, C.c_void_p(dk.ptr), C.c_void_p(dd.ptr), C.c_void_p(dn.ptr),
+        C.c_void_p(dk.ptr + P * cap * 28), C.c_void_p(dd.ptr + P * cap * 32), C.c_void_p(dn.ptr + P * 4),
+        cap, P, _lib.GridBounds(0, W, 0, H), None, 100, C.c_float(0.9), 1, C.c_void_p(dm.ptr),
+        C.c_void_p(dnm.ptr), None), matcher=True)
+    L.orbx_stream_synchronize(None)
+    got = dm.download((P, cap), np.int32)
+    gnm = dnm.download(P, np.int32)
+    assert m.status() & 8
+    (k1, d1), (k2, d2) = pairs[0]
+    r12, rnm, _ = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), np.stack([k1["x"], k1["y"]], 1),
+                                              100, 0.9, True)
+    assert gnm[0] == rnm and np.array_equal(got[0, :len(k1)], r12)
+    assert gnm[1] == 0 and (got[1] == -1).all()
+    assert m.status() == 0  # read and reset

@@ -60,7 +60,8 @@ def _download_set(pipe, k):
 
 
 def _oracle_frames(O, cfg, frames, idx):
-    oc = O.config(nfeatures=cfg["nfeatures"], width=cfg["W"], height=cfg["H"])
+    import bench
+    oc = bench.oracle_config(O, cfg)
     with ThreadPoolExecutor(8) as ex:  # the oracle's C calls release the GIL
         res = list(ex.map(lambda i: O.extract(oc, frames[i]), idx))
     return dict(zip(idx, res))
@@ -111,8 +112,10 @@ def _check_batches(O, cfg, frames, pipe, batches, check):
     assert np.mean([r[4] for r in res]) > 50
 
 
-@pytest.mark.parametrize("config", ["kitti", "euroc"])
+@pytest.mark.parametrize("config", ["kitti", "euroc", "kitti14", "intcatch1080"])
 def test_timed_pipeline_matches_oracle(pkg, O, config):
+    """kitti14: Examples/Monocular/KITTI14.yaml (10 levels, the >8-level orient+BRIEF
+    instantiation); intcatch1080: intcatch-1080p.yaml (1920x1080, 3 levels, 10/4)."""
     batches = 5
     args, cfg, frames, pipe, _ = _run_pipeline(["--config", config, "--pool", str(4 * 64)], batches)
     assert pipe.B == 64

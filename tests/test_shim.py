@@ -133,32 +133,47 @@ def test_shim_matcher_methods_match_oracle(pkg, O, tmp_path, op, kw):
 
 @pytest.mark.gpu
 def test_shim_stereo_frame_matches_oracle(pkg, O, tmp_path):
-    """The stereo Frame constructor through the shim: two ORBextractors, then
-    Frame::ComputeStereoMatches (src/Frame.cc:60-128, 465-639) over
-    orbm_compute_stereo_matches, against the oracle's extraction + stereo matching."""
+    """The stereo Frame constructor through the shim over 16 stereo pairs: two
+    ORBextractors driven from two std::threads per Frame, as the reference does
+    (src/Frame.cc:77-80), then Frame::ComputeStereoMatches (:465-639) over
+    orbm_compute_stereo_matches, against the oracle's extraction + stereo
+    matching. The first Frame of the process also races the two handles'
+    first launches (the per-device BRIEF table upload)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from orb_slam_cuda_amd.synth import stereo_pair
     assert os.path.exists(DRIVER)
-    W, H, bf = 1241, 376, 0.54 * 718.856
-    L, R = stereo_pair(21, W, H)
+    W, H, bf, n = 1241, 376, 0.54 * 718.856, 16
+    pairs = [stereo_pair(21 + i, W, H) for i in range(n)]
     lp, rp = tmp_path / "l.u8", tmp_path / "r.u8"
-    np.ascontiguousarray(L).tofile(lp)
-    np.ascontiguousarray(R).tofile(rp)
-    r = subprocess.run([DRIVER, "--stereo", str(lp), str(rp), str(W), str(H), repr(bf), str(tmp_path)],
-                       capture_output=True, text=True, timeout=120)
+    np.ascontiguousarray(np.stack([p[0] for p in pairs])).tofile(lp)
+    np.ascontiguousarray(np.stack([p[1] for p in pairs])).tofile(rp)
+    r = subprocess.run([DRIVER, "--stereo", str(lp), str(rp), str(n), str(W), str(H), repr(bf), str(tmp_path)],
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     cfg = O.config(nfeatures=2000, width=W, height=H)
-    kl, dl = O.extract(cfg, L)
-    kr, dr = O.extract(cfg, R)
-    assert np.array_equal(np.fromfile(tmp_path / "kpL.bin", dtype=kl.dtype).view(np.uint8), kl.view(np.uint8))
-    assert np.array_equal(np.fromfile(tmp_path / "kpR.bin", dtype=kr.dtype).view(np.uint8), kr.view(np.uint8))
+    info = O.level_info(cfg)
     mb = np.fromfile(tmp_path / "mb.bin", dtype=np.float32)[0]
     assert mb == np.float32(bf) / np.float32(718.856)
-    info = O.level_info(cfg)
-    ru, rd, rk = O.compute_stereo_matches(kl, dl, kr, dr, O.pyramid(cfg, L), O.pyramid(cfg, R), info["scale"],
-                                          info["inv_scale"], mb, np.float32(bf))
-    u = np.fromfile(tmp_path / "uright.bin", dtype=np.float32)
-    d = np.fromfile(tmp_path / "depth.bin", dtype=np.float32)
-    assert np.array_equal(u, ru) and np.array_equal(d, rd) and rk > 100
+
+    def ref(i):
+        L, R = pairs[i]
+        kl, dl = O.extract(cfg, L)
+        kr, dr = O.extract(cfg, R)
+        ru, rd, rk = O.compute_stereo_matches(kl, dl, kr, dr, O.pyramid(cfg, L), O.pyramid(cfg, R), info["scale"],
+                                              info["inv_scale"], mb, np.float32(bf))
+        return kl, dl, kr, dr, ru, rd, rk
+
+    with ThreadPoolExecutor(8) as ex:
+        refs = list(ex.map(ref, range(n)))
+    for i, (kl, dl, kr, dr, ru, rd, rk) in enumerate(refs):
+        got = lambda name, dt: np.fromfile(tmp_path / f"{name}{i}.bin", dtype=dt)
+        assert np.array_equal(got("kpL", kl.dtype).view(np.uint8), kl.view(np.uint8)), i
+        assert np.array_equal(got("kpR", kr.dtype).view(np.uint8), kr.view(np.uint8)), i
+        assert np.array_equal(got("descL", np.uint8).reshape(-1, 32), dl), i
+        assert np.array_equal(got("descR", np.uint8).reshape(-1, 32), dr), i
+        u, d = got("uright", np.float32), got("depth", np.float32)
+        assert np.array_equal(u, ru) and np.array_equal(d, rd) and rk > 100, i
 
 
 def test_shim_defines_every_reference_method():
@@ -214,3 +229,61 @@ def test_shim_rejects_unknown_scale_mode(tmp_path):
     r = subprocess.run([DRIVER, str(fpath), "1", "64", "64", "-", str(tmp_path)], capture_output=True, text=True,
                        timeout=60, env=env)
     assert r.returncode != 0 and "ORBX_SCALE_MODE" in r.stderr
+
+
+def test_shim_gettime_tracking_usage(tmp_path):
+    """Tracking's own use of the header's timing records (src/Tracking.cc:290,
+    172-190: GetTime(times, n, name, -1) scopes, then a loop over times_t)
+    compiles against the shim's ORBextractor.h and runs on the CPU."""
+    _build()
+    src = tmp_path / "t.cc"
+    src.write_text(
+        '#include <cstdio>\n#include "ORBextractor.h"\nusing namespace ORB_SLAM2;\n'
+        'int main() { std::vector<times_t> times; int n = 0;\n'
+        '  for (int k = 0; k < 3; ++k) { GetTime tmp(times, n++, "Track", -1); }\n'
+        '  for (times_t t : times) printf("%d;%s;%d;%d\\n", t.frame, t.name.c_str(), t.level, t.time >= 0);\n'
+        '  return 0; }\n')
+    exe = tmp_path / "t"
+    objs = [os.path.join(SHIM, "build", "src", "ORBextractor.o")]
+    subprocess.run(["g++", "-std=c++14", "-pthread", "-I", os.path.join(SHIM, "include"), "-I",
+                    os.path.join(SHIM, "cv"), "-I", os.path.join(ROOT, "include"), str(src), *objs,
+                    "-L", os.path.join(ROOT, "orb_slam_cuda_amd"), "-lorbx",
+                    f"-Wl,-rpath,{os.path.join(ROOT, 'orb_slam_cuda_amd')}", "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
+    assert out.split() == ["0;Track;-1;1", "1;Track;-1;1", "2;Track;-1;1"]
+
+
+@pytest.mark.gpu
+def test_shim_times_csv(pkg, tmp_path):
+    """ORBX_TIMING=1: every operator() call records the device stage times under
+    the reference's GetTime names plus "Total Time ORB extraction", and the
+    destructor appends them to ./times.csv in the reference's layout
+    (src/ORBextractor.cc:800-820): '#Frame;Name Processing function;Level;Time
+    spent (ns);Time spent (ms)' then 'frame;name;level;ns;ms;' rows."""
+    from orb_slam_cuda_amd.synth import SynthSequence
+    W, H, n = 1241, 376, 3
+    frames = SynthSequence(5, W, H).frames(n)
+    fpath = tmp_path / "frames.u8"
+    frames.tofile(fpath)
+    out = tmp_path / "out"
+    out.mkdir()
+    env = dict(os.environ, ORBX_TIMING="1")
+    r = subprocess.run([DRIVER, str(fpath), str(n), str(W), str(H), "-", str(out)], capture_output=True, text=True,
+                       timeout=120, env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "Avg computed frame ORB:" in r.stdout
+    lines = (tmp_path / "times.csv").read_text().splitlines()
+    assert lines[0] == "#Frame;Name Processing function;Level;Time spent (ns);Time spent (ms)"
+    rows = [l.split(";") for l in lines[1:]]
+    names = ["Pyramid/Resize", "Gaussian Blur", "FAST+Grid", "Make quadtree", "Compute angle+ORB descriptor+scale",
+             "Total Time ORB extraction"]
+    assert len(rows) == n * len(names)
+    for k, row in enumerate(rows):
+        assert len(row) == 6 and row[5] == ""
+        assert int(row[0]) == k // len(names) and row[1] == names[k % len(names)] and row[2] == "-1"
+        ns, ms = int(row[3]), float(row[4])
+        assert ns > 0 and abs(ms - ns / 1e6) <= 1e-3 * max(1.0, ms)
+    # stages of one call fit inside its host total
+    for f in range(n):
+        st = rows[f * len(names):(f + 1) * len(names)]
+        assert sum(int(r[3]) for r in st[:-1]) <= int(st[-1][3])
