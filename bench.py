@@ -70,7 +70,7 @@ STAGES = ["pyramid", "blur", "fast_grid", "quadtree", "orient_brief", "hamming_t
 KERNELS = {"bow_transform": "voc_descend_kernel + voc_assemble_kernel", "pyramid": "pyr_band_kernel", "blur": "blur_kernel", "fast_grid": "fast_cells_kernel",
            "bow_match": "search_bow_kernel<256>",
            "quadtree": "quadtree_kernel", "orient_brief": "orient_brief_kernel",
-           "hamming_top2": "hamming_top2_mfma_kernel", "search_init": "search_init_kernel"}
+           "hamming_top2": "hamming_top2_mfma_kernel", "search_init": "search_init_prep_kernel + search_init_query_kernel + search_init_resolve_kernel"}
 KP, DS = 28, 32  # bytes of one orbx_kp (cv::KeyPoint) and one descriptor
 
 CONFIGS = {
@@ -168,6 +168,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency leg")
     ap.add_argument("--no-host-stream", action="store_true", help="skip the host-streamed throughput leg")
     ap.add_argument("--host-steps", type=int, default=30, help="timed steps of the host-streamed leg")
+    ap.add_argument("--h2d-mode", choices=["1d", "2d", "kernel"], default="2d",
+                    help="host-streamed leg: upload padded frames (1d DMA), unpadded rows into the padded pitch "
+                         "(2d DMA rectangle), or unpadded rows by a copy kernel reading pinned host memory")
+    ap.add_argument("--h2d-kernel-wgs", type=int, default=128, help="workgroups of the --h2d-mode kernel copy")
     ap.add_argument("--h2d-split", type=int, default=2,
                     help="host-streamed leg: the batch upload in this many parts, each on a copy stream of its own "
                          "(a multiple of the extraction halves; an extraction half waits for its own parts only)")
@@ -187,7 +191,7 @@ def parse_args(argv=None):
 # ORBX_* variables the library reads (INTEGRATION.md "Environment variables").
 # Tuning: select among bit-exact code paths; allowed, and stamped into the line.
 ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_PYR_PLAN", "ORBX_QT_GENERIC",
-              "ORBX_INIT_LDS_KB", "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS",
+              "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS",
               "ORBX_BOW_ROUNDS",
               # the C++ shim's configuration (shim/src/ORBextractor.cc); bench.py does not read them
               "ORBX_DEVICE", "ORBX_SCALE_MODE", "ORBX_PATTERN"}
@@ -380,7 +384,12 @@ class MonoPipeline:
             raise SystemExit("--pool must be a multiple of --batch")
         self.nbatches = npool // B
         if host:
-            self.h_pool = _lib.HostArray((npool, H, pitch), np.uint8)
+            # 1d: the pool held at the device pitch (padded rows cross the link);
+            # 2d / kernel: unpadded rows, expanded to the pitch by the copy
+            self.h2d_mode = args.h2d_mode
+            hp = pitch if self.h2d_mode == "1d" else W
+            self.h_fbytes = H * hp
+            self.h_pool = _lib.HostArray((npool, H, hp), np.uint8)
             self.h_pool.a[:, :, :W] = frames_pool
             self.d_in = [_lib.DeviceArray(B * self.fbytes) for _ in range(self.NS)]  # input ring
         else:
@@ -500,14 +509,21 @@ class MonoPipeline:
         evs = self.evsets[k] if self.evsets is not None else None
         if self.host:
             # H2D of batch k into input slot k % 3, after extraction k-3 read it
-            src = self.h_pool.ptr + (k % self.nbatches) * B * self.fbytes
+            src = self.h_pool.ptr + (k % self.nbatches) * B * self.h_fbytes
             parts = len(self.s_h2ds)
             for i, sh in enumerate(self.s_h2ds):
                 if k >= NS:
                     sh.wait(self.ev_ext[k - NS])
                 lo, hi = i * B // parts, (i + 1) * B // parts
-                check(L.orbx_memcpy_htod_async(vp(self.d_in[k % NS].ptr + lo * self.fbytes),
-                                               vp(src + lo * self.fbytes), (hi - lo) * self.fbytes, sh.s))
+                dst = vp(self.d_in[k % NS].ptr + lo * self.fbytes)
+                hsrc = vp(src + lo * self.h_fbytes)
+                if self.h2d_mode == "1d":
+                    check(L.orbx_memcpy_htod_async(dst, hsrc, (hi - lo) * self.fbytes, sh.s))
+                elif self.h2d_mode == "2d":
+                    check(L.orbx_memcpy2d_htod_async(dst, self.pitch, hsrc, self.W, self.W, (hi - lo) * self.H, sh.s))
+                else:
+                    check(L.orbx_copy2d_kernel_async(dst, self.pitch, hsrc, self.W, self.W, (hi - lo) * self.H,
+                                                     a.h2d_kernel_wgs, sh.s))
                 self.ev_in[k][i].record(sh)
         fp = self.frames_ptr(k)
         for h, (ex, se) in enumerate(zip(self.exts, self.s_exts)):
@@ -896,18 +912,60 @@ def host_stream_leg(args, cfg, local, frames):
     (H2D on a copy stream, overlapped with the previous batch's compute) and
     its keypoints, descriptors, counts and matches come back (D2H on a second
     copy stream). PCIe-inclusive throughput; never `value`."""
+    link = link_peak(cfg, args.batch)
     pipe = MonoPipeline(args, cfg, local, frames, host=True, need_events=False)
     wall, _ = pipe.run(min(args.warmup, 10), args.host_steps, None)
     pipe.check_status()
     B, cap = pipe.B, pipe.cap
-    h2d = B * pipe.fbytes
+    h2d = B * pipe.h_fbytes
     d2h = B * (cap * (KP + DS) + 4) + (0 if args.no_match else B * (cap + 1) * 4)
+    h2d_rate = h2d * args.host_steps / wall / 1e9
     return {"value": round(B * args.host_steps / wall, 2), "unit": "frames/s", "steps": args.host_steps,
             "ms_per_step": round(wall / args.host_steps * 1e3, 4),
             "pcie_gb_per_s": round((h2d + d2h) * args.host_steps / wall / 1e9, 2),
-            "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
+            "h2d_gb_per_s": round(h2d_rate, 2), "link": link,
+            "h2d_frac_of_link_peak": round(h2d_rate / link["h2d_peak_GBps"], 3) if link.get("h2d_peak_GBps") else None,
+            "h2d_mode": args.h2d_mode, "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
             "what": f"pool of {len(frames)} frames in pinned host memory, batch uploaded per step, "
                     "keypoints + descriptors + counts" + ("" if args.no_match else " + matches") + " read back"}
+
+
+def link_peak(cfg, B, reps=20):
+    """The box's pinned host<->device copy rates alone (hipMemcpyAsync of one
+    padded batch from / to pinned memory, 1 and 2 streams): the ceiling the
+    host-streamed leg is compared with."""
+    from orb_slam_cuda_amd import _lib
+    L = _lib.lib()
+    vp = C.c_void_p
+    W, H = cfg["W"], cfg["H"]
+    nb = B * H * ((W + 63) & ~63)
+    h = _lib.HostArray(nb, np.uint8)
+    d = _lib.DeviceArray(nb)
+    ss = [_lib.Stream(), _lib.Stream()]
+    out = {"bytes": nb}
+    for name, kind in (("h2d", 0), ("d2h", 1)):
+        best = 0.0
+        for ns in (1, 2):
+            def once():
+                for i in range(ns):
+                    lo, hi = i * nb // ns, (i + 1) * nb // ns
+                    if kind == 0:
+                        _lib.check(L.orbx_memcpy_htod_async(vp(d.ptr + lo), vp(h.ptr + lo), hi - lo, ss[i].s))
+                    else:
+                        _lib.check(L.orbx_memcpy_dtoh_async(vp(h.ptr + lo), vp(d.ptr + lo), hi - lo, ss[i].s))
+            once()
+            for st in ss:
+                st.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                once()
+            for st in ss:
+                st.synchronize()
+            rate = nb * reps / (time.perf_counter() - t0) / 1e9
+            out[f"{name}_{ns}stream_GBps"] = round(rate, 2)
+            best = max(best, rate)
+        out[f"{name}_peak_GBps"] = round(best, 2)
+    return out
 
 
 def latency_leg(cfg, local, frames, no_match, n=200, warm=20):

@@ -259,10 +259,9 @@ typedef struct orbm_grid_bounds {
 /* ORBmatcher::SearchForInitialization on host buffers (synchronous).
  * prev_xy: 2*n1 floats, vbPrevMatched, updated in place. matches12: n1.
  * n1 / n2 are not bounded by the matcher's max_kps: only octave-0 keypoints
- * take part (compacted on the host; at most 65535 per frame, and their
- * per-keypoint tables must fit the kernel's LDS, ~4,000), and a pair whose
- * candidate lists exceed the per-pair workspace is re-run in a workspace
- * grown to its size, so dense inputs return results, not ORBX_ECAPACITY. */
+ * take part (compacted on the host; up to 10,000 per frame, the resolve
+ * kernel's LDS tables), and the kernels keep no candidate lists, so any
+ * window density is matched, never refused for want of scratch. */
 int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1,
                                    const uint8_t* desc1, int n1,
                                    const orbx_kp* kp2, const uint8_t* desc2,
@@ -277,9 +276,8 @@ int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1,
  * windows on F1's own keypoints (the initial mvbPrevMatched of
  * Tracking::MonocularInitialization, src/Tracking.cc:645-647; nothing is
  * written back then); d_matches12: pairs x kp_pitch; d_nmatches: pairs.
- * A pair whose candidate lists exceed the workspace (more than min(max_kps^2,
- * 4M) entries; with max_kps <= 2048 that cannot happen) gets no matches and
- * sets status bit 8 (orbm_get_status); never a truncated result. */
+ * kp_pitch <= min(max_kps, 10,000); any window density is matched (the
+ * kernels keep each query's 4 smallest keys, not its candidate list). */
 int orbm_search_for_initialization_batch(
     orbm_handle m, const orbx_kp* d_kp1, const uint8_t* d_desc1,
     const int* d_n1, const orbx_kp* d_kp2, const uint8_t* d_desc2,
@@ -670,6 +668,16 @@ int orbx_host_alloc(void** p, size_t bytes);
 int orbx_host_free(void* p);
 int orbx_memcpy_htod_async(void* dst, const void* src, size_t bytes, void* stream);
 int orbx_memcpy_dtoh_async(void* dst, const void* src, size_t bytes, void* stream);
+/* Rows of `width` bytes from a host image with row stride `spitch` into device
+ * rows of stride `dpitch` (the extractor's padded pitch), one DMA rectangle
+ * copy: frames cross the link unpadded. */
+int orbx_memcpy2d_htod_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                             size_t rows, void* stream);
+/* The same rectangle copy done by a kernel of `blocks` 256-thread workgroups
+ * reading pinned host memory (orbx_host_alloc) over the link directly, in
+ * 16-byte loads, instead of by the DMA engines. */
+int orbx_copy2d_kernel_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                             size_t rows, int blocks, void* stream);
 int orbx_stream_create(void** stream);
 /* A stream whose work the dispatcher prefers (high = 1) or defers (high = 0)
  * when both compete for compute units (hipStreamCreateWithPriority). */

@@ -192,6 +192,10 @@ def lib() -> C.CDLL:
         L.orbx_memcpy_dtod_async.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.orbx_memcpy_htod_async.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.orbx_memcpy_dtoh_async.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.orbx_memcpy2d_htod_async.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t,
+                                               C.c_size_t, C.c_void_p]
+        L.orbx_copy2d_kernel_async.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t,
+                                               C.c_size_t, C.c_int, C.c_void_p]
         L.orbx_host_alloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
         L.orbx_host_free.argtypes = [C.c_void_p]
         L.orbx_stream_create.argtypes = [C.POINTER(C.c_void_p)]

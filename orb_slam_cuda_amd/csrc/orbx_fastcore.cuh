@@ -43,17 +43,27 @@ __device__ __forceinline__ i16x2 corner_score16_x2_ring(const u16x2_t (&P)[16], 
     hi4[j] = __builtin_elementwise_max(hi[j], hi[(j + 1) & 7]);
     lo4[j] = __builtin_elementwise_min(lo[j], lo[(j + 1) & 7]);
   }
-  const u16x2_t big = {0xFFFF, 0xFFFF}, zero = {0, 0};
-  u16x2_t A = big, B = zero;
+  // runs of 8 from s, extended to the 9-arcs from s - 1 and s; the 16 arc
+  // extrema then meet in balanced trees (independent ops at every level: a
+  // serial min/max chain puts a hazard nop between its dependent packed ops)
+  u16x2_t ta[16], tb[16];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {  // runs of 8 from s, extended to the 9-arcs from s - 1 and s
+  for (int j = 0; j < 8; ++j) {
     const u16x2_t a = __builtin_elementwise_max(hi4[j], hi4[(j + 2) & 7]);
-    A = __builtin_elementwise_min(A, __builtin_elementwise_max(a, P[2 * j]));
-    A = __builtin_elementwise_min(A, __builtin_elementwise_max(a, P[(2 * j + 9) & 15]));
+    ta[2 * j] = __builtin_elementwise_max(a, P[2 * j]);
+    ta[2 * j + 1] = __builtin_elementwise_max(a, P[(2 * j + 9) & 15]);
     const u16x2_t b = __builtin_elementwise_min(lo4[j], lo4[(j + 2) & 7]);
-    B = __builtin_elementwise_max(B, __builtin_elementwise_min(b, P[2 * j]));
-    B = __builtin_elementwise_max(B, __builtin_elementwise_min(b, P[(2 * j + 9) & 15]));
+    tb[2 * j] = __builtin_elementwise_min(b, P[2 * j]);
+    tb[2 * j + 1] = __builtin_elementwise_min(b, P[(2 * j + 9) & 15]);
   }
+#pragma unroll
+  for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+    for (int j = 0; j < w; ++j) {
+      ta[j] = __builtin_elementwise_min(ta[j], ta[j + w]);
+      tb[j] = __builtin_elementwise_max(tb[j], tb[j + w]);
+    }
+  const u16x2_t A = ta[0], B = tb[0];
   const i16x2 vs = __builtin_bit_cast(i16x2, v);
   const short t = (short)threshold;
   const i16x2 tt = {t, t};

@@ -24,6 +24,24 @@
 #include "orbx_sincosf.h"
 
 namespace orbx {
+
+// Rectangle copy by the compute units (orbx_copy2d_kernel_async): a thread per
+// 16-byte destination chunk, grid-strided; the source may be pinned host
+// memory read over the link. A row's last chunk is clipped to its width.
+__global__ __launch_bounds__(256) void copy2d_kernel(uint8_t* __restrict__ d, size_t dp, const uint8_t* __restrict__ s,
+                                                     size_t sp, size_t w, size_t rows) {
+  const size_t cpr = (w + 15) / 16, total = cpr * rows;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t r = i / cpr, c = (i - r * cpr) * 16;
+    const uint8_t* src = s + r * sp + c;
+    uint8_t* dst = d + r * dp + c;
+    if (c + 16 <= w) {
+      *(uint4*)dst = *(const uint4*)src;  // unaligned source rows: the memory path takes unaligned dwordx4
+    } else {
+      for (size_t k = 0; k < 16 && c + k < w; ++k) dst[k] = src[k];
+    }
+  }
+}
 size_t quadtree_lds_bytes(const ExtractParams& P);
 extern const void* quadtree_kernel_ptr();
 size_t pyr_band_lds_bytes(const ExtractParams& P);
@@ -929,6 +947,20 @@ int orbx_memcpy_htod_async(void* d, const void* s, size_t b, void* st) {
 int orbx_memcpy_dtoh_async(void* d, const void* s, size_t b, void* st) {
   HIP_OK(hipMemcpyAsync(d, s, b, hipMemcpyDeviceToHost, (hipStream_t)st));
   return ORBX_OK;
+}
+int orbx_memcpy2d_htod_async(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t rows, void* st) {
+  if (!d || !s || w > dp || w > sp) return fail(ORBX_EINVAL, "bad 2D copy");
+  if (!w || !rows) return ORBX_OK;
+  HIP_OK(hipMemcpy2DAsync(d, dp, s, sp, w, rows, hipMemcpyHostToDevice, (hipStream_t)st));
+  return ORBX_OK;
+}
+int orbx_copy2d_kernel_async(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t rows, int blocks,
+                             void* st) {
+  if (!d || !s || w > dp || w > sp || blocks < 1 || (dp & 15)) return fail(ORBX_EINVAL, "bad 2D copy");
+  if (!w || !rows) return ORBX_OK;
+  hipLaunchKernelGGL(orbx::copy2d_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)st, (uint8_t*)d, dp,
+                     (const uint8_t*)s, sp, w, rows);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : fail(ORBX_EDEVICE, "copy kernel launch failed");
 }
 int orbx_memcpy_dtod_async(void* d, const void* s, size_t b, void* st) {
   HIP_OK(hipMemcpyAsync(d, s, b, hipMemcpyDeviceToDevice, (hipStream_t)st));

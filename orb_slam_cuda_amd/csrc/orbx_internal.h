@@ -150,19 +150,9 @@ int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_
                    uint8_t* d_desc, int* d_counts, void* stream, void** stage_events);
 
 // orbx_match.hip
-struct MatchBuffers {
-  uint32_t* cand;       // candidate (i2 | dist << 24) per pair
-  long long cand_cap;   // entries per pair
-  int* cand_off;        // per pair x kp_cap
-  int* err;
-};
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap,
                         const uint8_t* B, size_t b_pitch, const int* nB, int pairs, int* best_idx,
                         int* best, int* second, int* err, void* stream);
-int launch_search_init(const MatchBuffers& M, const orbx_kp* kp1, const uint8_t* desc1,
-                       const int* n1, const orbx_kp* kp2, const uint8_t* desc2, const int* n2,
-                       int kp_pitch, int pairs, orbm_grid_bounds b, float* prev_xy, int window,
-                       float nnratio, int check_ori, int* matches12, int* nmatches, void* stream);
 
 
 // orbx_stereo.hip — Frame::ComputeStereoMatches over a batch of rectified pairs.
@@ -181,23 +171,22 @@ size_t stereo_lds_bytes(int nrows, int kp_pitch, int jobs_cap);
 int launch_stereo(const StereoParams& P, const orbx_kp* kpL, const uint8_t* descL, const int* nL,
                   const orbx_kp* kpR, const uint8_t* descR, const int* nR, int pairs, float* uRight,
                   float* depth, int* sad, int* nkept, void* stream);
-// orbx_init.hip — SearchForInitialization, one (F1, F2) pair per workgroup
+// orbx_init.hip — SearchForInitialization: prep, key and resolve launches per batch of pairs
 struct InitParams {
   float minX, maxX, minY, maxY, invW, invH;  // F2 grid bounds
   float r;                                   // windowSize
   float nnratio;
   int check_ori;
   int kp_pitch;
-  int cand_lds;        // candidate entries that fit in LDS (set by the launcher)
-  long long cand_cap;  // global candidate entries per pair (fallback)
-  int stop;            // diagnostics: 0 = full kernel, k = return after phase k
-  long long* prof;     // diagnostics (ORBX_INIT_PROF): phase clocks per pair, or null
+  long long ws_ints;  // per-pair workspace stride in ints (set by the launcher)
+  int dshift, obits, dclamp;  // key layout (set by the launcher from nnratio)
+  uint32_t omask;
 };
-constexpr int kInitThreads = 1024;
 constexpr size_t kInitLdsBudget = 160 * 1024 - 512;
+size_t init_ws_bytes_per_pair(int kp_pitch);
 int launch_search_init(const InitParams& P, const orbx_kp* kp1, const uint8_t* desc1, const int* n1,
-                       const orbx_kp* kp2, const uint8_t* desc2, const int* n2, float* prev, uint32_t* cand,
-                       int* matches12, int* nmatches, int* err, int pairs, void* stream);
+                       const orbx_kp* kp2, const uint8_t* desc2, const int* n2, float* prev, int* ws,
+                       int* matches12, int* nmatches, int pairs, void* stream);
 // orbx_project.hip — SearchByProjection(Frame&, vector<MapPoint*>, th), one frame per workgroup
 struct ProjParams {
   float minX, maxX, minY, maxY, invW, invH;  // Frame grid bounds, FRAME_GRID_COLS/ROWS over their extent

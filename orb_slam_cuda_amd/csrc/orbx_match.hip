@@ -1498,10 +1498,10 @@ extern "C" const char* orbm_last_error(void) { return g_merr.c_str(); }
 struct orbx_matcher {
   int device = 0, max_pairs = 0, max_kps = 0;
   int sortn = 1;
-  long long cand_cap = 0;
-  uint32_t* cand = nullptr;
-  uint32_t* host_cand = nullptr;  // orbm_search_for_initialization's own workspace, grown on demand
-  long long host_cand_cap = 0;
+  int* init_ws = nullptr;  // SearchForInitialization: per-pair records, keys (init_ws_bytes_per_pair)
+  size_t init_ws_pair = 0;  // bytes per pair
+  int* host_init_ws = nullptr;  // orbm_search_for_initialization's own (its pitch is the call's)
+  size_t host_init_ws_bytes = 0;
   int* err = nullptr;
   int* stereo_sad = nullptr;  // [max_pairs][max_kps] SAD per left keypoint (-1 = none)
   int* bow_hist = nullptr;    // [max_pairs][32] SearchByBoW rotation histogram (+ match count), 0 between calls
@@ -1529,7 +1529,7 @@ static int stage_reserve(orbx_matcher* m, size_t bytes) {
 static int search_init_launch(orbx_matcher* m, const orbx_kp* d_kp1, const uint8_t* d_desc1, const int* d_n1,
                               const orbx_kp* d_kp2, const uint8_t* d_desc2, const int* d_n2, int kp_pitch, int pairs,
                               orbm_grid_bounds b, float* d_prev_xy, int window, float nnratio, int check_ori,
-                              int* d_matches12, int* d_nmatches, void* stream, uint32_t* cand, long long cand_cap) {
+                              int* d_matches12, int* d_nmatches, void* stream, int* ws) {
   InitParams P{};
   P.minX = b.min_x;
   P.maxX = b.max_x;
@@ -1542,43 +1542,12 @@ static int search_init_launch(orbx_matcher* m, const orbx_kp* d_kp1, const uint8
   P.nnratio = nnratio;
   P.check_ori = check_ori;
   P.kp_pitch = kp_pitch;
-  P.cand_cap = cand_cap;
-  P.stop = 0;
-#ifdef ORBX_DIAG  // diagnostics builds only (tools/variant.sh): stop after a phase, results incomplete
-  if (const char* st = getenv("ORBX_INIT_STOP")) P.stop = atoi(st);
-#endif
-  static long long* prof = nullptr;  // ORBX_INIT_PROF: phase clocks of every pair, averaged after the call
-  const bool do_prof = getenv("ORBX_INIT_PROF") != nullptr;
-  if (do_prof) {
-    if (pairs > 4096) return mfail(ORBX_EINVAL, "ORBX_INIT_PROF: at most 4096 pairs");
-    if (!prof) MHIP(hipMalloc(&prof, (size_t)4096 * 16 * 8));
-    MHIP(hipMemset(prof, 0, (size_t)pairs * 16 * 8));
-    P.prof = prof;
-  }
   if (m->ws.before((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "stream wait on the workspace failed");
-  const int rc = launch_search_init(P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, d_prev_xy, cand,
-                                    d_matches12, d_nmatches, m->err, pairs, stream);
+  const int rc = launch_search_init(P, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, d_prev_xy, ws, d_matches12,
+                                    d_nmatches, pairs, stream);
   if (!rc && m->ws.after((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "event record failed");
-  if (do_prof && !rc) {
-    std::vector<long long> h((size_t)pairs * 16);
-    MHIP(hipStreamSynchronize((hipStream_t)stream));
-    MHIP(hipMemcpy(h.data(), prof, h.size() * 8, hipMemcpyDeviceToHost));
-    double ph[9] = {0}, rounds = 0, conv = 0, tot = 0, snap = 0;
-    for (int q = 0; q < pairs; ++q) {
-      for (int k = 1; k < 9; ++k)
-        if (h[q * 16 + k]) ph[k] += (double)(h[q * 16 + k] - h[q * 16]);
-      rounds += h[q * 16 + 11];
-      snap += h[q * 16 + 9];
-      conv += h[q * 16 + 12];
-      tot += h[q * 16 + 13];
-    }
-    fprintf(stderr, "search_init phases (avg clocks from start): sort %.0f qlist %.0f count %.0f walk %.0f dist %.0f "
-            "rounds %.0f end %.0f | rounds %.1f converged %.2f candidates %.0f snapshots %.0f\n", ph[1] / pairs,
-            ph[2] / pairs, ph[3] / pairs, ph[4] / pairs, ph[5] / pairs, ph[7] / pairs, ph[8] / pairs,
-            rounds / pairs, conv / pairs, tot / pairs, snap / pairs);
-  }
   if (rc == ORBX_ECAPACITY)
-    return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization's LDS grid", kp_pitch);
+    return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization (<= 10,000)", kp_pitch);
   if (rc) return mfail(ORBX_EDEVICE, "search_init launch: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
 }
@@ -1594,10 +1563,8 @@ int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out) {
   m->max_pairs = max_pairs;
   m->max_kps = max_kps;
   while (m->sortn < max_kps) m->sortn <<= 1;
-  // candidate budget per pair: every level-0 pair of a 200 x 200 window is far
-  // below this; overflow is reported (ORBX_ECAPACITY), never truncated.
-  m->cand_cap = std::min<long long>((long long)max_kps * max_kps, 4ll << 20);
-  if (hipMalloc(&m->cand, (size_t)max_pairs * m->cand_cap * 4) != hipSuccess ||
+  m->init_ws_pair = init_ws_bytes_per_pair(max_kps);
+  if (hipMalloc(&m->init_ws, (size_t)max_pairs * m->init_ws_pair) != hipSuccess ||
       hipMalloc(&m->err, 16) != hipSuccess ||
       hipMalloc(&m->stereo_sad, (size_t)max_pairs * max_kps * 4) != hipSuccess ||
       hipMalloc(&m->bow_hist, (size_t)max_pairs * 32 * 4) != hipSuccess ||
@@ -1616,8 +1583,8 @@ int orbm_destroy(orbm_handle m) {
   if (m->stream) (void)hipStreamSynchronize(m->stream);
   if (m->ws.ev) (void)hipEventSynchronize(m->ws.ev);
   m->ws.release();
-  if (m->cand) (void)hipFree(m->cand);
-  if (m->host_cand) (void)hipFree(m->host_cand);
+  if (m->init_ws) (void)hipFree(m->init_ws);
+  if (m->host_init_ws) (void)hipFree(m->host_init_ws);
   if (m->err) (void)hipFree(m->err);
   if (m->stereo_sad) (void)hipFree(m->stereo_sad);
   if (m->bow_hist) (void)hipFree(m->bow_hist);
@@ -1669,7 +1636,7 @@ int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, co
     return mfail(ORBX_EINVAL, "pairs/kp_pitch exceed the matcher workspace");
   MHIP(hipSetDevice(m->device));
   return search_init_launch(m, d_kp1, d_desc1, d_n1, d_kp2, d_desc2, d_n2, kp_pitch, pairs, b, d_prev_xy, window,
-                            nnratio, check_ori, d_matches12, d_nmatches, stream, m->cand, m->cand_cap);
+                            nnratio, check_ori, d_matches12, d_nmatches, stream, m->init_ws);
 }
 
 int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1, const uint8_t* desc1, int n1,
@@ -1736,39 +1703,22 @@ int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1, const uint
   MHIP(hipMemcpyAsync(dk2, hk.data() + c1, (size_t)c2 * sizeof(orbx_kp), hipMemcpyHostToDevice, st));
   MHIP(hipMemcpyAsync(dd2, hd.data() + (size_t)c1 * 32, (size_t)c2 * 32, hipMemcpyHostToDevice, st));
   MHIP(hipMemcpyAsync(dn, hn, 8, hipMemcpyHostToDevice, st));
-  // the candidate lists of a dense pair can exceed the matcher's per-pair
-  // workspace: the kernel then reports the total it needs (err[1]) and this
-  // call grows a workspace of its own to that size and runs again, so no input
-  // the reference accepts is refused for want of scratch
-  int err[2] = {0, 0}, nm = 0;
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    MHIP(hipMemsetAsync(m->err, 0, 16, st));
-    if (attempt == 0) {
-      rc = search_init_launch(m, dk1, dd1, dn, dk2, dd2, dn + 1, pitch, 1, bounds, dprev, window, nnratio,
-                              check_ori, dm, dn + 2, st, m->cand, m->cand_cap);
-    } else {
-      const long long need = err[1];
-      if (need > m->host_cand_cap) {
-        MHIP(hipStreamSynchronize(st));
-        if (m->host_cand) (void)hipFree(m->host_cand);
-        m->host_cand = nullptr;
-        m->host_cand_cap = 0;
-        MHIP(hipMalloc(&m->host_cand, (size_t)need * 4));
-        m->host_cand_cap = need;
-      }
-      rc = search_init_launch(m, dk1, dd1, dn, dk2, dd2, dn + 1, pitch, 1, bounds, dprev, window, nnratio,
-                              check_ori, dm, dn + 2, st, m->host_cand, m->host_cand_cap);
+  // the call's own workspace, sized for its pitch (the octave-0 counts)
+  const size_t wsb = init_ws_bytes_per_pair(pitch);
+  if (wsb > m->host_init_ws_bytes) {
+    if (m->host_init_ws) {
+      MHIP(hipStreamSynchronize(st));
+      (void)hipFree(m->host_init_ws);
     }
-    if (rc) return rc;
-    MHIP(hipMemcpyAsync(err, m->err, 8, hipMemcpyDeviceToHost, st));
-    MHIP(hipStreamSynchronize(st));
-    if (!(err[0] & 8)) break;
+    m->host_init_ws = nullptr;
+    m->host_init_ws_bytes = 0;
+    MHIP(hipMalloc(&m->host_init_ws, wsb));
+    m->host_init_ws_bytes = wsb;
   }
-  MHIP(hipMemsetAsync(m->err, 0, 16, st));
-  if (err[0]) {
-    MHIP(hipStreamSynchronize(st));
-    return mfail(ORBX_ECAPACITY, "candidate workspace overflow (err 0x%x, need %d)", err[0], err[1]);
-  }
+  rc = search_init_launch(m, dk1, dd1, dn, dk2, dd2, dn + 1, pitch, 1, bounds, dprev, window, nnratio, check_ori, dm,
+                          dn + 2, st, m->host_init_ws);
+  if (rc) return rc;
+  int nm = 0;
   std::vector<int> hm(c1);
   MHIP(hipMemcpyAsync(&nm, dn + 2, 4, hipMemcpyDeviceToHost, st));
   MHIP(hipMemcpyAsync(hm.data(), dm, (size_t)c1 * 4, hipMemcpyDeviceToHost, st));

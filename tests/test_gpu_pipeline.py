@@ -148,14 +148,17 @@ def test_timed_pipeline_bow_match_matches_oracle(pkg, O):
     assert nm.mean() > 20
 
 
-@pytest.mark.parametrize("parts", [1, 2, 4])
-def test_host_streamed_pipeline_matches_oracle(pkg, O, parts):
+@pytest.mark.parametrize("mode,parts", [("2d", 1), ("2d", 2), ("2d", 4), ("1d", 2), ("kernel", 2)])
+def test_host_streamed_pipeline_matches_oracle(pkg, O, mode, parts):
     """The host-streamed leg (bench.py host_stream_leg): every batch uploaded
     from pinned host memory in `parts` pieces on their own copy streams, each
     extraction half waiting for its own pieces; outputs read back on a copy
-    stream. A missing upload edge would extract stale or partial frames."""
+    stream. Uploads: padded rows (1d DMA), unpadded rows into the device
+    pitch (2d DMA rectangle, the default) or by the copy kernel. A missing
+    upload edge would extract stale or partial frames."""
     batches = 4
-    args, cfg, frames, pipe, _ = _run_pipeline(["--pool", str(3 * 64), "--h2d-split", str(parts)], batches, host=True)
+    args, cfg, frames, pipe, _ = _run_pipeline(["--pool", str(3 * 64), "--h2d-split", str(parts), "--h2d-mode", mode],
+                                               batches, host=True)
     assert len(pipe.s_h2ds) == parts
     _check_batches(O, cfg, frames, pipe, batches, [batches - 2, batches - 1])
     # the read-back of the last batch equals the device outputs

@@ -20,7 +20,7 @@ run c4 --config stereo
 run c5 --config euroc
 run bowmatch --bow-match
 run bowmatch_serial --bow-match --serial
-ORBX_INIT_PROF=1 timeout -k 10 120 python3 tools/init_timing.py 64 > $OUT/init_prof.log 2>&1
+timeout -k 10 120 python3 tools/init_timing.py 64 > $OUT/init_prof.log 2>&1
 timeout -k 10 120 python3 tools/init_timing.py 64 >> $OUT/init_prof.log 2>&1
 bash tools/pmc_sq.sh $OUT/pmc_sq > $OUT/pmc_sq.log 2>&1
 echo all-done

@@ -1,6 +1,6 @@
 """Times orbm_search_for_initialization_batch (and orbm_hamming_top2) alone on a
-resident batch of 64 (t, t-1) pairs of extracted frames (tuning aid).
-env ORBX_INIT_STOP: 1 = after the grid sort, 2 = after pass 1, 3 = after pass 2."""
+resident batch of 64 (t, t-1) pairs of extracted frames (tuning aid; per-kernel
+times: run it under rocprofv3 --kernel-trace --stats).
 import ctypes as C
 import os
 import sys
@@ -52,5 +52,5 @@ for _ in range(N):
     run()
 e1.record(s)
 s.synchronize()
-print(f"{which} cap={cap} pairs={B} stop={os.environ.get('ORBX_INIT_STOP', '0')} ms_per_call={e0.elapsed_ms(e1) / N:.4f} "
+print(f"{which} cap={cap} pairs={B} ms_per_call={e0.elapsed_ms(e1) / N:.4f} "
       f"matches_mean={d_nm.download(B, np.int32).mean():.1f}")
