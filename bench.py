@@ -168,11 +168,17 @@ def parse_args(argv=None):
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency leg")
     ap.add_argument("--no-host-stream", action="store_true", help="skip the host-streamed throughput leg")
     ap.add_argument("--host-steps", type=int, default=30, help="timed steps of the host-streamed leg")
-    ap.add_argument("--h2d-mode", choices=["1d", "2d", "kernel"], default="2d",
+    ap.add_argument("--h2d-mode", choices=["1d", "2d", "kernel"], default="kernel",
                     help="host-streamed leg: upload padded frames (1d DMA), unpadded rows into the padded pitch "
-                         "(2d DMA rectangle), or unpadded rows by a copy kernel reading pinned host memory")
-    ap.add_argument("--h2d-kernel-wgs", type=int, default=128, help="workgroups of the --h2d-mode kernel copy")
-    ap.add_argument("--h2d-split", type=int, default=2,
+                         "(2d DMA rectangle: 0.13 GB/s on the box, tools/h2d_bench.py), or unpadded rows by a copy "
+                         "kernel reading pinned host memory (54 GB/s)")
+    ap.add_argument("--h2d-kernel-wgs", type=int, default=48,
+                    help="workgroups of the --h2d-mode kernel copy (48: 80%% of the link peak in the pipeline, "
+                         "16 / 32 / 64 / 96: 41 / 69 / 75 / 66%%)")
+    ap.add_argument("--no-h2d-priority", dest="h2d_priority", action="store_false",
+                    help="host-streamed leg: upload streams at normal priority (default high: the copy kernel's "
+                         "workgroups are dispatched ahead of the extraction's)")
+    ap.add_argument("--h2d-split", type=int, default=1,
                     help="host-streamed leg: the batch upload in this many parts, each on a copy stream of its own "
                          "(a multiple of the extraction halves; an extraction half waits for its own parts only)")
     ap.add_argument("--spawn", action="store_true", help="use the worker launcher even for --gpus 1")
@@ -421,12 +427,13 @@ class MonoPipeline:
             self.h_counts = [HA(B, np.int32) for _ in range(NS)]
             self.h_m12 = [HA(B * cap, np.int32) for _ in range(NS)]
             self.h_nm = [HA(B, np.int32) for _ in range(NS)]
-            self.s_h2d, self.s_d2h = _lib.Stream(), _lib.Stream()
+            hp = 1 if args.h2d_priority else None
+            self.s_h2d, self.s_d2h = _lib.Stream(hp), _lib.Stream()
             # --h2d-split N: the upload in N parts on N copy streams (half h waits for its own parts)
             nparts = args.h2d_split if not args.serial else 1
             if nparts < 1 or (nparts > 1 and (nparts % S or B % nparts)):
                 raise SystemExit(f"bench.py: --h2d-split {nparts} must divide the batch and be a multiple of --split")
-            self.s_h2ds = [self.s_h2d] + [_lib.Stream() for _ in range(nparts - 1)]
+            self.s_h2ds = [self.s_h2d] + [_lib.Stream(hp) for _ in range(nparts - 1)]
         prio = 1 if args.priority else None
         self.s_exts = [_lib.Stream(prio) for _ in range(S)]
         self.s_ext = self.s_exts[0]
@@ -914,7 +921,7 @@ def host_stream_leg(args, cfg, local, frames):
     copy stream). PCIe-inclusive throughput; never `value`."""
     link = link_peak(cfg, args.batch)
     pipe = MonoPipeline(args, cfg, local, frames, host=True, need_events=False)
-    wall, _ = pipe.run(min(args.warmup, 10), args.host_steps, None)
+    wall, issue = pipe.run(min(args.warmup, 10), args.host_steps, None)
     pipe.check_status()
     B, cap = pipe.B, pipe.cap
     h2d = B * pipe.h_fbytes
@@ -926,6 +933,8 @@ def host_stream_leg(args, cfg, local, frames):
             "h2d_gb_per_s": round(h2d_rate, 2), "link": link,
             "h2d_frac_of_link_peak": round(h2d_rate / link["h2d_peak_GBps"], 3) if link.get("h2d_peak_GBps") else None,
             "h2d_mode": args.h2d_mode, "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
+            "host_issue_ms_per_step": round(issue / args.host_steps * 1e3, 4),
+            "h2d_streams": len(pipe.s_h2ds), "h2d_priority": bool(args.h2d_priority),
             "what": f"pool of {len(frames)} frames in pinned host memory, batch uploaded per step, "
                     "keypoints + descriptors + counts" + ("" if args.no_match else " + matches") + " read back"}
 

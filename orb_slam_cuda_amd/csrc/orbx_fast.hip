@@ -141,77 +141,6 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
   return n1;
 }
 
-// (a) with 8 horizontally adjacent band pixels per lane (G = ceil(bw / 8)
-// lanes per band row, 64 / G rows per pass): half as many passes, each lane's
-// centre run read as 5 dwords and its up / down runs as 3 (11 dword reads per
-// 8 pixels against 16), the same per-pixel network and ordered compaction.
-template <int S, int OX>
-__device__ __forceinline__ int compass8(const LDSP uint8_t* roi, LDSP uint16_t* list, int bw, int bh, int t,
-                                        int lane) {
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-  constexpr int kC = OX + 3, kN4 = OX + 6, kN12 = OX;
-  constexpr int kCW = ((kN4 + 7) >> 2) + 1;           // centre dwords: bytes OX .. OX + 13
-  constexpr int kUW = ((kC + 7) >> 2) - (kC >> 2) + 1;  // up / down dwords: bytes kC .. kC + 7
-  const int G = (bw + 7) >> 3, RP = 64 / G;
-  const int r = lane / G, g = lane - r * G, x = 8 * g;
-  const bool lane_ok = r < RP;
-  uint64_t colm[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) colm[j] = __ballot(lane_ok && x + j < bw);
-  const u16x2 tt = {(unsigned short)t, (unsigned short)t};
-  int n1 = 0;
-  for (int by0 = 0; by0 < bh; by0 += RP) {
-    const int by = by0 + r;
-    const uint64_t rowm = __ballot(by < bh);
-    const LDSP uint32_t* rc = (const LDSP uint32_t*)(roi + u24mul(min(by, bh - 1) + 3, S)) + 2 * g;
-    const LDSP uint32_t* ru = rc - 3 * S / 4;  // 3 rows up: ring pixel 8
-    const LDSP uint32_t* rd = rc + 3 * S / 4;  // 3 rows down: ring pixel 0
-    uint32_t dc[kCW], du[kUW], dd[kUW];
-#pragma unroll
-    for (int k = 0; k < kCW; ++k) dc[k] = rc[k];
-#pragma unroll
-    for (int k = 0; k < kUW; ++k) {
-      du[k] = ru[(kC >> 2) + k];
-      dd[k] = rd[(kC >> 2) + k];
-    }
-    uint64_t m[8];
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {  // pixels 4q + h and 4q + h + 2
-        auto pair = [h](const uint32_t* d, int o) -> u16x2 {
-          const int b = (o & 3) + h;
-          const uint32_t sel = (uint32_t)b | 0x0C00u | ((uint32_t)(b + 2) << 16) | 0x0C000000u;
-          return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(d[(o >> 2) + 1], d[o >> 2], sel));
-        };
-        const u16x2 v = pair(dc, kC + 4 * q);
-        const u16x2 a0 = pair(dd, (kC & 3) + 4 * q), a4 = pair(dc, kN4 + 4 * q);
-        const u16x2 a8 = pair(du, (kC & 3) + 4 * q), a12 = pair(dc, kN12 + 4 * q);
-        const u16x2 s1 = __builtin_elementwise_min(a0, a4), l1 = __builtin_elementwise_max(a0, a4);
-        const u16x2 s2 = __builtin_elementwise_min(a8, a12), l2 = __builtin_elementwise_max(a8, a12);
-        const u16x2 a = __builtin_elementwise_max(s1, s2), b = __builtin_elementwise_min(l1, l2);
-        const u16x2 dk = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(v, tt), __builtin_elementwise_min(a, b));
-        const u16x2 br = __builtin_elementwise_sub_sat(__builtin_elementwise_max(a, b), v + tt);
-        const u16x2 any = dk | br;
-        m[4 * q + h] = __ballot(any.x != 0) & colm[4 * q + h] & rowm;
-        m[4 * q + h + 2] = __ballot(any.y != 0) & colm[4 * q + h + 2] & rowm;
-      }
-    int pos = n1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pos += mbcnt64(m[j]);
-    const uint16_t e = (uint16_t)((by << 8) | x);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (__builtin_amdgcn_inverse_ballot_w64(m[j])) list[pos++] = (uint16_t)(e + j);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) n1 += __popcll(m[j]);
-  }
-  return n1;
-}
-
-#ifndef ORBX_FAST_C8
-#define ORBX_FAST_C8 0  // 8 pixels per lane in the compass pass (A/B)
-#endif
 #ifndef ORBX_FAST_PK
 #define ORBX_FAST_PK 1  // packed-u16 compass pre-test (0: the scalar form, for A/B)
 #endif
@@ -352,21 +281,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   // (a) compass pre-test over all band pixels, row-major ordered compaction
   int n1 = 0;
   if constexpr (kTight) {
-#if ORBX_FAST_C8
-    switch (ox) {
-      case 0: n1 = compass8<kRoiStride, 0>(roi, list, bw, bh, t, lane); break;
-      case 1: n1 = compass8<kRoiStride, 1>(roi, list, bw, bh, t, lane); break;
-      case 2: n1 = compass8<kRoiStride, 2>(roi, list, bw, bh, t, lane); break;
-      default: n1 = compass8<kRoiStride, 3>(roi, list, bw, bh, t, lane); break;
-    }
-#else
     switch (ox) {
       case 0: n1 = compass4<kRoiStride, 0>(roi, list, bw, bh, t, lane); break;
       case 1: n1 = compass4<kRoiStride, 1>(roi, list, bw, bh, t, lane); break;
       case 2: n1 = compass4<kRoiStride, 2>(roi, list, bw, bh, t, lane); break;
       default: n1 = compass4<kRoiStride, 3>(roi, list, bw, bh, t, lane); break;
     }
-#endif
 #ifdef ORBX_FAST_LCAP
     n1 = min(n1, ORBX_FAST_LCAP);
 #endif

@@ -33,20 +33,22 @@
 //      queries listed in index order. A window's cell columns are one
 //      contiguous run of records, its cell rows a test.
 //   2. search_init_query_kernel (8 lanes per query, several workgroups per
-//      pair): each query's candidate count and its 4 smallest keys over its
+//      pair): each query's candidate count and its 8 smallest keys over its
 //      window's records. There are no candidate lists, so nothing can
 //      overflow.
 //   3. search_init_resolve_kernel (a workgroup per pair): Jacobi rounds, every
 //      query re-deciding from the previous round's accepted outcomes (per-o2
-//      claim lists) by walking its 4 keys; a query whose keys run out (fewer
-//      than 2 unblocked of 4, more than 4 candidates) is rescanned by a whole
+//      claim lists) by walking its 8 keys; a query whose keys run out (fewer
+//      than 2 unblocked of 8, more than 8 candidates) is rescanned by a whole
 //      wave over its window. A round without change is the fixed point; past
 //      kInitMaxRounds one wave runs the sequential greedy. Then the latest
 //      acceptor keeps each i2, rotation consistency (ComputeThreeMaxima), the
 //      outputs and the vbPrevMatched update.
 #include <algorithm>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "orbx_device.cuh"
 #include "orbx_wave.cuh"
@@ -57,11 +59,12 @@ constexpr int kInitGridCols = 64, kInitGridRows = 48;  // FRAME_GRID_COLS / ROWS
 constexpr int kInitHisto = 30;                         // HISTO_LENGTH
 constexpr int kInitThLow = 50;                         // TH_LOW
 constexpr int kInitMaxRounds = 48;
-constexpr int kInitK = 4;       // smallest keys kept per query
+constexpr int kInitK = 8;       // smallest keys kept per query (a rescan when fewer than 2 of them are unblocked)
 constexpr int kInitQLanes = 8;  // lanes per query in the key pass (a DPP half-row)
-constexpr int kInitPrepThreads = 256;
+constexpr int kInitPrepThreads = 1024;
 constexpr int kInitQueryThreads = 256;
 constexpr int kInitResolveThreads = 512;
+constexpr int kInitKeyRegs = 2;  // queries per resolve thread whose keys are held in registers
 constexpr uint32_t kKeyNone = 0xFFFFFFFFu;
 
 #define LDSP __attribute__((address_space(3)))
@@ -69,7 +72,7 @@ constexpr uint32_t kKeyNone = 0xFFFFFFFFu;
 // Per-pair workspace, ints: [0..64] column starts (64 = records in the grid),
 // [66] queries, [67] octave-0 F2 keypoints; then, for K = kp_pitch: records
 // (4K: x, y, key base, cell row), descriptors (8K), o2 -> i2 (K), query -> i1
-// (K), keys (4K), candidate counts (K).
+// (K), keys (kInitK K), candidate counts (K).
 struct InitWs {
   int* hdr;
   uint4* rec;
@@ -92,13 +95,13 @@ __device__ __forceinline__ InitWs init_ws(int* base, int K) {
   w.qi = p;
   p += K;
   w.keys = (uint4*)p;
-  p += 4 * (size_t)K;
+  p += (size_t)kInitK * K;
   w.qcnt = p;
   return w;
 }
 
 size_t init_ws_bytes_per_pair(int kp_pitch) {
-  return ((68 + (size_t)kp_pitch * (4 + 8 + 1 + 1 + 4 + 1)) * 4 + 255) & ~(size_t)255;
+  return ((68 + (size_t)kp_pitch * (4 + 8 + 1 + 1 + kInitK + 1)) * 4 + 255) & ~(size_t)255;
 }
 
 // Frame::PosInGrid: round() of a float, half away from zero
@@ -245,32 +248,36 @@ __global__ __launch_bounds__(kInitPrepThreads) void search_init_prep_kernel(
 }
 
 // ---------------------------------------------------------------- 2. keys
-// sorted insertion of k into the ascending 4-list t
-__device__ __forceinline__ void top4_insert(uint32_t (&t)[4], uint32_t k) {
+// sorted insertion of k into the ascending kInitK-list t
+__device__ __forceinline__ void topk_insert(uint32_t (&t)[kInitK], uint32_t k) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < kInitK; ++j) {
     const uint32_t lo = min(t[j], k);
     k = max(t[j], k);
     t[j] = lo;
   }
 }
-// the 4 smallest of two ascending 4-lists, ascending (bitonic merge)
-__device__ __forceinline__ void top4_merge(uint32_t (&t)[4], const uint32_t (&o)[4]) {
-  uint32_t c[4];
+// the kInitK smallest of two ascending lists, ascending: the elementwise
+// minimum against the reversed other list is bitonic, then a bitonic sort
+__device__ __forceinline__ void topk_merge(uint32_t (&t)[kInitK], const uint32_t (&o)[kInitK]) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) c[j] = min(t[j], o[3 - j]);
-  const uint32_t a = min(c[0], c[2]), b = max(c[0], c[2]), e = min(c[1], c[3]), f = max(c[1], c[3]);
-  t[0] = min(a, e);
-  t[1] = max(a, e);
-  t[2] = min(b, f);
-  t[3] = max(b, f);
+  for (int j = 0; j < kInitK; ++j) t[j] = min(t[j], o[kInitK - 1 - j]);
+#pragma unroll
+  for (int d = kInitK / 2; d >= 1; d >>= 1)
+#pragma unroll
+    for (int j = 0; j < kInitK; ++j)
+      if ((j & d) == 0) {
+        const uint32_t lo = min(t[j], t[j + d]), hi = max(t[j], t[j + d]);
+        t[j] = lo;
+        t[j + d] = hi;
+      }
 }
 template <int CTRL>
-__device__ __forceinline__ void top4_merge_dpp(uint32_t (&t)[4]) {
-  uint32_t o[4];
+__device__ __forceinline__ void topk_merge_dpp(uint32_t (&t)[kInitK]) {
+  uint32_t o[kInitK];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = (uint32_t)dpp_i<CTRL>(0, (int)t[j]);
-  top4_merge(t, o);
+  for (int j = 0; j < kInitK; ++j) o[j] = (uint32_t)dpp_i<CTRL>(0, (int)t[j]);
+  topk_merge(t, o);
 }
 
 __global__ __launch_bounds__(kInitQueryThreads) void search_init_query_kernel(
@@ -286,7 +293,9 @@ __global__ __launch_bounds__(kInitQueryThreads) void search_init_query_kernel(
   constexpr int kQPerWg = kInitQueryThreads / kInitQLanes;
   for (int qb = blockIdx.x * kQPerWg; qb < nq; qb += gridDim.x * kQPerWg) {
     const int q = qb + tid / kInitQLanes;
-    uint32_t t[4] = {kKeyNone, kKeyNone, kKeyNone, kKeyNone};
+    uint32_t t[kInitK];
+#pragma unroll
+    for (int j = 0; j < kInitK; ++j) t[j] = kKeyNone;
     int cnt = 0;
     int cx0, cx1, cy0, cy1;
     float x = 0.f, y = 0.f;
@@ -299,32 +308,59 @@ __global__ __launch_bounds__(kInitQueryThreads) void search_init_query_kernel(
       const int s1 = w.hdr[cx1 + 1];
       const uint4* qd = (const uint4*)(desc1 + (size_t)i1 * 32);
       const uint4 a0 = qd[0], a1 = qd[1];
-      for (int s = w.hdr[cx0] + l; s < s1; s += kInitQLanes) {
-        const uint4 rc = w.rec[s];
+      // two records per lane and step, both loads issued before either is used
+      for (int s = w.hdr[cx0] + l; s < s1; s += 2 * kInitQLanes) {
+        const int s2 = min(s + kInitQLanes, s1 - 1);
+        const uint4 rc = w.rec[s], rc2 = w.rec[s2];
         const uint4 b0 = w.desc[2 * s], b1 = w.desc[2 * s + 1];
+        const uint4 c0 = w.desc[2 * s2], c1 = w.desc[2 * s2 + 1];
         if (init_in_window(rc, x, y, cy0, cy1, P.r)) {
           const uint32_t d = (uint32_t)min(init_hamming(a0, a1, b0, b1), P.dclamp);
-          top4_insert(t, d << P.dshift | rc.z);
+          topk_insert(t, d << P.dshift | rc.z);
+          ++cnt;
+        }
+        if (s + kInitQLanes < s1 && init_in_window(rc2, x, y, cy0, cy1, P.r)) {
+          const uint32_t d = (uint32_t)min(init_hamming(a0, a1, c0, c1), P.dclamp);
+          topk_insert(t, d << P.dshift | rc2.z);
           ++cnt;
         }
       }
     }
     // the query's 8 lanes merge their lists (quad_perm 1032, 2301, then the
     // other quad of the half-row by row_half_mirror) and sum their counts
-    top4_merge_dpp<kDppQuad1032>(t);
-    top4_merge_dpp<kDppQuad2301>(t);
-    top4_merge_dpp<kDppHalfMirror>(t);
+    topk_merge_dpp<kDppQuad1032>(t);
+    topk_merge_dpp<kDppQuad2301>(t);
+    topk_merge_dpp<kDppHalfMirror>(t);
     cnt += dpp_i<kDppQuad1032>(0, cnt);
     cnt += dpp_i<kDppQuad2301>(0, cnt);
     cnt += dpp_i<kDppHalfMirror>(0, cnt);
-    if (q < nq && l == 0) {
-      w.keys[q] = make_uint4(t[0], t[1], t[2], t[3]);
-      w.qcnt[q] = cnt;
+    if (q < nq && l < kInitK / 4) {  // the first kInitK / 4 lanes store a uint4 each
+      uint32_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = t[j];
+#pragma unroll
+        for (int u = 1; u < kInitK / 4; ++u)
+          if (l == u) v[j] = t[4 * u + j];
+      }
+      w.keys[(size_t)q * (kInitK / 4) + l] = make_uint4(v[0], v[1], v[2], v[3]);
+      if (l == 0) w.qcnt[q] = cnt;
     }
   }
 }
 
 // ---------------------------------------------------------------- 3. resolve
+__device__ __forceinline__ void load_keys(const InitWs& w, int q, uint32_t (&key)[kInitK]) {
+#pragma unroll
+  for (int u = 0; u < kInitK / 4; ++u) {
+    const uint4 kk = w.keys[(size_t)q * (kInitK / 4) + u];
+    key[4 * u] = kk.x;
+    key[4 * u + 1] = kk.y;
+    key[4 * u + 2] = kk.z;
+    key[4 * u + 3] = kk.w;
+  }
+}
+
 // vMatchedDistance[o2] at query q's turn: the smallest distance of an earlier
 // query's claim on o2 in the snapshot (INT_MAX if none)
 __device__ __forceinline__ int init_claim_md(const LDSP int* head, const LDSP int* nxt, int o2, int q) {
@@ -403,6 +439,10 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
   // claimer of the snapshot; later vMatchedDistance / the keeper), nxt[K] (per
   // query: (next claimer + 1) << 9 | its distance; later the rotHist entry),
   // queue[K] (rescans; later vnMatches21), var[32], hist[32]
+  const long long t0 = P.prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  auto stamp = [&](int k) {
+    if (P.prof && tid == 0) P.prof[pr * 16 + k] = (long long)__builtin_amdgcn_s_memtime() - t0;
+  };
   LDSP int* res = (LDSP int*)smem;
   LDSP int* head = res + K;
   LDSP int* nxt = head + K;
@@ -415,15 +455,27 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
   }
   for (int i = tid; i < nq; i += NT) res[i] = -1;
   for (int i = tid; i < n0; i += NT) head[i] = -1;
+  // the keys of this thread's first queries stay in registers over the rounds
+  uint32_t kreg[kInitKeyRegs][kInitK];
+  int creg[kInitKeyRegs];
+#pragma unroll
+  for (int j = 0; j < kInitKeyRegs; ++j) {
+    const int q = min(tid + j * NT, max(nq - 1, 0));
+    load_keys(w, q, kreg[j]);
+    creg[j] = w.qcnt[q];
+  }
   __syncthreads();
   if (tid == 0) var[6] = 1;  // changed
   __syncthreads();
+  stamp(1);
   bool converged = false;
+  int rounds = 0;
   for (int round = 0; round < kInitMaxRounds; ++round) {
     if (var[6] == 0) {
       converged = true;
       break;
     }
+    ++rounds;
     __syncthreads();
     if (tid == 0) {
       var[6] = 0;
@@ -431,9 +483,17 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
     }
     __syncthreads();
     int changed = 0;
-    for (int q = tid; q < nq; q += NT) {
-      const uint4 kk = w.keys[q];
-      const uint32_t key[4] = {kk.x, kk.y, kk.z, kk.w};
+    for (int q = tid, j = 0; q < nq; q += NT, ++j) {
+      uint32_t key[kInitK];
+      int qc;
+      if (j < kInitKeyRegs) {
+#pragma unroll
+        for (int u = 0; u < kInitK; ++u) key[u] = kreg[j][u];
+        qc = creg[j];
+      } else {
+        load_keys(w, q, key);
+        qc = w.qcnt[q];
+      }
       uint32_t k1 = kKeyNone, k2 = kKeyNone;
       int found = 0;
 #pragma unroll
@@ -445,7 +505,7 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
         else k2 = key[j];
         ++found;
       }
-      if (found < 2 && w.qcnt[q] > kInitK) {
+      if (found < 2 && qc > kInitK) {
         queue[lds_atomic_add(&var[7], 1)] = q;  // keys ran out: a wave rescans the window
         continue;
       }
@@ -457,6 +517,7 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
     }
     __syncthreads();
     const int nrs = var[7];
+    if (P.prof && tid == 0) P.prof[pr * 16 + 9] += nrs;
     for (int j = wv; j < nrs; j += NT / 64) {
       const int q = queue[j];
       const int r = init_rescan_wave(P, w, kp1, desc1, prev, q,
@@ -479,6 +540,8 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
     }
     __syncthreads();
   }
+  stamp(2);
+  if (P.prof && tid == 0) P.prof[pr * 16 + 8] = rounds + (converged ? 0 : 1000);
   LDSP int* src = nxt;  // per query: the o2 its acceptance entered into rotHist, then its bin
   if (converged) {
     // the latest accepting query keeps each o2 (earlier ones were stolen
@@ -518,8 +581,8 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
     if (wv == 0) {
       int nm = 0;
       for (int q = 0; q < nq; ++q) {
-        const uint4 kk = w.keys[q];
-        const uint32_t key[4] = {kk.x, kk.y, kk.z, kk.w};
+        uint32_t key[kInitK];
+        load_keys(w, q, key);
         uint32_t k1 = kKeyNone, k2 = kKeyNone;
         int found = 0;
         for (int j = 0; j < kInitK && found < 2; ++j) {
@@ -554,6 +617,7 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
     }
     __syncthreads();
   }
+  stamp(3);
   // Rotation consistency (:473-512, ComputeThreeMaxima :1601-1642)
   const float factor = 1.0f / kInitHisto;
   if (P.check_ori) {
@@ -624,6 +688,7 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
     }
   }
   if (tid == 0) nmatches[pr] = var[0];
+  stamp(4);
 }
 
 static size_t init_resolve_lds_bytes(int kp_pitch) { return (size_t)kp_pitch * 16 + 256; }
@@ -655,8 +720,29 @@ int launch_search_init(const InitParams& P0, const orbx_kp* kp1, const uint8_t* 
                      prev, ws);
   const size_t lds = init_resolve_lds_bytes(P.kp_pitch);
   if (raise_lds_limit((const void*)search_init_resolve_kernel, lds)) return ORBX_EDEVICE;
+  // ORBX_INIT_PROF=1 (diagnostics): the resolve kernel's phase clocks, averaged
+  // over the pairs and printed after the call (synchronises)
+  static long long* prof = nullptr;
+  static const bool do_prof = getenv("ORBX_INIT_PROF") && getenv("ORBX_INIT_PROF")[0] == '1';
+  if (do_prof) {
+    if (pairs > 4096) return ORBX_EINVAL;
+    if (!prof && hipMalloc(&prof, (size_t)4096 * 16 * 8) != hipSuccess) return ORBX_EDEVICE;
+    if (hipMemsetAsync(prof, 0, (size_t)pairs * 16 * 8, s) != hipSuccess) return ORBX_EDEVICE;
+    P.prof = prof;
+  }
   hipLaunchKernelGGL(search_init_resolve_kernel, dim3(pairs), dim3(kInitResolveThreads), lds, s, P, kp1, desc1, kp2,
                      prev, ws, matches12, nmatches);
+  if (do_prof) {
+    std::vector<long long> h((size_t)pairs * 16);
+    if (hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(h.data(), prof, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+      return ORBX_EDEVICE;
+    double a[16] = {0};
+    for (int q = 0; q < pairs; ++q)
+      for (int k = 0; k < 16; ++k) a[k] += (double)h[q * 16 + k] / pairs;
+    fprintf(stderr, "search_init resolve (avg clocks from start): keys %.0f rounds %.0f keep %.0f rotation+out %.0f | "
+            "rounds %.2f rescans %.2f\n", a[1], a[2], a[3], a[4], a[8], a[9]);
+  }
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 

@@ -181,6 +181,7 @@ struct InitParams {
   long long ws_ints;  // per-pair workspace stride in ints (set by the launcher)
   int dshift, obits, dclamp;  // key layout (set by the launcher from nnratio)
   uint32_t omask;
+  long long* prof;  // diagnostics (ORBX_INIT_PROF=1): resolve-kernel phase clocks per pair, or null
 };
 constexpr size_t kInitLdsBudget = 160 * 1024 - 512;
 size_t init_ws_bytes_per_pair(int kp_pitch);

@@ -1,0 +1,13 @@
+#!/bin/bash
+set -e
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/host2; mkdir -p $O
+run() {  # name, args
+  n=$1; shift
+  timeout -k 10 150 python3 bench.py --steps 5 --warmup 2 --cpu-sample 0 --no-latency --host-steps 60 "$@" > $O/$n.log 2>&1 || { echo "$n failed"; tail -5 $O/$n.log; return 1; }
+  python3 -c "import json;d=json.loads(open('$O/$n.log').read().strip().splitlines()[-1]);h=d['host_stream'];print('$n',h['value'],h['h2d_gb_per_s'],h.get('h2d_frac_of_link_peak'),h['link']['h2d_peak_GBps'],'issue',h['host_issue_ms_per_step'],'ms',h['ms_per_step'])"
+}
+for rep in 1 2; do
+for w in 16 32 48 64 96; do run k${w}_$rep --h2d-mode kernel --h2d-priority --h2d-split 1 --h2d-kernel-wgs $w; done
+run dma_$rep --h2d-priority --h2d-split 1
+done

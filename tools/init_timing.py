@@ -1,6 +1,6 @@
 """Times orbm_search_for_initialization_batch (and orbm_hamming_top2) alone on a
 resident batch of 64 (t, t-1) pairs of extracted frames (tuning aid; per-kernel
-times: run it under rocprofv3 --kernel-trace --stats).
+times: run it under rocprofv3 --kernel-trace --stats)."""
 import ctypes as C
 import os
 import sys
