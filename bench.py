@@ -196,7 +196,7 @@ def parse_args(argv=None):
 
 # ORBX_* variables the library reads (INTEGRATION.md "Environment variables").
 # Tuning: select among bit-exact code paths; allowed, and stamped into the line.
-ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_PYR_PLAN", "ORBX_QT_GENERIC",
+ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_EXTRACT_ORDER", "ORBX_PYR_PLAN", "ORBX_QT_GENERIC",
               "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS",
               "ORBX_BOW_ROUNDS",
               # the C++ shim's configuration (shim/src/ORBextractor.cc); bench.py does not read them

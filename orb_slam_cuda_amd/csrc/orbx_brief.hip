@@ -37,6 +37,7 @@ __constant__ float4 c_brief_tests[2][256];
 #endif
 constexpr int kObThreads = ORBX_OB_THREADS;  // 256: 4 waves, 8 keypoints
 constexpr int kObKps = kObThreads / 32;
+static_assert(kObKps == kKpGroup, "a workgroup's keypoints must lie in one level's slot range");
 constexpr int kObRadius = 19;                // |rotated pattern offset| <= 18.4, rounded
 constexpr int kObRows = 2 * kObRadius + 1;   // 39
 // staged row stride: the 4 x 16-byte chunks of a row, padded so that the
@@ -105,41 +106,30 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
 #pragma unroll
   for (int k = 0; k < kIcPer; ++k) ic_v[k] = c_ic_coef[min(tid + k * kObThreads, 16 * 24 - 1)];
 
-  // levels of the wave's two half-wave slots, in scalar code: the slots are
-  // uniform per half (slot = bx * kObKps + 2 * wave + half)
-  const int slotA = bx * kObKps + 2 * __builtin_amdgcn_readfirstlane(tid >> 6), slotB = slotA + 1;
-  int lA = 0, lB = 0;
+  // the workgroup's level, in scalar code: level slot ranges start at
+  // multiples of kKpGroup (= kObKps) slots, so all of a workgroup's keypoints
+  // share one level
+  const int slot0 = bx * kObKps;
+  int l = 0;
 #pragma unroll
-  for (int i = 1; i < kLv; ++i) {
-    if (i < P.L && slotA >= P.lv[i].kbase) lA = i;
-    if (i < P.L && slotB >= P.lv[i].kbase) lB = i;
-  }
-  const bool hiHalf = (tid & 32) != 0;
-  const int l = hiHalf ? lB : lA;
-  const LevelGeom& gA = P.lv[lA];
-  const LevelGeom& gB = P.lv[lB];
-#define OB_PICK(a, b) (hiHalf ? (b) : (a))
-  const int g_kbase = OB_PICK(gA.kbase, gB.kbase), g_minBX = OB_PICK(gA.minBX, gB.minBX),
-            g_minBY = OB_PICK(gA.minBY, gB.minBY), g_w = OB_PICK(gA.w, gB.w), g_h = OB_PICK(gA.h, gB.h),
-            g_pitch = OB_PICK(gA.pitch, gB.pitch);
-  const long long g_off = OB_PICK(gA.off, gB.off), g_plane = OB_PICK(gA.plane, gB.plane);
-  const float g_scale = OB_PICK(gA.scale, gB.scale), g_size = OB_PICK(gA.size, gB.size);
-  const int lpitch = OB_PICK(lp.pitch[lA], lp.pitch[lB]);
-  const uint8_t* lbase = OB_PICK(lp.base[lA], lp.base[lB]);
-  const long long lfstride = OB_PICK(lp.fstride[lA], lp.fstride[lB]);
-#undef OB_PICK
-  // keypoints of the levels before each half's level, its own count, the total (scalar)
-  int cntA = 0, cntB = 0, beforeA = 0, beforeB = 0, tot = 0;
+  for (int i = 1; i < kLv; ++i)
+    if (i < P.L && slot0 >= P.lv[i].kbase) l = i;
+  const LevelGeom& g = P.lv[l];
+  const int g_kbase = g.kbase, g_minBX = g.minBX, g_minBY = g.minBY, g_w = g.w, g_h = g.h, g_pitch = g.pitch;
+  const long long g_off = g.off, g_plane = g.plane;
+  const float g_scale = g.scale, g_size = g.size;
+  const int lpitch = lp.pitch[l];
+  const uint8_t* lbase = lp.base[l];
+  const long long lfstride = lp.fstride[l];
+  // keypoints of the levels before l, its own count, the frame's total (scalar)
+  int cnt_l = 0, before = 0, tot = 0;
 #pragma unroll
   for (int i = 0; i < kLv; ++i) {
     const int ci = i < P.L ? c[i] : 0;
-    if (i == lA) cntA = ci;
-    if (i == lB) cntB = ci;
-    if (i < lA) beforeA += ci;
-    if (i < lB) beforeB += ci;
+    if (i == l) cnt_l = ci;
+    if (i < l) before += ci;
     tot += ci;
   }
-  const int cnt_l = hiHalf ? cntB : cntA, before = hiHalf ? beforeB : beforeA;
   if (bx == 0 && tid == 0) out_counts[f] = tot;
 
   // ---- the keypoint of this half-wave

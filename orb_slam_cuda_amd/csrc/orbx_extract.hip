@@ -8,6 +8,9 @@
 //   launch_orient_brief  (1)  IC_Angle + rBRIEF + scale/assemble    orbx_brief.hip
 // Optional events (caller-owned or the handle's ORBX_TIMING ones) bracket
 // every stage on the launch stream (ev[i], ev[i+1] around stage i).
+#include <cstdlib>
+#include <cstring>
+
 #include "orbx_device.cuh"
 
 namespace orbx {
@@ -32,18 +35,30 @@ int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_
   auto rec = [&](int i) {
     if (ev) (void)hipEventRecord((hipEvent_t)ev[i], stream);
   };
+  // stage order (A/B, ORBX_EXTRACT_ORDER): p pyramid, b blur, f FAST, q
+  // quadtree, o orient+BRIEF; the pyramid first, FAST before the quadtree and
+  // both the blur and the quadtree before orient+BRIEF. Event i+1 closes the
+  // i-th stage launched, so with another order the stage events follow it.
+  static const char* order = [] {
+    const char* e = getenv("ORBX_EXTRACT_ORDER");
+    if (!e || strlen(e) != 5 || e[0] != 'p' || e[4] != 'o' || !strchr(e, 'b') || !strchr(e, 'f') ||
+        !strchr(e, 'q') || strchr(e, 'q') < strchr(e, 'f'))
+      return "pbfqo";
+    return e;
+  }();
   int rc;
   rec(0);
-  if ((rc = launch_pyramid(Q, lp, X.rtab, batch, stream))) return rc;
-  rec(1);
-  if ((rc = launch_blur(Q, lp, X.blur, batch, stream))) return rc;
-  rec(2);
-  if ((rc = launch_fast(Q, lp, X.cells, X.slots, X.cell_counts, batch, stream))) return rc;
-  rec(3);
-  if ((rc = launch_quadtree(Q, X, batch, stream))) return rc;
-  rec(4);
-  if ((rc = launch_orient_brief(Q, lp, X, d_kps, d_desc, d_counts, batch, stream))) return rc;
-  rec(5);
+  for (int i = 0; i < 5; ++i) {
+    switch (order[i]) {
+      case 'p': rc = launch_pyramid(Q, lp, X.rtab, batch, stream); break;
+      case 'b': rc = launch_blur(Q, lp, X.blur, batch, stream); break;
+      case 'f': rc = launch_fast(Q, lp, X.cells, X.slots, X.cell_counts, batch, stream); break;
+      case 'q': rc = launch_quadtree(Q, X, batch, stream); break;
+      default: rc = launch_orient_brief(Q, lp, X, d_kps, d_desc, d_counts, batch, stream); break;
+    }
+    if (rc) return rc;
+    rec(i + 1);
+  }
   return ORBX_OK;
 }
 

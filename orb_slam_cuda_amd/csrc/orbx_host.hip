@@ -397,7 +397,9 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     g.hX = static_cast<float>(g.boxW) / g.nIni;
     g.kcap = std::max(g.N + 3, g.nIni);
     g.kbase = kbase;
-    kbase += g.kcap;
+    // levels start at multiples of kKpGroup slots, so an orient+BRIEF
+    // workgroup's keypoints all sit in one level
+    kbase += (g.kcap + kKpGroup - 1) / kKpGroup * kKpGroup;
     maxnodes = std::max(maxnodes, g.kcap + 4);
     g.scale = h->scale[l];
     g.size = (float)(int)(kPatchSize * h->scale[l]);

@@ -51,6 +51,10 @@ struct LevelGeom {
   int xtab2;             // band pyramid column table: {sx, a0 | a1 << 16}, replicate folded in
 };
 
+// keypoint slots per orient+BRIEF workgroup; every level's slot range starts
+// at a multiple of it (orbx_host.hip plan)
+constexpr int kKpGroup = 8;
+
 struct CellGeom {
   int16_t c0, r0, c1, r1;  // ROI [c0,c1) x [r0,r1) in level coordinates
   int slot_off;            // first key slot (frame-relative)
