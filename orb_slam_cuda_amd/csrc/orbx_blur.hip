@@ -8,7 +8,9 @@
 namespace orbx {
 
 // Separable 7-tap fixed-point Gaussian, BORDER_REFLECT_101 at the level edges.
-// Tile = 128 x 64 outputs per 256-thread block (64 rows: 1.1x halo rows instead of 1.2x; measured best of 16..80). The input tile (+3 halo, 16-B
+// Tile = 128 x 48 outputs per 256-thread block (alone 64 rows was best of
+// 16..80, 1.1x halo rows; in the pipelined step 48 rows, 22.5 instead of 29 KB
+// of LDS, gave +0.5-1 % over six interleaved pairs). The input tile (+3 halo, 16-B
 // aligned: columns [x0-16, x0+144)) is staged with 16-byte loads (byte loads
 // with reflection only where a chunk leaves the image).
 //   row pass:    v_dot4_u32_u8 of a pixel dword with a tap dword: 10 dot4 per
@@ -17,7 +19,7 @@ namespace orbx {
 //   column pass: v_dot2_u32_u16 of such a row pair with a tap pair: 4 dot2
 //                per output, then (acc + 2^15) >> 16.
 #ifndef ORBX_BLUR_TH
-#define ORBX_BLUR_TH 64
+#define ORBX_BLUR_TH 48
 #endif
 #ifndef ORBX_BLUR_TW
 #define ORBX_BLUR_TW 128

@@ -61,9 +61,15 @@ constexpr int kInitThLow = 50;                         // TH_LOW
 constexpr int kInitMaxRounds = 48;
 constexpr int kInitK = 8;       // smallest keys kept per query (a rescan when fewer than 2 of them are unblocked)
 constexpr int kInitQLanes = 8;  // lanes per query in the key pass (a DPP half-row)
-constexpr int kInitPrepThreads = 1024;
+#ifndef ORBX_INIT_PREP_THREADS
+#define ORBX_INIT_PREP_THREADS 1024
+#endif
+#ifndef ORBX_INIT_RESOLVE_THREADS
+#define ORBX_INIT_RESOLVE_THREADS 512
+#endif
+constexpr int kInitPrepThreads = ORBX_INIT_PREP_THREADS;
 constexpr int kInitQueryThreads = 256;
-constexpr int kInitResolveThreads = 512;
+constexpr int kInitResolveThreads = ORBX_INIT_RESOLVE_THREADS;
 constexpr int kInitKeyRegs = 2;  // queries per resolve thread whose keys are held in registers
 constexpr uint32_t kKeyNone = 0xFFFFFFFFu;
 
