@@ -30,6 +30,9 @@ typedef short i16x2 __attribute__((ext_vector_type(2)));
 //   b0 = min(-a0, v - max over arcs of (min of p)),  score = -b0 - 1
 // (no per-pixel d = v - p subtractions).
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+#ifndef ORBX_FAST_ARCPAIR
+#define ORBX_FAST_ARCPAIR 0
+#endif
 __device__ __forceinline__ i16x2 corner_score16_x2_ring(const u16x2_t (&P)[16], u16x2_t v, int threshold) {
   u16x2_t hi[8], lo[8];
 #pragma unroll
@@ -43,6 +46,27 @@ __device__ __forceinline__ i16x2 corner_score16_x2_ring(const u16x2_t (&P)[16], 
     hi4[j] = __builtin_elementwise_max(hi[j], hi[(j + 1) & 7]);
     lo4[j] = __builtin_elementwise_min(lo[j], lo[(j + 1) & 7]);
   }
+#if ORBX_FAST_ARCPAIR
+  // runs of 8 from s = 2j + 1, extended to the two 9-arcs from s - 1 and s:
+  // min(max(r, p[s-1]), max(r, p[s+8])) = max(r, min(p[s-1], p[s+8])), so a
+  // pair of arcs costs two ops and 8 pair extrema meet in the trees
+  u16x2_t ta[8], tb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const u16x2_t a = __builtin_elementwise_max(hi4[j], hi4[(j + 2) & 7]);
+    const u16x2_t b = __builtin_elementwise_min(lo4[j], lo4[(j + 2) & 7]);
+    const u16x2_t e0 = P[2 * j], e1 = P[(2 * j + 9) & 15];
+    ta[j] = __builtin_elementwise_max(a, __builtin_elementwise_min(e0, e1));
+    tb[j] = __builtin_elementwise_min(b, __builtin_elementwise_max(e0, e1));
+  }
+#pragma unroll
+  for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+    for (int j = 0; j < w; ++j) {
+      ta[j] = __builtin_elementwise_min(ta[j], ta[j + w]);
+      tb[j] = __builtin_elementwise_max(tb[j], tb[j + w]);
+    }
+#else
   // runs of 8 from s, extended to the 9-arcs from s - 1 and s; the 16 arc
   // extrema then meet in balanced trees (independent ops at every level: a
   // serial min/max chain puts a hazard nop between its dependent packed ops)
@@ -63,14 +87,24 @@ __device__ __forceinline__ i16x2 corner_score16_x2_ring(const u16x2_t (&P)[16], 
       ta[j] = __builtin_elementwise_min(ta[j], ta[j + w]);
       tb[j] = __builtin_elementwise_max(tb[j], tb[j + w]);
     }
+#endif
   const u16x2_t A = ta[0], B = tb[0];
   const i16x2 vs = __builtin_bit_cast(i16x2, v);
+#if ORBX_FAST_ARCPAIR
+  // score = max(t, v - A, B - v) - 1; the max with t only lifts pixels that
+  // are not detected (score < t either way) and is dropped: the result equals
+  // cornerScore<16> for every detected pixel and stays < t for the others
+  (void)threshold;
+  const i16x2 one = {1, 1};
+  return __builtin_elementwise_max(vs - __builtin_bit_cast(i16x2, A), __builtin_bit_cast(i16x2, B) - vs) - one;
+#else
   const short t = (short)threshold;
   const i16x2 tt = {t, t};
   const i16x2 a0 = __builtin_elementwise_max(tt, vs - __builtin_bit_cast(i16x2, A));
   const i16x2 b0 = __builtin_elementwise_min(-a0, vs - __builtin_bit_cast(i16x2, B));
   const i16x2 one = {1, 1};
   return -b0 - one;
+#endif
 }
 
 }  // namespace orbx

@@ -46,6 +46,7 @@ size_t quadtree_lds_bytes(const ExtractParams& P);
 extern const void* quadtree_kernel_ptr();
 size_t pyr_band_lds_bytes(const ExtractParams& P);
 extern const void* pyr_band_kernel_ptr();
+extern int pyr_band_occupancy(size_t lds);
 }  // namespace orbx
 
 using namespace orbx;
@@ -497,6 +498,13 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     }
     if (raise_lds_limit(pyr_band_kernel_ptr(), mx))
       return fail(ORBX_EDEVICE, "LDS limit of pyr_band_kernel: %s", hipGetErrorString(hipGetLastError()));
+    for (int i = 0; i < P.pyr_nplans; ++i) {
+      ExtractParams Q = P;
+      select_pyr_plan(Q, i);
+      pl.P.pyr_plan[i].occ = pyr_band_occupancy(pyr_band_lds_bytes(Q));
+      if (getenv("ORBX_PYR_PROF") && getenv("ORBX_PYR_PROF")[0] == '1')
+        fprintf(stderr, "pyr plan %d: %d workgroups per CU\n", i, pl.P.pyr_plan[i].occ);
+    }
   }
   if (raise_lds_limit(quadtree_kernel_ptr(), quadtree_lds_bytes(P)))
     return fail(ORBX_EDEVICE, "LDS limit of quadtree_kernel: %s", hipGetErrorString(hipGetLastError()));

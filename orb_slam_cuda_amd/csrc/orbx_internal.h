@@ -84,6 +84,7 @@ struct ExtractParams {
   struct PyrPlan {
     int nbands, bands, lds_a, lds_b, lds_y;
     int cost;  // largest per-band pixel count over the levels (level 0 staged + computed rows)
+    int occ;   // resident workgroups per CU at this plan's LDS (occupancy API, set at plan time)
   } pyr_plan[6];
   int pyr_nplans;
   int gauss[7];                // 7-tap Gaussian fixed-point kernel (sum 257)
@@ -99,13 +100,14 @@ inline void select_pyr_plan(ExtractParams& P, int i) {
   P.pyr_lds_y = q.lds_y;
 }
 
-// The band plan for a launch of `batch` frames: fewest (rounds of `slots`
-// resident workgroups) x (the tallest band's pixel count).
-inline int pick_pyr_plan(const ExtractParams& P, int batch, int slots) {
+// The band plan for a launch of `batch` frames: fewest (rounds of the
+// plan's resident workgroups, cus x occ) x (the tallest band's pixel count).
+inline int pick_pyr_plan(const ExtractParams& P, int batch, int cus) {
   int best = 0;
   long long best_t = -1;
   for (int i = 0; i < P.pyr_nplans; ++i) {
     const long long wgs = (long long)P.pyr_plan[i].nbands * batch;
+    const long long slots = (long long)cus * std::max(1, P.pyr_plan[i].occ);
     const long long t = ((wgs + slots - 1) / slots) * (long long)P.pyr_plan[i].cost;
     if (best_t < 0 || t < best_t) {
       best = i;

@@ -140,6 +140,14 @@ __global__ __launch_bounds__(256) void pyr_resize_kernel(
 #define ORBX_PYR_THREADS 512
 #endif
 constexpr int kPyrBandThreads = ORBX_PYR_THREADS;
+// waves per SIMD the band kernel is compiled for (5: <= 96 VGPRs, two
+// 512-thread workgroups per CU; 6 would allow three at <= 53 KB of LDS)
+#ifndef ORBX_PYR_R2
+#define ORBX_PYR_R2 0  // two rows per thread iteration (A/B)
+#endif
+#ifndef ORBX_PYR_WPE
+#define ORBX_PYR_WPE 5
+#endif
 
 // Rows of one level for one thread: all 32 source bytes of a row pair are
 // read before any is used, so one LDS wait covers them.
@@ -163,6 +171,61 @@ __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtr
   const LevelGeom& g = P.lv[l];
   const int spitch = P.lv[l - 1].lpitch, w = g.w;
   uint8_t* G0 = (uint8_t*)lp.base[l] + f * lp.fstride[l];
+#if ORBX_PYR_R2
+  // two of the thread's rows per iteration: both rows' 64 source bytes are
+  // read before either is computed (one LDS wait for both)
+  for (int r = cd.x + r0; r <= cd.y; r += 2 * rstep) {
+    const bool two = r + rstep <= cd.y;
+    const int2 ya = yt_rows[r - cd.x], yb = yt_rows[(two ? r + rstep : r) - cd.x];
+    int p[2][4][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int2 yt = h ? yb : ya;
+      const uint8_t* s0 = src + __mul24((yt.x & 0xFFFF) - src_lo, spitch);
+      const uint8_t* s1 = src + __mul24((yt.x >> 16) - src_lo, spitch);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        p[h][0][q] = s0[sx[q]];
+        p[h][1][q] = s0[sx[q] + 1];
+        p[h][2][q] = s1[sx[q]];
+        p[h][3][q] = s1[sx[q] + 1];
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int rr = h ? r + rstep : r;
+      const int2 yt = h ? yb : ya;
+      int v[8];
+      if (AREA2X) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (p[h][0][q] + p[h][1][q] + p[h][2][q] + p[h][3][q] + 2) >> 2;
+      } else {
+        const int b0 = (short)(yt.y & 0xFFFF), b1 = (short)(yt.y >> 16);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int D0 = __mul24(p[h][0][q], a0v[q]) + __mul24(p[h][1][q], a1v[q]);
+          const int D1 = __mul24(p[h][2][q], a0v[q]) + __mul24(p[h][3][q], a1v[q]);
+          v[q] = sat_u8((__mul24(D0, b0) + __mul24(D1, b1) + (1 << 21)) >> 22);
+        }
+      }
+      uint8_t* lrow = dst + __mul24(rr - cd.x, g.lpitch);
+      const bool owned = rr >= own.x && rr <= own.y;
+      uint8_t* drow = G0 + (long long)rr * lp.pitch[l];
+      static_assert(kPyrRun == 2, "the two-row loop writes runs of 2");
+#pragma unroll
+      for (int k = 0; k < kPyrRuns; ++k) {
+        const int xk = pyr_col(gi, G, 2 * k);
+        const uint16_t pk = (uint16_t)(sat_u8(v[2 * k]) | (sat_u8(v[2 * k + 1]) << 8));
+        *(uint16_t*)(lrow + xk) = pk;
+        if (owned) {
+          if (xk + 2 <= w) *(uint16_t*)(drow + xk) = pk;
+          else if (xk < w) drow[xk] = (uint8_t)pk;
+        }
+      }
+    }
+  }
+#else
   for (int r = cd.x + r0; r <= cd.y; r += rstep) {
     const int2 yt = yt_rows[r - cd.x];
     const uint8_t* s0 = src + __mul24((yt.x & 0xFFFF) - src_lo, spitch);
@@ -218,9 +281,10 @@ __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtr
       }
     }
   }
+#endif
 }
 
-__global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams P, LevelPtrs lp,
+__global__ __launch_bounds__(kPyrBandThreads) __attribute__((amdgpu_waves_per_eu(ORBX_PYR_WPE))) void pyr_band_kernel(ExtractParams P, LevelPtrs lp,
                                                                    const int2* __restrict__ rtab, int* dbg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
@@ -345,6 +409,11 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(ExtractParams
 
 size_t pyr_band_lds_bytes(const ExtractParams& P) { return (size_t)P.pyr_lds_a + P.pyr_lds_b + P.pyr_lds_y + 16; }
 const void* pyr_band_kernel_ptr() { return (const void*)pyr_band_kernel; }
+int pyr_band_occupancy(size_t lds) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pyr_band_kernel, kPyrBandThreads, lds) != hipSuccess) return 1;
+  return std::max(1, n);
+}
 
 static int launch_band(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab, int batch, hipStream_t s) {
   static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_PYR_PROF=1)
@@ -384,8 +453,8 @@ static int launch_band(const ExtractParams& P, const LevelPtrs& lp, const int2* 
 int launch_pyramid(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab, int batch, hipStream_t s) {
   if (P.L < 2) return ORBX_OK;
   if (P.pyr_fused) {
-    // two resident 512-thread workgroups per CU (every plan's LDS <= 78 KB),
-    // unless the plan is the one-per-CU fallback
+    // each plan's resident workgroups per CU (LDS and the kernel's registers)
+    // were found at plan time
     static const int cus = [] {
       int dev = 0, n = 256;
       (void)hipGetDevice(&dev);
@@ -396,7 +465,7 @@ int launch_pyramid(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab
     ExtractParams Q = P;
     select_pyr_plan(Q, forced >= 0 && forced < P.pyr_nplans
                            ? forced
-                           : pick_pyr_plan(P, batch, pyr_band_lds_bytes(P) > 80 * 1024 ? cus : 2 * cus));
+                           : pick_pyr_plan(P, batch, cus));
     return launch_band(Q, lp, rtab, batch, s);
   }
   for (int l = 1; l < P.L; ++l) {

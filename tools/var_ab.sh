@@ -9,6 +9,8 @@ O=gpurun_out/$TAG; mkdir -p $O
 stop() { echo "$1 exited $2: stopping"; exit 1; }
 timeout -k 10 400 python -u -m pytest tests/test_gpu_extract.py tests/test_gpu_configs.py -x -q --timeout 200 --timeout-method thread > $O/tests_base.log 2>&1
 rc=$?; echo "base parity rc=$rc: $(tail -n 1 $O/tests_base.log)"; [ $rc -ne 0 ] && { tail -n 40 $O/tests_base.log; exit 1; }
+ORBX_PYR_PROF=1 timeout -k 10 100 python3 bench.py --allow-diag --serial --steps 1 --warmup 1 --cpu-sample 0 --no-latency --no-host-stream --pool 64 > $O/pyrprof.log 2>&1 || stop pyrprof $?
+grep -E "^pyr plan|^pyr_band" $O/pyrprof.log | sort | uniq -c | head -20
 ok=""
 for v in "$@"; do
   ORBX_LIB_VARIANT=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_extract.py -x -q --timeout 200 --timeout-method thread > $O/tests_$v.log 2>&1
