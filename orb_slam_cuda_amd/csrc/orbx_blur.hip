@@ -24,9 +24,6 @@ namespace orbx {
 #ifndef ORBX_BLUR_TW
 #define ORBX_BLUR_TW 128
 #endif
-#ifndef ORBX_BLUR_BUF
-#define ORBX_BLUR_BUF 0  // interior tiles staged by buffer loads at uniform row-block offsets
-#endif
 constexpr int kBlurTW = ORBX_BLUR_TW, kBlurTH = ORBX_BLUR_TH, kBlurInW = kBlurTW + 32;
 constexpr int kBlurPairs = (kBlurTH + 6 + 1) / 2;  // 19 staged row pairs
 
@@ -60,40 +57,6 @@ __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp
   // stage rows y0-3 .. y0+TH+2, columns x0-16 .. x0+TW+15
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   constexpr int kChunks = kBlurInW / 16, kItems = (kBlurTH + 6) * kChunks, kPer = (kItems + 255) / 256;
-#if ORBX_BLUR_BUF
-  constexpr int kRB = 256 / kChunks, kBlk = (kBlurTH + 6 + kRB - 1) / kRB;  // rows per load block, blocks
-  if (lp.aligned16[l] && y0 >= 3 && y0 + kBlurTH + 3 <= H) {
-    // tiles whose staged rows need no reflection: thread -> (row tid / kChunks
-    // of a kRB-row block, chunk tid % kChunks), load k at the uniform offset
-    // k * kRB * pitch (the buffer instruction's SGPR offset): no per-load
-    // address math; columns clamped as below, then the same edge columns
-    const int xmax = min(pitch, (W + 15) & ~15) - 16;
-    const int rb = min(tid / kChunks, kRB - 1), ch = tid - (tid / kChunks) * kChunks;
-    const int gx = min(max(x0 - 16 + ch * 16, 0), xmax);
-    const int nrec = (H - 1) * pitch + xmax + 16;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S, (short)0, nrec, 0x00020000);
-    const int voff = (y0 - 3 + rb) * pitch + gx;
-    const bool lane_ok = tid < kRB * kChunks;
-    u32x4 v[kBlk];
-#pragma unroll
-    for (int k = 0; k < kBlk; ++k)
-      if (lane_ok && k * kRB + rb < kBlurTH + 6)
-        v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * kRB * pitch, 0));
-#pragma unroll
-    for (int k = 0; k < kBlk; ++k)
-      if (lane_ok && k * kRB + rb < kBlurTH + 6) *(u32x4*)&in[k * kRB + rb][ch * 16] = v[k];
-    const bool left = x0 == 0, right = x0 + kBlurTW + 3 > W;
-    if (left || right) {
-      __syncthreads();
-      for (int i = tid; i < (kBlurTH + 6) * 6; i += 256) {
-        const int r = i / 6, kk = i - r * 6;
-        int x = kk < 3 ? -1 - kk : W + kk - 3;
-        if ((kk < 3 && !left) || (kk >= 3 && !right) || x - x0 + 16 >= kBlurInW) continue;
-        in[r][x - x0 + 16] = in[r][reflect101(x, W) - x0 + 16];
-      }
-    }
-  } else
-#endif
   if (lp.aligned16[l]) {
     // every chunk is a 16-byte load from inside its (row-reflected) source
     // row: chunks left of column 0 or past ceil16(W) load a clamped chunk of

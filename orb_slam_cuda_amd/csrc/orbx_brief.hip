@@ -47,9 +47,6 @@ constexpr int kObRows = 2 * kObRadius + 1;   // 39
 #define ORBX_OB_STRIDE 64
 #endif
 constexpr int kObStride = ORBX_OB_STRIDE;
-#ifndef ORBX_OB_BUF
-#define ORBX_OB_BUF 0  // blurred patch staged by buffer loads at uniform row-block offsets
-#endif
 static_assert(kObStride >= 64 && kObStride % 8 == 0, "rows hold 4 chunks, 8-byte aligned");
 // IC coefficient rows in LDS: 24 dwords each, padded to an odd stride so the
 // 16 |v| rows a wave reads at once fall in distinct banks
@@ -146,18 +143,18 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   // IC rows (lane v - 15 = patch row: the row's 31 pixels within 9 dwords from
   // the dword boundary below x - 15; they reach at most byte x + 20 <= w of a
   // row <= h - 5, so they stay inside the level). Every load is unconditional
-  // (lanes without a chunk, or of an empty slot, read the buffer start) so
-  // that no branch join waits for them; only the LDS stores are predicated.
+  // (an empty slot reads around its dummy keypoint, the IC rows the level
+  // start) so that no branch join waits for them.
   const int c0 = (x - kObRadius) & ~15;
   const int pitch = lpitch;
   constexpr int kChunks = kObRows * 4, kPerLane = (kChunks + 31) / 32;
   uint4 pv[kPerLane];
-#if ORBX_OB_BUF
   // lane -> (row lane / 4 of an 8-row block, chunk lane % 4): load k is row
-  // block k at the uniform offset 8k * pitch (the buffer instruction's SGPR
-  // offset) through one descriptor over the frame's level plane, so no lane
-  // computes an address per load. Chunks past a row end read the next row
-  // and the row below the patch reads 0 past the plane end; neither is sampled.
+  // block k at the lane's offset + 8k * pitch (one add) through one
+  // descriptor over the frame's level plane, so no lane computes a 64-bit
+  // address per load. Chunks past a row end read the next row, and the row
+  // below the patch reads 0 past the plane end (the range check covers the
+  // VGPR offset); neither is sampled.
   static_assert(kPerLane * 8 >= kObRows, "row blocks cover the patch");
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(blur + g_off + f * g_plane), (short)0, (int)g_plane, 0x00020000);
@@ -165,19 +162,9 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
 #pragma unroll
   for (int k = 0; k < kPerLane; ++k) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 t = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, pvoff, 8 * k * g_pitch, 0));
+    const u32x4 t = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, pvoff + 8 * k * g_pitch, 0, 0));
     pv[k] = make_uint4(t.x, t.y, t.z, t.w);
   }
-#else
-  const uint8_t* brow = blur + g_off + f * g_plane + (long long)(y - kObRadius) * g_pitch + c0;
-#pragma unroll
-  for (int k = 0; k < kPerLane; ++k) {
-    const int i = min(lane + 32 * k, kChunks - 1), r = i >> 2, ch = i & 3;
-    // chunks past the row end (c0 and the pitch are multiples of 16) are never sampled
-    const bool ok = valid && c0 + ch * 16 + 16 <= g_pitch;
-    pv[k] = *(const uint4*)(ok ? brow + (long long)r * g_pitch + ch * 16 : blur);
-  }
-#endif
   const uint8_t* rp = lbase + f * lfstride + (long long)(y - kHalfPatch + min(lane, kPatchSize - 1)) * pitch +
                       (x - kHalfPatch);
   const uint32_t* q = valid ? (const uint32_t*)((uintptr_t)rp & ~(uintptr_t)3) : (const uint32_t*)lbase;
@@ -194,19 +181,14 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
       const int i = tid + k * kObThreads;
       s_ictab[(i / 24) * kIcStride + i % 24] = ic_v[k];
     }
-  // unpredicated stores (an empty slot writes its own unused patch, lanes past
-  // the last chunk rewrite it with the same bytes), so no load waits in a branch
+  // an empty slot writes its own unused patch; the loads hold row
+  // (lane / 4) + 8k, and the rows past the patch are not stored
   {
     uint8_t* dst = s_patch[hk];
 #pragma unroll
     for (int k = 0; k < kPerLane; ++k) {
-#if ORBX_OB_BUF
-      // the buffer loads hold row (lane / 4) + 8k: the rows past the patch are not stored
       const int i = lane + 32 * k, r = i >> 2, ch = i & 3;
       if ((k + 1) * 32 > kChunks && i >= kChunks) continue;
-#else
-      const int i = min(lane + 32 * k, kChunks - 1), r = i >> 2, ch = i & 3;
-#endif
       if constexpr (kObStride % 16 == 0) {
         *(uint4*)(dst + r * kObStride + ch * 16) = pv[k];
       } else {  // 8-byte aligned rows: two b64 stores (a misaligned b128 store replays)

@@ -23,7 +23,7 @@
 // unless it is empty, and writes the keys in row-major order (the order
 // cv::FAST emits them) into the cell's fixed slot range. Every compaction is
 // an ordered ballot compaction, so row-major order is preserved throughout.
-#if (defined(ORBX_FAST_SAMEROI) || defined(ORBX_FAST_NOLOAD) || defined(ORBX_FAST_LCAP)) && !defined(ORBX_DIAG)
+#if (defined(ORBX_FAST_SAMEROI) || defined(ORBX_FAST_LCAP)) && !defined(ORBX_DIAG)
 #error "result-changing diagnostic switches need -DORBX_DIAG"
 #endif
 #include <algorithm>
@@ -46,18 +46,6 @@ namespace orbx {
 // staging, the scalar compass). The tight strides keep a wave's LDS near
 // 6 KB instead of ~8 KB and run the dword compass (compass4).
 constexpr int kTightE = 4;  // staging element of the tight strides
-#ifndef ORBX_FAST_SBAL
-#define ORBX_FAST_SBAL 0  // score-pass ballots masked by uniform lane masks
-#endif
-#ifndef ORBX_FAST_R5
-#define ORBX_FAST_R5 0  // tight staging by whole rows per load (buffer loads, uniform row offsets)
-#endif
-#ifndef ORBX_FAST_SDW
-#define ORBX_FAST_SDW 0  // survivor ring read as dwords / 8-byte rows (unaligned LDS reads)
-#endif
-#ifndef ORBX_FAST_PEEL
-#define ORBX_FAST_PEEL 0  // compass passes wholly inside the band skip the row mask
-#endif
 #ifndef ORBX_FAST_T1
 #define ORBX_FAST_T1 44  // tight strides (bank-conflict experiments: tools/variant.sh)
 #endif
@@ -65,12 +53,6 @@ constexpr int kTightE = 4;  // staging element of the tight strides
 #define ORBX_FAST_T2 48
 #endif
 constexpr int kRoiTight = ORBX_FAST_T1, kRoiTight2 = ORBX_FAST_T2, kRoiWide = 80;
-// 64-byte rows staged in 16-byte chunks from the 16-byte boundary below c0
-// (ROIs of <= 49 bytes), read by the dword compass (A/B: ORBX_FAST_S64=1)
-constexpr int kRoiMid = 64;
-#ifndef ORBX_FAST_S64
-#define ORBX_FAST_S64 0
-#endif
 static_assert(kRoiTight < kRoiTight2 && kRoiTight2 < kRoiWide && kRoiTight % 4 == 0 && kRoiTight2 % 4 == 0,
               "tight strides in increasing order, whole dwords");
 
@@ -167,20 +149,13 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
     n1 += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
   };
   int by0 = 0;
-#if ORBX_FAST_PEEL
   for (; by0 + RP <= bh; by0 += RP) pass(by0, std::true_type{});
   if (by0 < bh) pass(by0, std::false_type{});
-#else
-  for (; by0 < bh; by0 += RP) pass(by0, std::false_type{});
-#endif
   return n1;
 }
 
 #ifndef ORBX_FAST_PK
 #define ORBX_FAST_PK 1  // packed-u16 compass pre-test (0: the scalar form, for A/B)
-#endif
-#ifndef ORBX_FAST_GLDS
-#define ORBX_FAST_GLDS 0  // tight-stride staging by LDS-DMA (global_load_lds) instead of registers
 #endif
 #ifndef ORBX_FAST_WAVES
 #define ORBX_FAST_WAVES 8  // VGPR budget: 8 waves per SIMD (<= 64 VGPRs; 41 used)
@@ -244,16 +219,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   constexpr bool kDword = kRoiStride == kRoiTight || kRoiStride == kRoiTight2;  // dword staging
   constexpr bool kTight = kRoiStride != kRoiWide;                                 // the dword compass
   const int a0 = kDword ? (cg.c0 & ~(kTightE - 1)) : (cg.c0 & ~15), ox = cg.c0 - a0;
-  // unpredicated staging: lanes past the last piece load and store it again
-  // (same bytes), so all of a lane's loads stay in registers and in flight
-#if ORBX_FAST_R5
   if (lp.aligned16[l] && kDword) {
     // whole rows per load instruction: lane -> (row lq < kRP, dword ld), so
-    // load k is row block k at the uniform offset k * kRP * pitch (the buffer
-    // instruction's SGPR offset) and LDS offset k * kRP * stride: no per-piece
-    // address math. The buffer range ends at the level plane's last readable
-    // byte, so rows past the ROI (up to kRP - 1) never read outside the frame
-    // (they land in LDS below the ROI, in the score map cleared afterwards).
+    // load k is row block k at the lane's offset + k * kRP * pitch (one add)
+    // and LDS offset k * kRP * stride (the instruction's immediate): no
+    // per-piece index math. The buffer range (which checks the VGPR offset)
+    // ends at the level plane's last readable byte, so the row blocks past a
+    // short ROI read 0 beyond the plane instead of faulting; they land in LDS
+    // below the ROI, in the score map cleared afterwards.
     constexpr int kPR = kRoiStride / kTightE, kRP = 64 / kPR;
     const int lq0 = lane / kPR, lq = min(lq0, kRP - 1), ld = lq0 < kRP ? lane - lq0 * kPR : kPR - 1;
     const int voff = u24mul(lq, pitch) + 4 * ld, roff = lq * kRoiStride + 4 * ld;
@@ -267,68 +240,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     static_assert(kK * kRP * kRoiStride <= 41 * kRoiStride + 1024, "extra row blocks stay in the wave's LDS");
     uint32_t v[kK];
 #pragma unroll
-    for (int k = 0; k < kK; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, k * kRP * pitch, 0);
+    for (int k = 0; k < kK; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + k * kRP * pitch, 0, 0);
 #pragma unroll
     for (int k = 0; k < kK; ++k) *(LDSP uint32_t*)(roi + roff + k * kRP * kRoiStride) = v[k];
     for (int k = kK; k < nk; ++k)
-      *(LDSP uint32_t*)(roi + roff + k * kRP * kRoiStride) = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, k * kRP * pitch, 0);
-  } else
-#endif
-#if ORBX_FAST_GLDS
-  if (lp.aligned16[l] && kDword) {
-    // the ROI's rows are contiguous in LDS (kRoiStride / 4 dwords each), so
-    // dword i of the ROI is lane i % 64 of LDS-DMA instruction i / 64: every
-    // dword goes straight from memory to LDS (no VGPR round trip, no ds_write)
-    constexpr int kPR = kRoiStride / kTightE;
-    const int nd = (cg.c1 - a0 + kTightE - 1) / kTightE, total = rh * kPR;
-    constexpr int kK = (41 * kPR + 63) / 64;  // a 41-row ROI unrolled, taller ones loop
-    auto piece = [&](int k) {
-      const int i = lane + 64 * k, q = i / kPR, d = min(i - q * kPR, nd - 1);
-      if (i < total)
-        __builtin_amdgcn_global_load_lds((const void*)(rows + a0 + (int)__umul24((unsigned)q, (unsigned)pitch) + kTightE * d),
-                                         (LDSP void*)(roi + 256 * k), 4, 0, 0);
-    };
-#pragma unroll
-    for (int k = 0; k < kK; ++k)
-      if (64 * k < total) piece(k);
-    for (int k = kK; 64 * k < total; ++k) piece(k);
-  } else
-#endif
-  if (lp.aligned16[l] && kDword) {
-    // dwords from the one at or below c0 (<= kRoiStride / 4 per row), kK per
-    // lane in flight
-    typedef unsigned int piece_t __attribute__((ext_vector_type(kTightE / 4)));
-    // a fixed kPR pieces per staged row, so the lane -> (row, piece) split is
-    // a division by a constant; pieces past the ROI's last one (nd) and rows
-    // past the last (rh) reload that piece / row (same bytes, same LDS slot)
-    constexpr int kPR = kRoiStride / kTightE;
-    constexpr int kK = (41 * kPR + 63) / 64 > 8 ? (41 * kPR + 63) / 64 : 8;  // a 41-row ROI in one burst
-    const int nd = (cg.c1 - a0 + kTightE - 1) / kTightE, total = rh * kPR;
-    piece_t v[kK];
-    int ro[kK], lo[kK];
-#pragma unroll
-    for (int k = 0; k < kK; ++k) {
-      const int i = lane + 64 * k, q = i / kPR;
-      const int r = min(q, rh - 1), d = min(i - q * kPR, nd - 1);
-      ro[k] = r * kRoiStride + kTightE * d;
-      lo[k] = (int)__umul24((unsigned)r, (unsigned)pitch) + kTightE * d;
-    }
-#pragma unroll
-    for (int k = 0; k < kK; ++k) {
-#ifdef ORBX_FAST_NOLOAD  // diagnostics: no global loads (synthetic bytes)
-      v[k] = (piece_t)(0x01010101u * (uint32_t)((lane * 37 + k * 11 + cell) & 255));
-#else
-      v[k] = *(const piece_t*)(rows + a0 + lo[k]);
-#endif
-    }
-#pragma unroll
-    for (int k = 0; k < kK; ++k) *(LDSP piece_t*)(roi + ro[k]) = v[k];
-    for (int i = lane + 64 * kK; i < total; i += 64) {
-      const int q = i / kPR;
-      const int r = min(q, rh - 1), d = min(i - q * kPR, nd - 1);
-      *(LDSP piece_t*)(roi + r * kRoiStride + kTightE * d) =
-          *(const piece_t*)(rows + (int)__umul24((unsigned)r, (unsigned)pitch) + a0 + kTightE * d);
-    }
+      *(LDSP uint32_t*)(roi + roff + k * kRP * kRoiStride) = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + k * kRP * pitch, 0, 0);
   } else if (lp.aligned16[l]) {
     // the ROI's 16-byte chunks, 4 per lane (tall cells loop for the rest)
     const int nch = (cg.c1 - a0 + 15) >> 4, total = rh * nch;
@@ -442,66 +358,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     const int eA = list[min(iA, n1 - 1)], eB = list[min(iB, n1 - 1)];
     const LDSP uint8_t* cA = band + u24mul(eA >> 8, kRoiStride) + (eA & 255);
     const LDSP uint8_t* cB = band + u24mul(eB >> 8, kRoiStride) + (eB & 255);
-#if ORBX_FAST_SDW
-    // the ring in 7 reads per pixel instead of 17 byte reads: rows +-3 as one
-    // dword from x - 1, rows -2..2 as 8 bytes from x - 3 (unaligned LDS reads);
-    // each (A, B) pair of ring bytes is one v_perm_b32
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    constexpr int S = kRoiStride;
-    u32x2 qa[5], qb[5];
-    uint32_t ta[2], tb[2];
-    ta[0] = *(const LDSP uint32_t*)(cA + 3 * S - 1);
-    ta[1] = *(const LDSP uint32_t*)(cA - 3 * S - 1);
-    tb[0] = *(const LDSP uint32_t*)(cB + 3 * S - 1);
-    tb[1] = *(const LDSP uint32_t*)(cB - 3 * S - 1);
-#pragma unroll
-    for (int d = 0; d < 5; ++d) {  // rows -2, -1, 0, 1, 2
-      qa[d] = *(const LDSP u32x2*)(cA + (d - 2) * S - 3);
-      qb[d] = *(const LDSP u32x2*)(cB + (d - 2) * S - 3);
-    }
-    // u16x2 {A's byte ia of a, B's byte ib of b}
-    auto pk = [](uint32_t a, int ia, uint32_t b, int ib) -> u16x2_t {
-      const uint32_t sel = (uint32_t)ia | 0x0C00u | ((uint32_t)(4 + ib) << 16) | 0x0C000000u;
-      return __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(b, a, sel));
-    };
-    // byte j of an 8-byte row read (j = 0 is x - 3)
-    auto pq = [&](int d, int j) -> u16x2_t { return pk(qa[d][j >> 2], j & 3, qb[d][j >> 2], j & 3); };
-    const u16x2_t v = pq(2, 3);
-    u16x2_t R[16];
-    R[15] = pk(ta[0], 0, tb[0], 0);  // row +3: x - 1, x, x + 1
-    R[0] = pk(ta[0], 1, tb[0], 1);
-    R[1] = pk(ta[0], 2, tb[0], 2);
-    R[9] = pk(ta[1], 0, tb[1], 0);   // row -3
-    R[8] = pk(ta[1], 1, tb[1], 1);
-    R[7] = pk(ta[1], 2, tb[1], 2);
-    R[14] = pq(4, 1);  // row +2: x - 2, x + 2
-    R[2] = pq(4, 5);
-    R[10] = pq(0, 1);  // row -2
-    R[6] = pq(0, 5);
-    R[13] = pq(3, 0);  // row +1: x - 3, x + 3
-    R[3] = pq(3, 6);
-    R[11] = pq(1, 0);  // row -1
-    R[5] = pq(1, 6);
-    R[12] = pq(2, 0);  // row 0
-    R[4] = pq(2, 6);
-#else
     const u16x2_t v = {(unsigned short)cA[0], (unsigned short)cB[0]};
     u16x2_t R[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) R[k] = (u16x2_t){(unsigned short)cA[ring_off<kRoiStride>(k)], (unsigned short)cB[ring_off<kRoiStride>(k)]};
-#endif
-    const i16x2 s = corner_score16_x2_ring(R, v, t);
-#if ORBX_FAST_SBAL
+    const i16x2 s = corner_score16_x2_ring(R, v);
     // the chunk's valid entries as uniform lane masks (no per-lane compare),
     // the stores predicated by the masks themselves
     const int nA = n1 - i0, nB = nA - 64;
     const uint64_t vA = nA >= 64 ? ~0ull : (1ull << nA) - 1, vB = nB >= 64 ? ~0ull : nB <= 0 ? 0ull : (1ull << nB) - 1;
     const uint64_t mA = __ballot(s.x >= t) & vA, mB = __ballot(s.y >= t) & vB;
     const bool dA = __builtin_amdgcn_inverse_ballot_w64(mA), dB = __builtin_amdgcn_inverse_ballot_w64(mB);
-#else
-    const bool dA = iA < n1 && s.x >= t, dB = iB < n1 && s.y >= t;
-    const uint64_t mA = __ballot(dA), mB = __ballot(dB);
-#endif
     if (dA) {
       list[n2 + mbcnt64(mA)] = (uint16_t)eA;
       sc[u24mul((eA >> 8) + 1, sw) + (eA & 255) + 1] = (uint8_t)s.x;
@@ -522,19 +389,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   auto nms = [&](int i, bool* ki, bool* km) {  // detected entry i kept at iniThFAST / minThFAST
     const int e = list[i];
     const LDSP uint8_t* q = sc + u24mul((e >> 8) + 1, sw) + (e & 255) + 1;
-#if ORBX_FAST_SDW
-    // the 3x3 neighbourhood as three unaligned dword reads
-    const uint32_t up = *(const LDSP uint32_t*)(q - sw - 1), mid = *(const LDSP uint32_t*)(q - 1),
-                   dn = *(const LDSP uint32_t*)(q + sw - 1);
-    auto byte = [](uint32_t w, int j) { return (int)((w >> (8 * j)) & 255u); };
-    const int s = byte(mid, 1);
-    bool gi = s >= ti && s > 0, gm = s >= tm && s > 0;
-    const int nbv[8] = {byte(mid, 0), byte(mid, 2), byte(up, 0), byte(up, 1), byte(up, 2), byte(dn, 0), byte(dn, 1), byte(dn, 2)};
-#else
     const int s = q[0];
     bool gi = s >= ti && s > 0, gm = s >= tm && s > 0;
     const int nbv[8] = {q[-1], q[1], q[-sw - 1], q[-sw], q[-sw + 1], q[sw - 1], q[sw], q[sw + 1]};
-#endif
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int x = nbv[j];
@@ -592,7 +449,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
 // (+ the 3 bytes of its first staged dword below c0)
 static int fast_stride(const ExtractParams& P) {
   const int need = P.fast_bw_max + 6 + kTightE - 1;
-  if (ORBX_FAST_S64 && P.fast_bw_max + 6 + 15 <= kRoiMid) return kRoiMid;
   return need <= kRoiTight ? kRoiTight : need <= kRoiTight2 ? kRoiTight2 : kRoiWide;
 }
 
@@ -634,11 +490,6 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
     else if (stride == kRoiTight2)
       hipLaunchKernelGGL(fast_cells_kernel<kRoiTight2>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
                          lp, cells, slots, cell_counts, prof ? dbg : nullptr);
-#if ORBX_FAST_S64
-    else if (stride == kRoiMid)
-      hipLaunchKernelGGL(fast_cells_kernel<kRoiMid>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
-                         lp, cells, slots, cell_counts, prof ? dbg : nullptr);
-#endif
     else
       hipLaunchKernelGGL(fast_cells_kernel<kRoiWide>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
                          lp, cells, slots, cell_counts, prof ? dbg : nullptr);

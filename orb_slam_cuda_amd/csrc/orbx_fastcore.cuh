@@ -18,22 +18,18 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 // updates that cannot change a0 / b0 (the partial arc minimum already bounds
 // the full one), so
 //   a0 = max(t, max over the 16 arcs of 9 of min(d)),
-//   b0 = min(-a0, min over the 16 arcs of 9 of max(d)),  score = -b0 - 1.
-// The 9-arcs starting at k and k+1 (k even) share the 8-run starting at k+1,
-// so the run minima come from a min tree over the odd starts only. A pixel
-// is FAST-detected at t iff its score is >= t.
-typedef short i16x2 __attribute__((ext_vector_type(2)));
+//   b0 = min(-a0, min over the 16 arcs of 9 of max(d)),  score = -b0 - 1
+//      = max(t, max over arcs of min(d), -(min over arcs of max(d))) - 1.
 // Computed from the ring pixels p[k] themselves (u16x2, one pixel per half)
 // and the centre v: min over an arc of (v - p) = v - max over the arc of p
-// (exact in integers), so the trees run on p and v enters once:
-//   a0 = max(t, v - min over arcs of (max of p)),
-//   b0 = min(-a0, v - max over arcs of (min of p)),  score = -b0 - 1
-// (no per-pixel d = v - p subtractions).
+// (exact in integers), so with A = min over arcs of (max of p) and
+// B = max over arcs of (min of p), score = max(t, v - A, B - v) - 1. A pixel
+// is FAST-detected at t iff its score is >= t; the max with t only lifts
+// pixels that are not detected, so it is dropped: the value returned equals
+// cornerScore<16> for every detected pixel and is < t for the others.
+typedef short i16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
-#ifndef ORBX_FAST_ARCPAIR
-#define ORBX_FAST_ARCPAIR 0
-#endif
-__device__ __forceinline__ i16x2 corner_score16_x2_ring(const u16x2_t (&P)[16], u16x2_t v, int threshold) {
+__device__ __forceinline__ i16x2 corner_score16_x2_ring(const u16x2_t (&P)[16], u16x2_t v) {
   u16x2_t hi[8], lo[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {  // runs of 2 from odd start s = 2j + 1
@@ -46,7 +42,6 @@ __device__ __forceinline__ i16x2 corner_score16_x2_ring(const u16x2_t (&P)[16], 
     hi4[j] = __builtin_elementwise_max(hi[j], hi[(j + 1) & 7]);
     lo4[j] = __builtin_elementwise_min(lo[j], lo[(j + 1) & 7]);
   }
-#if ORBX_FAST_ARCPAIR
   // runs of 8 from s = 2j + 1, extended to the two 9-arcs from s - 1 and s:
   // min(max(r, p[s-1]), max(r, p[s+8])) = max(r, min(p[s-1], p[s+8])), so a
   // pair of arcs costs two ops and 8 pair extrema meet in the trees
@@ -66,45 +61,10 @@ __device__ __forceinline__ i16x2 corner_score16_x2_ring(const u16x2_t (&P)[16], 
       ta[j] = __builtin_elementwise_min(ta[j], ta[j + w]);
       tb[j] = __builtin_elementwise_max(tb[j], tb[j + w]);
     }
-#else
-  // runs of 8 from s, extended to the 9-arcs from s - 1 and s; the 16 arc
-  // extrema then meet in balanced trees (independent ops at every level: a
-  // serial min/max chain puts a hazard nop between its dependent packed ops)
-  u16x2_t ta[16], tb[16];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const u16x2_t a = __builtin_elementwise_max(hi4[j], hi4[(j + 2) & 7]);
-    ta[2 * j] = __builtin_elementwise_max(a, P[2 * j]);
-    ta[2 * j + 1] = __builtin_elementwise_max(a, P[(2 * j + 9) & 15]);
-    const u16x2_t b = __builtin_elementwise_min(lo4[j], lo4[(j + 2) & 7]);
-    tb[2 * j] = __builtin_elementwise_min(b, P[2 * j]);
-    tb[2 * j + 1] = __builtin_elementwise_min(b, P[(2 * j + 9) & 15]);
-  }
-#pragma unroll
-  for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-    for (int j = 0; j < w; ++j) {
-      ta[j] = __builtin_elementwise_min(ta[j], ta[j + w]);
-      tb[j] = __builtin_elementwise_max(tb[j], tb[j + w]);
-    }
-#endif
   const u16x2_t A = ta[0], B = tb[0];
   const i16x2 vs = __builtin_bit_cast(i16x2, v);
-#if ORBX_FAST_ARCPAIR
-  // score = max(t, v - A, B - v) - 1; the max with t only lifts pixels that
-  // are not detected (score < t either way) and is dropped: the result equals
-  // cornerScore<16> for every detected pixel and stays < t for the others
-  (void)threshold;
   const i16x2 one = {1, 1};
   return __builtin_elementwise_max(vs - __builtin_bit_cast(i16x2, A), __builtin_bit_cast(i16x2, B) - vs) - one;
-#else
-  const short t = (short)threshold;
-  const i16x2 tt = {t, t};
-  const i16x2 a0 = __builtin_elementwise_max(tt, vs - __builtin_bit_cast(i16x2, A));
-  const i16x2 b0 = __builtin_elementwise_min(-a0, vs - __builtin_bit_cast(i16x2, B));
-  const i16x2 one = {1, 1};
-  return -b0 - one;
-#endif
 }
 
 }  // namespace orbx

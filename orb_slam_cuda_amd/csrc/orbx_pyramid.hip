@@ -142,9 +142,6 @@ __global__ __launch_bounds__(256) void pyr_resize_kernel(
 constexpr int kPyrBandThreads = ORBX_PYR_THREADS;
 // waves per SIMD the band kernel is compiled for (5: <= 96 VGPRs, two
 // 512-thread workgroups per CU; 6 would allow three at <= 53 KB of LDS)
-#ifndef ORBX_PYR_R2
-#define ORBX_PYR_R2 0  // two rows per thread iteration (A/B)
-#endif
 #ifndef ORBX_PYR_WPE
 #define ORBX_PYR_WPE 5
 #endif
@@ -171,61 +168,6 @@ __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtr
   const LevelGeom& g = P.lv[l];
   const int spitch = P.lv[l - 1].lpitch, w = g.w;
   uint8_t* G0 = (uint8_t*)lp.base[l] + f * lp.fstride[l];
-#if ORBX_PYR_R2
-  // two of the thread's rows per iteration: both rows' 64 source bytes are
-  // read before either is computed (one LDS wait for both)
-  for (int r = cd.x + r0; r <= cd.y; r += 2 * rstep) {
-    const bool two = r + rstep <= cd.y;
-    const int2 ya = yt_rows[r - cd.x], yb = yt_rows[(two ? r + rstep : r) - cd.x];
-    int p[2][4][8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int2 yt = h ? yb : ya;
-      const uint8_t* s0 = src + __mul24((yt.x & 0xFFFF) - src_lo, spitch);
-      const uint8_t* s1 = src + __mul24((yt.x >> 16) - src_lo, spitch);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        p[h][0][q] = s0[sx[q]];
-        p[h][1][q] = s0[sx[q] + 1];
-        p[h][2][q] = s1[sx[q]];
-        p[h][3][q] = s1[sx[q] + 1];
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !two) break;
-      const int rr = h ? r + rstep : r;
-      const int2 yt = h ? yb : ya;
-      int v[8];
-      if (AREA2X) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = (p[h][0][q] + p[h][1][q] + p[h][2][q] + p[h][3][q] + 2) >> 2;
-      } else {
-        const int b0 = (short)(yt.y & 0xFFFF), b1 = (short)(yt.y >> 16);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int D0 = __mul24(p[h][0][q], a0v[q]) + __mul24(p[h][1][q], a1v[q]);
-          const int D1 = __mul24(p[h][2][q], a0v[q]) + __mul24(p[h][3][q], a1v[q]);
-          v[q] = sat_u8((__mul24(D0, b0) + __mul24(D1, b1) + (1 << 21)) >> 22);
-        }
-      }
-      uint8_t* lrow = dst + __mul24(rr - cd.x, g.lpitch);
-      const bool owned = rr >= own.x && rr <= own.y;
-      uint8_t* drow = G0 + (long long)rr * lp.pitch[l];
-      static_assert(kPyrRun == 2, "the two-row loop writes runs of 2");
-#pragma unroll
-      for (int k = 0; k < kPyrRuns; ++k) {
-        const int xk = pyr_col(gi, G, 2 * k);
-        const uint16_t pk = (uint16_t)(sat_u8(v[2 * k]) | (sat_u8(v[2 * k + 1]) << 8));
-        *(uint16_t*)(lrow + xk) = pk;
-        if (owned) {
-          if (xk + 2 <= w) *(uint16_t*)(drow + xk) = pk;
-          else if (xk < w) drow[xk] = (uint8_t)pk;
-        }
-      }
-    }
-  }
-#else
   for (int r = cd.x + r0; r <= cd.y; r += rstep) {
     const int2 yt = yt_rows[r - cd.x];
     const uint8_t* s0 = src + __mul24((yt.x & 0xFFFF) - src_lo, spitch);
@@ -281,7 +223,7 @@ __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtr
       }
     }
   }
-#endif
+
 }
 
 __global__ __launch_bounds__(kPyrBandThreads) __attribute__((amdgpu_waves_per_eu(ORBX_PYR_WPE))) void pyr_band_kernel(ExtractParams P, LevelPtrs lp,
