@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 evidence, part B: per-config bench lines + rocprofv3 stats (C2, C4,
+# Round-4 evidence, part B (run after part A and tools/collect_r04.sh): per-config bench lines + rocprofv3 stats (C2, C4,
 # C5, C3 + BoW, the KITTI14 / intcatch-1080p settings), SQ counters of the
 # serial C3 bench, FAST and search_init phase clocks, the link microbench.
 set -e
@@ -25,4 +25,11 @@ python3 tools/sq_valu.py $O/sq/summary.txt $O/sq_valu.json
 ORBX_FAST_PROF=1 timeout -k 10 100 python3 bench.py --allow-diag --serial --steps 1 --warmup 1 --cpu-sample 0 --no-latency --no-host-stream --pool 64 2>&1 | grep "^fast" > $O/fast_phases.txt
 ORBX_INIT_PROF=1 timeout -k 10 100 python3 tools/init_timing.py 64 > $O/init_phases.txt 2>&1
 timeout -k 10 120 python3 tools/h2d_bench.py > $O/h2d.json
+# the default bench line again, now reading this commit's counter files
+# (pmc_traffic.json from part A, collected into profiles/ before this call;
+# sq_valu.json from the passes above)
+cp $O/sq_valu.json profiles/sq_valu.json
+mkdir -p gpurun_out/ev4c
+timeout -k 10 400 python3 bench.py > gpurun_out/ev4c/bench_default.log 2>&1
+tail -n 1 gpurun_out/ev4c/bench_default.log | cut -c1-200
 echo all-done
