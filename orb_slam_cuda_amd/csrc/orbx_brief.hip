@@ -229,15 +229,24 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
   // GET_VALUE(idx): center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)]
   const uint8_t* pc = s_patch[hk] + kObRadius * kObStride + (x - c0);
   uint32_t dword[8];
+  // a test's two points as packed float pairs (the table holds {x0, x1, y0,
+  // y1}): each product and sum rounded as the reference rounds it (packed
+  // v_pk_mul_f32 / v_pk_add_f32, no contraction), then cvRound as one more
+  // add: fl(v + 1.5 * 2^23) holds round-half-even(v) in its low mantissa bits
+  // (|v| < 2^22), so the patch offset ry * stride + rx is an integer
+  // multiply-add of the two sums' bit patterns, the magic constant's share
+  // folded into the patch pointer (32-bit wrap-around arithmetic)
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  const f32x2_t aa = {a, a}, bb = {b, b}, mg = {12582912.0f, 12582912.0f};
+  const uint8_t* pcm = pc - (uint32_t)(0x4B400000u * (uint32_t)(kObStride + 1));
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const float4 t = s_tests[lane + 32 * k];
-    const float px0 = t.x, py0 = t.y, px1 = t.z, py1 = t.w;
-    const int ry0 = __float2int_rn(__fadd_rn(__fmul_rn(px0, b), __fmul_rn(py0, a)));
-    const int rx0 = __float2int_rn(__fsub_rn(__fmul_rn(px0, a), __fmul_rn(py0, b)));
-    const int ry1 = __float2int_rn(__fadd_rn(__fmul_rn(px1, b), __fmul_rn(py1, a)));
-    const int rx1 = __float2int_rn(__fsub_rn(__fmul_rn(px1, a), __fmul_rn(py1, b)));
-    const uint64_t m = __ballot(pc[ry0 * kObStride + rx0] < pc[ry1 * kObStride + rx1]);
+    const f32x2_t X = {t.x, t.y}, Y = {t.z, t.w};
+    const f32x2_t fy = (X * bb + Y * aa) + mg, fx = (X * aa - Y * bb) + mg;
+    const uint32_t i0 = __float_as_uint(fy.x) * (uint32_t)kObStride + __float_as_uint(fx.x);
+    const uint32_t i1 = __float_as_uint(fy.y) * (uint32_t)kObStride + __float_as_uint(fx.y);
+    const uint64_t m = __ballot(pcm[i0] < pcm[i1]);
     dword[k] = (uint32_t)((tid & 32) ? (m >> 32) : m);
   }
 
@@ -294,7 +303,8 @@ int launch_orient_brief(const ExtractParams& P, const LevelPtrs& lp, const Extra
         for (int i = 0; i < 256; ++i) {
           int q[4];
           brief_test(m, i, q);
-          t[m][i] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+          t[m][i] = make_float4((float)q[0], (float)q[2], (float)q[1], (float)q[3]);  // {x0, x1, y0, y1}
+
         }
       if (hipMemcpyToSymbol(HIP_SYMBOL(c_brief_tests), t, sizeof(t)) != hipSuccess) return ORBX_EDEVICE;
       // umax of the r = 15 circle (ORBextractor ctor :540-555; PATCH_SIZE is fixed at 31)

@@ -160,19 +160,25 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
 #ifndef ORBX_FAST_WAVES
 #define ORBX_FAST_WAVES 8  // VGPR budget: 8 waves per SIMD (<= 64 VGPRs; 41 used)
 #endif
-template <int kRoiStride>
+// kProf: the ORBX_FAST_PROF instantiation with the phase stamps (the shipped
+// one carries no diagnostics code)
+template <int kRoiStride, bool kProf>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WAVES))) void fast_cells_kernel(ExtractParams P, LevelPtrs lp,
                                                         const CellGeom* __restrict__ cells,
                                                         uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_counts, int* dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+  const unsigned long long t_begin = kProf ? __builtin_amdgcn_s_memtime() : 0ull;
   auto stamp = [&](int k) {
-    if (dbg && threadIdx.x == 0)
+    if (kProf && threadIdx.x == 0)
       dbg[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + k] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
   };
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-  const int cell = wg % P.ncells_total, f = wg / P.ncells_total, lane = threadIdx.x;
+  // the frame by a multiply-high with the plan's magic (exact for every id
+  // of the launch, checked at plan time), the cell by one multiply-add: no
+  // division on the path to the cell record load
+  const int f = P.ncells_magic ? (int)__umulhi((unsigned)wg, P.ncells_magic) : wg / P.ncells_total;
+  const int cell = wg - f * P.ncells_total, lane = threadIdx.x;
   CellGeom cg;
   {
     // the whole 16-byte cell record in one scalar load (int16 fields unpacked
@@ -186,7 +192,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     cg.cap = (int16_t)(raw.w & 0xFFFF);
     cg.level = (int16_t)(raw.w >> 16);
     // diagnostics: clock at which the cell record arrived (the test waits for it)
-    if (dbg && threadIdx.x == 0 && raw.w != -1)
+    if (kProf && threadIdx.x == 0 && raw.w != -1)
       dbg[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + 7] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
   }
   int* cnt = cell_counts + (long long)f * P.ncells_total + cell;
@@ -439,7 +445,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   }
   if (lane == 0) *cnt = min(base, (int)cg.cap);
   stamp(4);
-  if (dbg && lane == 0) {
+  if (kProf && lane == 0) {
     dbg[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + 5] = n1;
     dbg[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + 6] = n2;
   }
@@ -484,15 +490,13 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
 #endif
   for (int rep = 0; rep < reps; ++rep) {
     const int stride = fast_stride(P);
-    if (stride == kRoiTight)
-      hipLaunchKernelGGL(fast_cells_kernel<kRoiTight>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
-                         lp, cells, slots, cell_counts, prof ? dbg : nullptr);
-    else if (stride == kRoiTight2)
-      hipLaunchKernelGGL(fast_cells_kernel<kRoiTight2>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
-                         lp, cells, slots, cell_counts, prof ? dbg : nullptr);
-    else
-      hipLaunchKernelGGL(fast_cells_kernel<kRoiWide>, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P,
-                         lp, cells, slots, cell_counts, prof ? dbg : nullptr);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P, lp, cells, slots,
+                         cell_counts, dbg);
+    };
+    if (stride == kRoiTight) prof ? go(fast_cells_kernel<kRoiTight, true>) : go(fast_cells_kernel<kRoiTight, false>);
+    else if (stride == kRoiTight2) prof ? go(fast_cells_kernel<kRoiTight2, true>) : go(fast_cells_kernel<kRoiTight2, false>);
+    else prof ? go(fast_cells_kernel<kRoiWide, true>) : go(fast_cells_kernel<kRoiWide, false>);
   }
   if (prof) {
     std::vector<int> h((size_t)nwg * 8);

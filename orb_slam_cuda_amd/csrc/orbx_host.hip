@@ -442,6 +442,16 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   if (maxnodes > 65000) return fail(ORBX_EINVAL, "nfeatures too large for the quadtree node table");
   P.slots_per_frame = slot;
   P.ncells_total = (int)pl.cells.size();
+  {
+    // FAST's frame index without a division: mulhi(id, m) with m = ceil(2^32 / d)
+    // equals id / d while id * (m * d - 2^32) < 2^32 (ids < d * B)
+    const unsigned long long d = (unsigned long long)P.ncells_total;
+    P.ncells_magic = 0u;
+    if (d > 1) {
+      const unsigned long long m = ((1ull << 32) + d - 1) / d, e = m * d - (1ull << 32);
+      if (d * (unsigned long long)B * e < (1ull << 32)) P.ncells_magic = (unsigned)m;
+    }
+  }
   P.kp_per_frame = kbase;
   P.maxnodes = maxnodes;
   int sn = 1;

@@ -65,6 +65,7 @@ struct ExtractParams {
   int L, B;
   int t_low, t_ini, t_min;
   int slots_per_frame, ncells_total;
+  unsigned ncells_magic;       // ceil(2^32 / ncells_total) when frame = mulhi(id, magic) is exact for every id of the plan's batch, else 0
   int kp_per_frame;            // == output capacity per frame
   int maxnodes, sortn;         // quadtree node-table size, bitonic size (pow2)
   int max_cells_level;         // largest ncells of any level
