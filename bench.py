@@ -910,7 +910,7 @@ def pmc_bytes(kernel):
         pmc = json.load(open(pmc_path))
     except Exception:
         return None
-    want = kernel.split(" ")[0]  # profile keys carry template arguments ("fast_cells_kernel<44>")
+    want = kernel.split(" ")[0]  # profile keys carry template arguments ("fast_cells_kernel<44, false>")
     return next((v.get("bytes_per_launch") for k, v in pmc.items() if k.split("<")[0] == want), None)
 
 
