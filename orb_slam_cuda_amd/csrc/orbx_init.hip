@@ -61,8 +61,11 @@ constexpr int kInitThLow = 50;                         // TH_LOW
 constexpr int kInitMaxRounds = 48;
 constexpr int kInitK = 8;       // smallest keys kept per query (a rescan when fewer than 2 of them are unblocked)
 constexpr int kInitQLanes = 8;  // lanes per query in the key pass (a DPP half-row)
+// 512: a prep workgroup waits for 8 free wave slots beside the extraction
+// streams instead of 16 (pipelined search_init stage 0.13-0.14 -> 0.113-0.115
+// ms per 64 pairs, frames/s equal within the run-to-run spread, tools/init_ab3.sh)
 #ifndef ORBX_INIT_PREP_THREADS
-#define ORBX_INIT_PREP_THREADS 1024
+#define ORBX_INIT_PREP_THREADS 512
 #endif
 #ifndef ORBX_INIT_RESOLVE_THREADS
 #define ORBX_INIT_RESOLVE_THREADS 512
