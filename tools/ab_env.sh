@@ -1,6 +1,6 @@
 #!/bin/bash
 # Interleaved pipelined-bench A/B of environment settings (tuning knobs), R rounds.
-# Usage: R=2 tools/ab_env.sh "" "ORBX_INIT_LDS_KB=64" ...
+# Usage: R=2 tools/ab_env.sh "" "ORBX_EXTRACT_ORDER=pfbqo" ...
 cd "$GRAFT_REPO_ROOT"
 for r in $(seq ${R:-2}); do
   for e in "$@"; do
