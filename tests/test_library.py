@@ -126,3 +126,55 @@ def test_prepare_pose_level_mode():
     _lib.check(_lib.lib().orbm_prepare_pose(_lib.ORBM_PROJ_SIM3, C.byref(_lib.camera(700, 700, 600, 180, 0.5, 350, S)),
                                             None, 0, C.byref(p)), matcher=True)
     assert np.allclose(np.array(p.Rt).reshape(3, 4), T)
+
+
+def test_fast_frame_index_magic_is_exact():
+    """FAST's frame index (orbx_fast.hip) is mulhi(id, m) with m = ceil(2^32 / d),
+    d = cells per frame, which orbx_host.hip enables only while
+    d * B * (m * d - 2^32) < 2^32. Checked here at the worst ids (the last
+    id of each frame, where the remainder is d - 1) for every d the planner can
+    produce and the largest B that passes the check, plus a random sample."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    for d in list(range(2, 5001)) + [8191, 12000, 40000]:
+        m = ((1 << 32) + d - 1) // d
+        e = m * d - (1 << 32)
+        bmax = ((1 << 32) - 1) // (d * e) if e else 1 << 20
+        bmax = min(bmax, 1 << 14)
+        if bmax < 1:
+            continue
+        ids = [(q + 1) * d - 1 for q in range(0, bmax, max(1, bmax // 64))] + [d * bmax - 1]
+        ids += [int(x) for x in rng.integers(0, d * bmax, 16)]
+        for i in ids:
+            assert (i * m) >> 32 == i // d, (d, bmax, i)
+
+
+def test_brief_cvround_by_magic_add():
+    """orient_brief_kernel rounds a test coordinate with fl(v + 1.5 * 2^23) and
+    reads the integer from the sum's bit pattern; the reference's cvRound is
+    round-half-even (lrint). Checked in float32 for every coordinate the
+    kernels form: fl(fl(x*b) + fl(y*a)) and fl(fl(x*a) - fl(y*b)) over all
+    512 pattern points (both tables) and 20,000 random (a, b) = (cos, sin)
+    pairs, plus every quarter-integer in [-40, 40]."""
+    import numpy as np
+    from orb_slam_cuda_amd import _lib
+    pts = []
+    for mode in (0, 1):
+        arr = (C.c_int * 1024)()
+        assert _lib.lib().orbx_get_pattern(mode, arr) == 0
+        t = np.frombuffer(arr, dtype=np.int32).reshape(256, 4)
+        pts.append(t[:, 0:2])
+        pts.append(t[:, 2:4])
+    p = np.unique(np.concatenate(pts).astype(np.float32), axis=0)
+    x, y = p[:, 0:1], p[:, 1:2]
+    rng = np.random.default_rng(3)
+    ang = rng.uniform(0, 2 * np.pi, 20000).astype(np.float32)
+    a, b = np.cos(ang).astype(np.float32)[None, :], np.sin(ang).astype(np.float32)[None, :]
+    vy = (x * b).astype(np.float32) + (y * a).astype(np.float32)
+    vx = (x * a).astype(np.float32) - (y * b).astype(np.float32)
+    q = np.arange(-160, 161, dtype=np.float32) / np.float32(4)
+    for v in (vy.ravel(), vx.ravel(), q):
+        v = v.astype(np.float32)
+        s = (v + np.float32(12582912.0)).astype(np.float32)
+        got = s.view(np.int32).astype(np.int64) - 0x4B400000
+        assert np.array_equal(got, np.rint(v).astype(np.int64))
