@@ -166,6 +166,8 @@ def parse_args(argv=None):
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
                     help="stream that copies a batch's last frame for the next batch's first pair")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency leg")
+    ap.add_argument("--no-shim-latency", action="store_true",
+                    help="skip the drop-in C++ shim's per-call latency leg (a child process)")
     ap.add_argument("--no-host-stream", action="store_true", help="skip the host-streamed throughput leg")
     ap.add_argument("--host-steps", type=int, default=30, help="timed steps of the host-streamed leg")
     ap.add_argument("--h2d-mode", choices=["1d", "2d", "kernel"], default="kernel",
@@ -811,8 +813,11 @@ def run_mono(args, cfg, rank, world, local, dist):
     gc.collect()
     lat = host = cpu = cpu1 = tie_rule = None
     solo = world == 1
+    shim_lat = None
     if rank == 0 and solo and not args.no_latency:
         lat = latency_leg(cfg, local, frames[:32], args.no_match)
+        if not args.no_shim_latency and (W, H, NF) == (1241, 376, 2000) and ext_params(cfg)[2] == 8:
+            shim_lat = shim_latency_leg(frames[:32], W, H, local)
     if rank == 0 and solo and not args.no_host_stream and args.host_steps > 0:
         host = host_stream_leg(args, cfg, local, frames)
     if rank == 0 and solo and args.cpu_sample > 0:
@@ -854,6 +859,7 @@ def run_mono(args, cfg, rank, world, local, dist):
             "cpu_baseline": cpu,
             "cpu_baseline_1thread": cpu1,
             "latency": lat,
+            "shim_latency": shim_lat,
             "host_stream": host,
             "quadtree_tie_straddle": tie,
             "tie_rule_disagreement": tie_rule,
@@ -1030,6 +1036,47 @@ def latency_leg(cfg, local, frames, no_match, n=200, warm=20):
         ts = np.array(ts) * 1e3
         out["search_init_ms"] = {"median": round(float(np.median(ts)), 4),
                                  "p99": round(float(np.percentile(ts, 99)), 4), "calls": n}
+    return out
+
+
+SHIM_DRIVER = os.path.join(ROOT, "shim", "build", "orbx_shim_driver")
+
+
+def shim_latency_leg(frames, W, H, local, n=200, warm=20):
+    """The drop-in C++ classes as Tracking calls them, per frame: a fresh child
+    process (shim/build/orbx_shim_driver --latency) times orbx_extract alone,
+    ORBextractor::operator() (src/Frame.cc:246-252; with and without the pinned
+    host mvImagePyramid) and the stereo Frame constructor (two extraction
+    threads + ComputeStereoMatches, src/Frame.cc:60-128) on the host clock,
+    median / p99 over n calls after warm ones. KITTI-shaped mono frames; the
+    stereo pairs are synth.stereo_pair's."""
+    import subprocess
+    import tempfile
+    from orb_slam_cuda_amd.synth import stereo_pair
+    if not os.path.exists(SHIM_DRIVER):
+        return {"error": f"{SHIM_DRIVER} not built (python __graft_entry__.py builds it)"}
+    nf = len(frames)
+    pairs = [stereo_pair(1000 + i, W, H) for i in range(nf)]
+    with tempfile.TemporaryDirectory() as d:
+        paths = [os.path.join(d, x) for x in ("mono.u8", "left.u8", "right.u8")]
+        np.ascontiguousarray(np.stack(frames), np.uint8).tofile(paths[0])
+        np.ascontiguousarray(np.stack([p[0] for p in pairs]), np.uint8).tofile(paths[1])
+        np.ascontiguousarray(np.stack([p[1] for p in pairs]), np.uint8).tofile(paths[2])
+        env = dict(os.environ, ORBX_DEVICE=str(local))
+        try:
+            r = subprocess.run([SHIM_DRIVER, "--latency", *paths, str(nf), str(W), str(H), str(n), str(warm)],
+                               capture_output=True, text=True, timeout=300, env=env)
+        except subprocess.TimeoutExpired:
+            return {"error": "shim driver timed out (300 s)"}
+    if r.returncode != 0:
+        return {"error": f"shim driver rc {r.returncode}: {r.stderr.strip()[-300:]}"}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    base = out["orbx_extract_ms"]["median"]
+    out["operator_over_orbx_extract"] = round(out["operator_ms"]["median"] / base, 3)
+    out["stereo_frame_over_operator"] = round(out["stereo_frame_ms"]["median"] / out["operator_ms"]["median"], 3)
+    out["what"] = ("child process, host clock per call: orbx_extract (C-ABI, host buffers); "
+                   "ORBextractor::operator() with the pinned host mvImagePyramid (default) and without; "
+                   "stereo Frame = two operator() threads + ComputeStereoMatches on the device outputs")
     return out
 
 

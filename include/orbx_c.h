@@ -21,6 +21,8 @@
  *   orbx_get_levels_info   GetLevels + per-level sizes / mnFeaturesPerLevel
  *   orbx_get_level         public mvImagePyramid[level]  include/ORBextractor.h:116
  *                          (read by Frame::ComputeStereoMatches src/Frame.cc:472,562,579)
+ *   orbx_set_host_pyramid / orbx_get_host_pyramid  the same, filled by
+ *                          orbx_extract itself into pinned memory (opt-in)
  *   orbm_descriptor_distance  ORBmatcher::DescriptorDistance
  *                          include/ORBmatcher.h:44, src/ORBmatcher.cc:1647-1663
  *   orbm_search_for_initialization  ORBmatcher::SearchForInitialization
@@ -155,9 +157,25 @@ int orbx_get_levels_info(orbx_handle h, int* nlevels, int* level_w,
                          int* level_h, int* nfeatures_per_level);
 /* Copy pyramid level `level` of frame `frame` of the last extraction to host
  * (mvImagePyramid). `blurred`=1 returns the 7x7 Gaussian-blurred level used
- * for the descriptors instead (stage probe). */
+ * for the descriptors instead (stage probe). Waits for the handle's own last
+ * launch only (not the device); served from the host pyramid below when that
+ * holds the level. */
 int orbx_get_level(orbx_handle h, int frame, int level, int blurred,
                    uint8_t* out, size_t out_stride);
+/* Host pyramid: the reference's public mvImagePyramid (include/ORBextractor.h:116),
+ * filled in place by ComputePyramid (src/ORBextractor.cc:1837-1863) and read
+ * by Frame::ComputeStereoMatches (src/Frame.cc:472,562,579). With enable != 0
+ * every later orbx_extract also leaves its frame's pyramid in handle-owned
+ * pinned host memory: the levels >= 1 are copied on a branch of the call's
+ * graph forked right after the pyramid kernel (the copy overlaps FAST ..
+ * BRIEF), level 0 is the call's own pinned input staging. Off by default. */
+int orbx_set_host_pyramid(orbx_handle h, int enable);
+/* The host pyramid of the last orbx_extract: levels[l] / pitches[l] (bytes
+ * between rows) for l < nlevels, valid until the next extraction on the
+ * handle (as the reference's buffers are until its next operator() call).
+ * ORBX_EINVAL when it is off or the last extraction was a batch call. */
+int orbx_get_host_pyramid(orbx_handle h, const uint8_t** levels, size_t* pitches,
+                          int cap_levels);
 /* Stage probe: FAST + per-cell NMS candidates of (frame, level) of the last
  * extraction, in reference order, as keypoints (x,y relative to the border
  * box, response = FAST score). */
@@ -215,16 +233,14 @@ int orbm_create(int device, int max_pairs, int max_kps, orbm_handle* out);
 int orbm_destroy(orbm_handle m);
 
 /* Device status word of the matcher's batched kernels since the last call
- * (0 = ok; bit 8: SearchForInitialization candidate overflow, that pair got
- * no matches; bit 16: orbm_hamming_top2 input over its limits, nA[p] > a_cap
+ * (0 = ok; bit 16: orbm_hamming_top2 input over its limits, nA[p] > a_cap
  * or nB[p] > 65535, the excess rows / candidates were not searched; bit 32:
  * orbm_search_by_bow_batch saw a count above kp_pitch or a FeatureVector
- * index outside [0, n), which was skipped). SearchForInitialization's
- * candidate lists hold every keypoint of each query's window cells (before
- * the |dx|, |dy| < r test): up to min(max_kps^2, 4M) entries per pair in the
- * global fallback, past which bit 8 is set. Waits
- * for the device; `reset` != 0 clears it. The synchronous entry points check
- * and clear it themselves.
+ * index outside [0, n), which was skipped). SearchForInitialization keeps no
+ * candidate lists (8 smallest keys per query) and never sets it. Waits for
+ * the matcher's own launches that may set it (on whatever streams they ran),
+ * not for the device; `reset` != 0 clears it. The synchronous entry points
+ * check and clear it themselves.
  *
  * Device workspaces (candidate lists, stereo SAD, pose picks, SearchByBoW row
  * records and histograms) belong to the
@@ -259,8 +275,8 @@ typedef struct orbm_grid_bounds {
 /* ORBmatcher::SearchForInitialization on host buffers (synchronous).
  * prev_xy: 2*n1 floats, vbPrevMatched, updated in place. matches12: n1.
  * n1 / n2 are not bounded by the matcher's max_kps: only octave-0 keypoints
- * take part (compacted on the host; up to 10,000 per frame, the resolve
- * kernel's LDS tables), and the kernels keep no candidate lists, so any
+ * take part (compacted on the host; up to the batch call's bound below per
+ * frame: 10,192 at the reference's 0.9, 8192 at 0.7), and the kernels keep no candidate lists, so any
  * window density is matched, never refused for want of scratch. */
 int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1,
                                    const uint8_t* desc1, int n1,
@@ -276,8 +292,13 @@ int orbm_search_for_initialization(orbm_handle m, const orbx_kp* kp1,
  * windows on F1's own keypoints (the initial mvbPrevMatched of
  * Tracking::MonocularInitialization, src/Tracking.cc:645-647; nothing is
  * written back then); d_matches12: pairs x kp_pitch; d_nmatches: pairs.
- * kp_pitch <= min(max_kps, 10,000); any window density is matched (the
- * kernels keep each query's 4 smallest keys, not its candidate list). */
+ * kp_pitch <= min(max_kps, 10,192, 2^(20 - dbits)); any window density is
+ * matched (the kernels keep each query's 8 smallest keys, kInitK, not its
+ * candidate list). 10,192 is the resolve kernel's LDS; dbits depends on
+ * nnratio: distances are clamped to 2^dbits - 1 with the smallest dbits in
+ * 6..9 for which nnratio * (2^dbits - 1) > 50, so the bound is 10,192 for
+ * nnratio > 0.794, 8192 above 0.394, 4096 above 0.196 and 2048 below.
+ * ECAPACITY's message names the bound that applied. */
 int orbm_search_for_initialization_batch(
     orbm_handle m, const orbx_kp* d_kp1, const uint8_t* d_desc1,
     const int* d_n1, const orbx_kp* d_kp2, const uint8_t* d_desc2,
@@ -543,6 +564,15 @@ int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle rig
                                 const orbx_kp* kpR, const uint8_t* descR, int nR,
                                 float mb, float mbf, float* uRight, float* depth,
                                 int* nkept);
+/* The same for the frames of the two handles' last orbx_extract calls, as the
+ * stereo Frame constructor runs it right after its two extractions
+ * (src/Frame.cc:77-89): keypoints and descriptors are read where those calls
+ * left them on the device (no host-to-device copy). nL = the left call's
+ * keypoint count (mvKeys.size()); outputs as above. ORBX_EINVAL when either
+ * handle's last extraction was a batch call. */
+int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handle right,
+                                     float mb, float mbf, float* uRight, float* depth,
+                                     int nL, int* nkept);
 
 /* Batched device-resident variant: pair p = left frame (left_frame0 + p) of
  * `left`'s last orbx_extract_batch and right frame (right_frame0 + p) of

@@ -98,6 +98,8 @@ def lib() -> C.CDLL:
         L.orbx_get_scales.argtypes = [C.c_void_p] + [C.c_void_p] * 4
         L.orbx_get_levels_info.argtypes = [C.c_void_p] + [C.c_void_p] * 4
         L.orbx_get_level.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t]
+        L.orbx_set_host_pyramid.argtypes = [C.c_void_p, C.c_int]
+        L.orbx_get_host_pyramid.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.orbx_get_fast_candidates.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
                                                C.POINTER(C.c_int)]
         L.orbx_get_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
@@ -128,6 +130,9 @@ def lib() -> C.CDLL:
         L.orbm_compute_stereo_matches.argtypes = [
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
             C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
+        L.orbm_compute_stereo_matches_last.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_int,
+            C.POINTER(C.c_int)]
         L.orbm_compute_stereo_matches_batch.argtypes = [
             C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_void_p,

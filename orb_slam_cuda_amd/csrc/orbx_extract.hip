@@ -17,7 +17,7 @@ namespace orbx {
 
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames, int batch,
                    size_t frame_pitch, size_t row_stride, orbx_kp* d_kps, uint8_t* d_desc, int* d_counts,
-                   void* stream_, void** ev) {
+                   void* stream_, void** ev, void* pyr_event) {
   hipStream_t stream = (hipStream_t)stream_;
   ExtractParams Q = P;
   Q.B = batch;
@@ -57,6 +57,8 @@ int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_
       default: rc = launch_orient_brief(Q, lp, X, d_kps, d_desc, d_counts, batch, stream); break;
     }
     if (rc) return rc;
+    if (order[i] == 'p' && pyr_event && hipEventRecord((hipEvent_t)pyr_event, stream) != hipSuccess)
+      return ORBX_EDEVICE;
     rec(i + 1);
   }
   return ORBX_OK;

@@ -51,6 +51,10 @@ extern int pyr_band_occupancy(size_t lds);
 
 using namespace orbx;
 
+// offset of the descriptors in orbx_extract's output block (16-byte aligned
+// for orient_brief's 16-byte stores)
+static size_t out_desc_off(int cap_frame) { return (16 + (size_t)cap_frame * sizeof(orbx_kp) + 15) & ~(size_t)15; }
+
 static thread_local std::string g_err;
 static int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -116,6 +120,8 @@ struct orbx_extractor {
   size_t h_in_bytes = 0, h_out_bytes = 0;
   hipGraphExec_t graph = nullptr;
   int graph_w = 0, graph_h = 0;
+  bool graph_hp = false;  // the graph holds the host-pyramid copy branch
+  bool last_single = false;  // the last extraction was orbx_extract (outputs in d_out)
   int warm_w = 0, warm_h = 0;  // size of the last plain (uncaptured) call: capture from the next one
   int last_batch = 0;
   const uint8_t* last_frames = nullptr;
@@ -125,6 +131,17 @@ struct orbx_extractor {
   void* user_ev[ORBX_STAGE_EVENTS] = {};
   bool has_user_ev = false;
   WsOrder ws;  // stream order of the plan buffers (pyramid, blur, slots, quadtree)
+  // host pyramid (orbx_set_host_pyramid): orbx_extract also copies levels >= 1
+  // of its frame into pinned memory, on a graph branch forked right after the
+  // pyramid stage and joined at the end of the call (the copy overlaps FAST ..
+  // BRIEF); level 0 is the pinned input staging itself
+  bool host_pyr = false;
+  bool host_pyr_valid = false;  // h_pyr holds the last orbx_extract's levels
+  void* h_pyr = nullptr;
+  size_t h_pyr_bytes = 0;
+  long long h_pyr_off[kMaxLevels] = {};  // level l's offset in h_pyr (l >= 1)
+  hipStream_t pstream = nullptr;         // the copy branch's stream (capture fork)
+  hipEvent_t pev[2] = {};                // pyramid done, copy done
   std::mutex mu;
 };
 
@@ -571,6 +588,20 @@ int orbx::extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int
   return ORBX_OK;
 }
 
+int orbx::extractor_last_output(orbx_handle h, const int** d_count, const orbx_kp** d_kps, const uint8_t** d_desc,
+                                int* cap) {
+  if (!h) return fail(ORBX_EINVAL, "null extractor handle");
+  if (!h->last_single || !h->d_out.p)
+    return fail(ORBX_EINVAL, "the extractor's last extraction was not an orbx_extract call");
+  const int c = h->plan.P.kp_per_frame;
+  uint8_t* d = h->d_out.as<uint8_t>();
+  *d_count = (const int*)d;
+  *d_kps = (const orbx_kp*)(d + 16);
+  *d_desc = d + out_desc_off(c);
+  *cap = c;
+  return ORBX_OK;
+}
+
 // Dynamic-LDS limits are per kernel and device, shared by every handle of the
 // process: only ever raise them (a handle with a smaller plan must not lower
 // the limit a larger one launches with).
@@ -649,8 +680,13 @@ int orbx_destroy(orbx_handle h) {
   if (h->ws.ev) (void)hipEventSynchronize(h->ws.ev);
   h->ws.release();
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
+  if (h->pstream) (void)hipStreamSynchronize(h->pstream);
   if (h->h_in) (void)hipHostFree(h->h_in);
   if (h->h_out) (void)hipHostFree(h->h_out);
+  if (h->h_pyr) (void)hipHostFree(h->h_pyr);
+  for (auto& e : h->pev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->pstream) (void)hipStreamDestroy(h->pstream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return ORBX_OK;
@@ -674,6 +710,8 @@ int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch, size_t
   h->last_frames = d_frames;
   h->last_fpitch = frame_pitch;
   h->last_rstride = row_stride;
+  h->host_pyr_valid = false;  // the pinned host pyramid is of an earlier orbx_extract
+  h->last_single = false;
   if (rc) return fail(rc, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
 }
@@ -695,23 +733,52 @@ static int host_reserve(void** p, size_t* have, size_t need) {
   return ORBX_OK;
 }
 
-// offset of the descriptors in orbx_extract's output block (16-byte aligned
-// for orient_brief's 16-byte stores)
-static size_t out_desc_off(int cap_frame) { return (16 + (size_t)cap_frame * sizeof(orbx_kp) + 15) & ~(size_t)15; }
+
+// Host-pyramid layout: frame 0's levels 1..L-1 packed at their device pitches.
+// With max_batch 1 the device planes of levels >= 1 are one contiguous block
+// (level-major [l][B][h][pitch]), so the copy is one linear D2H.
+static size_t host_pyr_layout(orbx_extractor* h) {
+  const ExtractParams& P = h->plan.P;
+  size_t off = 0;
+  for (int l = 1; l < P.L; ++l) {
+    h->h_pyr_off[l] = (long long)off;
+    off += (size_t)P.lv[l].plane;
+  }
+  return off;
+}
 
 static int issue_one_frame(orbx_extractor* h, size_t pitch, int hh, int cap_frame) {
   hipStream_t s = h->stream;
   HIP_OK(hipMemcpyAsync(h->d_in.p, h->h_in, pitch * hh, hipMemcpyHostToDevice, s));
   uint8_t* d = h->d_out.as<uint8_t>();
   const size_t doff = out_desc_off(cap_frame);
-  const int rc = launch_extract(h->plan.P, buffers_of(h->plan), h->d_in.as<uint8_t>(), 1, pitch * hh, pitch,
-                                (orbx_kp*)(d + 16), d + doff, (int*)d, s, h->timing ? (void**)h->ev : nullptr);
+  const ExtractParams& P = h->plan.P;
+  const bool hp = h->host_pyr && P.L > 1;
+  const int rc = launch_extract(P, buffers_of(h->plan), h->d_in.as<uint8_t>(), 1, pitch * hh, pitch,
+                                (orbx_kp*)(d + 16), d + doff, (int*)d, s, h->timing ? (void**)h->ev : nullptr,
+                                hp ? (void*)h->pev[0] : nullptr);
   if (rc) return fail(rc, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+  if (hp) {
+    // fork: the pyramid levels go to pinned host memory beside FAST .. BRIEF
+    HIP_OK(hipStreamWaitEvent(h->pstream, h->pev[0], 0));
+    const uint8_t* pyr = h->plan.pyr.as<uint8_t>();
+    uint8_t* hpyr = (uint8_t*)h->h_pyr;
+    if (h->plan.B == 1) {
+      const size_t bytes = (size_t)(P.lv[P.L - 1].off + P.lv[P.L - 1].plane - P.lv[1].off);
+      HIP_OK(hipMemcpyAsync(hpyr, pyr + P.lv[1].off, bytes, hipMemcpyDeviceToHost, h->pstream));
+    } else {
+      for (int l = 1; l < P.L; ++l)
+        HIP_OK(hipMemcpyAsync(hpyr + h->h_pyr_off[l], pyr + P.lv[l].off, (size_t)P.lv[l].plane,
+                              hipMemcpyDeviceToHost, h->pstream));
+    }
+    HIP_OK(hipEventRecord(h->pev[1], h->pstream));
+  }
   // count, keypoints and descriptors in one copy, then the status word over
   // bytes 4..7 of the block's header (same stream: in this order)
   uint8_t* o = (uint8_t*)h->h_out;
   HIP_OK(hipMemcpyAsync(o, d, doff + (size_t)cap_frame * 32, hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(o + 4, h->plan.err.p, 4, hipMemcpyDeviceToHost, s));
+  if (hp) HIP_OK(hipStreamWaitEvent(s, h->pev[1], 0));  // join
   return ORBX_OK;
 }
 
@@ -754,6 +821,16 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
       (rc = host_reserve(&h->h_out, &h->h_out_bytes, out_bytes)))
     return rc;
   if (!h->stream) HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  h->host_pyr_valid = false;
+  if (h->graph && h->graph_hp != h->host_pyr) drop_graph();  // captured with / without the copy branch
+  if (h->host_pyr) {
+    const size_t pb = host_pyr_layout(h);
+    if (h->h_pyr_bytes < pb) drop_graph();
+    if ((rc = host_reserve(&h->h_pyr, &h->h_pyr_bytes, std::max<size_t>(pb, 64)))) return rc;
+    if (!h->pstream) HIP_OK(hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking));
+    for (auto& e : h->pev)
+      if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   for (int y = 0; y < hh; ++y) memcpy((uint8_t*)h->h_in + (size_t)y * pitch, img + (size_t)y * stride, w);
   // the plan buffers may still be in use by a batch call on another stream
   if (h->ws.before(h->stream)) return fail(ORBX_EDEVICE, "stream wait on the handle's last use failed");
@@ -781,6 +858,7 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
       }
       h->graph_w = w;
       h->graph_h = hh;
+      h->graph_hp = h->host_pyr;
     }
     HIP_OK(hipGraphLaunch(h->graph, h->stream));
   } else {
@@ -790,10 +868,12 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   }
   if (h->ws.after(h->stream)) return fail(ORBX_EDEVICE, "event record failed");
   h->last_batch = 1;
+  h->last_single = true;
   h->last_frames = h->d_in.as<uint8_t>();
   h->last_fpitch = pitch * hh;
   h->last_rstride = pitch;
   HIP_OK(hipStreamSynchronize(h->stream));
+  h->host_pyr_valid = h->host_pyr;
   const int* head = (const int*)h->h_out;
   const int cnt = head[0], err = head[1];
   if (err) {
@@ -837,14 +917,61 @@ int orbx_get_levels_info(orbx_handle h, int* nlevels, int* lw, int* lh, int* nf)
   return ORBX_OK;
 }
 
+// Synchronous reads of a handle's buffers wait for the handle's own last
+// launch (its workspace event, recorded on whatever stream that launch used),
+// never for the whole device: another handle's work (the other extractor of a
+// stereo pair, on another thread) goes on. The copies run on the handle's stream.
+static int handle_quiesce(orbx_extractor* h) {
+  HIP_OK(hipSetDevice(h->cfg.device));
+  if (h->ws.used) HIP_OK(hipEventSynchronize(h->ws.ev));
+  if (!h->stream) HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  return ORBX_OK;
+}
+static int handle_d2h(orbx_extractor* h, void* dst, const void* src, size_t bytes) {
+  HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return ORBX_OK;
+}
+
+int orbx_set_host_pyramid(orbx_handle h, int enable) {
+  if (!h) return fail(ORBX_EINVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->host_pyr = enable != 0;
+  h->host_pyr_valid = false;
+  return ORBX_OK;
+}
+
+int orbx_get_host_pyramid(orbx_handle h, const uint8_t** levels, size_t* pitches, int cap_levels) {
+  if (!h || !levels || !pitches) return fail(ORBX_EINVAL, "null argument");
+  const ExtractParams& P = h->plan.P;
+  if (cap_levels < P.L) return fail(ORBX_ECAPACITY, "%d levels do not fit %d entries", P.L, cap_levels);
+  if (!h->host_pyr_valid)
+    return fail(ORBX_EINVAL, "no host pyramid: enable it (orbx_set_host_pyramid) before an orbx_extract call");
+  const size_t pitch0 = ((size_t)P.lv[0].w + 63) & ~(size_t)63;  // orbx_extract's staging pitch
+  levels[0] = (const uint8_t*)h->h_in;
+  pitches[0] = pitch0;
+  for (int l = 1; l < P.L; ++l) {
+    levels[l] = (const uint8_t*)h->h_pyr + h->h_pyr_off[l];
+    pitches[l] = (size_t)P.lv[l].pitch;
+  }
+  return ORBX_OK;
+}
+
 int orbx_get_level(orbx_handle h, int frame, int level, int blurred, uint8_t* out, size_t out_stride) {
   if (!h || !out) return fail(ORBX_EINVAL, "null argument");
   const Plan& pl = h->plan;
   if (level < 0 || level >= pl.P.L || frame < 0 || frame >= h->last_batch)
     return fail(ORBX_EINVAL, "no such frame/level");
-  HIP_OK(hipSetDevice(h->cfg.device));
-  HIP_OK(hipDeviceSynchronize());  // the last extraction may have run on a caller stream
   const LevelGeom& g = pl.P.lv[level];
+  if (h->host_pyr_valid && !blurred && frame == 0) {
+    // the pinned copy orbx_extract already made
+    const uint8_t* lv[kMaxLevels];
+    size_t lp[kMaxLevels];
+    if (int rc = orbx_get_host_pyramid(h, lv, lp, kMaxLevels)) return rc;
+    for (int y = 0; y < g.h; ++y) memcpy(out + (size_t)y * out_stride, lv[level] + (size_t)y * lp[level], g.w);
+    return ORBX_OK;
+  }
+  if (int rc = handle_quiesce(h)) return rc;
   const ExtractBuffers X = buffers_of(pl);
   const uint8_t* src;
   size_t spitch;
@@ -858,7 +985,8 @@ int orbx_get_level(orbx_handle h, int frame, int level, int blurred, uint8_t* ou
     src = X.pyr + g.off + (long long)frame * g.plane;
     spitch = g.pitch;
   }
-  HIP_OK(hipMemcpy2D(out, out_stride, src, spitch, g.w, g.h, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy2DAsync(out, out_stride, src, spitch, g.w, g.h, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
   return ORBX_OK;
 }
 
@@ -867,15 +995,16 @@ int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out, 
   const Plan& pl = h->plan;
   if (level < 0 || level >= pl.P.L || frame < 0 || frame >= h->last_batch)
     return fail(ORBX_EINVAL, "no such frame/level");
-  HIP_OK(hipSetDevice(h->cfg.device));
-  HIP_OK(hipDeviceSynchronize());  // the last extraction may have run on a caller stream
+  if (int rc = handle_quiesce(h)) return rc;
   const LevelGeom& g = pl.P.lv[level];
   std::vector<int> cnt(g.ncells);
   std::vector<uint32_t> slots(std::max(g.nslots, 1));
-  HIP_OK(hipMemcpy(cnt.data(), pl.cell_counts.as<int>() + (size_t)frame * pl.P.ncells_total + g.cell0,
-                   g.ncells * 4, hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(slots.data(), pl.slots.as<uint32_t>() + (size_t)frame * pl.P.slots_per_frame + g.slot0,
-                   (size_t)g.nslots * 4, hipMemcpyDeviceToHost));
+  if (int rc = handle_d2h(h, cnt.data(), pl.cell_counts.as<int>() + (size_t)frame * pl.P.ncells_total + g.cell0,
+                          g.ncells * 4))
+    return rc;
+  if (int rc = handle_d2h(h, slots.data(), pl.slots.as<uint32_t>() + (size_t)frame * pl.P.slots_per_frame + g.slot0,
+                          (size_t)g.nslots * 4))
+    return rc;
   int k = 0;
   for (int c = 0; c < g.ncells; ++c) {
     const CellGeom& cg = pl.cells[g.cell0 + c];
@@ -892,13 +1021,13 @@ int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out, 
 
 int orbx_get_status(orbx_handle h, int reset, int* status) {
   if (!h || !status) return fail(ORBX_EINVAL, "null argument");
-  HIP_OK(hipSetDevice(h->cfg.device));
-  if (h->ws.ev) HIP_OK(hipEventSynchronize(h->ws.ev));
+  if (int rc = handle_quiesce(h)) return rc;
   int e = 0;
-  HIP_OK(hipMemcpy(&e, h->plan.err.p, 4, hipMemcpyDeviceToHost));
+  if (int rc = handle_d2h(h, &e, h->plan.err.p, 4)) return rc;
   // cleared on the handle's stream, ordered after the batches that set it
   if (reset && e) {
     HIP_OK(hipMemsetAsync(h->plan.err.p, 0, 16, h->stream));
+    if (h->ws.after(h->stream)) return fail(ORBX_EDEVICE, "event record failed");
     HIP_OK(hipStreamSynchronize(h->stream));
   }
   *status = e;
@@ -912,11 +1041,10 @@ int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out) {
   if (frame0 < 0 || nframes < 1 || frame0 + nframes > h->last_batch)
     return fail(ORBX_EINVAL, "frames [%d, %d) not in the last extraction (%d frames)", frame0, frame0 + nframes,
                 h->last_batch);
-  HIP_OK(hipSetDevice(h->cfg.device));
-  HIP_OK(hipDeviceSynchronize());  // the last extraction may have run on a caller stream
+  if (int rc = handle_quiesce(h)) return rc;
   const int L = pl.P.L;
   std::vector<int> t((size_t)nframes * L * 4);
-  HIP_OK(hipMemcpy(t.data(), pl.qties.as<int>() + (size_t)frame0 * L * 4, t.size() * 4, hipMemcpyDeviceToHost));
+  if (int rc = handle_d2h(h, t.data(), pl.qties.as<int>() + (size_t)frame0 * L * 4, t.size() * 4)) return rc;
   for (size_t i = 0; i < (size_t)nframes * L; ++i)
     for (int k = 0; k < 3; ++k) out[i * 3 + k] = t[i * 4 + k];
   return ORBX_OK;

@@ -81,7 +81,9 @@ constexpr uint32_t kKeyNone = 0xFFFFFFFFu;
 // Per-pair workspace, ints: [0..64] column starts (64 = records in the grid),
 // [66] queries, [67] octave-0 F2 keypoints; then, for K = kp_pitch: records
 // (4K: x, y, key base, cell row), descriptors (8K), o2 -> i2 (K), query -> i1
-// (K), keys (kInitK K), candidate counts (K).
+// (K), keys (kInitK K), candidate counts (K). The two K-int tables are padded
+// to Kp = K rounded up to 4 ints, so `keys` stays 16-byte aligned (dwordx4)
+// for any (odd) pitch.
 struct InitWs {
   int* hdr;
   uint4* rec;
@@ -99,10 +101,11 @@ __device__ __forceinline__ InitWs init_ws(int* base, int K) {
   p += 4 * (size_t)K;
   w.desc = (uint4*)p;
   p += 8 * (size_t)K;
+  const size_t Kp = ((size_t)K + 3) & ~(size_t)3;
   w.o2map = p;
-  p += K;
+  p += Kp;
   w.qi = p;
-  p += K;
+  p += Kp;
   w.keys = (uint4*)p;
   p += (size_t)kInitK * K;
   w.qcnt = p;
@@ -110,7 +113,8 @@ __device__ __forceinline__ InitWs init_ws(int* base, int K) {
 }
 
 size_t init_ws_bytes_per_pair(int kp_pitch) {
-  return ((68 + (size_t)kp_pitch * (4 + 8 + 1 + 1 + kInitK + 1)) * 4 + 255) & ~(size_t)255;
+  const size_t Kp = ((size_t)kp_pitch + 3) & ~(size_t)3;
+  return ((68 + (size_t)kp_pitch * (4 + 8 + kInitK + 1) + 2 * Kp) * 4 + 255) & ~(size_t)255;
 }
 
 // Frame::PosInGrid: round() of a float, half away from zero
@@ -492,37 +496,37 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
     }
     __syncthreads();
     int changed = 0;
-    for (int q = tid, j = 0; q < nq; q += NT, ++j) {
-      uint32_t key[kInitK];
-      int qc;
-      if (j < kInitKeyRegs) {
-#pragma unroll
-        for (int u = 0; u < kInitK; ++u) key[u] = kreg[j][u];
-        qc = creg[j];
-      } else {
-        load_keys(w, q, key);
-        qc = w.qcnt[q];
-      }
+    auto visit = [&](int q, const uint32_t* key, int qc) {
       uint32_t k1 = kKeyNone, k2 = kKeyNone;
       int found = 0;
 #pragma unroll
-      for (int j = 0; j < kInitK; ++j) {
-        if (found == 2 || key[j] == kKeyNone) continue;
-        const int d = (int)(key[j] >> P.dshift), o2 = (int)(key[j] & P.omask);
+      for (int u = 0; u < kInitK; ++u) {
+        if (found == 2 || key[u] == kKeyNone) continue;
+        const int d = (int)(key[u] >> P.dshift), o2 = (int)(key[u] & P.omask);
         if (init_claim_md(head, nxt, o2, q) <= d) continue;  // (:444-445)
-        if (found == 0) k1 = key[j];
-        else k2 = key[j];
+        if (found == 0) k1 = key[u];
+        else k2 = key[u];
         ++found;
       }
       if (found < 2 && qc > kInitK) {
         queue[lds_atomic_add(&var[7], 1)] = q;  // keys ran out: a wave rescans the window
-        continue;
+        return;
       }
       const int r = init_decide(k1, k2, P);
       if (res[q] != r) {
         res[q] = r;
         changed = 1;
       }
+    };
+    // the register-held queries with compile-time indices (no dynamic
+    // register indexing, which would go through scratch), then the rest
+#pragma unroll
+    for (int j = 0; j < kInitKeyRegs; ++j)
+      if (tid + j * NT < nq) visit(tid + j * NT, kreg[j], creg[j]);
+    for (int q = tid + kInitKeyRegs * NT; q < nq; q += NT) {
+      uint32_t key[kInitK];
+      load_keys(w, q, key);
+      visit(q, key, w.qcnt[q]);
     }
     __syncthreads();
     const int nrs = var[7];
@@ -702,14 +706,27 @@ __global__ __launch_bounds__(kInitResolveThreads) void search_init_resolve_kerne
 
 static size_t init_resolve_lds_bytes(int kp_pitch) { return (size_t)kp_pitch * 16 + 256; }
 
+static int init_dbits(float nnratio) {
+  int dbits = 6;
+  while (dbits < 9 && !((float)((1 << dbits) - 1) * nnratio > (float)kInitThLow)) ++dbits;
+  return dbits;
+}
+
+// The largest kp_pitch launch_search_init accepts at this nnratio: o2 must fit
+// the key's 20 - dbits bits, the resolve kernel's tables one workgroup's LDS.
+int search_init_max_pitch(float nnratio) {
+  const int by_key = 1 << (20 - init_dbits(nnratio));
+  const int by_lds = (int)((kInitLdsBudget - 256) / 16);
+  return std::min(by_key, by_lds);
+}
+
 int launch_search_init(const InitParams& P0, const orbx_kp* kp1, const uint8_t* desc1, const int* n1,
                        const orbx_kp* kp2, const uint8_t* desc2, const int* n2, float* prev, int* ws,
                        int* matches12, int* nmatches, int pairs, void* stream) {
   InitParams P = P0;
   // the key layout for this ratio: the fewest distance bits whose clamp value
   // still passes the ratio test for every acceptable best (see the header)
-  int dbits = 6;
-  while (dbits < 9 && !((float)((1 << dbits) - 1) * P.nnratio > (float)kInitThLow)) ++dbits;
+  const int dbits = init_dbits(P.nnratio);
   P.dshift = 32 - dbits;
   P.obits = 20 - dbits;
   P.omask = (1u << P.obits) - 1;

@@ -152,9 +152,12 @@ struct ExtractBuffers {
   int* err;            // device error word
 };
 
+// pyr_event (optional): recorded on `stream` right after the pyramid stage, so
+// a caller can fork work that only needs the pyramid (orbx_extract's host copy)
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames,
                    int batch, size_t frame_pitch, size_t row_stride, orbx_kp* d_kps,
-                   uint8_t* d_desc, int* d_counts, void* stream, void** stage_events);
+                   uint8_t* d_desc, int* d_counts, void* stream, void** stage_events,
+                   void* pyr_event = nullptr);
 
 // orbx_match.hip
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap,
@@ -192,6 +195,7 @@ struct InitParams {
 };
 constexpr size_t kInitLdsBudget = 160 * 1024 - 512;
 size_t init_ws_bytes_per_pair(int kp_pitch);
+int search_init_max_pitch(float nnratio);  // kp_pitch bound of launch_search_init at this ratio
 int launch_search_init(const InitParams& P, const orbx_kp* kp1, const uint8_t* desc1, const int* n1,
                        const orbx_kp* kp2, const uint8_t* desc2, const int* n2, float* prev, int* ws,
                        int* matches12, int* nmatches, int pairs, void* stream);
@@ -267,9 +271,52 @@ struct WsOrder {
     used = false;
   }
 };
+// The streams a handle's status-word writers last ran on, each with an event
+// recorded after its last such launch: a status poll waits for these events,
+// not for the device (other handles' and threads' work goes on).
+struct StreamMarks {
+  static constexpr int kMax = 16;
+  hipStream_t s[kMax] = {};
+  hipEvent_t ev[kMax] = {};
+  int n = 0;
+  int mark(hipStream_t st) {
+    int i = 0;
+    while (i < n && s[i] != st) ++i;
+    if (i == n) {
+      if (n == kMax) {  // forget the oldest stream after waiting for it
+        if (hipEventSynchronize(ev[0]) != hipSuccess) return ORBX_EDEVICE;
+        hipEvent_t e0 = ev[0];
+        for (int k = 1; k < n; ++k) { s[k - 1] = s[k]; ev[k - 1] = ev[k]; }
+        ev[n - 1] = e0;
+        i = n - 1;
+      } else {
+        if (!ev[i] && hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return ORBX_EDEVICE;
+        ++n;
+      }
+      s[i] = st;
+    }
+    return hipEventRecord(ev[i], st) == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+  }
+  int wait() {
+    for (int i = 0; i < n; ++i)
+      if (hipEventSynchronize(ev[i]) != hipSuccess) return ORBX_EDEVICE;
+    return ORBX_OK;
+  }
+  void release() {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : ev) e = nullptr;
+    n = 0;
+  }
+};
 // orbx_host.hip: the workspace order of an extractor (its pyramid is read by
 // the stereo matcher)
 WsOrder* extractor_ws(orbx_handle h);
+// orbx_host.hip: where the handle's last orbx_extract left its frame's
+// outputs on the device (count, keypoints at a pitch of `cap`, descriptors);
+// ORBX_EINVAL when the last extraction was not an orbx_extract call
+int extractor_last_output(orbx_handle h, const int** d_count, const orbx_kp** d_kps, const uint8_t** d_desc,
+                          int* cap);
 // orbx_host.hip: raise a kernel's dynamic-LDS limit on the current device to at
 // least `bytes` (never lowers it; process-wide, thread-safe)
 int raise_lds_limit(const void* fn, size_t bytes);

@@ -1511,6 +1511,7 @@ struct orbx_matcher {
   size_t pose_picks_cap = 0;
   hipStream_t stream = nullptr;
   WsOrder ws;  // stream order of cand / stereo_sad / pose_picks / bow_* across caller streams
+  StreamMarks errm;  // streams of the launches that may set `err` (top-2, SearchByBoW)
   // staging for the synchronous entry points
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -1547,7 +1548,8 @@ static int search_init_launch(orbx_matcher* m, const orbx_kp* d_kp1, const uint8
                                     d_nmatches, pairs, stream);
   if (!rc && m->ws.after((hipStream_t)stream)) return mfail(ORBX_EDEVICE, "event record failed");
   if (rc == ORBX_ECAPACITY)
-    return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization (<= 10,000)", kp_pitch);
+    return mfail(ORBX_ECAPACITY, "kp_pitch %d too large for SearchForInitialization at nnratio %g (<= %d)", kp_pitch,
+                 (double)nnratio, search_init_max_pitch(nnratio));
   if (rc) return mfail(ORBX_EDEVICE, "search_init launch: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
 }
@@ -1583,6 +1585,8 @@ int orbm_destroy(orbm_handle m) {
   if (m->stream) (void)hipStreamSynchronize(m->stream);
   if (m->ws.ev) (void)hipEventSynchronize(m->ws.ev);
   m->ws.release();
+  (void)m->errm.wait();
+  m->errm.release();
   if (m->init_ws) (void)hipFree(m->init_ws);
   if (m->host_init_ws) (void)hipFree(m->host_init_ws);
   if (m->err) (void)hipFree(m->err);
@@ -1599,12 +1603,16 @@ int orbm_destroy(orbm_handle m) {
 int orbm_get_status(orbm_handle m, int reset, int* status) {
   if (!m || !status) return mfail(ORBX_EINVAL, "null argument");
   MHIP(hipSetDevice(m->device));
-  MHIP(hipDeviceSynchronize());  // the matcher's kernels run on caller streams
+  // the kernels that set the word ran on caller streams: wait for those
+  // launches (their stream marks), not for the device
+  if (m->errm.wait()) return mfail(ORBX_EDEVICE, "status: event wait failed");
+  if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
   int e = 0;
-  MHIP(hipMemcpy(&e, m->err, 4, hipMemcpyDeviceToHost));
+  MHIP(hipMemcpyAsync(&e, m->err, 4, hipMemcpyDeviceToHost, m->stream));
+  MHIP(hipStreamSynchronize(m->stream));
   if (reset && e) {
-    MHIP(hipMemsetAsync(m->err, 0, 16, nullptr));
-    MHIP(hipStreamSynchronize(nullptr));
+    MHIP(hipMemsetAsync(m->err, 0, 16, m->stream));
+    MHIP(hipStreamSynchronize(m->stream));
   }
   *status = e;
   return ORBX_OK;
@@ -1624,7 +1632,8 @@ int orbm_hamming_top2(orbm_handle m, const uint8_t* d_A, size_t a_pitch, const i
   MHIP(hipSetDevice(m->device));
   const int rc = launch_hamming_top2(d_A, a_pitch, d_nA, a_cap, d_B, b_pitch, d_nB, pairs, d_best_idx, d_best,
                                      d_second, m->err, stream);
-  return rc ? mfail(rc, "launch failed") : ORBX_OK;
+  if (rc) return mfail(rc, "launch failed");
+  return m->errm.mark((hipStream_t)stream) ? mfail(ORBX_EDEVICE, "event record failed") : ORBX_OK;
 }
 
 int orbm_search_for_initialization_batch(orbm_handle m, const orbx_kp* d_kp1, const uint8_t* d_desc1,
@@ -1801,6 +1810,7 @@ int orbm_search_by_bow(orbm_handle m, const uint8_t* descA, const float* angleA,
   if ((rc = launch_search_bow(A, B, 1, nnratio, check_ori, kf_vs_kf, (int*)d[12], std::max(nout, 1), (int*)d[14],
                               (int*)d[13], (size_t)std::max(nout, 1), (int*)d[16], 32, &clean, m->err, st)))
     return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
+  if (m->errm.mark(st)) return mfail(ORBX_EDEVICE, "event record failed");
   int nm = 0;
   MHIP(hipMemcpyAsync(&nm, d[14], 4, hipMemcpyDeviceToHost, st));
   if (nout) MHIP(hipMemcpyAsync(out, d[12], (size_t)nout * 4, hipMemcpyDeviceToHost, st));
@@ -1832,7 +1842,7 @@ int orbm_search_by_bow_batch(orbm_handle m, int pairs, int kp_pitch, int node_pi
                                    (size_t)m->max_pairs * m->max_kps, m->bow_hist, (size_t)m->max_pairs * 32,
                                    &m->bow_clean, m->err, stream);
   if (rc) return mfail(rc, "search_bow launch: %s", hipGetErrorString(hipGetLastError()));
-  if (m->ws.after(s)) return mfail(ORBX_EDEVICE, "event record failed");
+  if (m->ws.after(s) || m->errm.mark(s)) return mfail(ORBX_EDEVICE, "event record failed");
   return ORBX_OK;
 }
 
@@ -1925,6 +1935,46 @@ int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle rig
   if (rc) return rc;
   int kept = 0;
   MHIP(hipMemcpyAsync(&kept, dn + 2, 4, hipMemcpyDeviceToHost, st));
+  if (nL) {
+    MHIP(hipMemcpyAsync(uRight, du, (size_t)nL * 4, hipMemcpyDeviceToHost, st));
+    MHIP(hipMemcpyAsync(depth, dd, (size_t)nL * 4, hipMemcpyDeviceToHost, st));
+  }
+  MHIP(hipStreamSynchronize(st));
+  *nkept = kept;
+  return ORBX_OK;
+}
+
+// Frame::ComputeStereoMatches right after the stereo constructor's two
+// extractions (src/Frame.cc:77-89): the keypoints and descriptors are read
+// where the two orbx_extract calls left them on the device, so only mvuRight
+// and mvDepth cross the link.
+int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handle right, float mb, float mbf,
+                                     float* uRight, float* depth, int nL, int* nkept) {
+  if (!m || !left || !right || !nkept || nL < 0 || (nL && (!uRight || !depth))) return mfail(ORBX_EINVAL, "bad argument");
+  const int* dnL = nullptr;
+  const int* dnR = nullptr;
+  const orbx_kp *dkl = nullptr, *dkr = nullptr;
+  const uint8_t *ddl = nullptr, *ddr = nullptr;
+  int capL = 0, capR = 0;
+  if (extractor_last_output(left, &dnL, &dkl, &ddl, &capL) || extractor_last_output(right, &dnR, &dkr, &ddr, &capR))
+    return mfail(ORBX_EINVAL, "stereo (last extraction): %s", orbx_last_error());
+  if (capL != capR) return mfail(ORBX_EINVAL, "left and right extractors have different capacities");
+  if (nL > capL) return mfail(ORBX_EINVAL, "nL %d above the left extraction's capacity %d", nL, capL);
+  if (capL > m->max_kps) return mfail(ORBX_ECAPACITY, "extractor capacity %d above max_kps %d", capL, m->max_kps);
+  MHIP(hipSetDevice(m->device));
+  const size_t bytes = (size_t)capL * 8 + 64;
+  int rc;
+  if ((rc = stage_reserve(m, bytes))) return rc;
+  float* du = (float*)m->stage;
+  float* dd = du + capL;
+  int* dk = (int*)(dd + capL);
+  if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+  hipStream_t st = m->stream;
+  rc = orbm_compute_stereo_matches_batch(m, left, 0, right, 0, dkl, ddl, dnL, dkr, ddr, dnR, capL, 1, mb, mbf, du, dd,
+                                         dk, st);
+  if (rc) return rc;
+  int kept = 0;
+  MHIP(hipMemcpyAsync(&kept, dk, 4, hipMemcpyDeviceToHost, st));
   if (nL) {
     MHIP(hipMemcpyAsync(uRight, du, (size_t)nL * 4, hipMemcpyDeviceToHost, st));
     MHIP(hipMemcpyAsync(depth, dd, (size_t)nL * 4, hipMemcpyDeviceToHost, st));

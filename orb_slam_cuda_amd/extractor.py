@@ -134,6 +134,25 @@ class ORBextractor:
         """Pyramid of the last extraction (public member, include/ORBextractor.h:116)."""
         return [self.level_image(l) for l in range(self.nlevels)]
 
+    def set_host_pyramid(self, enable: bool = True) -> None:
+        """orbx_set_host_pyramid: later calls also leave their frame's pyramid in
+        pinned host memory (copied beside FAST .. BRIEF inside the call)."""
+        check(lib().orbx_set_host_pyramid(self._h, int(enable)))
+
+    def host_pyramid(self) -> list[np.ndarray]:
+        """The pinned host pyramid of the last call (orbx_get_host_pyramid), copied out."""
+        L = self.nlevels
+        ptrs = (C.c_void_p * L)()
+        pitches = (C.c_size_t * L)()
+        check(lib().orbx_get_host_pyramid(self._h, ptrs, pitches, L))
+        info = self.levels_info()
+        out = []
+        for l in range(L):
+            h, w, p = int(info["h"][l]), int(info["w"][l]), int(pitches[l])
+            buf = (C.c_uint8 * (h * p)).from_address(ptrs[l])
+            out.append(np.frombuffer(buf, np.uint8).reshape(h, p)[:, :w].copy())
+        return out
+
     def fast_candidates(self, level: int, frame: int = 0) -> np.ndarray:
         """Stage probe: per-cell FAST+NMS output of the last extraction (pre-quadtree)."""
         cap = 1 << 20

@@ -150,6 +150,22 @@ def ComputeStereoMatches(F: Frame, extractorLeft, extractorRight, matcher: "ORBm
     return kept.value
 
 
+def ComputeStereoMatchesLast(F: Frame, extractorLeft, extractorRight, matcher: "ORBmatcher") -> int:
+    """Frame::ComputeStereoMatches as the stereo constructor runs it, right after its two
+    extractions (src/Frame.cc:77-89): the keypoints and descriptors are the ones the two
+    extractors' last calls left on the device (orbm_compute_stereo_matches_last); F.mvKeys
+    must be the left call's output. Fills F.mvuRight / F.mvDepth, returns the kept count."""
+    n = len(F.mvKeysUn)
+    uR = np.full(n, -1.0, np.float32)
+    dep = np.full(n, -1.0, np.float32)
+    kept = C.c_int(0)
+    check(lib().orbm_compute_stereo_matches_last(
+        matcher.handle, extractorLeft.handle, extractorRight.handle, C.c_float(F.mb), C.c_float(F.mbf),
+        ptr(uR), ptr(dep), n, C.byref(kept)), matcher=True)
+    F.mvuRight, F.mvDepth = uR, dep
+    return kept.value
+
+
 @dataclass
 class KeyFrame:
     mvKeysUn: np.ndarray

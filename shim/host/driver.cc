@@ -11,10 +11,16 @@
 //   orbx_shim_driver --scene SCENE.bin OUT.bin   (one ORBmatcher method on a test scene, scene.cc)
 //   orbx_shim_driver --stereo LEFT.u8 RIGHT.u8 NPAIRS W H BF OUTDIR
 //                                 (stereo Frames, two extraction threads each, + ComputeStereoMatches)
+//   orbx_shim_driver --latency MONO.u8 LEFT.u8 RIGHT.u8 NFRAMES W H NCALLS WARM
+//                                 (per-call host times of the drop-in path, one JSON line)
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <stdexcept>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "Frame.h"
@@ -84,6 +90,160 @@ static int run_stereo(const char* left, const char* right, int npairs, int W, in
   return 0;
 }
 
+static bool read_file(const char* path, std::vector<uint8_t>& v) {
+  FILE* f = fopen(path, "rb");
+  const bool ok = f && fread(v.data(), 1, v.size(), f) == v.size();
+  if (f) fclose(f);
+  if (!ok) fprintf(stderr, "cannot read %s\n", path);
+  return ok;
+}
+
+// median / p99 of per-call times (ms) as a JSON object
+static std::string stats(std::vector<double> t) {
+  std::sort(t.begin(), t.end());
+  const double med = t[t.size() / 2], p99 = t[std::min(t.size() - 1, (size_t)(0.99 * (double)t.size()))];
+  char buf[128];
+  snprintf(buf, sizeof buf, "{\"median\": %.4f, \"p99\": %.4f, \"calls\": %zu}", med, p99, t.size());
+  return buf;
+}
+
+// The per-frame cost of the drop-in classes as Tracking pays it (bench.py's
+// shim_latency leg): NCALLS timed calls after WARM untimed ones, cycling over
+// NFRAMES images, each call timed on the host clock around
+//   orbx_extract        the C-ABI call alone (its own handle, host buffers)
+//   operator()          ORBextractor::operator() (src/Frame.cc:246-252), with
+//                       and without the pinned host pyramid (ORBX_HOST_PYRAMID)
+//   stereo Frame        the stereo constructor: left and right operator() on two
+//                       std::threads + ComputeStereoMatches (src/Frame.cc:60-128)
+// Prints one JSON object.
+static int run_latency(const char* mono, const char* left, const char* right, int nfr, int W, int H, int ncalls,
+                       int warm) {
+  const size_t plane = (size_t)W * H;
+  std::vector<uint8_t> M(plane * nfr), Lp(plane * nfr), Rp(plane * nfr);
+  if (!read_file(mono, M) || !read_file(left, Lp) || !read_file(right, Rp)) return 2;
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t0) { return std::chrono::duration<double, std::milli>(clk::now() - t0).count(); };
+  std::string out = "{";
+  {
+    orbx_config c = {};
+    c.nfeatures = 2000;
+    c.scale_factor = 1.2f;
+    c.nlevels = 8;
+    c.ini_th_fast = 20;
+    c.min_th_fast = 7;
+    c.width = W;
+    c.height = H;
+    c.max_batch = 1;
+    const char* dev = getenv("ORBX_DEVICE");
+    c.device = dev ? atoi(dev) : 0;
+    orbx_handle h = nullptr;
+    if (orbx_create(&c, &h) != ORBX_OK) throw std::runtime_error(orbx_last_error());
+    const int cap = orbx_frame_capacity(h);
+    std::vector<orbx_kp> kp(cap);
+    std::vector<uint8_t> desc((size_t)cap * 32);
+    std::vector<double> t;
+    for (int i = 0; i < warm + ncalls; ++i) {
+      int n = 0;
+      const auto t0 = clk::now();
+      if (orbx_extract(h, M.data() + (size_t)(i % nfr) * plane, W, H, W, kp.data(), cap, desc.data(), &n) != ORBX_OK)
+        throw std::runtime_error(orbx_last_error());
+      if (i >= warm) t.push_back(ms_since(t0));
+    }
+    orbx_destroy(h);
+    out += "\"orbx_extract_ms\": " + stats(t);
+  }
+  for (int hp = 1; hp >= 0; --hp) {
+    setenv("ORBX_HOST_PYRAMID", hp ? "1" : "0", 1);
+    ORBextractor ext(2000, 1.2f, 8, 20, 7, W, H);
+    std::vector<cv::KeyPoint> kps;
+    cv::Mat desc;
+    std::vector<double> t;
+    for (int i = 0; i < warm + ncalls; ++i) {
+      cv::Mat im(H, W, CV_8U, M.data() + (size_t)(i % nfr) * plane, W);
+      const auto t0 = clk::now();
+      ext(im, cv::noArray(), kps, desc);
+      if (i >= warm) t.push_back(ms_since(t0));
+    }
+    out += std::string(", \"operator_ms") + (hp ? "" : "_no_host_pyramid") + "\": " + stats(t);
+  }
+  Frame::fx = Frame::fy = 718.856f;
+  Frame::cx = 607.1928f;
+  Frame::cy = 185.2157f;
+  Frame::invfx = Frame::invfy = 1.0f / 718.856f;
+  const float bf = 0.54f * 718.856f;
+  for (int hp = 0; hp <= 1; ++hp) {
+    setenv("ORBX_HOST_PYRAMID", hp ? "1" : "0", 1);
+    ORBextractor le(2000, 1.2f, 8, 20, 7, W, H), re(2000, 1.2f, 8, 20, 7, W, H);
+    std::vector<double> t;
+    size_t kept = 0;
+    for (int i = 0; i < warm + ncalls; ++i) {
+      const size_t o = (size_t)(i % nfr) * plane;
+      cv::Mat l(H, W, CV_8U, Lp.data() + o, W), r(H, W, CV_8U, Rp.data() + o, W);
+      const auto t0 = clk::now();
+      Frame F(l, r, &le, &re, nullptr, bf);
+      if (i >= warm) {
+        t.push_back(ms_since(t0));
+        for (float u : F.mvuRight) kept += u >= 0;
+      }
+    }
+    char buf[96];
+    snprintf(buf, sizeof buf, "\"stereo_matches_per_frame\": %.1f, ", (double)kept / ncalls);
+    out += std::string(", ") + (hp ? "" : buf) + "\"stereo_frame_ms" + (hp ? "_host_pyramid" : "") + "\": " + stats(t);
+  }
+  {
+    // the stereo constructor's parts (no host pyramid): the two extraction
+    // threads alone, the two extractions on one thread, ComputeStereoMatches alone
+    setenv("ORBX_HOST_PYRAMID", "0", 1);
+    ORBextractor le(2000, 1.2f, 8, 20, 7, W, H), re(2000, 1.2f, 8, 20, 7, W, H);
+    std::vector<double> t2, t1, tm;
+    std::vector<cv::KeyPoint> kl, kr;
+    cv::Mat dl, dr;
+    for (int i = 0; i < warm + ncalls; ++i) {
+      const size_t o = (size_t)(i % nfr) * plane;
+      cv::Mat l(H, W, CV_8U, Lp.data() + o, W), r(H, W, CV_8U, Rp.data() + o, W);
+      auto t0 = clk::now();
+      std::thread a([&] { le(l, cv::noArray(), kl, dl); });
+      std::thread b([&] { re(r, cv::noArray(), kr, dr); });
+      a.join();
+      b.join();
+      if (i >= warm) t2.push_back(ms_since(t0));
+      t0 = clk::now();
+      le(l, cv::noArray(), kl, dl);
+      re(r, cv::noArray(), kr, dr);
+      if (i >= warm) t1.push_back(ms_since(t0));
+      std::vector<float> u(kl.size()), d(kl.size());
+      int k = 0;
+      t0 = clk::now();
+      if (orbm_compute_stereo_matches_last(ORBmatcher::Handle(), le.handle(), re.handle(), 0.54f, bf, u.data(),
+                                           d.data(), (int)kl.size(), &k) != ORBX_OK)
+        throw std::runtime_error(orbm_last_error());
+      if (i >= warm) tm.push_back(ms_since(t0));
+    }
+    out += ", \"stereo_parts\": {\"extract_two_threads_ms\": " + stats(t2) +
+           ", \"extract_one_thread_ms\": " + stats(t1) + ", \"compute_stereo_matches_ms\": " + stats(tm);
+    // ComputeStereoMatches' workgroups per pair (ORBX_STEREO_GROUPS, read per call)
+    for (int g : {8, 16, 32, 64}) {
+      setenv("ORBX_STEREO_GROUPS", std::to_string(g).c_str(), 1);
+      std::vector<double> tg;
+      std::vector<float> u(kl.size()), d(kl.size());
+      for (int i = 0; i < warm + ncalls; ++i) {
+        int k = 0;
+        const auto t0 = clk::now();
+        if (orbm_compute_stereo_matches_last(ORBmatcher::Handle(), le.handle(), re.handle(), 0.54f, bf, u.data(),
+                                             d.data(), (int)kl.size(), &k) != ORBX_OK)
+          throw std::runtime_error(orbm_last_error());
+        if (i >= warm) tg.push_back(ms_since(t0));
+      }
+      out += ", \"compute_stereo_matches_g" + std::to_string(g) + "_ms\": " + stats(tg);
+    }
+    unsetenv("ORBX_STEREO_GROUPS");
+    out += "}";
+  }
+  unsetenv("ORBX_HOST_PYRAMID");
+  printf("%s}\n", out.c_str());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc == 2 && std::string(argv[1]) == "--version") {
     printf("%s\n", orbx_version());
@@ -91,6 +251,9 @@ int main(int argc, char** argv) {
   }
   try {
     if (argc == 4 && std::string(argv[1]) == "--scene") return run_scene(argv[2], argv[3]);
+    if (argc == 10 && std::string(argv[1]) == "--latency")
+      return run_latency(argv[2], argv[3], argv[4], atoi(argv[5]), atoi(argv[6]), atoi(argv[7]), atoi(argv[8]),
+                         atoi(argv[9]));
     if (argc == 9 && std::string(argv[1]) == "--stereo")
       return run_stereo(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), (float)atof(argv[7]), argv[8]);
   } catch (const std::exception& e) {
@@ -128,9 +291,13 @@ int main(int argc, char** argv) {
       const Frame& F = frames.back();
       write_file(out + "/kp" + std::to_string(i) + ".bin", F.mvKeys.data(), F.mvKeys.size() * sizeof(cv::KeyPoint));
       write_file(out + "/desc" + std::to_string(i) + ".bin", F.mDescriptors.data, (size_t)F.N * 32);
-      // mvImagePyramid of this frame's extraction, level 1 (read by stereo matching)
-      const cv::Mat& L1 = extractor.mvImagePyramid[1];
-      write_file(out + "/pyr1_" + std::to_string(i) + ".bin", L1.data, (size_t)L1.rows * L1.step);
+      // mvImagePyramid of this frame's extraction, every level (read by stereo
+      // matching), rows at the level width
+      for (size_t l = 0; l < extractor.mvImagePyramid.size(); ++l) {
+        const cv::Mat Ll = extractor.mvImagePyramid[l].clone();
+        write_file(out + "/pyr" + std::to_string(l) + "_" + std::to_string(i) + ".bin", Ll.data,
+                   (size_t)Ll.rows * Ll.step);
+      }
     }
     if (nfr >= 2) {
       Frame &F1 = frames[0], &F2 = frames[1];

@@ -64,6 +64,12 @@ class ORBextractor {
   std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2; }
   std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
 
+  // The pyramid of the last call (src/ORBextractor.cc:1837-1863): headers over
+  // the handle's pinned host copy, which orbx_extract fills beside the other
+  // kernels (orbx_set_host_pyramid); valid until the next call, as the
+  // reference's own buffers are. ORBX_HOST_PYRAMID=0 skips the copy (the
+  // levels are then empty: the shim's ComputeStereoMatches reads the device
+  // pyramids, the reference's only reader, src/Frame.cc:472-579).
   std::vector<cv::Mat> mvImagePyramid;
 
   // Per-stage device times of the last call, named as the reference's
@@ -97,6 +103,8 @@ class ORBextractor {
   orbx_handle h_ = nullptr;
   int cap_ = 0;
   bool timing_ = false;
+  bool host_pyr_ = true;
+  std::vector<int> lw_, lh_;  // level sizes (orbx_get_levels_info, refreshed on a new image size)
 };
 
 }  // namespace ORB_SLAM2

@@ -1,8 +1,8 @@
 // Frame's statics (src/Frame.cc:31-34 defines them for the reference) and the
 // drop-in body of Frame::ComputeStereoMatches (src/Frame.cc:465-639): the
-// keypoints of both images and the two extractors' pyramids of this frame's
-// extraction go to orbm_compute_stereo_matches, which fills mvuRight and
-// mvDepth (-1 where a keypoint has no stereo match).
+// keypoints, descriptors and pyramids of the two extractors' last calls are
+// matched where they lie on the device (orbm_compute_stereo_matches_last),
+// which fills mvuRight and mvDepth (-1 where a keypoint has no stereo match).
 #include "Frame.h"
 
 #include <stdexcept>
@@ -19,11 +19,12 @@ void Frame::ComputeStereoMatches() {
   mvDepth = std::vector<float>(N, -1.0f);
   if (N == 0) return;
   int kept = 0;
-  const int rc = orbm_compute_stereo_matches(
-      ORBmatcher::Handle(), mpORBextractorLeft->handle(), mpORBextractorRight->handle(),
-      reinterpret_cast<const orbx_kp*>(mvKeys.data()), mDescriptors.ptr<uint8_t>(), N,
-      reinterpret_cast<const orbx_kp*>(mvKeysRight.data()), mDescriptorsRight.ptr<uint8_t>(),
-      (int)mvKeysRight.size(), mb, mbf, mvuRight.data(), mvDepth.data(), &kept);
+  // the stereo constructor calls this right after its two extractions
+  // (src/Frame.cc:77-89): the keypoints and descriptors are read where those
+  // calls left them on the device, only mvuRight / mvDepth come back
+  const int rc = orbm_compute_stereo_matches_last(ORBmatcher::Handle(), mpORBextractorLeft->handle(),
+                                                  mpORBextractorRight->handle(), mb, mbf, mvuRight.data(),
+                                                  mvDepth.data(), N, &kept);
   if (rc != ORBX_OK) throw std::runtime_error(std::string("liborbx: ") + orbm_last_error());
 }
 }  // namespace ORB_SLAM2

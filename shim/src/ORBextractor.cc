@@ -3,6 +3,7 @@
 #include "ORBextractor.h"
 
 #include <chrono>
+#include <climits>
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
@@ -55,12 +56,17 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
   mvInvLevelSigma2.resize(nlevels);
   orbx_check(orbx_get_scales(h_, mvScaleFactor.data(), mvInvScaleFactor.data(), mvLevelSigma2.data(),
                              mvInvLevelSigma2.data()));
-  std::vector<int> lw(nlevels), lh(nlevels);
+  lw_.resize(nlevels);
+  lh_.resize(nlevels);
   mnFeaturesPerLevel.resize(nlevels);
   int nl = 0;
-  orbx_check(orbx_get_levels_info(h_, &nl, lw.data(), lh.data(), mnFeaturesPerLevel.data()));
+  orbx_check(orbx_get_levels_info(h_, &nl, lw_.data(), lh_.data(), mnFeaturesPerLevel.data()));
   cap_ = orbx_frame_capacity(h_);
   if (cap_ <= 0) throw std::runtime_error("liborbx: bad frame capacity");
+  const char* hp = getenv("ORBX_HOST_PYRAMID");
+  host_pyr_ = !(hp && hp[0] == '0');
+  orbx_check(orbx_set_host_pyramid(h_, host_pyr_ ? 1 : 0));
+  mvImagePyramid.resize(nlevels);
   // ORBX_TIMING=1: the library records its stage events (orbx_create reads the
   // same variable) and every call's stage times go to `times`
   const char* tm = getenv("ORBX_TIMING");
@@ -91,24 +97,36 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask*/, s
   const auto start = std::chrono::steady_clock::now();
   {
   GetTime total(this, "Total Time ORB extraction", -1);  // :1548 (recorded only with ORBX_TIMING=1)
+  // keypoints and descriptors are written straight into the outputs at their
+  // capacity and trimmed to the count (no staging copy)
   _keypoints.resize(cap_);
-  cv::Mat desc(cap_, 32, CV_8U);
+  _descriptors.create(cap_, 32, CV_8U);
+  cv::Mat& desc = _descriptors.getMatRef();
   int n = 0;
+  if (image.cols != lw_[0] || image.rows != lh_[0]) {
+    // a new image size re-plans the handle (the reference accepts any size per
+    // call): one call with no outputs plans it, then the capacity is known
+    orbx_check(orbx_extract(h_, image.data, image.cols, image.rows, image.step, nullptr, INT_MAX, nullptr, &n));
+    cap_ = orbx_frame_capacity(h_);
+    int nl = 0;
+    orbx_check(orbx_get_levels_info(h_, &nl, lw_.data(), lh_.data(), mnFeaturesPerLevel.data()));
+    _keypoints.resize(cap_);
+    _descriptors.create(cap_, 32, CV_8U);
+  }
   orbx_check(orbx_extract(h_, image.data, image.cols, image.rows, image.step,
                           reinterpret_cast<orbx_kp*>(_keypoints.data()), cap_, desc.data, &n));
   _keypoints.resize(n);
   if (n == 0)
     _descriptors.release();  // :1716-1717
   else
-    desc.rowRange(0, n).copyTo(_descriptors);  // _descriptors.create(nkeypoints, 32, CV_8U) :1719
-  // mvImagePyramid: read by Frame::ComputeStereoMatches (src/Frame.cc:472-579)
-  mvImagePyramid.resize(nlevels);
-  std::vector<int> lw(nlevels), lh(nlevels), nfl(nlevels);
-  int nl = 0;
-  orbx_check(orbx_get_levels_info(h_, &nl, lw.data(), lh.data(), nfl.data()));
-  for (int l = 0; l < nlevels; ++l) {
-    mvImagePyramid[l].create(lh[l], lw[l], CV_8U);
-    orbx_check(orbx_get_level(h_, /*frame=*/0, l, /*blurred=*/0, mvImagePyramid[l].data, mvImagePyramid[l].step));
+    desc = desc.rowRange(0, n);  // _descriptors.create(nkeypoints, 32, CV_8U) :1719
+  // mvImagePyramid: headers over the pinned host copy of this call's pyramid
+  if (host_pyr_) {
+    const uint8_t* lv[16];
+    size_t lp[16];
+    orbx_check(orbx_get_host_pyramid(h_, lv, lp, 16));
+    for (int l = 0; l < nlevels; ++l)
+      mvImagePyramid[l] = cv::Mat(lh_[l], lw_[l], CV_8U, const_cast<uint8_t*>(lv[l]), lp[l]);
   }
   if (timing_) {
     // the device stages under the reference's GetTime names; one launch covers

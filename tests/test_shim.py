@@ -73,9 +73,11 @@ def test_shim_host_matches_oracle(pkg, O, tmp_path):
         assert len(kp) == len(rkp) > 1000
         assert np.array_equal(kp.view(np.uint8), rkp.view(np.uint8)), f"frame {i} keypoints"
         assert np.array_equal(desc, rdesc), f"frame {i} descriptors"
-        lvl = O.pyramid_level(cfg, frames[i], 1)
-        pyr = np.fromfile(out / f"pyr1_{i}.bin", dtype=np.uint8).reshape(lvl.shape)
-        assert np.array_equal(pyr, lvl), f"frame {i} mvImagePyramid[1]"
+        # mvImagePyramid: headers over the pinned copy orbx_extract made beside its kernels
+        for l in range(8):
+            lvl = frames[i] if l == 0 else O.pyramid_level(cfg, frames[i], l)
+            pyr = np.fromfile(out / f"pyr{l}_{i}.bin", dtype=np.uint8).reshape(lvl.shape)
+            assert np.array_equal(pyr, lvl), f"frame {i} mvImagePyramid[{l}]"
         kps.append(rkp)
         descs.append(rdesc)
     (k1, k2), (d1, d2) = kps, descs
