@@ -202,7 +202,7 @@ ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_EXTRACT_ORDER", "ORBX_P
               "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS",
               "ORBX_BOW_ROUNDS",
               # the C++ shim's configuration (shim/src/ORBextractor.cc); bench.py does not read them
-              "ORBX_DEVICE", "ORBX_SCALE_MODE", "ORBX_PATTERN"}
+              "ORBX_DEVICE", "ORBX_SCALE_MODE", "ORBX_PATTERN", "ORBX_HOST_PYRAMID"}
 # Diagnostics: phase clocks synchronise after every launch, *_STOP / FAST_TWICE
 # skip or repeat work (they only act in -DORBX_DIAG builds), ORBX_LIB_VARIANT
 # loads an A/B build of the library. A timed region under any of them is not
@@ -355,16 +355,26 @@ def run_stub(args, rank, world, dist):
     """CPU stand-in for the GPU work (launcher tests): rank r 'processes'
     batch x steps frames in (1 + r) x 10 ms; everything else is the real
     control plane and reporting path."""
+    from orb_slam_cuda_amd import sharding
+    cfg = CONFIGS[args.config]
+    # what rank r would stream: its own sequence (seed) of frames of the config's shape
+    mine = {"rank": rank, "seed": sharding.sequence_seed(rank), "frame": f"{cfg['W']}x{cfg['H']}",
+            "nfeatures": cfg["nfeatures"], "frames": args.batch * args.steps}
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
     time.sleep(0.01 * (1 + rank))
     wall = time.perf_counter() - t0
     agg = aggregate(args.batch * args.steps, wall, dist, world)
+    ranks = [mine]
+    if dist is not None:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(agg["value"], 2), "unit": "frames/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "per_rank_frames_per_s": agg["per_rank"],
-                          "frames_total": agg["frames"], "data": "stub (no GPU work)",
+                          "frames_total": agg["frames"], "job_wall_s": round(agg["wall"], 6), "ranks": ranks,
+                          "config": {"workload": cfg["workload"]}, "data": "stub (no GPU work)",
                           "orbx_env": audit_env(args.allow_diag)}), flush=True)
 
 

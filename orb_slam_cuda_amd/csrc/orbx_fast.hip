@@ -56,6 +56,10 @@ constexpr int kRoiTight = ORBX_FAST_T1, kRoiTight2 = ORBX_FAST_T2, kRoiWide = 80
 static_assert(kRoiTight < kRoiTight2 && kRoiTight2 < kRoiWide && kRoiTight % 4 == 0 && kRoiTight2 % 4 == 0,
               "tight strides in increasing order, whole dwords");
 
+// the FAST grid's border box starts at EDGE_THRESHOLD - 3 on every level
+// (minBorderX/Y, src/ORBextractor.cc:1133-1134)
+constexpr int kFastMinB = kEdgeThreshold - 3;
+
 // 24-bit multiply (full-rate v_mul_u32_u24; the compiler cannot prove the
 // operand ranges and otherwise picks the quarter-rate 32/64-bit forms)
 __device__ __forceinline__ int u24mul(int a, int b) { return (int)__umul24((unsigned)a, (unsigned)b); }
@@ -81,8 +85,12 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
   typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
   // byte offsets, from the group's first dword, of the group's centres, +3 and -3 neighbours
   constexpr int kC = OX + 3, kN4 = OX + 6, kN12 = OX;
-  const int G = (bw + 3) >> 2, RP = 64 / G;
-  const int r = lane / G, g = lane - r * G, x = 4 * g;
+  // 64 / G and lane / G by one reciprocal: G <= 15, so (n + 0.5) / G is at
+  // least 1/30 from an integer and rcp's 1-ulp error cannot move the floor
+  const int G = (bw + 3) >> 2;
+  const float rg = __builtin_amdgcn_rcpf((float)G);
+  const int RP = __builtin_amdgcn_readfirstlane((int)(64.5f * rg));  // uniform: the pass loop stays scalar
+  const int r = (int)(((float)lane + 0.5f) * rg), g = lane - r * G, x = 4 * g;
   const bool lane_ok = r < RP;
   uint64_t colm[4];
 #pragma unroll
@@ -165,6 +173,7 @@ __device__ __forceinline__ int compass4(const LDSP uint8_t* roi, LDSP uint16_t* 
 template <int kRoiStride, bool kProf>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WAVES))) void fast_cells_kernel(ExtractParams P, LevelPtrs lp,
                                                         const CellGeom* __restrict__ cells,
+                                                        const uint8_t* __restrict__ pyr,
                                                         uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_counts, int* dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -180,10 +189,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   const int f = P.ncells_magic ? (int)__umulhi((unsigned)wg, P.ncells_magic) : wg / P.ncells_total;
   const int cell = wg - f * P.ncells_total, lane = threadIdx.x;
   CellGeom cg;
+  int row_off, rec_pitch, rec_fstride, geo;
   {
-    // the whole 16-byte cell record in one scalar load (int16 fields unpacked
-    // from it, so no 16-bit vector load sits on the critical path)
-    const int4 raw = ((const int4*)cells)[cell];
+    // the whole 32-byte cell record in one scalar load (int16 fields unpacked
+    // from it, so no 16-bit vector load sits on the critical path); with the
+    // level's staging parameters inside it, nothing after it is indexed by level
+    const int4 raw = ((const int4*)cells)[2 * cell], raw2 = ((const int4*)cells)[2 * cell + 1];
+    // both record halves and level 0's kernel arguments in one burst of
+    // scalar loads (else the compiler defers the second half and the
+    // arguments past the skipped-cell test: a second memory latency)
+    asm volatile("" ::"s"(raw.x), "s"(raw.y), "s"(raw.z), "s"(raw.w), "s"(raw2.x), "s"(raw2.y), "s"(raw2.z), "s"(raw2.w), "s"(lp.pitch[0]),
+                 "s"(lp.aligned16[0]), "s"(lp.base[0]), "s"(lp.fstride[0]), "s"(pyr));
     cg.c0 = (int16_t)(raw.x & 0xFFFF);
     cg.r0 = (int16_t)(raw.x >> 16);
     cg.c1 = (int16_t)(raw.y & 0xFFFF);
@@ -191,6 +207,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     cg.slot_off = raw.z;
     cg.cap = (int16_t)(raw.w & 0xFFFF);
     cg.level = (int16_t)(raw.w >> 16);
+    row_off = raw2.x;
+    rec_pitch = raw2.y;
+    rec_fstride = raw2.z;
+    geo = raw2.w;
     // diagnostics: clock at which the cell record arrived (the test waits for it)
     if (kProf && threadIdx.x == 0 && raw.w != -1)
       dbg[(blockIdx.x + blockIdx.y * gridDim.x) * 8 + 7] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
@@ -214,18 +234,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   // written (phase (d) reads only the list and the score map)
   LDSP uint64_t* ball = (LDSP uint64_t*)roi;
 
-  const int l = cg.level;
-  const LevelGeom& g = P.lv[l];
-  const int pitch = lp.pitch[l];
+  // level 0 (pitch 0 in the record) is the caller's frames: its base, frame
+  // stride and row stride are kernel arguments at fixed offsets, loaded
+  // beside the record; levels >= 1 are all in the record
+  const bool lvl0 = rec_pitch == 0;
+  const int pitch = lvl0 ? lp.pitch[0] : rec_pitch;
+  const bool aligned16 = lvl0 ? lp.aligned16[0] != 0 : true;
 #ifdef ORBX_FAST_SAMEROI  // diagnostics (tools/variant.sh): every cell of a level stages frame 0's first ROI
-  const uint8_t* rows = lp.base[l] + (long long)g.minBY * pitch + (g.minBX - cg.c0);
+  const uint8_t* rows = (lvl0 ? lp.base[0] : pyr + (row_off - cg.r0 * pitch)) + (long long)kFastMinB * pitch +
+                        (kFastMinB - cg.c0);
 #else
-  const uint8_t* rows = lp.base[l] + f * lp.fstride[l] + (long long)cg.r0 * pitch;
+  const uint8_t* rows = lvl0 ? lp.base[0] + f * lp.fstride[0] + (long long)row_off * pitch
+                             : pyr + (long long)f * rec_fstride + row_off;
 #endif
   constexpr bool kDword = kRoiStride == kRoiTight || kRoiStride == kRoiTight2;  // dword staging
   constexpr bool kTight = kRoiStride != kRoiWide;                                 // the dword compass
   const int a0 = kDword ? (cg.c0 & ~(kTightE - 1)) : (cg.c0 & ~15), ox = cg.c0 - a0;
-  if (lp.aligned16[l] && kDword) {
+  if (aligned16 && kDword) {
     // whole rows per load instruction: lane -> (row lq < kRP, dword ld), so
     // load k is row block k at the lane's offset + k * kRP * pitch (one add)
     // and LDS offset k * kRP * stride (the instruction's immediate): no
@@ -236,7 +261,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     constexpr int kPR = kRoiStride / kTightE, kRP = 64 / kPR;
     const int lq0 = lane / kPR, lq = min(lq0, kRP - 1), ld = lq0 < kRP ? lane - lq0 * kPR : kPR - 1;
     const int voff = u24mul(lq, pitch) + 4 * ld, roff = lq * kRoiStride + 4 * ld;
-    const int nrec = (g.h - 1 - cg.r0) * pitch + ((g.w + 15) & ~15) - a0;
+    const int nrec = (geo & 0xFFFF) * pitch + (geo >> 16) - a0;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)(rows + a0), (short)0, nrec, 0x00020000);
     const int nk = (rh + kRP - 1) / kRP;
@@ -251,7 +276,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
     for (int k = 0; k < kK; ++k) *(LDSP uint32_t*)(roi + roff + k * kRP * kRoiStride) = v[k];
     for (int k = kK; k < nk; ++k)
       *(LDSP uint32_t*)(roi + roff + k * kRP * kRoiStride) = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + k * kRP * pitch, 0, 0);
-  } else if (lp.aligned16[l]) {
+  } else if (aligned16) {
     // the ROI's 16-byte chunks, 4 per lane (tall cells loop for the rest)
     const int nch = (cg.c1 - a0 + 15) >> 4, total = rh * nch;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 here ends up in scratch)
@@ -410,7 +435,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORBX_FAST_WA
   uint32_t* out = slots + (long long)f * P.slots_per_frame + cg.slot_off;
   auto emit = [&](int e, int pos) {  // the kept pixel's key, row-major position pos in the cell's slots
     const int by = e >> 8, bx = e & 255;
-    const int x = cg.c0 + 3 + bx - g.minBX, y = cg.r0 + 3 + by - g.minBY;
+    const int x = cg.c0 + 3 + bx - kFastMinB, y = cg.r0 + 3 + by - kFastMinB;
     if (pos < cg.cap) out[pos] = pack_key(x, y, sc[(by + 1) * sw + bx + 1]);
   };
   int base = 0;
@@ -488,11 +513,13 @@ int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cel
 #else
   constexpr int reps = 1;
 #endif
+  // the pyramid buffer the cell records' level >= 1 offsets refer to
+  const uint8_t* pyr = P.L > 1 ? lp.base[1] - P.lv[1].off : nullptr;
   for (int rep = 0; rep < reps; ++rep) {
     const int stride = fast_stride(P);
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P, lp, cells, slots,
-                         cell_counts, dbg);
+      hipLaunchKernelGGL(kern, dim3(P.ncells_total, batch), dim3(64), fast_lds_bytes(P), s, P, lp, cells, pyr,
+                         slots, cell_counts, dbg);
     };
     if (stride == kRoiTight) prof ? go(fast_cells_kernel<kRoiTight, true>) : go(fast_cells_kernel<kRoiTight, false>);
     else if (stride == kRoiTight2) prof ? go(fast_cells_kernel<kRoiTight2, true>) : go(fast_cells_kernel<kRoiTight2, false>);

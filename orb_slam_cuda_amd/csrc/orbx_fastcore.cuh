@@ -5,12 +5,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "orbx_wave.cuh"
+
 namespace orbx {
 
-// popcount of the bits of m below this lane
-__device__ __forceinline__ int mbcnt64(uint64_t m) {
-  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 
 // FAST-9/16 "cornerScore<16>" of OpenCV 3.x (d[k] = v - ring[k]) for two pixels at once,
 // packed i16x2 (one pixel per half).

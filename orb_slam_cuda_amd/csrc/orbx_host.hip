@@ -400,6 +400,10 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
         }
         cg.slot_off = slot;
         slot += cg.cap;
+        cg.pitch = l == 0 ? 0 : g.pitch;
+        cg.row_off = l == 0 ? cg.r0 : (int)(lvl_off + (long long)cg.r0 * g.pitch);
+        cg.fstride = l == 0 ? 0 : (int)g.plane;
+        cg.geo = (g.h - 1 - cg.r0) | (((g.w + 15) & ~15) << 16);
         pl.cells.push_back(cg);
       }
     }
@@ -455,6 +459,8 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
       }
     }
   }
+  if (lvl_off > INT_MAX)  // FAST's cell records hold 32-bit plane offsets
+    return fail(ORBX_EINVAL, "max_batch %d: the pyramid planes take %lld bytes, over 2 GiB", B, lvl_off);
   plan_band_pyramid(P, pl.rtab);
   if (maxnodes > 65000) return fail(ORBX_EINVAL, "nfeatures too large for the quadtree node table");
   P.slots_per_frame = slot;

@@ -59,7 +59,16 @@ struct CellGeom {
   int16_t c0, r0, c1, r1;  // ROI [c0,c1) x [r0,r1) in level coordinates
   int slot_off;            // first key slot (frame-relative)
   int16_t cap, level;      // slot capacity (0 = cell skipped by the reference)
+  // FAST staging, precomputed at plan time so that a wave needs no
+  // level-indexed parameter after its one record load (orbx_fast.hip).
+  // Levels >= 1 live in the plan's pyramid buffer; level 0 is the caller's
+  // frames, whose row stride the kernel applies (pitch == 0 marks level 0).
+  int row_off;   // levels >= 1: byte offset of the ROI's row r0 in frame 0's plane (from the pyramid buffer); level 0: r0
+  int pitch;     // levels >= 1: the level's row pitch; 0 for level 0
+  int fstride;   // levels >= 1: bytes between two frames' planes
+  int geo;       // (h - 1 - r0) | ceil16(w) << 16: the buffer range's rows below r0 and last readable column
 };
+static_assert(sizeof(CellGeom) == 32, "one 32-byte scalar load per FAST wave");
 
 struct ExtractParams {
   int L, B;

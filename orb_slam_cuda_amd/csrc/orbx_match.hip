@@ -1515,6 +1515,8 @@ struct orbx_matcher {
   // staging for the synchronous entry points
   void* stage = nullptr;
   size_t stage_bytes = 0;
+  void* h_stage = nullptr;  // pinned host staging (orbm_compute_stereo_matches_last)
+  size_t h_stage_bytes = 0;
 };
 
 static int stage_reserve(orbx_matcher* m, size_t bytes) {
@@ -1595,6 +1597,7 @@ int orbm_destroy(orbm_handle m) {
   if (m->bow_rec) (void)hipFree(m->bow_rec);
   if (m->pose_picks) (void)hipFree(m->pose_picks);
   if (m->stage) (void)hipFree(m->stage);
+  if (m->h_stage) (void)hipHostFree(m->h_stage);
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
   return ORBX_OK;
@@ -1871,9 +1874,12 @@ int orbm_compute_stereo_matches_batch(orbm_handle m, orbx_handle left, int left_
   P.kp_pitch = kp_pitch;
   P.mb = mb;
   P.mbf = mbf;
-  // ~256 workgroups (one per CU) over the batch; each stages its pair's right
-  // keypoints and descriptors in LDS
-  P.groups = std::max(1, std::min(8, (256 + pairs - 1) / pairs));
+  // ~256 workgroups (one per CU) over the batch, 8 per pair for batches of
+  // 32+ pairs; each stages its pair's right keypoints and descriptors in LDS.
+  // Few pairs (the stereo Frame's one) take up to 64 per pair: the left
+  // keypoints each wave walks through one after another set the latency
+  // (one pair: 0.107 ms with 8, 0.085 ms with 64, shim_latency's stereo_parts)
+  P.groups = std::max(1, std::min(64, (256 + pairs - 1) / pairs));
   if (const char* e = getenv("ORBX_STEREO_GROUPS")) P.groups = std::max(1, atoi(e));  // tuning experiments
   P.stop = 0;
 #ifdef ORBX_DIAG  // diagnostics builds only: stop after a phase, results incomplete
@@ -1962,25 +1968,34 @@ int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handl
   if (nL > capL) return mfail(ORBX_EINVAL, "nL %d above the left extraction's capacity %d", nL, capL);
   if (capL > m->max_kps) return mfail(ORBX_ECAPACITY, "extractor capacity %d above max_kps %d", capL, m->max_kps);
   MHIP(hipSetDevice(m->device));
-  const size_t bytes = (size_t)capL * 8 + 64;
+  // outputs {kept, -, -, -, uRight[nL], depth[nL]} in one block: one copy back
+  // into the matcher's pinned staging
+  const size_t bytes = 16 + (size_t)capL * 8;
   int rc;
   if ((rc = stage_reserve(m, bytes))) return rc;
-  float* du = (float*)m->stage;
+  if (m->h_stage_bytes < bytes) {
+    if (m->h_stage) (void)hipHostFree(m->h_stage);
+    m->h_stage = nullptr;
+    m->h_stage_bytes = 0;
+    MHIP(hipHostMalloc(&m->h_stage, bytes, hipHostMallocDefault));
+    m->h_stage_bytes = bytes;
+  }
+  int* dk = (int*)m->stage;
+  float* du = (float*)m->stage + 4;  // uRight: capL floats (the kernels' pitch), then depth
   float* dd = du + capL;
-  int* dk = (int*)(dd + capL);
   if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
   hipStream_t st = m->stream;
   rc = orbm_compute_stereo_matches_batch(m, left, 0, right, 0, dkl, ddl, dnL, dkr, ddr, dnR, capL, 1, mb, mbf, du, dd,
                                          dk, st);
   if (rc) return rc;
-  int kept = 0;
-  MHIP(hipMemcpyAsync(&kept, dk, 4, hipMemcpyDeviceToHost, st));
-  if (nL) {
-    MHIP(hipMemcpyAsync(uRight, du, (size_t)nL * 4, hipMemcpyDeviceToHost, st));
-    MHIP(hipMemcpyAsync(depth, dd, (size_t)nL * 4, hipMemcpyDeviceToHost, st));
-  }
+  uint8_t* h = (uint8_t*)m->h_stage;
+  MHIP(hipMemcpyAsync(h, dk, 16 + (size_t)capL * 8, hipMemcpyDeviceToHost, st));
   MHIP(hipStreamSynchronize(st));
-  *nkept = kept;
+  *nkept = ((const int*)h)[0];
+  if (nL) {
+    memcpy(uRight, h + 16, (size_t)nL * 4);
+    memcpy(depth, h + 16 + (size_t)capL * 4, (size_t)nL * 4);
+  }
   return ORBX_OK;
 }
 

@@ -11,6 +11,11 @@
 
 namespace orbx {
 
+// popcount of the bits of m below this lane
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ int dpp_i(int old, int v) {
   return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, 0xf, false);

@@ -64,12 +64,13 @@ class ORBextractor {
   std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2; }
   std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
 
-  // The pyramid of the last call (src/ORBextractor.cc:1837-1863): headers over
-  // the handle's pinned host copy, which orbx_extract fills beside the other
-  // kernels (orbx_set_host_pyramid); valid until the next call, as the
-  // reference's own buffers are. ORBX_HOST_PYRAMID=0 skips the copy (the
-  // levels are then empty: the shim's ComputeStereoMatches reads the device
-  // pyramids, the reference's only reader, src/Frame.cc:472-579).
+  // The pyramid of the last call (src/ORBextractor.cc:1837-1863). Opt-in
+  // (ORBX_HOST_PYRAMID=1): headers over the handle's pinned host copy, which
+  // orbx_extract then fills beside the other kernels (orbx_set_host_pyramid),
+  // valid until the next call as the reference's own buffers are. Off by
+  // default the levels stay empty: the reference's only reader,
+  // ComputeStereoMatches (src/Frame.cc:472-579), reads the device pyramids
+  // here, and the copy would cost ~30 us per call.
   std::vector<cv::Mat> mvImagePyramid;
 
   // Per-stage device times of the last call, named as the reference's

@@ -63,8 +63,11 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
   orbx_check(orbx_get_levels_info(h_, &nl, lw_.data(), lh_.data(), mnFeaturesPerLevel.data()));
   cap_ = orbx_frame_capacity(h_);
   if (cap_ <= 0) throw std::runtime_error("liborbx: bad frame capacity");
+  // ORBX_HOST_PYRAMID=1: mvImagePyramid filled on every call (opt-in: the copy
+  // costs ~30 us per call, bench.py shim_latency, and the reference's only
+  // reader, ComputeStereoMatches, reads the device pyramids here)
   const char* hp = getenv("ORBX_HOST_PYRAMID");
-  host_pyr_ = !(hp && hp[0] == '0');
+  host_pyr_ = hp && hp[0] == '1';
   orbx_check(orbx_set_host_pyramid(h_, host_pyr_ ? 1 : 0));
   mvImagePyramid.resize(nlevels);
   // ORBX_TIMING=1: the library records its stage events (orbx_create reads the

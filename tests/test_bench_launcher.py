@@ -39,6 +39,32 @@ def test_launcher_spawns_n_workers_and_aggregates(n):
     assert abs(out["value"] - out["frames_total"] / (out["frames_total"] / n / per[-1])) / out["value"] < 0.05
 
 
+def test_launcher_c5_shape_eight_ranks():
+    """C5's shape (8 x EuRoC 752x480, one sequence per GPU) through the launcher
+    with stub workers: eight ranks, eight distinct sequences, the aggregate is
+    the sum of the ranks' frames over the slowest rank's wall time."""
+    pytest.importorskip("torch")
+    n, batch, steps = 8, 8, 3
+    r = _run(["--gpus", str(n), "--config", "euroc", "--steps", str(steps), "--warmup", "1", "--batch", str(batch),
+              "--stub-worker"], timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["config"]["workload"].startswith("C5")
+    ranks = out["ranks"]
+    assert [x["rank"] for x in ranks] == list(range(n))
+    assert len({x["seed"] for x in ranks}) == n  # one distinct sequence per GPU
+    assert all(x["frame"] == "752x480" and x["nfeatures"] == 1000 for x in ranks)
+    assert out["frames_total"] == sum(x["frames"] for x in ranks) == n * batch * steps
+    per = out["per_rank_frames_per_s"]
+    assert len(per) == n and min(per) == per[-1]  # rank 7 sleeps longest
+    # value = all frames / the slowest rank's time (not a sum or mean of rates)
+    assert abs(out["value"] - out["frames_total"] / out["job_wall_s"]) / out["value"] < 1e-3
+    assert abs(out["job_wall_s"] - batch * steps / per[-1]) / out["job_wall_s"] < 0.01
+    assert out["value"] < sum(per)
+
+
 def test_gpus_must_match_torchrun_world():
     pytest.importorskip("torch")
     r = _run(["--gpus", "2", "--stub-worker"], {"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
