@@ -61,20 +61,6 @@ __device__ __forceinline__ QNode child_box(const QNode& nd, int q) {
   return c;
 }
 
-// root i of a level: the column [hX * i, hX * (i + 1)) of the border box
-// (src/ORBextractor.cc:903-914), independent of the keys
-__device__ __forceinline__ QNode root_box(float hX, int boxH, int i) {
-  QNode nd;
-  nd.x0 = (int16_t)(int)__fmul_rn(hX, (float)i);
-  nd.x1 = (int16_t)(int)__fmul_rn(hX, (float)(i + 1));
-  nd.y0 = 0;
-  nd.y1 = (int16_t)boxH;
-  return nd;
-}
-// levels with at most this many roots count keys per (root, quadrant) with
-// wave ballots instead of LDS atomics
-constexpr int kQtBallotRoots = 8;
-
 __device__ __forceinline__ int nonempty(int4 c) { return (c.x > 0) + (c.y > 0) + (c.z > 0) + (c.w > 0); }
 
 #ifndef ORBX_QT_MINW
@@ -92,7 +78,8 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
   const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
   int dbg_rounds = 0, dbg_sorted = 0;
   // phase clocks (ORBX_QT_PROF): scalars, not an array, so nothing lands in scratch
-  unsigned long long dbg_p0 = 0, dbg_p1 = 0, dbg_p2 = 0, dbg_p3 = 0, dbg_p4 = 0, dbg_t = 0, dbg_init = 0, dbg_i1 = 0, dbg_i2 = 0;
+  unsigned long long dbg_p0 = 0, dbg_p1 = 0, dbg_p2 = 0, dbg_p3 = 0, dbg_p4 = 0, dbg_t = 0, dbg_init = 0, dbg_i1 = 0,
+                     dbg_i2 = 0;
   auto ph = [&](int k) {
     if (!dbg) return;
     const unsigned long long t = __builtin_amdgcn_s_memtime(), d = t - dbg_t;
@@ -153,32 +140,26 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
     // gather the K keys: cell c's keys (slot_off(c) .. + count) go to coff[c] ..
     if (tid == 0) coff[g.ncells] = K;
     __syncthreads();
-    // one key per lane, its cell the last c with coff[c] <= k (a binary search
-    // of the scanned counts, four keys' searches interleaved), so all of a
-    // thread's key loads are in flight at once: one memory latency instead of
-    // the dependent per-cell rounds of a cell-per-thread copy
-    const int nc = g.ncells;
-    const int top = nc > 1 ? 1 << (31 - __builtin_clz(nc - 1)) : 0;  // largest power of 2 < nc
-    for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
-      int kk[4], c[4];
+    // per cell: its keys are one contiguous slot run; the first eight are
+    // loaded together (most cells hold fewer), the rest in groups of four
+    for (int c = tid; c < g.ncells; c += kQtThreads) {
+      const int b = coff[c], n = coff[c + 1] - b;
+      const uint32_t* src = fslots + s_soff[c];
+      uint32_t v8[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        kk[u] = min(k0 + u * kQtThreads, K - 1);
-        c[u] = 0;
+      for (int i = 0; i < 8; ++i) v8[i] = i < n ? src[i] : 0u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (i < n) keys[b + i] = v8[i];
+      int i = 8;
+      for (; i + 4 <= n; i += 4) {
+        const uint32_t v0 = src[i], v1 = src[i + 1], v2 = src[i + 2], v3 = src[i + 3];
+        keys[b + i] = v0;
+        keys[b + i + 1] = v1;
+        keys[b + i + 2] = v2;
+        keys[b + i + 3] = v3;
       }
-      for (int step = top; step > 0; step >>= 1) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int t = c[u] + step;
-          if (t < nc && coff[t] <= kk[u]) c[u] = t;
-        }
-      }
-      uint32_t v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = fslots[s_soff[c[u]] + (kk[u] - coff[c[u]])];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (k0 + u * kQtThreads < K) keys[k0 + u * kQtThreads] = v[u];
+      for (; i < n; ++i) keys[b + i] = src[i];
     }
   }
   const unsigned long long t_gather = __builtin_amdgcn_s_memtime();
@@ -195,7 +176,11 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
     for (int i = 0; i < nIni; ++i) {
       const int c = rootCnt[i];
       if (c > 0) {
-        const QNode nd = root_box(g.hX, g.boxH, i);
+        QNode nd;
+        nd.x0 = (int16_t)(int)__fmul_rn(g.hX, (float)i);
+        nd.x1 = (int16_t)(int)__fmul_rn(g.hX, (float)(i + 1));
+        nd.y0 = 0;
+        nd.y1 = (int16_t)g.boxH;
         nodeA[n] = nd;
         nkA[n] = c;
         seqA[n] = 0;
@@ -242,7 +227,7 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
       dp[2] = (int)dbg_p2;
       dp[3] = (int)dbg_p3;
       dp[4] = (int)dbg_p4;
-      dp[5] = (int)dbg_init;
+      dp[5] = (int)dbg_init;  // lean rounds: roots counted, roots built, first child counts done
       dp[6] = (int)dbg_i1;
       dp[7] = (int)dbg_i2;
     }
@@ -258,6 +243,24 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
     constexpr int NW = kQtThreads / 64;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     uint32_t* s_key = (uint32_t*)ord;  // sorted rounds: size << 16 | creation per node
+    for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
+      uint32_t kk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) kk[u] = k0 + u * kQtThreads < K ? keys[k0 + u * kQtThreads] : 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (k0 + u * kQtThreads < K) {
+          const int r = (int)__fdiv_rn((float)key_x(kk[u]), g.hX);  // vpIniNodes[kp.pt.x/hX]
+          knode[k0 + u * kQtThreads] = (uint16_t)r;
+          atomicAdd(&rootCnt[r], 1);
+        }
+      }
+    }
+    __syncthreads();
+    if (dbg) dbg_i1 = __builtin_amdgcn_s_memtime() - t_begin;
+    build_roots(true);
+    __syncthreads();
+    if (dbg) dbg_i2 = __builtin_amdgcn_s_memtime() - t_begin;
     QNode* nA = nodeA;
     QNode* nB = nodeB;
     int* kA = nkA;
@@ -268,105 +271,25 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
     int4* cB = cc2;
     int2* mA = s_mid;
     int2* mB = s_mid2;
-    if (nIni <= kQtBallotRoots) {
-      // every key's root AND its quadrant in that root in one pass (root
-      // boxes, so their halves, do not depend on the keys), counted per wave
-      // with ballots over the 4 x nIni (root, quadrant) bins: LDS atomics on a
-      // handful of addresses are serialised by the LDS (the root and first
-      // child passes took 7k + 5k clocks for KITTI level 0's 2,432 keys)
-      int* bins = tB;  // free until the rounds
-      for (int i = tid; i < 4 * nIni; i += kQtThreads) bins[i] = 0;
-      __syncthreads();
-      for (int kb = wv * 64; kb < K; kb += kQtThreads) {  // wave-uniform trip count: the ballots see the whole wave
-        const int k = kb + lane;
-        const bool in = k < K;
-        const uint32_t kk = in ? keys[k] : 0u;
-        const int r = (int)__fdiv_rn((float)key_x(kk), g.hX);  // vpIniNodes[kp.pt.x/hX]
-        int mx, my;
-        halves(root_box(g.hX, g.boxH, r), &mx, &my);
-        const int q = (key_x(kk) >= mx ? 1 : 0) + (key_y(kk) >= my ? 2 : 0);
-        const int b = in ? 4 * r + q : -1;
-        if (in) knode[k] = (uint16_t)((r << 2) | q);  // root index for now
-        for (int j = 0; j < 4 * nIni; ++j) {
-          const int c = __popcll(__ballot(b == j));
-          if (lane == 0 && c) atomicAdd(&bins[j], c);
-        }
+    // first child counts: a key counts into its node's quadrant if the node holds > 1 key
+    for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
+      uint32_t kk[4];
+      int n[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool in = k0 + u * kQtThreads < K;
+        kk[u] = in ? keys[k0 + u * kQtThreads] : 0u;
+        n[u] = in ? knode[k0 + u * kQtThreads] : 0;
       }
-      __syncthreads();
-      if (dbg) dbg_i1 = __builtin_amdgcn_s_memtime() - t_begin;
-      // the non-empty roots in column order (one wave: nIni <= 64); rootCnt[i]
-      // becomes root i's list position (-1: empty, erased)
-      if (tid < 64) {
-        int cq[4] = {0, 0, 0, 0}, c = 0;
-        if (tid < nIni)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            cq[q] = bins[4 * tid + q];
-            c += cq[q];
-          }
-        const uint64_t ne = __ballot(tid < nIni && c > 0);
-        const int pos = mbcnt64(ne);
-        if (tid < nIni && c > 0) {
-          const QNode nd = root_box(g.hX, g.boxH, tid);
-          int mx, my;
-          halves(nd, &mx, &my);
-          nodeA[pos] = nd;
-          nkA[pos] = c;
-          seqA[pos] = 0;
-          s_mid[pos] = make_int2(mx, my);
-          cc[pos] = c > 1 ? make_int4(cq[0], cq[1], cq[2], cq[3]) : make_int4(0, 0, 0, 0);  // one key never splits
-        }
-        if (tid < nIni) rootCnt[tid] = c > 0 ? pos : -1;
-        if (tid == 0) {
-          s_var[0] = __popcll(ne);  // list size
-          s_var[1] = 0;             // sorted-phase flag
-          s_var[6] = s_var[7] = s_var[8] = 0;  // tie-straddle events / group nodes / kept keys
-        }
-      }
-      __syncthreads();
-      if (dbg) dbg_i2 = __builtin_amdgcn_s_memtime() - t_begin;
-      if (s_var[0] != nIni)  // an empty root was erased: root index -> list position
-        for (int k = tid; k < K; k += kQtThreads)
-          knode[k] = (uint16_t)((rootCnt[knode[k] >> 2] << 2) | (knode[k] & 3));
-    } else {
-      for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
-        uint32_t kk[4];
+      for (int u = 0; u < 4; ++u) n[u] = rootCnt[n[u]];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) kk[u] = k0 + u * kQtThreads < K ? keys[k0 + u * kQtThreads] : 0u;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (k0 + u * kQtThreads < K) {
-            const int r = (int)__fdiv_rn((float)key_x(kk[u]), g.hX);  // vpIniNodes[kp.pt.x/hX]
-            knode[k0 + u * kQtThreads] = (uint16_t)r;
-            atomicAdd(&rootCnt[r], 1);
-          }
-        }
-      }
-      __syncthreads();
-      if (dbg) dbg_i1 = __builtin_amdgcn_s_memtime() - t_begin;
-      build_roots(true);
-      __syncthreads();
-      if (dbg) dbg_i2 = __builtin_amdgcn_s_memtime() - t_begin;
-      // first child counts: a key counts into its node's quadrant if the node holds > 1 key
-      for (int k0 = tid; k0 < K; k0 += 4 * kQtThreads) {
-        uint32_t kk[4];
-        int n[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const bool in = k0 + u * kQtThreads < K;
-          kk[u] = in ? keys[k0 + u * kQtThreads] : 0u;
-          n[u] = in ? knode[k0 + u * kQtThreads] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) n[u] = rootCnt[n[u]];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (k0 + u * kQtThreads < K) {
-            const int2 md = mA[n[u]];
-            const int q = (key_x(kk[u]) >= md.x ? 1 : 0) + (key_y(kk[u]) >= md.y ? 2 : 0);
-            if (kA[n[u]] > 1) atomicAdd(((int*)&cA[n[u]]) + q, 1);
-            knode[k0 + u * kQtThreads] = (uint16_t)((n[u] << 2) | q);
-          }
+      for (int u = 0; u < 4; ++u) {
+        if (k0 + u * kQtThreads < K) {
+          const int2 md = mA[n[u]];
+          const int q = (key_x(kk[u]) >= md.x ? 1 : 0) + (key_y(kk[u]) >= md.y ? 2 : 0);
+          if (kA[n[u]] > 1) atomicAdd(((int*)&cA[n[u]]) + q, 1);
+          knode[k0 + u * kQtThreads] = (uint16_t)((n[u] << 2) | q);
         }
       }
     }
@@ -977,7 +900,8 @@ int launch_quadtree(const ExtractParams& P, const ExtractBuffers& X, int batch, 
         ga += h[(f * P.L + l) * 8 + 7];
       }
       fprintf(stderr, "quadtree L%d: avg cycles rounds %.0f total %.0f (max %d) rounds %.1f sorted %.1f K %.0f out %.0f"
-              " | scan %.0f gather %.0f roots %.0f built %.0f init %.0f | count %.0f order %.0f sortorder %.0f table %.0f rehome %.0f\n",
+              " | scan %.0f gather %.0f roots %.0f built %.0f init %.0f | count %.0f order %.0f sortorder %.0f table %.0f"
+              " rehome %.0f\n",
               l, a[0] / batch, a[1] / batch, mx, a[2] / batch, a[3] / batch, a[4] / batch, a[5] / batch,
               sc / batch, ga / batch, q[6] / batch, q[7] / batch, q[5] / batch, q[0] / batch, q[1] / batch, q[4] / batch, q[2] / batch, q[3] / batch);
     }
