@@ -48,10 +48,13 @@ constexpr int kObRows = 2 * kObRadius + 1;   // 39
 #endif
 constexpr int kObStride = ORBX_OB_STRIDE;
 static_assert(kObStride >= 64 && kObStride % 8 == 0, "rows hold 4 chunks, 8-byte aligned");
-// IC coefficient rows in LDS: 24 dwords each, padded to an odd stride so the
-// 16 |v| rows a wave reads at once fall in distinct banks
+// IC coefficient rows in LDS: 24 dwords each, read as 6 ds_read_b128 per lane
+// (bank = dword mod 64, 16-lane groups); at a stride of 28 dwords (4 x odd)
+// the 16 |v| rows start on 16 distinct multiples of 4 banks, so a group's
+// reads never share a bank (24 put rows 4 apart on one bank: LDS bank-conflict
+// cycles per 32-frame launch 4.58 M -> 3.91 M, time equal; round 5)
 #ifndef ORBX_OB_ICSTRIDE
-#define ORBX_OB_ICSTRIDE 24
+#define ORBX_OB_ICSTRIDE 28
 #endif
 constexpr int kIcStride = ORBX_OB_ICSTRIDE;
 
