@@ -1,10 +1,11 @@
 #!/bin/bash
-# Round-4 evidence, part B (run after part A and tools/collect_r04.sh): per-config bench lines + rocprofv3 stats (C2, C4,
+# A round's evidence, part B (ROUND=rNN; run after part A and tools/collect.sh): per-config bench lines + rocprofv3 stats (C2, C4,
 # C5, C3 + BoW, the KITTI14 / intcatch-1080p settings), SQ counters of the
 # serial C3 bench, FAST and search_init phase clocks, the link microbench.
 set -e
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/ev4b; mkdir -p $O
+R=${ROUND:-r05}
+O=gpurun_out/ev_${R}b; mkdir -p $O
 cd /tmp; export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
 run() {  # name, bench args
   local name=$1; shift
@@ -20,7 +21,11 @@ run bowmatch --bow-match
 run bowmatch_serial --bow-match --serial
 run kitti14 --config kitti14
 run intcatch1080 --config intcatch1080
-bash tools/pmc_sq.sh gpurun_out/ev4b/sq > $O/sq.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/intcatch1080_serial -o run -- \
+  python3 bench.py --cpu-sample 0 --no-latency --no-host-stream --steps 30 --warmup 5 --serial --config intcatch1080 \
+  > $O/intcatch1080_serial.log 2>&1
+bash tools/qt_prof.sh > $O/qt_phases.txt 2>&1
+bash tools/pmc_sq.sh $O/sq > $O/sq.log 2>&1
 python3 tools/sq_valu.py $O/sq/summary.txt $O/sq_valu.json
 ORBX_FAST_PROF=1 timeout -k 10 100 python3 bench.py --allow-diag --serial --steps 1 --warmup 1 --cpu-sample 0 --no-latency --no-host-stream --pool 64 2>&1 | grep "^fast" > $O/fast_phases.txt
 ORBX_INIT_PROF=1 timeout -k 10 100 python3 tools/init_timing.py 64 > $O/init_phases.txt 2>&1
@@ -29,7 +34,7 @@ timeout -k 10 120 python3 tools/h2d_bench.py > $O/h2d.json
 # (pmc_traffic.json from part A, collected into profiles/ before this call;
 # sq_valu.json from the passes above)
 cp $O/sq_valu.json profiles/sq_valu.json
-mkdir -p gpurun_out/ev4c
-timeout -k 10 400 python3 bench.py > gpurun_out/ev4c/bench_default.log 2>&1
-tail -n 1 gpurun_out/ev4c/bench_default.log | cut -c1-200
+mkdir -p gpurun_out/ev_${R}c
+timeout -k 10 400 python3 bench.py > gpurun_out/ev_${R}c/bench_default.log 2>&1
+tail -n 1 gpurun_out/ev_${R}c/bench_default.log | cut -c1-200
 echo all-done
