@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void copy2d_kernel(uint8_t* __restrict__ d, si
   }
 }
 size_t quadtree_lds_bytes(const ExtractParams& P);
-extern const void* quadtree_kernel_ptr();
+extern const void* quadtree_kernel_ptr(int big);
 size_t pyr_band_lds_bytes(const ExtractParams& P);
 extern const void* pyr_band_kernel_ptr();
 extern int pyr_band_occupancy(size_t lds);
@@ -487,12 +487,18 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     P.qt_lean = maxnodes < 16384 && !(e && e[0] == '1');
   }
   {
-    // keep the LDS footprint at 80 KiB so two quadtree blocks fit one CU
+    // keep the LDS footprint at 80 KiB so two quadtree blocks fit one CU,
+    // unless the node tables alone nearly fill that (large levels: 1920x1080
+    // has 102 KB of them). Then a block takes a whole CU: 1024 threads (its
+    // key passes, which set its time there, on twice the lanes) and 160 KiB,
+    // the rest of it for keys
 #ifndef ORBX_QT_LDS_KB
 #define ORBX_QT_LDS_KB 80
 #endif
     const size_t base = quadtree_lds_bytes(P);
-    const size_t budget = ORBX_QT_LDS_KB * 1024;
+    const size_t small = ORBX_QT_LDS_KB * 1024, big = 160 * 1024 - 512;
+    P.qt_big = base + 16 * 1024 > small ? 1 : 0;
+    const size_t budget = P.qt_big ? big : small;
     P.kcap_lds = base < budget ? (int)((budget - base) / 6) & ~15 : 0;
   }
   pl.P = P;
@@ -539,7 +545,7 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
         fprintf(stderr, "pyr plan %d: %d workgroups per CU\n", i, pl.P.pyr_plan[i].occ);
     }
   }
-  if (raise_lds_limit(quadtree_kernel_ptr(), quadtree_lds_bytes(P)))
+  if (raise_lds_limit(quadtree_kernel_ptr(P.qt_big), quadtree_lds_bytes(P)))
     return fail(ORBX_EDEVICE, "LDS limit of quadtree_kernel: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
 }

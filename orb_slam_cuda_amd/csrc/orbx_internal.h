@@ -80,6 +80,7 @@ struct ExtractParams {
   int max_cells_level;         // largest ncells of any level
   int kcap_lds;                // quadtree keys kept in LDS up to this count
   int qt_lean;                 // quadtree: lean rounds (packed 16-bit key nodes, maxnodes < 16384), else the generic ones
+  int qt_big;                  // quadtree: node tables past 64 KB of LDS: 1024-thread blocks, a whole CU's LDS each
   int fast_rh_max;             // largest FAST cell ROI height
   int fast_bw_max, fast_bh_max;  // largest FAST detection band
   int pattern_upstream;

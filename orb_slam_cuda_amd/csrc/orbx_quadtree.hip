@@ -66,6 +66,10 @@ __device__ __forceinline__ int nonempty(int4 c) { return (c.x > 0) + (c.y > 0) +
 #ifndef ORBX_QT_MINW
 #define ORBX_QT_MINW 1
 #endif
+// kQtThreads: 512 (every plan whose node tables leave room for two blocks per
+// CU) or 1024 (large levels, whose blocks take a CU each and whose key passes
+// then run on twice the lanes)
+template <int kQtThreads>
 __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(ExtractParams P, const int* __restrict__ cell_counts,
                                                               const uint32_t* __restrict__ slots,
                                                               const CellGeom* __restrict__ cells,
@@ -869,16 +873,23 @@ size_t quadtree_lds_bytes(const ExtractParams& P) {
          r16(4ull * P.kcap_lds) + r16(2ull * P.kcap_lds);
 }
 
-const void* quadtree_kernel_ptr() { return (const void*)quadtree_kernel; }
+const void* quadtree_kernel_ptr(int big) {
+  return big ? (const void*)quadtree_kernel<1024> : (const void*)quadtree_kernel<kQtThreads>;
+}
 
 int launch_quadtree(const ExtractParams& P, const ExtractBuffers& X, int batch, hipStream_t s) {
   static int* dbg = nullptr;  // diagnostics only: per-(frame, level) cycles and rounds (ORBX_QT_PROF=1)
   static const bool prof = getenv("ORBX_QT_PROF") && getenv("ORBX_QT_PROF")[0] == '1';
   const int nwg = P.L * batch;
   if (prof && !dbg) (void)hipMalloc(&dbg, (size_t)nwg * 64);
-  hipLaunchKernelGGL(quadtree_kernel, dim3(P.L, batch), dim3(kQtThreads), quadtree_lds_bytes(P), s, P,
-                     X.cell_counts, X.slots, X.cells, X.qscratch, X.qnode_scratch, X.qkeys, X.qcounts, X.qties, X.err,
-                     prof ? dbg : nullptr);
+  if (P.qt_big)
+    hipLaunchKernelGGL(quadtree_kernel<1024>, dim3(P.L, batch), dim3(1024), quadtree_lds_bytes(P), s, P,
+                       X.cell_counts, X.slots, X.cells, X.qscratch, X.qnode_scratch, X.qkeys, X.qcounts, X.qties, X.err,
+                       prof ? dbg : nullptr);
+  else
+    hipLaunchKernelGGL(quadtree_kernel<kQtThreads>, dim3(P.L, batch), dim3(kQtThreads), quadtree_lds_bytes(P), s, P,
+                       X.cell_counts, X.slots, X.cells, X.qscratch, X.qnode_scratch, X.qkeys, X.qcounts, X.qties, X.err,
+                       prof ? dbg : nullptr);
   if (prof) {
     std::vector<int> h((size_t)nwg * 16);
     (void)hipStreamSynchronize(s);
