@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cstdarg>
 #include <climits>
@@ -142,6 +143,10 @@ struct orbx_extractor {
   long long h_pyr_off[kMaxLevels] = {};  // level l's offset in h_pyr (l >= 1)
   hipStream_t pstream = nullptr;         // the copy branch's stream (capture fork)
   hipEvent_t pev[2] = {};                // pyramid done, copy done
+  // ORBX_EXTRACT_PROF=1 (diagnostics): orbx_extract's host phases, summed
+  // and printed by orbx_destroy: staging copy, issue, wait, copy-out
+  double prof_s[4] = {};
+  long long prof_n = 0;
   std::mutex mu;
 };
 
@@ -693,6 +698,10 @@ int orbx_destroy(orbx_handle h) {
   h->ws.release();
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
   if (h->pstream) (void)hipStreamSynchronize(h->pstream);
+  if (h->prof_n)
+    fprintf(stderr, "orbx_extract host phases over %lld calls (us): stage %.1f issue %.1f wait %.1f out %.1f\n", h->prof_n,
+            h->prof_s[0] / h->prof_n * 1e6, h->prof_s[1] / h->prof_n * 1e6, h->prof_s[2] / h->prof_n * 1e6,
+            h->prof_s[3] / h->prof_n * 1e6);
   if (h->h_in) (void)hipHostFree(h->h_in);
   if (h->h_out) (void)hipHostFree(h->h_out);
   if (h->h_pyr) (void)hipHostFree(h->h_pyr);
@@ -843,7 +852,11 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
     for (auto& e : h->pev)
       if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
+  static const bool prof = getenv("ORBX_EXTRACT_PROF") && getenv("ORBX_EXTRACT_PROF")[0] == '1';
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t0 = prof ? now() : 0;
   for (int y = 0; y < hh; ++y) memcpy((uint8_t*)h->h_in + (size_t)y * pitch, img + (size_t)y * stride, w);
+  const double t1 = prof ? now() : 0;
   // the plan buffers may still be in use by a batch call on another stream
   if (h->ws.before(h->stream)) return fail(ORBX_EDEVICE, "stream wait on the handle's last use failed");
   static const bool use_graph = !(getenv("ORBX_EXTRACT_GRAPH") && getenv("ORBX_EXTRACT_GRAPH")[0] == '0');
@@ -884,7 +897,9 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   h->last_frames = h->d_in.as<uint8_t>();
   h->last_fpitch = pitch * hh;
   h->last_rstride = pitch;
+  const double t2 = prof ? now() : 0;
   HIP_OK(hipStreamSynchronize(h->stream));
+  const double t3 = prof ? now() : 0;
   h->host_pyr_valid = h->host_pyr;
   const int* head = (const int*)h->h_out;
   const int cnt = head[0], err = head[1];
@@ -902,6 +917,14 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   const uint8_t* o = (const uint8_t*)h->h_out + 16;
   if (kps) memcpy(kps, o, (size_t)cnt * sizeof(orbx_kp));
   if (desc) memcpy(desc, (const uint8_t*)h->h_out + out_desc_off(cap_frame), (size_t)cnt * 32);
+  if (prof) {
+    const double t4 = now();
+    h->prof_s[0] += t1 - t0;
+    h->prof_s[1] += t2 - t1;
+    h->prof_s[2] += t3 - t2;
+    h->prof_s[3] += t4 - t3;
+    ++h->prof_n;
+  }
   return ORBX_OK;
 }
 
