@@ -414,3 +414,61 @@ def test_batch_search_init_dense_pair(pkg, O):
         r12, rnm, _ = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), np.stack([k1["x"], k1["y"]], 1),
                                                   100, 0.9, True)
         assert gnm[p] == rnm and np.array_equal(got[p, :len(k1)], r12), p
+
+
+@pytest.mark.parametrize("cap,ratio", [(2101, 0.9), (2099, 0.7), (1999, 0.75)])
+def test_batch_search_init_odd_pitch(pkg, O, cap, ratio):
+    """Odd keypoint pitches (the per-pair workspace's key table
+    must stay 16-byte aligned whatever the pitch; its int tables are padded to
+    4 ints) at three ratios (6-, 7- and 7-bit distance clamps): exact against
+    the oracle, status clean."""
+    import ctypes as C
+
+    from orb_slam_cuda_amd import _lib
+    W, H = 1241, 376
+    pairs = [_pair(O, 40), _pair(O, 41), _pair(O, 42)]
+    P = len(pairs)
+    kp = np.zeros((2 * P, cap), pkg.KP_DTYPE)
+    de = np.zeros((2 * P, cap, 32), np.uint8)
+    n = np.zeros(2 * P, np.int32)
+    for p, ((k1, d1), (k2, d2)) in enumerate(pairs):
+        k1, d1, k2, d2 = k1[:cap], d1[:cap], k2[:cap], d2[:cap]
+        kp[p, :len(k1)], de[p, :len(k1)], n[p] = k1, d1, len(k1)
+        kp[P + p, :len(k2)], de[P + p, :len(k2)], n[P + p] = k2, d2, len(k2)
+    dk, dd, dn = (_lib.DeviceArray(a.nbytes) for a in (kp, de, n))
+    dk.upload(kp), dd.upload(de), dn.upload(n)
+    dm, dnm = _lib.DeviceArray(P * cap * 4), _lib.DeviceArray(P * 4)
+    m = pkg.ORBmatcher(ratio, True, max_pairs=P, max_kps=cap)
+    L = _lib.lib()
+    _lib.check(L.orbm_search_for_initialization_batch(
+        m.handle, C.c_void_p(dk.ptr), C.c_void_p(dd.ptr), C.c_void_p(dn.ptr),
+        C.c_void_p(dk.ptr + P * cap * 28), C.c_void_p(dd.ptr + P * cap * 32), C.c_void_p(dn.ptr + P * 4),
+        cap, P, _lib.GridBounds(0, W, 0, H), None, 100, C.c_float(ratio), 1, C.c_void_p(dm.ptr),
+        C.c_void_p(dnm.ptr), None), matcher=True)
+    L.orbx_stream_synchronize(None)
+    got = dm.download((P, cap), np.int32)
+    gnm = dnm.download(P, np.int32)
+    assert m.status() == 0
+    for p in range(P):
+        k1, d1, k2, d2 = kp[p, :n[p]], de[p, :n[p]], kp[P + p, :n[P + p]], de[P + p, :n[P + p]]
+        r12, rnm, _ = O.search_for_initialization(k1, d1, k2, d2, (0, W, 0, H), np.stack([k1["x"], k1["y"]], 1),
+                                                  100, ratio, True)
+        assert gnm[p] == rnm and np.array_equal(got[p, :len(k1)], r12), p
+
+
+def test_search_init_capacity_message_names_the_bound(pkg):
+    """ECAPACITY at a pitch past 2^(20 - dbits): the message names the bound of
+    the call's ratio, 8192 at 0.7."""
+    import ctypes as C
+
+    from orb_slam_cuda_amd import _lib
+    cap = 8200
+    m = pkg.ORBmatcher(0.7, True, max_pairs=1, max_kps=cap)
+    L = _lib.lib()
+    d = _lib.DeviceArray(cap * 32 * 2 + 64)
+    rc = L.orbm_search_for_initialization_batch(
+        m.handle, C.c_void_p(d.ptr), C.c_void_p(d.ptr), C.c_void_p(d.ptr), C.c_void_p(d.ptr), C.c_void_p(d.ptr),
+        C.c_void_p(d.ptr), cap, 1, _lib.GridBounds(0, 1241, 0, 376), None, 100, C.c_float(0.7), 1,
+        C.c_void_p(d.ptr), C.c_void_p(d.ptr), None)
+    assert rc == _lib.ORBX_ECAPACITY
+    assert b"8192" in L.orbm_last_error()
