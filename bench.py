@@ -200,7 +200,7 @@ def parse_args(argv=None):
 # Tuning: select among bit-exact code paths; allowed, and stamped into the line.
 ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_EXTRACT_ORDER", "ORBX_PYR_PLAN", "ORBX_QT_GENERIC",
               "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS",
-              "ORBX_BOW_ROUNDS",
+              "ORBX_BOW_ROUNDS", "ORBX_PYR_KEEP",
               # the C++ shim's configuration (shim/src/ORBextractor.cc); bench.py does not read them
               "ORBX_DEVICE", "ORBX_SCALE_MODE", "ORBX_PATTERN", "ORBX_HOST_PYRAMID"}
 # Diagnostics: phase clocks synchronise after every launch, *_STOP / FAST_TWICE

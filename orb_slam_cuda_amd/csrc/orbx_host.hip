@@ -256,83 +256,203 @@ static void resize_tables(int sw, int sh, int dw, int dh, std::vector<int2>& xt,
 // own rows plus every source row its level-(l+1) rows read. Level 0 rows are
 // only read. R shrinks until the two LDS row buffers fit; if even R = 1 does
 // not, the per-level kernel is used.
+// Column tiles split every band the same way (rows and columns are
+// separable): tile c of the last level owns an even-aligned share of its
+// columns; walking down, its columns at level l start at the first source
+// column of its first column at level l+1 (rounded down to even, so that the
+// owned ranges of every level start even and a 2-column store never straddles
+// two tiles), and it computes every source column its level-(l+1) columns read.
+// Per (tile, level) the table holds {comp_lo, comp_hi}, {own_lo, own_hi} and
+// {LDS row pitch, LDS origin}: the column of LDS byte 0 (level 0, staged in
+// 16-byte chunks: comp_lo rounded down to 16; else comp_lo).
+struct PyrCols {
+  int nct = 1;
+  std::vector<int> lo, chi, ohi;  // [tile][level]
+  int lpitch[kMaxLevels] = {};    // LDS row pitch per level (the widest tile)
+};
+
+static bool plan_pyr_cols(const ExtractParams& P, const std::vector<int2>& rtab, int nct, PyrCols& C) {
+  const int L = P.L, WL = P.lv[L - 1].w;
+  if (nct > 1 && WL / nct < 32) return false;  // tiles of >= 32 last-level columns
+  C.nct = nct;
+  C.lo.assign((size_t)nct * L, 0);
+  C.chi.assign((size_t)nct * L, 0);
+  C.ohi.assign((size_t)nct * L, 0);
+  // source columns of output column x at level l (>= 1): sx and sx + 1 (xtab2
+  // folds the 2x area case in as {2x, 0}); past the last column, the last one's
+  auto src_lo_x = [&](int l, int x) { return rtab[P.lv[l].xtab2 + std::min(x, P.lv[l].w - 1)].x; };
+  auto src_hi_x = [&](int l, int x) { return rtab[P.lv[l].xtab2 + std::min(x, P.lv[l].w - 1)].x + 1; };
+  for (int c = 0; c < nct; ++c) {
+    C.lo[c * L + L - 1] = c == 0 ? 0 : ((int)((long long)c * WL / nct) & ~1);
+    C.chi[c * L + L - 1] = C.ohi[c * L + L - 1] = (c + 1 < nct ? ((int)((long long)(c + 1) * WL / nct) & ~1) : WL) - 1;
+  }
+  for (int l = L - 2; l >= 0; --l)
+    for (int c = 0; c < nct; ++c) C.lo[c * L + l] = c == 0 ? 0 : (src_lo_x(l + 1, C.lo[c * L + l + 1]) & ~1);
+  for (int l = L - 2; l >= 0; --l)
+    for (int c = 0; c < nct; ++c) {
+      const int own_hi = c + 1 < nct ? C.lo[(c + 1) * L + l] - 1 : P.lv[l].w - 1;
+      if (own_hi < C.lo[c * L + l]) return false;  // a tile with no column of its own
+      C.ohi[c * L + l] = own_hi;
+      C.chi[c * L + l] = std::max(src_hi_x(l + 1, C.chi[c * L + l + 1]), l > 0 ? own_hi : 0);
+    }
+  for (int l = 0; l < L; ++l) {
+    int p = 0;
+    for (int c = 0; c < nct; ++c) {
+      const int lo = C.lo[c * L + l], hi = C.chi[c * L + l];
+      // level 0: 16-byte chunks from lo & ~15 up to column hi (the last sx + 1
+      // read; past the image it reads an unstaged byte, weighted 0); other
+      // levels: the 2-column runs of G = ceil(width / 8) groups end <= 6 past hi
+      p = std::max(p, l == 0 ? ((hi - (lo & ~15) + 1 + 15) & ~15) : ((hi - lo + 1 + 8 + 15) & ~15));
+    }
+    C.lpitch[l] = p;
+  }
+  return true;
+}
+
 static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
   P.pyr_fused = 0;
   const int L = P.L;
   if (L < 2) return;
-  for (int l = 0; l < L; ++l) P.lv[l].lpitch = (P.lv[l].w + 8 + 15) & ~15;
   auto src_lo = [&](int l, int y) { return P.lv[l].area2x ? 2 * y : (rtab[P.lv[l].ytab + y].x & 0xFFFF); };
   auto src_hi = [&](int l, int y) { return P.lv[l].area2x ? 2 * y + 1 : (rtab[P.lv[l].ytab + y].x >> 16); };
   const int HL = P.lv[L - 1].h;
-  // prefer bands small enough for two workgroups per CU (the kernel is
-  // latency-bound: more resident waves beat less halo recompute)
-  // Several band heights R are planned (R0 = HL/18 and up to five taller);
-  // launch_pyramid picks the one whose workgroup count best fits the chip for
-  // the launch's batch (576 workgroups on 512 slots cost two full rounds).
+  // Candidate tilings: band heights R (R0 = HL/18 and up to five taller, down
+  // to R0/3) x 1, 2 or 4 column tiles, those whose LDS allows two workgroups
+  // per CU (the kernel is latency-bound: more resident waves beat less halo
+  // recompute). launch_pyramid picks per launch the plan whose workgroup
+  // count fits the chip best for the launch's batch (576 workgroups on 512
+  // slots cost two full rounds); up to 8 plans are kept: the best of the
+  // candidates for batches of 1 .. 64 and B, and the default (R0, one tile).
   const size_t budgets[2] = {78 * 1024, 160 * 1024 - 1024};
   const int R0 = std::max(1, (HL + 17) / 18);
-  P.pyr_nplans = 0;
-  for (int pass = 0; pass < 2 && P.pyr_nplans == 0; ++pass)
-  for (int R = pass == 0 ? R0 + 5 : R0; R >= std::max(1, R0 / 3) && P.pyr_nplans < 6; --R) {
-    const size_t budget = budgets[pass];
-    const int nb = (HL + R - 1) / R;
-    std::vector<int> lo((size_t)nb * L), chi((size_t)nb * L), ohi((size_t)nb * L);
-    for (int b = 0; b < nb; ++b) {
-      lo[b * L + L - 1] = b * R;
-      chi[b * L + L - 1] = ohi[b * L + L - 1] = std::min((b + 1) * R, HL) - 1;
-    }
-    for (int l = L - 2; l >= 0; --l)
-      for (int b = 0; b < nb; ++b) lo[b * L + l] = b == 0 ? 0 : src_lo(l + 1, lo[b * L + l + 1]);
-    for (int l = L - 2; l >= 0; --l)
+  struct Cand {
+    int R, nb, nct;
+    size_t need0, need1, ybytes;
+    long long cost;
+    std::vector<int> lo, chi, ohi;
+    PyrCols cols;
+  };
+  std::vector<Cand> cands;
+  PyrCols colplans[3];
+  bool colok[3];
+  for (int k = 0; k < 3; ++k) colok[k] = plan_pyr_cols(P, rtab, 1 << k, colplans[k]);
+  for (int pass = 0; pass < 2 && cands.empty(); ++pass)
+    for (int R = pass == 0 ? R0 + 5 : R0; R >= std::max(1, R0 / 3); --R) {
+      const int nb = (HL + R - 1) / R;
+      if (!cands.empty() && cands.back().nb == nb) continue;  // same band count as a taller R
+      std::vector<int> lo((size_t)nb * L), chi((size_t)nb * L), ohi((size_t)nb * L);
       for (int b = 0; b < nb; ++b) {
-        const int own_hi = b + 1 < nb ? lo[(b + 1) * L + l] - 1 : P.lv[l].h - 1;
-        ohi[b * L + l] = own_hi;
-        chi[b * L + l] = std::max(src_hi(l + 1, chi[b * L + l + 1]), l > 0 ? own_hi : 0);
+        lo[b * L + L - 1] = b * R;
+        chi[b * L + L - 1] = ohi[b * L + L - 1] = std::min((b + 1) * R, HL) - 1;
       }
-    size_t need[2] = {0, 0};
-    for (int l = 0; l < L; ++l) {
-      int rows = 0;
-      for (int b = 0; b < nb; ++b) rows = std::max(rows, chi[b * L + l] - lo[b * L + l] + 1);
-      need[l & 1] = std::max(need[l & 1], (size_t)rows * P.lv[l].lpitch);
-    }
-    need[0] = (need[0] + 15) & ~(size_t)15;
-    need[1] = (need[1] + 15) & ~(size_t)15;
-    size_t ybytes = 0;
-    for (int b = 0; b < nb; ++b) {
-      size_t s = 0;
-      for (int l = 1; l < L; ++l) s += (size_t)(chi[b * L + l] - lo[b * L + l] + 1) * 8;
-      ybytes = std::max(ybytes, s);
-    }
-    if (need[0] + need[1] + ybytes + 16 > budget) continue;
-    if (P.pyr_nplans > 0 && P.pyr_plan[P.pyr_nplans - 1].nbands == nb) continue;  // same band count as a taller R
-    long long cost = 0;
-    for (int b = 0; b < nb; ++b) {
-      long long c = 0;
-      for (int l = 0; l < L; ++l) c += (long long)(chi[b * L + l] - lo[b * L + l] + 1) * P.lv[l].w;
-      cost = std::max(cost, c);
-    }
-    ExtractParams::PyrPlan& q = P.pyr_plan[P.pyr_nplans++];
-    q.nbands = nb;
-    q.lds_a = (int)need[0];
-    q.lds_b = (int)need[1];
-    q.lds_y = (int)ybytes;
-    q.bands = (int)rtab.size();
-    q.cost = (int)cost;
-    for (int b = 0; b < nb; ++b)
-      for (int l = 0; l < L; ++l) {
-        rtab.push_back(make_int2(lo[b * L + l], chi[b * L + l]));
-        rtab.push_back(make_int2(lo[b * L + l], ohi[b * L + l]));
+      for (int l = L - 2; l >= 0; --l)
+        for (int b = 0; b < nb; ++b) lo[b * L + l] = b == 0 ? 0 : src_lo(l + 1, lo[b * L + l + 1]);
+      for (int l = L - 2; l >= 0; --l)
+        for (int b = 0; b < nb; ++b) {
+          const int own_hi = b + 1 < nb ? lo[(b + 1) * L + l] - 1 : P.lv[l].h - 1;
+          ohi[b * L + l] = own_hi;
+          chi[b * L + l] = std::max(src_hi(l + 1, chi[b * L + l + 1]), l > 0 ? own_hi : 0);
+        }
+      size_t ybytes = 0;
+      for (int b = 0; b < nb; ++b) {
+        size_t s = 0;
+        for (int l = 1; l < L; ++l) s += (size_t)(chi[b * L + l] - lo[b * L + l] + 1) * 8;
+        ybytes = std::max(ybytes, s);
       }
-    if (pass == 1) break;  // the large-LDS fallback: one workgroup per CU, one plan
+      for (int k = 0; k < 3; ++k) {
+        if (!colok[k]) continue;
+        const PyrCols& C = colplans[k];
+        size_t need[2] = {0, 0};
+        for (int l = 0; l < L; ++l) {
+          int rows = 0;
+          for (int b = 0; b < nb; ++b) rows = std::max(rows, chi[b * L + l] - lo[b * L + l] + 1);
+          need[l & 1] = std::max(need[l & 1], (size_t)rows * C.lpitch[l]);
+        }
+        need[0] = (need[0] + 15) & ~(size_t)15;
+        need[1] = (need[1] + 15) & ~(size_t)15;
+        if (need[0] + need[1] + ybytes + 16 > budgets[pass]) continue;
+        long long cost = 0;
+        for (int b = 0; b < nb; ++b)
+          for (int c = 0; c < C.nct; ++c) {
+            long long s = 0;
+            for (int l = 0; l < L; ++l)
+              s += (long long)(chi[b * L + l] - lo[b * L + l] + 1) * (C.chi[c * L + l] - C.lo[c * L + l] + 1);
+            cost = std::max(cost, s);
+          }
+        cands.push_back(Cand{R, nb, C.nct, need[0], need[1], ybytes, cost, lo, chi, ohi, C});
+      }
+      if (pass == 1 && !cands.empty()) break;  // the large-LDS fallback: one workgroup per CU, one band height
+    }
+  if (cands.empty()) return;
+  // the plans kept: the one-tile plans (band heights as before column tiles
+  // existed; the default first: R0's or the nearest), then for small batches
+  // the column-tiled plan that pick_pyr_plan would take in one round
+  std::vector<int> keep;
+  // experiments (tools/pyr_plans.py): ORBX_PYR_KEEP="nb:nct,nb:nct,..." keeps
+  // exactly those candidates (up to 8, in that order)
+  const char* ek = getenv("ORBX_PYR_KEEP");
+  if (ek) {
+    for (const char* p = ek; *p && keep.size() < 8;) {
+      int nb = 0, nct = 0, used = 0;
+      if (sscanf(p, "%d:%d%n", &nb, &nct, &used) != 2) break;
+      for (int i = 0; i < (int)cands.size(); ++i)
+        if (cands[i].nb == nb && cands[i].nct == nct) keep.push_back(i);
+      p += used;
+      if (*p == ',') ++p;
+    }
   }
-  if (P.pyr_nplans == 0) return;
-  // default plan (R0's or the nearest): the LDS attribute covers the largest
+  if (keep.empty()) {
+    int def = -1;
+    for (int i = 0; i < (int)cands.size(); ++i)
+      if (cands[i].nct == 1 &&
+          (def < 0 || std::abs(cands[i].nb - (HL + R0 - 1) / R0) < std::abs(cands[def].nb - (HL + R0 - 1) / R0)))
+        def = i;
+    if (def < 0) def = 0;
+    keep.push_back(def);
+    for (int i = 0; i < (int)cands.size() && keep.size() < 5; ++i)
+      if (cands[i].nct == 1 && i != def) keep.push_back(i);
+    // (the picker's rule on a 256-CU chip, two workgroups per CU)
+    for (int bt : {1, 2, 4, 8, 16}) {
+      int best = -1;
+      for (const long long lim : {256, 512}) {
+        for (int i = 0; i < (int)cands.size(); ++i)
+          if (cands[i].nct > 1 && (long long)cands[i].nb * cands[i].nct * bt <= lim &&
+              (best < 0 || cands[i].cost < cands[best].cost))
+            best = i;
+        if (best >= 0) break;
+      }
+      if (best >= 0 && keep.size() < 8 && std::find(keep.begin(), keep.end(), best) == keep.end()) keep.push_back(best);
+    }
+  }
+  P.pyr_nplans = 0;
+  for (int i : keep) {
+    const Cand& c = cands[i];
+    ExtractParams::PyrPlan& q = P.pyr_plan[P.pyr_nplans++];
+    q.nbands = c.nb;
+    q.nct = c.nct;
+    q.lds_a = (int)c.need0;
+    q.lds_b = (int)c.need1;
+    q.lds_y = (int)c.ybytes;
+    q.cost = (int)c.cost;
+    q.occ = 0;
+    q.bands = (int)rtab.size();
+    for (int b = 0; b < c.nb; ++b)
+      for (int l = 0; l < L; ++l) {
+        rtab.push_back(make_int2(c.lo[b * L + l], c.chi[b * L + l]));
+        rtab.push_back(make_int2(c.lo[b * L + l], c.ohi[b * L + l]));
+      }
+    q.ctiles = (int)rtab.size();
+    const PyrCols& C = c.cols;
+    for (int t = 0; t < C.nct; ++t)
+      for (int l = 0; l < L; ++l) {
+        const int lo = C.lo[t * L + l];
+        rtab.push_back(make_int2(lo, C.chi[t * L + l]));
+        rtab.push_back(make_int2(lo, C.ohi[t * L + l]));
+        rtab.push_back(make_int2(C.lpitch[l], l == 0 ? (lo & ~15) : lo));
+      }
+  }
   P.pyr_fused = 1;
-  int def = 0;
-  for (int i = 0; i < P.pyr_nplans; ++i)
-    if (std::abs(P.pyr_plan[i].nbands - (HL + R0 - 1) / R0) < std::abs(P.pyr_plan[def].nbands - (HL + R0 - 1) / R0))
-      def = i;
-  select_pyr_plan(P, def);
+  select_pyr_plan(P, 0);  // the default; launch_pyramid picks per launch
 }
 
 static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
@@ -531,8 +651,9 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   HIP_OK(hipMemset(pl.err.p, 0, 16));
   if (P.pyr_fused && getenv("ORBX_PYR_PROF") && getenv("ORBX_PYR_PROF")[0] == '1')
     for (int i = 0; i < P.pyr_nplans; ++i)
-      fprintf(stderr, "pyr plan %d: %d bands, lds %d + %d + %d, cost %d\n", i, P.pyr_plan[i].nbands,
-              P.pyr_plan[i].lds_a, P.pyr_plan[i].lds_b, P.pyr_plan[i].lds_y, P.pyr_plan[i].cost);
+      fprintf(stderr, "pyr plan %d: %d bands x %d column tiles, lds %d + %d + %d, cost %d\n", i,
+              P.pyr_plan[i].nbands, P.pyr_plan[i].nct, P.pyr_plan[i].lds_a, P.pyr_plan[i].lds_b, P.pyr_plan[i].lds_y,
+              P.pyr_plan[i].cost);
   if (P.pyr_fused) {
     size_t mx = 0;
     for (int i = 0; i < P.pyr_nplans; ++i) {

@@ -32,7 +32,6 @@ constexpr int kQtThreads = ORBX_QT_THREADS;  // quadtree workgroup size
 
 struct LevelGeom {
   int w, h, pitch;
-  int lpitch;        // LDS row pitch of this level in the band pyramid kernel
   long long plane;   // bytes of one frame's plane (h * pitch)
   long long off;     // byte offset of this level's planes in the pyramid / blur buffers
   // INTER_LINEAR resize from level l-1 (l >= 1): offsets into the resize table
@@ -84,19 +83,21 @@ struct ExtractParams {
   int fast_rh_max;             // largest FAST cell ROI height
   int fast_bw_max, fast_bh_max;  // largest FAST detection band
   int pattern_upstream;
-  // band pyramid (orbx_pyramid.hip): one workgroup per (frame, band of rows)
+  // band pyramid (orbx_pyramid.hip): one workgroup per (frame, band of rows, column tile)
   int pyr_fused;               // 0 = one launch per level instead
   int pyr_nbands;              // bands per frame
   int pyr_bands;               // int2 offset in the resize table: per (band, level) {comp_lo, comp_hi}, {own_lo, own_hi}
+  int pyr_nct;                 // column tiles per band
+  int pyr_ctiles;              // int2 offset: per (tile, level) {comp_lo, comp_hi}, {own_lo, own_hi}, {LDS pitch, LDS origin}
   int pyr_lds_a, pyr_lds_b;    // LDS bytes of the even-level and odd-level row buffers
   int pyr_lds_y;               // LDS bytes of the band's staged row coefficients
-  // alternative band heights, one picked per launch (launch_pyramid): the
-  // workgroup count nbands x batch against two resident workgroups per CU
+  // alternative tilings, one picked per launch (launch_pyramid): the
+  // workgroup count nbands x nct x batch against the resident workgroups per CU
   struct PyrPlan {
-    int nbands, bands, lds_a, lds_b, lds_y;
-    int cost;  // largest per-band pixel count over the levels (level 0 staged + computed rows)
+    int nbands, nct, bands, ctiles, lds_a, lds_b, lds_y;
+    int cost;  // largest per-tile pixel count over the levels (level 0 staged + computed rows x columns)
     int occ;   // resident workgroups per CU at this plan's LDS (occupancy API, set at plan time)
-  } pyr_plan[6];
+  } pyr_plan[8];
   int pyr_nplans;
   int gauss[7];                // 7-tap Gaussian fixed-point kernel (sum 257)
   LevelGeom lv[kMaxLevels];
@@ -106,20 +107,38 @@ inline void select_pyr_plan(ExtractParams& P, int i) {
   const ExtractParams::PyrPlan& q = P.pyr_plan[i];
   P.pyr_nbands = q.nbands;
   P.pyr_bands = q.bands;
+  P.pyr_nct = q.nct;
+  P.pyr_ctiles = q.ctiles;
   P.pyr_lds_a = q.lds_a;
   P.pyr_lds_b = q.lds_b;
   P.pyr_lds_y = q.lds_y;
 }
 
-// The band plan for a launch of `batch` frames: fewest (rounds of the
-// plan's resident workgroups, cus x occ) x (the tallest band's pixel count).
+// The band plan for a launch of `batch` frames. When some plan's workgroups
+// all fit the chip at once, the one with the smallest largest-tile pixel
+// count, first among plans of at most one workgroup per CU (a second one
+// shares its CU), then among those the resident slots (cus x occ) hold: a
+// single frame or a small batch then spreads over band x column tiles.
+// Otherwise (large batches, the chip full anyway) the one-tile plan with the
+// fewest (rounds of resident workgroups) x (largest tile pixel count), as
+// measured best for 32-frame launches.
 inline int pick_pyr_plan(const ExtractParams& P, int batch, int cus) {
-  int best = 0;
+  int best = -1;
+  for (int pass = 0; pass < 2 && best < 0; ++pass)
+    for (int i = 0; i < P.pyr_nplans; ++i) {
+      const ExtractParams::PyrPlan& q = P.pyr_plan[i];
+      const long long wgs = (long long)q.nbands * q.nct * batch;
+      const long long lim = pass == 0 ? (long long)cus : (long long)cus * std::max(1, q.occ);
+      if (wgs <= lim && (best < 0 || q.cost < P.pyr_plan[best].cost)) best = i;
+    }
+  if (best >= 0) return best;
   long long best_t = -1;
+  best = 0;
   for (int i = 0; i < P.pyr_nplans; ++i) {
-    const long long wgs = (long long)P.pyr_plan[i].nbands * batch;
-    const long long slots = (long long)cus * std::max(1, P.pyr_plan[i].occ);
-    const long long t = ((wgs + slots - 1) / slots) * (long long)P.pyr_plan[i].cost;
+    const ExtractParams::PyrPlan& q = P.pyr_plan[i];
+    if (q.nct != 1) continue;
+    const long long wgs = (long long)q.nbands * batch, slots = (long long)cus * std::max(1, q.occ);
+    const long long t = ((wgs + slots - 1) / slots) * (long long)q.cost;
     if (best_t < 0 || t < best_t) {
       best = i;
       best_t = t;
@@ -135,6 +154,8 @@ struct LevelPtrs {
   int pitch[kMaxLevels];          // bytes between rows
   int aligned16[kMaxLevels];      // base, pitch and frame stride all 16-byte aligned
 };
+// both travel as kernel arguments of every extraction kernel (4 KB limit)
+static_assert(sizeof(ExtractParams) + sizeof(LevelPtrs) + 128 <= 4096, "kernel arguments over 4 KB");
 
 __host__ __device__ inline uint32_t pack_key(int x, int y, int score) {
   return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)score << 24);

@@ -128,14 +128,18 @@ __global__ __launch_bounds__(256) void pyr_resize_kernel(
 }
 
 // ---------------------------------------------------------------- band pyramid
-// All levels in ONE launch: a workgroup owns a band of rows of the last
-// level and, walking the chain back, the rows of every level that band
-// depends on. It stages the level-0 rows once (16-byte loads, all in flight),
-// then builds level 1, 2, ... in LDS, each from the previous level's rows in
-// LDS, and writes to HBM only the rows it owns at each level (bands partition
-// every level's rows; the few source rows two bands share are recomputed by
-// both instead of exchanged). Row ranges per (band, level) come from the host
-// (orbx_host.hip build_plan): comp = rows computed, own = rows written.
+// All levels in ONE launch: a workgroup owns a tile of the last level (a
+// band of rows x a column tile) and, walking the chain back, the rows and
+// columns of every level that tile depends on. It stages the level-0 tile
+// once (16-byte loads, all in flight), then builds level 1, 2, ... in LDS,
+// each from the previous level's tile in LDS, and writes to HBM only the rows
+// and columns it owns at each level (tiles partition every level; the few
+// source rows and columns two tiles share are recomputed by both instead of
+// exchanged). Ranges per (band, level) and (column tile, level) come from the
+// host (orbx_host.hip plan_band_pyramid / plan_pyr_cols): comp = computed,
+// own = written. Column tiles let a single frame (or a small batch) spread
+// over more workgroups than row bands alone allow, at a few recomputed
+// columns per tile edge.
 #ifndef ORBX_PYR_THREADS
 #define ORBX_PYR_THREADS 512
 #endif
@@ -160,13 +164,14 @@ constexpr int kPyrRun = ORBX_PYR_RUN, kPyrRuns = 8 / kPyrRun;
 static_assert(kPyrRun == 2 || kPyrRun == 4, "runs of 2 or 4 columns");
 __device__ __forceinline__ int pyr_col(int gi, int G, int q) { return kPyrRun * (gi + (q / kPyrRun) * G) + q % kPyrRun; }
 
+// One level of a (band, column tile): rows cd of the level, columns x0 ..
+// x0 + 8G - 1 (G = ceil(comp width / 8) thread groups; sx[] are LDS-relative
+// source columns). Rows and columns owned by the tile go to HBM as well.
 template <bool AREA2X>
-__device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtrs& lp, int l, int f,
-                                          const uint8_t* src, uint8_t* dst, const int2* yt_rows, int src_lo,
-                                          int2 cd, int2 own, int r0, int rstep, int gi, int G, const int (&sx)[8],
-                                          const int (&a0v)[8], const int (&a1v)[8]) {
-  const LevelGeom& g = P.lv[l];
-  const int spitch = P.lv[l - 1].lpitch, w = g.w;
+__device__ __forceinline__ void band_rows(const LevelPtrs& lp, int l, int f, const uint8_t* src, int spitch,
+                                          uint8_t* dst, int dpitch, const int2* yt_rows, int src_lo, int2 cd,
+                                          int2 own, int2 ownx, int x0, int r0, int rstep, int gi, int G,
+                                          const int (&sx)[8], const int (&a0v)[8], const int (&a1v)[8]) {
   uint8_t* G0 = (uint8_t*)lp.base[l] + f * lp.fstride[l];
   for (int r = cd.x + r0; r <= cd.y; r += rstep) {
     const int2 yt = yt_rows[r - cd.x];
@@ -195,7 +200,7 @@ __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtr
         v[q] = sat_u8((__mul24(D0, b0) + __mul24(D1, b1) + (1 << 21)) >> 22);
       }
     }
-    uint8_t* lrow = dst + __mul24(r - cd.x, g.lpitch);
+    uint8_t* lrow = dst + __mul24(r - cd.x, dpitch);
     const bool owned = r >= own.x && r <= own.y;
     uint8_t* drow = G0 + (long long)r * lp.pitch[l];
     if constexpr (kPyrRun == 4) {
@@ -204,36 +209,39 @@ __device__ __forceinline__ void band_rows(const ExtractParams& P, const LevelPtr
       *(uint32_t*)(lrow + xa) = pa;
       *(uint32_t*)(lrow + xb) = pb;
       if (owned) {
-        // level pitch and xa, xb are multiples of 4
-        if (xa + 4 <= w) *(uint32_t*)(drow + xa) = pa;
-        else for (int q = 0; xa + q < w; ++q) drow[xa + q] = (uint8_t)(pa >> (8 * q));
-        if (xb + 4 <= w) *(uint32_t*)(drow + xb) = pb;
-        else for (int q = 0; xb + q < w; ++q) drow[xb + q] = (uint8_t)(pb >> (8 * q));
+        for (int q = 0; q < 4; ++q) {
+          const int ga = x0 + xa + q, gb = x0 + xb + q;
+          if (ga >= ownx.x && ga <= ownx.y) drow[ga] = (uint8_t)(pa >> (8 * q));
+          if (gb >= ownx.x && gb <= ownx.y) drow[gb] = (uint8_t)(pb >> (8 * q));
+        }
       }
     } else {
 #pragma unroll
       for (int k = 0; k < kPyrRuns; ++k) {
         const int xk = pyr_col(gi, G, 2 * k);
         const uint16_t pk = (uint16_t)(sat_u8(v[2 * k]) | (sat_u8(v[2 * k + 1]) << 8));
-        *(uint16_t*)(lrow + xk) = pk;  // the LDS row holds the run even past w (pitch >= w + 8)
-        if (owned) {
-          if (xk + 2 <= w) *(uint16_t*)(drow + xk) = pk;
-          else if (xk < w) drow[xk] = (uint8_t)pk;
+        *(uint16_t*)(lrow + xk) = pk;  // the LDS row holds the run even past the computed columns
+        // owned ranges start at even columns (plan_pyr_cols), so a run is
+        // owned whole or not at all, but at the level's last column
+        const int gx = x0 + xk;
+        if (owned && gx >= ownx.x && gx <= ownx.y) {
+          if (gx < ownx.y) *(uint16_t*)(drow + gx) = pk;
+          else drow[gx] = (uint8_t)pk;
         }
       }
     }
   }
-
 }
 
 __global__ __launch_bounds__(kPyrBandThreads) __attribute__((amdgpu_waves_per_eu(ORBX_PYR_WPE))) void pyr_band_kernel(ExtractParams P, LevelPtrs lp,
                                                                    const int2* __restrict__ rtab, int* dbg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
-  const int nb = P.pyr_nbands, L = P.L, tid = threadIdx.x;
+  const int nb = P.pyr_nbands, nct = P.pyr_nct, L = P.L, tid = threadIdx.x;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int f = wg / nb, band = wg - f * nb;
-  const int2* bt = rtab + P.pyr_bands + (long long)band * L * 2;  // {comp}, {own} per level
+  const int f = wg / (nb * nct), tile = wg - f * (nb * nct), band = tile / nct, ct = tile - band * nct;
+  const int2* bt = rtab + P.pyr_bands + (long long)band * L * 2;  // {comp}, {own} rows per level
+  const int2* xt = rtab + P.pyr_ctiles + (long long)ct * L * 3;   // {comp}, {own} columns, {LDS pitch, origin}
   uint8_t* const bufA = smem;
   uint8_t* const bufB = smem + P.pyr_lds_a;
   // the band's row coefficients of every level, staged once: a global load
@@ -273,14 +281,17 @@ __global__ __launch_bounds__(kPyrBandThreads) __attribute__((amdgpu_waves_per_eu
     }
   }
 
-  // ---- stage level-0 rows [comp_lo, comp_hi], full width, 4 loads in flight per thread
+  // ---- stage level-0 rows [comp_lo, comp_hi] x the tile's columns, 4 loads in flight per thread
   {
-    const int2 c0 = bt[0];
-    const int rows = c0.y - c0.x + 1, W0 = P.lv[0].w, lp0 = P.lv[0].lpitch, pitch = lp.pitch[0];
-    const uint8_t* S = lp.base[0] + f * lp.fstride[0] + (long long)c0.x * pitch;
+    const int2 c0 = bt[0], x0c = xt[0], x0p = xt[2];
+    const int rows = c0.y - c0.x + 1, lp0 = x0p.x, org = x0p.y, pitch = lp.pitch[0];
+    // the last staged column: the tile's last computed one, inside the image
+    // (a source column past it is only read with weight 0)
+    const int xe = min(x0c.y, P.lv[0].w - 1);
+    const uint8_t* S = lp.base[0] + f * lp.fstride[0] + (long long)c0.x * pitch + org;
     if (lp.aligned16[0]) {
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      const int nch = (W0 + 15) >> 4, total = rows * nch;
+      const int nch = ((xe - org) >> 4) + 1, total = rows * nch;
       // unpredicated (indices past the end repeat the last chunk)
       for (int i0 = tid; i0 < total; i0 += 4 * kPyrBandThreads) {
         u32x4 v[4];
@@ -301,47 +312,53 @@ __global__ __launch_bounds__(kPyrBandThreads) __attribute__((amdgpu_waves_per_eu
       if (tid >= total && tid < ytot) s_yt[tid] = yval;
     } else {
       if (tid < ytot) s_yt[tid] = yval;
+      const int ncol = xe - org + 1;
       for (int r = 0; r < rows; ++r)
-        for (int c = tid; c < W0; c += kPyrBandThreads) bufA[r * lp0 + c] = S[(long long)r * pitch + c];
+        for (int c = tid; c < ncol; c += kPyrBandThreads) bufA[r * lp0 + c] = S[(long long)r * pitch + c];
     }
   }
 
   // column coefficients: level l+1's are fetched while level l is computed
   int2 nxt[8];
-  // a thread's 8 columns are kPyrRuns runs (pyr_col) with G = ceil(w/8):
-  // neighbouring lanes read source bytes a run's width x 1.2 apart
+  // a thread's 8 columns are kPyrRuns runs (pyr_col) with G = ceil(width/8)
+  // over the tile's computed columns: neighbouring lanes read source bytes a
+  // run's width x 1.2 apart
   auto fetch_cols = [&](int l) {
     const LevelGeom& g = P.lv[l];
-    const int G = (g.w + 7) >> 3, gi = tid % G;
+    const int2 xc = xt[3 * l];
+    const int G = (xc.y - xc.x + 1 + 7) >> 3, gi = tid % G;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) nxt[q] = rtab[g.xtab2 + min(pyr_col(gi, G, q), g.w - 1)];
+    for (int q = 0; q < 8; ++q) nxt[q] = rtab[g.xtab2 + min(xc.x + pyr_col(gi, G, q), g.w - 1)];
   };
   fetch_cols(1);
   lds_sync();  // LDS only: the owned rows written to HBM are not read back here
   if (dbg && tid == 0) dbg[blockIdx.x * 16] = (int)(__builtin_amdgcn_s_memtime() - t_begin);
 
-  // ---- levels 1 .. L-1: thread -> 8 output columns (two runs of 4), rows strided
+  // ---- levels 1 .. L-1: thread -> 8 output columns (runs of 2), rows strided
   int yoff = 0;
   for (int l = 1; l < L; ++l) {
     const LevelGeom& g = P.lv[l];
     const uint8_t* src = (l & 1) ? bufA : bufB;
     uint8_t* dst = (l & 1) ? bufB : bufA;
     const int2 cs = bt[2 * (l - 1)], cd = bt[2 * l], own = bt[2 * l + 1];
-    const int G = (g.w + 7) >> 3, rstep = kPyrBandThreads / G;
+    const int2 xc = xt[3 * l], xo = xt[3 * l + 1], sp = xt[3 * (l - 1) + 2], dp = xt[3 * l + 2];
+    const int G = (xc.y - xc.x + 1 + 7) >> 3, rstep = kPyrBandThreads / G;
     const int gi = tid % G, r0 = tid / G;
     int sx[8], a0v[8], a1v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      sx[q] = nxt[q].x;
+      sx[q] = nxt[q].x - sp.y;  // LDS-relative: the source level's row starts at column sp.y
       a0v[q] = (short)(nxt[q].y & 0xFFFF);
       a1v[q] = (short)(nxt[q].y >> 16);
     }
     if (l + 1 < L) fetch_cols(l + 1);
     if (r0 < rstep) {
       if (g.area2x)
-        band_rows<true>(P, lp, l, f, src, dst, s_yt + yoff, cs.x, cd, own, r0, rstep, gi, G, sx, a0v, a1v);
+        band_rows<true>(lp, l, f, src, sp.x, dst, dp.x, s_yt + yoff, cs.x, cd, own, xo, xc.x, r0, rstep, gi, G, sx,
+                        a0v, a1v);
       else
-        band_rows<false>(P, lp, l, f, src, dst, s_yt + yoff, cs.x, cd, own, r0, rstep, gi, G, sx, a0v, a1v);
+        band_rows<false>(lp, l, f, src, sp.x, dst, dp.x, s_yt + yoff, cs.x, cd, own, xo, xc.x, r0, rstep, gi, G, sx,
+                         a0v, a1v);
     }
     yoff += cd.y - cd.x + 1;
     lds_sync();
@@ -361,7 +378,7 @@ static int launch_band(const ExtractParams& P, const LevelPtrs& lp, const int2* 
   static int* dbg = nullptr;  // diagnostics only: per-workgroup phase cycles (ORBX_PYR_PROF=1)
   static int dbg_cap = 0;
   static const bool prof = getenv("ORBX_PYR_PROF") && getenv("ORBX_PYR_PROF")[0] == '1';
-  const int nwg = P.pyr_nbands * batch;
+  const int nwg = P.pyr_nbands * P.pyr_nct * batch;
   if (prof && nwg > dbg_cap) {
     if (dbg) (void)hipFree(dbg);
     (void)hipMalloc(&dbg, (size_t)nwg * 16 * 4);
@@ -380,12 +397,12 @@ static int launch_band(const ExtractParams& P, const LevelPtrs& lp, const int2* 
         avg[k] += h[w * 16 + k];
         mx[k] = std::max(mx[k], h[w * 16 + k]);
       }
-    fprintf(stderr, "pyr_band plans (bands/cost/lds):");
+    fprintf(stderr, "pyr_band plans (bands x tiles/cost/lds):");
     for (int i = 0; i < P.pyr_nplans; ++i)
-      fprintf(stderr, " %d/%d/%d", P.pyr_plan[i].nbands, P.pyr_plan[i].cost,
+      fprintf(stderr, " %dx%d/%d/%d", P.pyr_plan[i].nbands, P.pyr_plan[i].nct, P.pyr_plan[i].cost,
               P.pyr_plan[i].lds_a + P.pyr_plan[i].lds_b + P.pyr_plan[i].lds_y + 16);
     fprintf(stderr, "\n");
-    fprintf(stderr, "pyr_band: %d WGs (%d bands); phase cycles avg/max:", nwg, P.pyr_nbands);
+    fprintf(stderr, "pyr_band: %d WGs (%d bands x %d tiles); phase cycles avg/max:", nwg, P.pyr_nbands, P.pyr_nct);
     for (int k = 0; k < P.L; ++k) fprintf(stderr, " [%d] %.0f/%d", k, avg[k] / nwg, mx[k]);
     fprintf(stderr, "\n");
   }
@@ -403,7 +420,10 @@ int launch_pyramid(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
       return n;
     }();
-    static const int forced = getenv("ORBX_PYR_PLAN") ? atoi(getenv("ORBX_PYR_PLAN")) : -1;  // experiments only
+    // experiments and the per-plan parity test: read per launch (a captured
+    // graph keeps the plan it was captured with)
+    const char* fp = getenv("ORBX_PYR_PLAN");
+    const int forced = fp ? atoi(fp) : -1;
     ExtractParams Q = P;
     select_pyr_plan(Q, forced >= 0 && forced < P.pyr_nplans
                            ? forced

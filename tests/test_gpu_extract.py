@@ -295,3 +295,23 @@ def test_batch_mode_f_parity(pkg, O):
     for i in range(B):
         rkp, rdesc = O.extract(cfg, frames[i])
         assert_same(kps[i, :n[i]], descs[i, :n[i]], rkp, rdesc)
+
+
+@pytest.mark.parametrize("W,H,nl,sf", [(1241, 376, 8, 1.2), (752, 480, 8, 1.2), (1920, 1080, 3, 1.2),
+                                       (641, 243, 8, 1.2), (1280, 720, 4, 2.0), (1241, 376, 5, 1.5)])
+def test_every_pyramid_plan(pkg, O, monkeypatch, W, H, nl, sf):
+    """Every band x column-tile plan of the one-launch pyramid (ORBX_PYR_PLAN
+    forces plan i per launch; an index past the plan count falls back to the
+    picker) gives the oracle's levels: raw and blurred, and the keypoints."""
+    from orb_slam_cuda_amd.synth import synth_frame
+    img = synth_frame(W + nl, W, H)
+    cfg = O.config(nfeatures=1000, width=W, height=H, nlevels=nl, scale_factor=sf)
+    ref = [O.pyramid_level(cfg, img, l) for l in range(nl)]
+    rkp, rdesc = O.extract(cfg, img)
+    for i in range(8):
+        monkeypatch.setenv("ORBX_PYR_PLAN", str(i))
+        ext = pkg.ORBextractor(1000, sf, nl, 20, 7, W, H)  # a fresh handle: its first call runs unrecorded
+        kp, desc = ext(img)
+        for l in range(1, nl):
+            assert np.array_equal(ext.level_image(l), ref[l]), (i, l)
+        assert_same(kp, desc, rkp, rdesc)
