@@ -119,6 +119,8 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
   int* s_wave = (int*)take(512);          // ... per-wave partials (scan totals, counts, sums; 16 each)
   int* s_tmp = (int*)take(64);
   int* s_var = (int*)take(64);
+  uint32_t* candk = (uint32_t*)take(4ull * MN);  // lean sorted rounds: candidates' sort keys ...
+  int* candn = (int*)take(4ull * MN);            // ... and their nodes
   uint32_t* lkeys = (uint32_t*)take(4ull * P.kcap_lds);
   uint16_t* lnode = (uint16_t*)take(2ull * P.kcap_lds);
 
@@ -202,6 +204,7 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
     s_var[0] = n;  // list size
     s_var[1] = 0;  // sorted-phase flag
     s_var[6] = s_var[7] = s_var[8] = 0;  // tie-straddle events / group nodes / kept keys
+    s_var[10] = 0;  // lean sorted rounds' candidate count
   };
   const int N = g.N;
   uint32_t* out = qkeys + (long long)f * P.kp_per_frame + g.kbase;
@@ -404,34 +407,31 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
         // holds size << 16 | creation, distinct among the candidates, 0 for
         // the others; each candidate counts the larger keys.
         int* s_pos = (int*)s_sort;  // sorted rank -> node
-        int cands = 0;
-        for (int i = tid; i < size; i += kQtThreads) {
-          const uint32_t ki = s_key[i];
-          int r = -1;
-          if (ki) {
-            r = 0;
-            int j = 0;
-            for (; j + 16 <= size; j += 16) {  // sixteen broadcast keys in flight
-              u32x4 v[4];
+        // the candidates and their keys were listed (in no particular order)
+        // when the keys were written: a candidate's rank counts the larger
+        // keys among the candidates only
+        const int ncand = s_var[10];
+        for (int c = tid; c < ncand; c += kQtThreads) {
+          const uint32_t ki = candk[c];
+          int r = 0, j = 0;
+          for (; j + 16 <= ncand; j += 16) {  // sixteen broadcast keys in flight
+            u32x4 v[4];
 #pragma unroll
-              for (int u = 0; u < 4; ++u) v[u] = *(const u32x4*)(s_key + j + 4 * u);
+            for (int u = 0; u < 4; ++u) v[u] = *(const u32x4*)(candk + j + 4 * u);
 #pragma unroll
-              for (int u = 0; u < 4; ++u)
-                r += (v[u].x > ki ? 1 : 0) + (v[u].y > ki ? 1 : 0) + (v[u].z > ki ? 1 : 0) + (v[u].w > ki ? 1 : 0);
-            }
-            for (; j < size; ++j) r += s_key[j] > ki ? 1 : 0;
-            s_pos[r] = i;
-            tA[r] = nonempty(cA[i]) - 1;
-            ++cands;
+            for (int u = 0; u < 4; ++u)
+              r += (v[u].x > ki ? 1 : 0) + (v[u].y > ki ? 1 : 0) + (v[u].z > ki ? 1 : 0) + (v[u].w > ki ? 1 : 0);
           }
+          for (; j < ncand; ++j) r += candk[j] > ki ? 1 : 0;
+          const int i = candn[c];
+          s_pos[r] = i;
+          tA[r] = nonempty(cA[i]) - 1;
           rank[i] = r;
         }
-        cands = wave_sum_dpp(cands);
-        if (lane == 0) s_wave[16 + wv] = cands;
+        for (int i = tid; i < size; i += kQtThreads)
+          if (!s_key[i]) rank[i] = -1;
         lds_sync();
-        int ncand = 0;
-#pragma unroll
-        for (int i = 0; i < NW; ++i) ncand += s_wave[16 + i];
+        if (tid == 0) s_var[10] = 0;  // every thread has read the count (the next list's candidates count afresh)
         // split ranks: the prefix of ranks j with size + E_j < N, E_j = sum
         // of (children - 1) over the ranks before j (per-thread rank chunks)
         const int cper = (ncand + kQtThreads - 1) / kQtThreads;
@@ -545,8 +545,16 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
       }
       // the breadth phase ends once one more full round would overshoot N (:1015)
       if (!finish && !sorted_phase && newSize + 3 * nExp > N) sorted_phase = true;
-      if (!finish && sorted_phase)  // the next round's sort keys (the new list is kB, qB)
-        for (int i = tid; i < newSize; i += kQtThreads) s_key[i] = kB[i] > 1 ? ((uint32_t)kB[i] << 16) | (uint32_t)qB[i] : 0u;
+      if (!finish && sorted_phase)  // the next round's sort keys (the new list is kB, qB) and its candidate list
+        for (int i = tid; i < newSize; i += kQtThreads) {
+          const uint32_t key = kB[i] > 1 ? ((uint32_t)kB[i] << 16) | (uint32_t)qB[i] : 0u;
+          s_key[i] = key;
+          if (key) {
+            const int c = atomicAdd(&s_var[10], 1);
+            candk[c] = key;
+            candn[c] = i;
+          }
+        }
       size = newSize;
       {
         QNode* t0 = nA; nA = nB; nB = t0;
@@ -869,7 +877,7 @@ size_t quadtree_lds_bytes(const ExtractParams& P) {
   const size_t MN = P.maxnodes, SN = P.sortn;
   return r16(8 * SN) + 2 * r16(sizeof(QNode) * MN) + 4 * r16(4 * MN) + r16(16 * MN) + 2 * r16(4 * (MN + 1)) +
          2 * r16(4 * MN) + 2 * r16(4 * (P.max_cells_level + 1)) + r16(8 * MN) + r16(16 * MN) + r16(8 * MN) + 512 +
-         2 * r16(64) +
+         2 * r16(64) + 2 * r16(4 * MN) +
          r16(4ull * P.kcap_lds) + r16(2ull * P.kcap_lds);
 }
 
