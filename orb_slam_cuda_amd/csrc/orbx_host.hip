@@ -336,8 +336,11 @@ static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
   PyrCols colplans[3];
   bool colok[3];
   for (int k = 0; k < 3; ++k) colok[k] = plan_pyr_cols(P, rtab, 1 << k, colplans[k]);
-  for (int pass = 0; pass < 2 && cands.empty(); ++pass)
-    for (int R = pass == 0 ? R0 + 5 : R0; R >= std::max(1, R0 / 3); --R) {
+  // band heights from a quarter of the last level (4 bands: one workgroup
+  // per CU for a 32-64-frame batch once tiled) down to R0 / 3
+  const int Rmax = std::max(R0 + 5, (HL + 3) / 4);
+  for (int pass = 1; pass < 2; ++pass)
+    for (int R = Rmax; R >= std::max(1, R0 / 3); --R) {
       const int nb = (HL + R - 1) / R;
       if (!cands.empty() && cands.back().nb == nb) continue;  // same band count as a taller R
       std::vector<int> lo((size_t)nb * L), chi((size_t)nb * L), ohi((size_t)nb * L);
@@ -381,7 +384,6 @@ static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
           }
         cands.push_back(Cand{R, nb, C.nct, need[0], need[1], ybytes, cost, lo, chi, ohi, C});
       }
-      if (pass == 1 && !cands.empty()) break;  // the large-LDS fallback: one workgroup per CU, one band height
     }
   if (cands.empty()) return;
   // the plans kept: the one-tile plans (band heights as before column tiles
@@ -402,27 +404,34 @@ static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
     }
   }
   if (keep.empty()) {
+    // the default (R0's band height or the nearest, one tile), then what the
+    // launch-time rule (pick_pyr_plan) takes for batches of 1 .. 64 and B on
+    // a 256-CU chip (two workgroups per CU up to 78 KB of LDS, else one: the
+    // occupancy API sets the real count afterwards), then one-tile plans near R0
     int def = -1;
     for (int i = 0; i < (int)cands.size(); ++i)
-      if (cands[i].nct == 1 &&
+      if (cands[i].nct == 1 && cands[i].need0 + cands[i].need1 + cands[i].ybytes + 16 <= budgets[0] &&
           (def < 0 || std::abs(cands[i].nb - (HL + R0 - 1) / R0) < std::abs(cands[def].nb - (HL + R0 - 1) / R0)))
         def = i;
     if (def < 0) def = 0;
     keep.push_back(def);
-    for (int i = 0; i < (int)cands.size() && keep.size() < 5; ++i)
-      if (cands[i].nct == 1 && i != def) keep.push_back(i);
-    // (the picker's rule on a 256-CU chip, two workgroups per CU)
-    for (int bt : {1, 2, 4, 8, 16}) {
-      int best = -1;
-      for (const long long lim : {256, 512}) {
-        for (int i = 0; i < (int)cands.size(); ++i)
-          if (cands[i].nct > 1 && (long long)cands[i].nb * cands[i].nct * bt <= lim &&
-              (best < 0 || cands[i].cost < cands[best].cost))
-            best = i;
-        if (best >= 0) break;
-      }
-      if (best >= 0 && keep.size() < 8 && std::find(keep.begin(), keep.end(), best) == keep.end()) keep.push_back(best);
+    std::vector<ExtractParams::PyrPlan> sim(cands.size());
+    for (size_t i = 0; i < cands.size(); ++i) {
+      sim[i].nbands = cands[i].nb;
+      sim[i].nct = cands[i].nct;
+      sim[i].cost = (int)cands[i].cost;
+      sim[i].occ = cands[i].need0 + cands[i].need1 + cands[i].ybytes + 16 <= budgets[0] ? 2 : 1;
     }
+    const int batches[8] = {1, 2, 4, 8, 16, 32, 64, P.B};
+    for (int bt : batches) {
+      const int best = pick_pyr_plan(sim.data(), (int)sim.size(), bt, 256);
+      if (keep.size() < 8 && std::find(keep.begin(), keep.end(), best) == keep.end()) keep.push_back(best);
+    }
+    for (int d = 1; keep.size() < 8 && d < (int)cands.size(); ++d)
+      for (int i : {def - d, def + d})
+        if (i >= 0 && i < (int)cands.size() && cands[i].nct == 1 && keep.size() < 8 &&
+            std::find(keep.begin(), keep.end(), i) == keep.end())
+          keep.push_back(i);
   }
   P.pyr_nplans = 0;
   for (int i : keep) {

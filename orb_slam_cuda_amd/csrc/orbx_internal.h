@@ -114,37 +114,45 @@ inline void select_pyr_plan(ExtractParams& P, int i) {
   P.pyr_lds_y = q.lds_y;
 }
 
-// The band plan for a launch of `batch` frames. When some plan's workgroups
-// all fit the chip at once, the one with the smallest largest-tile pixel
-// count, first among plans of at most one workgroup per CU (a second one
-// shares its CU), then among those the resident slots (cus x occ) hold: a
-// single frame or a small batch then spreads over band x column tiles.
-// Otherwise (large batches, the chip full anyway) the one-tile plan with the
-// fewest (rounds of resident workgroups) x (largest tile pixel count), as
-// measured best for 32-frame launches.
-inline int pick_pyr_plan(const ExtractParams& P, int batch, int cus) {
-  int best = -1;
-  for (int pass = 0; pass < 2 && best < 0; ++pass)
-    for (int i = 0; i < P.pyr_nplans; ++i) {
-      const ExtractParams::PyrPlan& q = P.pyr_plan[i];
-      const long long wgs = (long long)q.nbands * q.nct * batch;
-      const long long lim = pass == 0 ? (long long)cus : (long long)cus * std::max(1, q.occ);
-      if (wgs <= lim && (best < 0 || q.cost < P.pyr_plan[best].cost)) best = i;
+// Estimated launch time of a tiling: the largest tile's pixel count times
+// the workgroups the busiest CU runs (wpc = ceil(workgroups / CUs)), less
+// 13 % per co-resident one (occ per CU: LDS and registers). Measured on
+// gfx950 (tools/pyr_plans.py, 32 KITTI frames alone): a CU's second resident
+// band workgroup adds ~87 % of the first's time, a third ~80 %.
+inline long long pyr_plan_time(long long cost, long long wgs, int cus, int occ) {
+  const long long wpc = (wgs + cus - 1) / cus;
+  const long long res = std::min<long long>(wpc, std::max(1, occ));
+  return cost * (100 * wpc - 13 * (res - 1));
+}
+
+// The band plan for a launch of `batch` frames. The one-tile plans compete
+// by (rounds of resident workgroups) x (largest tile's pixel count), the
+// rule measured best over band heights for 32-frame launches; a column-tiled
+// plan replaces that pick when pyr_plan_time puts it at least 15 % faster
+// (the estimate's error on the measured plans: tools/pyr_plans.py). A single
+// frame then spreads over many small tiles (KITTI: 53 bands x 4, one per
+// CU), a 32-frame KITTI batch over 4 x 4 large ones (less halo recompute).
+inline int pick_pyr_plan(const ExtractParams::PyrPlan* plans, int n, int batch, int cus) {
+  int i1 = -1, i2 = -1;
+  long long t1 = -1, t2 = -1;
+  for (int i = 0; i < n; ++i) {
+    const ExtractParams::PyrPlan& q = plans[i];
+    const long long wgs = (long long)q.nbands * q.nct * batch;
+    if (q.nct == 1) {
+      const long long slots = (long long)cus * std::max(1, q.occ);
+      const long long t = ((wgs + slots - 1) / slots) * (long long)q.cost;
+      if (t1 < 0 || t < t1) i1 = i, t1 = t;
     }
-  if (best >= 0) return best;
-  long long best_t = -1;
-  best = 0;
-  for (int i = 0; i < P.pyr_nplans; ++i) {
-    const ExtractParams::PyrPlan& q = P.pyr_plan[i];
-    if (q.nct != 1) continue;
-    const long long wgs = (long long)q.nbands * batch, slots = (long long)cus * std::max(1, q.occ);
-    const long long t = ((wgs + slots - 1) / slots) * (long long)q.cost;
-    if (best_t < 0 || t < best_t) {
-      best = i;
-      best_t = t;
-    }
+    const long long t = pyr_plan_time(q.cost, wgs, cus, q.occ);
+    if (t2 < 0 || t < t2) i2 = i, t2 = t;
   }
-  return best;
+  if (i1 < 0) return i2 < 0 ? 0 : i2;
+  const ExtractParams::PyrPlan& q1 = plans[i1];
+  const long long t1m = pyr_plan_time(q1.cost, (long long)q1.nbands * batch, cus, q1.occ);
+  return (plans[i2].nct > 1 && t2 * 115 < t1m * 100) ? i2 : i1;
+}
+inline int pick_pyr_plan(const ExtractParams& P, int batch, int cus) {
+  return pick_pyr_plan(P.pyr_plan, P.pyr_nplans, batch, cus);
 }
 
 // Pointers to level data for one launch. Level 0 is the caller's frames.

@@ -24,6 +24,18 @@ d.upload(img)
 ext = pkg.ORBextractor(2000, 1.2, NL, 20, 7, W, H, max_batch=B)
 cap = ext.frame_capacity
 dk, dd, dc = _lib.DeviceArray(B * cap * 28), _lib.DeviceArray(B * cap * 32), _lib.DeviceArray(B * 4)
+# the plan table, from a child process with ORBX_PYR_PROF=1 (profiling in
+# this process would add a sync and a copy to every launch)
+import re  # noqa: E402
+import subprocess  # noqa: E402
+code = ("import sys; sys.path.insert(0, %r); import orb_slam_cuda_amd as pkg; "
+        "pkg.ORBextractor(2000, 1.2, %d, 20, 7, %d, %d, max_batch=%d)") % (
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), NL, W, H, B)
+env = dict(os.environ, ORBX_PYR_PROF="1")
+env.pop("ORBX_TIMING", None)
+out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True).stderr
+names = {int(m.group(1)): f"{m.group(2)}:{m.group(3)}" for m in
+         re.finditer(r"pyr plan (\d+): (\d+) bands x (\d+) column tiles", out)}
 res = []
 for plan in list(range(8)) + [-1]:
     if plan >= 0:
@@ -36,6 +48,5 @@ for plan in list(range(8)) + [-1]:
         if i >= 5:
             t.append(ext.stage_times()["Pyramid/Resize"])
     res.append((plan, float(np.median(t)) * 1e3))
-keep = os.environ.get("ORBX_PYR_KEEP", "").split(",")
-lab = lambda p: keep[p] if 0 <= p < len(keep) and keep[p] else ("pick" if p < 0 else str(p))
+lab = lambda p: names.get(p, "pick" if p < 0 else f"{p}(none)")
 print(f"B {B} {W}x{H} L {NL}: pyramid us per plan:", ", ".join(f"{lab(p)}: {v:.1f}" for p, v in res))
