@@ -304,6 +304,9 @@ static bool plan_pyr_cols(const ExtractParams& P, const std::vector<int2>& rtab,
       // levels: the 2-column runs of G = ceil(width / 8) groups end <= 6 past hi
       p = std::max(p, l == 0 ? ((hi - (lo & ~15) + 1 + 15) & ~15) : ((hi - lo + 1 + 8 + 15) & ~15));
     }
+    // experiments: ORBX_PYR_PADMOD=m pads every LDS row pitch to m mod 128
+    if (const char* e = getenv("ORBX_PYR_PADMOD"))
+      while (p % 128 != atoi(e) % 128) p += 16;
     C.lpitch[l] = p;
   }
   return true;
