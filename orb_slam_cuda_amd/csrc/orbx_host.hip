@@ -305,8 +305,11 @@ static bool plan_pyr_cols(const ExtractParams& P, const std::vector<int2>& rtab,
       p = std::max(p, l == 0 ? ((hi - (lo & ~15) + 1 + 15) & ~15) : ((hi - lo + 1 + 8 + 15) & ~15));
     }
     // experiments: ORBX_PYR_PADMOD=m pads every LDS row pitch to m mod 128
-    if (const char* e = getenv("ORBX_PYR_PADMOD"))
-      while (p % 128 != atoi(e) % 128) p += 16;
+    // (level 0 keeps its 16-byte rows: m rounded down to 16 there)
+    if (const char* e = getenv("ORBX_PYR_PADMOD")) {
+      const int m = (l == 0 ? atoi(e) & ~15 : atoi(e)) % 128, step = l == 0 ? 16 : 4;
+      while (p % 128 != m) p += step;
+    }
     C.lpitch[l] = p;
   }
   return true;
@@ -319,13 +322,10 @@ static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
   auto src_lo = [&](int l, int y) { return P.lv[l].area2x ? 2 * y : (rtab[P.lv[l].ytab + y].x & 0xFFFF); };
   auto src_hi = [&](int l, int y) { return P.lv[l].area2x ? 2 * y + 1 : (rtab[P.lv[l].ytab + y].x >> 16); };
   const int HL = P.lv[L - 1].h;
-  // Candidate tilings: band heights R (R0 = HL/18 and up to five taller, down
-  // to R0/3) x 1, 2 or 4 column tiles, those whose LDS allows two workgroups
-  // per CU (the kernel is latency-bound: more resident waves beat less halo
-  // recompute). launch_pyramid picks per launch the plan whose workgroup
-  // count fits the chip best for the launch's batch (576 workgroups on 512
-  // slots cost two full rounds); up to 8 plans are kept: the best of the
-  // candidates for batches of 1 .. 64 and B, and the default (R0, one tile).
+  // Candidate tilings: band heights R from a quarter of the last level down
+  // to R0/3 (R0 = HL/18) x 1, 2 or 4 column tiles, within a CU's LDS (two
+  // workgroups per CU up to budgets[0]). launch_pyramid picks one per launch
+  // (pick_pyr_plan); up to 8 are kept (below).
   const size_t budgets[2] = {78 * 1024, 160 * 1024 - 1024};
   const int R0 = std::max(1, (HL + 17) / 18);
   struct Cand {
@@ -342,52 +342,51 @@ static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
   // band heights from a quarter of the last level (4 bands: one workgroup
   // per CU for a 32-64-frame batch once tiled) down to R0 / 3
   const int Rmax = std::max(R0 + 5, (HL + 3) / 4);
-  for (int pass = 1; pass < 2; ++pass)
-    for (int R = Rmax; R >= std::max(1, R0 / 3); --R) {
-      const int nb = (HL + R - 1) / R;
-      if (!cands.empty() && cands.back().nb == nb) continue;  // same band count as a taller R
-      std::vector<int> lo((size_t)nb * L), chi((size_t)nb * L), ohi((size_t)nb * L);
-      for (int b = 0; b < nb; ++b) {
-        lo[b * L + L - 1] = b * R;
-        chi[b * L + L - 1] = ohi[b * L + L - 1] = std::min((b + 1) * R, HL) - 1;
-      }
-      for (int l = L - 2; l >= 0; --l)
-        for (int b = 0; b < nb; ++b) lo[b * L + l] = b == 0 ? 0 : src_lo(l + 1, lo[b * L + l + 1]);
-      for (int l = L - 2; l >= 0; --l)
-        for (int b = 0; b < nb; ++b) {
-          const int own_hi = b + 1 < nb ? lo[(b + 1) * L + l] - 1 : P.lv[l].h - 1;
-          ohi[b * L + l] = own_hi;
-          chi[b * L + l] = std::max(src_hi(l + 1, chi[b * L + l + 1]), l > 0 ? own_hi : 0);
-        }
-      size_t ybytes = 0;
-      for (int b = 0; b < nb; ++b) {
-        size_t s = 0;
-        for (int l = 1; l < L; ++l) s += (size_t)(chi[b * L + l] - lo[b * L + l] + 1) * 8;
-        ybytes = std::max(ybytes, s);
-      }
-      for (int k = 0; k < 3; ++k) {
-        if (!colok[k]) continue;
-        const PyrCols& C = colplans[k];
-        size_t need[2] = {0, 0};
-        for (int l = 0; l < L; ++l) {
-          int rows = 0;
-          for (int b = 0; b < nb; ++b) rows = std::max(rows, chi[b * L + l] - lo[b * L + l] + 1);
-          need[l & 1] = std::max(need[l & 1], (size_t)rows * C.lpitch[l]);
-        }
-        need[0] = (need[0] + 15) & ~(size_t)15;
-        need[1] = (need[1] + 15) & ~(size_t)15;
-        if (need[0] + need[1] + ybytes + 16 > budgets[pass]) continue;
-        long long cost = 0;
-        for (int b = 0; b < nb; ++b)
-          for (int c = 0; c < C.nct; ++c) {
-            long long s = 0;
-            for (int l = 0; l < L; ++l)
-              s += (long long)(chi[b * L + l] - lo[b * L + l] + 1) * (C.chi[c * L + l] - C.lo[c * L + l] + 1);
-            cost = std::max(cost, s);
-          }
-        cands.push_back(Cand{R, nb, C.nct, need[0], need[1], ybytes, cost, lo, chi, ohi, C});
-      }
+  for (int R = Rmax; R >= std::max(1, R0 / 3); --R) {
+    const int nb = (HL + R - 1) / R;
+    if (!cands.empty() && cands.back().nb == nb) continue;  // same band count as a taller R
+    std::vector<int> lo((size_t)nb * L), chi((size_t)nb * L), ohi((size_t)nb * L);
+    for (int b = 0; b < nb; ++b) {
+      lo[b * L + L - 1] = b * R;
+      chi[b * L + L - 1] = ohi[b * L + L - 1] = std::min((b + 1) * R, HL) - 1;
     }
+    for (int l = L - 2; l >= 0; --l)
+      for (int b = 0; b < nb; ++b) lo[b * L + l] = b == 0 ? 0 : src_lo(l + 1, lo[b * L + l + 1]);
+    for (int l = L - 2; l >= 0; --l)
+      for (int b = 0; b < nb; ++b) {
+        const int own_hi = b + 1 < nb ? lo[(b + 1) * L + l] - 1 : P.lv[l].h - 1;
+        ohi[b * L + l] = own_hi;
+        chi[b * L + l] = std::max(src_hi(l + 1, chi[b * L + l + 1]), l > 0 ? own_hi : 0);
+      }
+    size_t ybytes = 0;
+    for (int b = 0; b < nb; ++b) {
+      size_t s = 0;
+      for (int l = 1; l < L; ++l) s += (size_t)(chi[b * L + l] - lo[b * L + l] + 1) * 8;
+      ybytes = std::max(ybytes, s);
+    }
+    for (int k = 0; k < 3; ++k) {
+      if (!colok[k]) continue;
+      const PyrCols& C = colplans[k];
+      size_t need[2] = {0, 0};
+      for (int l = 0; l < L; ++l) {
+        int rows = 0;
+        for (int b = 0; b < nb; ++b) rows = std::max(rows, chi[b * L + l] - lo[b * L + l] + 1);
+        need[l & 1] = std::max(need[l & 1], (size_t)rows * C.lpitch[l]);
+      }
+      need[0] = (need[0] + 15) & ~(size_t)15;
+      need[1] = (need[1] + 15) & ~(size_t)15;
+      if (need[0] + need[1] + ybytes + 16 > budgets[1]) continue;  // a CU's LDS (occupancy 1 above budgets[0])
+      long long cost = 0;
+      for (int b = 0; b < nb; ++b)
+        for (int c = 0; c < C.nct; ++c) {
+          long long s = 0;
+          for (int l = 0; l < L; ++l)
+            s += (long long)(chi[b * L + l] - lo[b * L + l] + 1) * (C.chi[c * L + l] - C.lo[c * L + l] + 1);
+          cost = std::max(cost, s);
+        }
+      cands.push_back(Cand{R, nb, C.nct, need[0], need[1], ybytes, cost, lo, chi, ohi, C});
+    }
+  }
   if (cands.empty()) return;
   // the plans kept: the one-tile plans (band heights as before column tiles
   // existed; the default first: R0's or the nearest), then for small batches

@@ -160,6 +160,9 @@ constexpr int kPyrBandThreads = ORBX_PYR_THREADS;
 #ifndef ORBX_PYR_RUN
 #define ORBX_PYR_RUN 2
 #endif
+#ifndef ORBX_PYR_ROWFAST
+#define ORBX_PYR_ROWFAST 0  // A/B: thread -> (column group, row) with rows fastest
+#endif
 constexpr int kPyrRun = ORBX_PYR_RUN, kPyrRuns = 8 / kPyrRun;
 static_assert(kPyrRun == 2 || kPyrRun == 4, "runs of 2 or 4 columns");
 __device__ __forceinline__ int pyr_col(int gi, int G, int q) { return kPyrRun * (gi + (q / kPyrRun) * G) + q % kPyrRun; }
@@ -326,7 +329,11 @@ __global__ __launch_bounds__(kPyrBandThreads) __attribute__((amdgpu_waves_per_eu
   auto fetch_cols = [&](int l) {
     const LevelGeom& g = P.lv[l];
     const int2 xc = xt[3 * l];
+#if ORBX_PYR_ROWFAST
+    const int G = (xc.y - xc.x + 1 + 7) >> 3, gi = min(tid / (kPyrBandThreads / G), G - 1);
+#else
     const int G = (xc.y - xc.x + 1 + 7) >> 3, gi = tid % G;
+#endif
 #pragma unroll
     for (int q = 0; q < 8; ++q) nxt[q] = rtab[g.xtab2 + min(xc.x + pyr_col(gi, G, q), g.w - 1)];
   };
@@ -343,7 +350,12 @@ __global__ __launch_bounds__(kPyrBandThreads) __attribute__((amdgpu_waves_per_eu
     const int2 cs = bt[2 * (l - 1)], cd = bt[2 * l], own = bt[2 * l + 1];
     const int2 xc = xt[3 * l], xo = xt[3 * l + 1], sp = xt[3 * (l - 1) + 2], dp = xt[3 * l + 2];
     const int G = (xc.y - xc.x + 1 + 7) >> 3, rstep = kPyrBandThreads / G;
+#if ORBX_PYR_ROWFAST
+    // rows fastest: a half-wave's lanes read one column group of ~rstep rows
+    const int gi = tid / rstep, r0 = tid < rstep * G ? tid - gi * rstep : rstep;
+#else
     const int gi = tid % G, r0 = tid / G;
+#endif
     int sx[8], a0v[8], a1v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
