@@ -315,3 +315,30 @@ def test_every_pyramid_plan(pkg, O, monkeypatch, W, H, nl, sf):
         for l in range(1, nl):
             assert np.array_equal(ext.level_image(l), ref[l]), (i, l)
         assert_same(kp, desc, rkp, rdesc)
+
+
+def test_pyramid_plans_random_geometries(pkg, O, monkeypatch):
+    """Every kept band x column-tile plan on seeded random image sizes, scale
+    factors and level counts (the plan's walk-down rules on shapes the named
+    configs do not have): raw pyramid levels equal the oracle's."""
+    from orb_slam_cuda_amd.synth import synth_frame
+    rng = np.random.default_rng(2024)
+    done = 0
+    while done < 10:
+        W, H = int(rng.integers(300, 2000)), int(rng.integers(200, 1100))
+        sf = float(rng.choice([1.1, 1.2, 1.25, 1.5, 2.0]))
+        nl = int(rng.integers(2, 9))
+        try:
+            pkg.ORBextractor(500, sf, nl, 20, 7, W, H)
+        except pkg.OrbxError:
+            continue  # a level below one FAST cell: refused, as the reference cannot run it
+        img = synth_frame(W * 7 + H, W, H)
+        cfg = O.config(nfeatures=500, width=W, height=H, nlevels=nl, scale_factor=sf)
+        ref = [O.pyramid_level(cfg, img, l) for l in range(nl)]
+        for i in range(8):
+            monkeypatch.setenv("ORBX_PYR_PLAN", str(i))
+            ext = pkg.ORBextractor(500, sf, nl, 20, 7, W, H)
+            ext(img)
+            for l in range(1, nl):
+                assert np.array_equal(ext.level_image(l), ref[l]), (W, H, sf, nl, i, l)
+        done += 1
