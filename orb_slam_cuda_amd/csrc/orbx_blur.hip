@@ -35,23 +35,19 @@ __device__ __forceinline__ uint32_t dot2(uint32_t pair, uint32_t taps, uint32_t 
   return __builtin_amdgcn_udot2(__builtin_bit_cast(us2_t, pair), __builtin_bit_cast(us2_t, taps), acc, false);
 }
 
-__global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp, uint8_t* __restrict__ blur) {
+__global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp, const int2* __restrict__ rtab,
+                                                   uint8_t* __restrict__ blur) {
   __shared__ __attribute__((aligned(16))) uint8_t in[kBlurPairs * 2][kBlurInW];
   __shared__ __attribute__((aligned(16))) uint32_t tmp[kBlurPairs][kBlurTW];  // {row 2p, row 2p+1} u16 sums
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-  const int f = wg / gridDim.x, tid = threadIdx.x;
-  int t = wg % gridDim.x, l = 0;
-  for (; l < P.L; ++l) {
-    const LevelGeom& g = P.lv[l];
-    const int n = ((g.w + kBlurTW - 1) / kBlurTW) * ((g.h + kBlurTH - 1) / kBlurTH);
-    if (t < n) break;
-    t -= n;
-  }
-  if (l >= P.L) return;
+  // the frame by a multiply-high (exact for every id of the plan's batch,
+  // checked at plan time), the tile's level and origin by one table load: no
+  // division and no level search before the tile's first address
+  const int f = P.blur_magic ? (int)__umulhi((unsigned)wg, P.blur_magic) : wg / P.blur_ntiles, tid = threadIdx.x;
+  const int e = rtab[P.blur_tiles + wg - f * P.blur_ntiles].x;
+  const int l = e & 15, x0 = (e >> 4) & 0xFFF, y0 = e >> 16;
   const LevelGeom& g = P.lv[l];
   const int W = g.w, H = g.h;
-  const int tx = (W + kBlurTW - 1) / kBlurTW;
-  const int x0 = (t % tx) * kBlurTW, y0 = (t / tx) * kBlurTH;
   const uint8_t* S = lp.base[l] + f * lp.fstride[l];
   const int pitch = lp.pitch[l];
   // stage rows y0-3 .. y0+TH+2, columns x0-16 .. x0+TW+15
@@ -189,11 +185,14 @@ __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp
   }
 }
 
-int launch_blur(const ExtractParams& P, const LevelPtrs& lp, uint8_t* blur, int batch, hipStream_t s) {
-  int tiles = 0;
-  for (int l = 0; l < P.L; ++l)
-    tiles += ((P.lv[l].w + kBlurTW - 1) / kBlurTW) * ((P.lv[l].h + kBlurTH - 1) / kBlurTH);
-  hipLaunchKernelGGL(blur_kernel, dim3(tiles, batch), dim3(256), 0, s, P, lp, blur);
+void blur_tile_dims(int* tw, int* th) {
+  *tw = kBlurTW;
+  *th = kBlurTH;
+}
+
+int launch_blur(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab, uint8_t* blur, int batch,
+                hipStream_t s) {
+  hipLaunchKernelGGL(blur_kernel, dim3(P.blur_ntiles, batch), dim3(256), 0, s, P, lp, rtab, blur);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 

@@ -115,7 +115,7 @@ __device__ int block_scan_excl(int* a, int n, int* s_tmp) {
 
 // Host launchers of the stage kernels (one translation unit each).
 int launch_pyramid(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab, int batch, hipStream_t s);
-int launch_blur(const ExtractParams& P, const LevelPtrs& lp, uint8_t* blur, int batch, hipStream_t s);
+int launch_blur(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab, uint8_t* blur, int batch, hipStream_t s);
 int launch_fast(const ExtractParams& P, const LevelPtrs& lp, const CellGeom* cells, uint32_t* slots,
                 int* cell_counts, int batch, hipStream_t s);
 int launch_quadtree(const ExtractParams& P, const ExtractBuffers& X, int batch, hipStream_t s);

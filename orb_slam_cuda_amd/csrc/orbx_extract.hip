@@ -51,7 +51,7 @@ int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_
   for (int i = 0; i < 5; ++i) {
     switch (order[i]) {
       case 'p': rc = launch_pyramid(Q, lp, X.rtab, batch, stream); break;
-      case 'b': rc = launch_blur(Q, lp, X.blur, batch, stream); break;
+      case 'b': rc = launch_blur(Q, lp, X.rtab, X.blur, batch, stream); break;
       case 'f': rc = launch_fast(Q, lp, X.cells, X.slots, X.cell_counts, batch, stream); break;
       case 'q': rc = launch_quadtree(Q, X, batch, stream); break;
       default: rc = launch_orient_brief(Q, lp, X, d_kps, d_desc, d_counts, batch, stream); break;
