@@ -319,8 +319,9 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
         qB[pos] = qA[n];
         mB[pos] = mA[n];
         cB[pos] = make_int4(0, 0, 0, 0);
-        tB[n] = pos;
-        rank[n] = -1;  // the re-homing reads kept nodes' positions from tB (sorted rounds keep ranked candidates too)
+        // the re-homing reads a key's new node at cA[n][q] whether its node
+        // was split (the child's position, place_split) or kept (here, all four)
+        cA[n] = make_int4(pos, pos, pos, pos);
       };
       auto place_split = [&](int n, int j, int base) {
         const int4 c = cA[n];
@@ -517,10 +518,7 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
           pk[u] = in ? knode[k0 + u * kQtThreads] : 0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int n = pk[u] >> 2;
-          nn[u] = rank[n] < 0 ? tB[n] : ((const int*)&cA[n])[pk[u] & 3];
-        }
+        for (int u = 0; u < 4; ++u) nn[u] = ((const int*)cA)[pk[u]];  // pk = node << 2 | quadrant
         if (!finish) {
           int2 md[4];
           int big[4];
