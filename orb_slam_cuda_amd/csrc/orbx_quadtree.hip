@@ -472,12 +472,21 @@ __global__ __launch_bounds__(kQtThreads, ORBX_QT_MINW) void quadtree_kernel(Extr
         // tie-straddle exposure (generic path)
         if (m > 0 && m < ncand && (s_key[s_pos[m - 1]] >> 16) == (s_key[s_pos[m]] >> 16)) {
           const uint32_t sz = s_key[s_pos[m - 1]] >> 16;
+          // (uniform branch) per-thread counts, one atomic per wave and counter:
+          // the group's nodes all hit the same two counters
+          int g7 = 0, g8 = 0;
           for (int j = tid; j < ncand; j += kQtThreads) {
             const int n = s_pos[j];
             if ((s_key[n] >> 16) == sz) {
-              atomicAdd(&s_var[7], 1);
-              atomicAdd(&s_var[8], j < m ? nonempty(cA[n]) : 1);
+              g7 += 1;
+              g8 += j < m ? nonempty(cA[n]) : 1;
             }
+          }
+          g7 = wave_sum_dpp(g7);
+          g8 = wave_sum_dpp(g8);
+          if (lane == 0 && g7) {
+            atomicAdd(&s_var[7], g7);
+            atomicAdd(&s_var[8], g8);
           }
           if (tid == 0) s_var[6] += 1;
         }
