@@ -24,8 +24,9 @@ namespace orbx {
 #ifndef ORBX_BLUR_TW
 #define ORBX_BLUR_TW 128
 #endif
-constexpr int kBlurTW = ORBX_BLUR_TW, kBlurTH = ORBX_BLUR_TH, kBlurInW = kBlurTW + 32;
-constexpr int kBlurPairs = (kBlurTH + 6 + 1) / 2;  // 19 staged row pairs
+// small tiles for launches that would not fill the chip with the large ones
+// (a single frame: 272 tiles of 128 x 48 for 256 CUs, ~1000 of 64 x 32)
+constexpr int kBlurTWs = 64, kBlurTHs = 32;
 
 typedef unsigned short us2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t dot4(uint32_t px, uint32_t taps, uint32_t acc) {
@@ -35,16 +36,19 @@ __device__ __forceinline__ uint32_t dot2(uint32_t pair, uint32_t taps, uint32_t 
   return __builtin_amdgcn_udot2(__builtin_bit_cast(us2_t, pair), __builtin_bit_cast(us2_t, taps), acc, false);
 }
 
+template <int kBlurTW, int kBlurTH>
 __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp, const int2* __restrict__ rtab,
-                                                   uint8_t* __restrict__ blur) {
+                                                   int tiles, int ntiles, unsigned magic, uint8_t* __restrict__ blur) {
+  constexpr int kBlurInW = kBlurTW + 32;
+  constexpr int kBlurPairs = (kBlurTH + 6 + 1) / 2;  // staged row pairs (19 for 48-row tiles)
   __shared__ __attribute__((aligned(16))) uint8_t in[kBlurPairs * 2][kBlurInW];
   __shared__ __attribute__((aligned(16))) uint32_t tmp[kBlurPairs][kBlurTW];  // {row 2p, row 2p+1} u16 sums
   const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
   // the frame by a multiply-high (exact for every id of the plan's batch,
   // checked at plan time), the tile's level and origin by one table load: no
   // division and no level search before the tile's first address
-  const int f = P.blur_magic ? (int)__umulhi((unsigned)wg, P.blur_magic) : wg / P.blur_ntiles, tid = threadIdx.x;
-  const int e = rtab[P.blur_tiles + wg - f * P.blur_ntiles].x;
+  const int f = magic ? (int)__umulhi((unsigned)wg, magic) : wg / ntiles, tid = threadIdx.x;
+  const int e = rtab[tiles + wg - f * ntiles].x;
   const int l = e & 15, x0 = (e >> 4) & 0xFFF, y0 = e >> 16;
   const LevelGeom& g = P.lv[l];
   const int W = g.w, H = g.h;
@@ -185,14 +189,26 @@ __global__ __launch_bounds__(256) void blur_kernel(ExtractParams P, LevelPtrs lp
   }
 }
 
-void blur_tile_dims(int* tw, int* th) {
-  *tw = kBlurTW;
-  *th = kBlurTH;
+void blur_tile_dims(int small, int* tw, int* th) {
+  *tw = small ? kBlurTWs : ORBX_BLUR_TW;
+  *th = small ? kBlurTHs : ORBX_BLUR_TH;
 }
 
 int launch_blur(const ExtractParams& P, const LevelPtrs& lp, const int2* rtab, uint8_t* blur, int batch,
                 hipStream_t s) {
-  hipLaunchKernelGGL(blur_kernel, dim3(P.blur_ntiles, batch), dim3(256), 0, s, P, lp, rtab, blur);
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n;
+  }();
+  // the large tiles once they give every CU two workgroups
+  if ((long long)P.blur_ntiles[0] * batch >= 2ll * cus)
+    hipLaunchKernelGGL((blur_kernel<ORBX_BLUR_TW, ORBX_BLUR_TH>), dim3(P.blur_ntiles[0], batch), dim3(256), 0, s, P,
+                       lp, rtab, P.blur_tiles[0], P.blur_ntiles[0], P.blur_magic[0], blur);
+  else
+    hipLaunchKernelGGL((blur_kernel<kBlurTWs, kBlurTHs>), dim3(P.blur_ntiles[1], batch), dim3(256), 0, s, P, lp,
+                       rtab, P.blur_tiles[1], P.blur_ntiles[1], P.blur_magic[1], blur);
   return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 

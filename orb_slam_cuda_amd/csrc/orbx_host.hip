@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void copy2d_kernel(uint8_t* __restrict__ d, si
 size_t quadtree_lds_bytes(const ExtractParams& P);
 extern const void* quadtree_kernel_ptr(int big);
 size_t pyr_band_lds_bytes(const ExtractParams& P);
-void blur_tile_dims(int* tw, int* th);
+void blur_tile_dims(int small, int* tw, int* th);
 extern const void* pyr_band_kernel_ptr();
 extern int pyr_band_occupancy(size_t lds);
 }  // namespace orbx
@@ -599,20 +599,20 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   if (lvl_off > INT_MAX)  // FAST's cell records hold 32-bit plane offsets
     return fail(ORBX_EINVAL, "max_batch %d: the pyramid planes take %lld bytes, over 2 GiB", B, lvl_off);
   plan_band_pyramid(P, pl.rtab);
-  {
-    // blur tiles, level-major, row-major inside a level (orbx_blur.hip)
+  for (int v = 0; v < 2; ++v) {
+    // blur tiles, large and small, level-major, row-major inside a level (orbx_blur.hip)
     int tw = 0, th = 0;
-    blur_tile_dims(&tw, &th);
-    P.blur_tiles = (int)pl.rtab.size();
+    blur_tile_dims(v, &tw, &th);
+    P.blur_tiles[v] = (int)pl.rtab.size();
     for (int l = 0; l < L; ++l)
       for (int y0 = 0; y0 < P.lv[l].h; y0 += th)
         for (int x0 = 0; x0 < P.lv[l].w; x0 += tw) pl.rtab.push_back(make_int2(l | (x0 << 4) | (y0 << 16), 0));
-    P.blur_ntiles = (int)pl.rtab.size() - P.blur_tiles;
-    const unsigned long long d = (unsigned long long)P.blur_ntiles;
-    P.blur_magic = 0u;
+    P.blur_ntiles[v] = (int)pl.rtab.size() - P.blur_tiles[v];
+    const unsigned long long d = (unsigned long long)P.blur_ntiles[v];
+    P.blur_magic[v] = 0u;
     if (d > 1) {
       const unsigned long long m = ((1ull << 32) + d - 1) / d, e = m * d - (1ull << 32);
-      if (d * (unsigned long long)B * e < (1ull << 32)) P.blur_magic = (unsigned)m;
+      if (d * (unsigned long long)B * e < (1ull << 32)) P.blur_magic[v] = (unsigned)m;
     }
   }
   if (maxnodes > 65000) return fail(ORBX_EINVAL, "nfeatures too large for the quadtree node table");

@@ -100,11 +100,12 @@ struct ExtractParams {
   } pyr_plan[8];
   int pyr_nplans;
   int gauss[7];                // 7-tap Gaussian fixed-point kernel (sum 257)
-  // blur tiles (orbx_blur.hip): per frame, blur_ntiles entries of the resize
-  // table from blur_tiles on, level | x0 << 4 | y0 << 16 each; the frame of a
-  // workgroup id by a multiply-high with blur_magic when exact (else 0)
-  int blur_tiles, blur_ntiles;
-  unsigned blur_magic;
+  // blur tiles (orbx_blur.hip), [0] large / [1] small: per frame,
+  // blur_ntiles entries of the resize table from blur_tiles on, level | x0 << 4
+  // | y0 << 16 each; the frame of a workgroup id by a multiply-high with
+  // blur_magic when exact (else 0)
+  int blur_tiles[2], blur_ntiles[2];
+  unsigned blur_magic[2];
   LevelGeom lv[kMaxLevels];
 };
 
