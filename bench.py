@@ -1086,7 +1086,8 @@ def shim_latency_leg(frames, W, H, local, n=200, warm=20):
     out["operator_over_orbx_extract"] = round(out["operator_ms"]["median"] / base, 3)
     out["stereo_frame_over_operator"] = round(out["stereo_frame_ms"]["median"] / out["operator_ms"]["median"], 3)
     out["what"] = ("child process, host clock per call: orbx_extract (C-ABI, host buffers); "
-                   "ORBextractor::operator() with the pinned host mvImagePyramid (default) and without; "
+                   "ORBextractor::operator() as shipped (operator_ms: no host mvImagePyramid, the default) and "
+                   "with the opt-in pinned host copy (operator_ms_host_pyramid, ORBX_HOST_PYRAMID=1); "
                    "stereo Frame = two operator() threads + ComputeStereoMatches on the device outputs")
     return out
 

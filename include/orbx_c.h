@@ -113,9 +113,18 @@ typedef struct orbx_config {
   int nlevels;        /* ORBextractor.nLevels (1..16)            */
   int ini_th_fast;    /* ORBextractor.iniThFAST                  */
   int min_th_fast;    /* ORBextractor.minThFAST                  */
-  int width, height;  /* frame size (Camera.width / Camera.height) */
+  int width, height;  /* frame size (Camera.width / Camera.height); 0 x 0 in
+                       * mode U = unknown until the first orbx_extract, as
+                       * Tracking passes for the mono yamls that lack the keys
+                       * (src/Tracking.cc:124-133): the plan is then built on
+                       * the first image (mode F needs the size: EINVAL) */
   int device;         /* HIP device ordinal                       */
-  int max_batch;      /* frames per orbx_extract_batch call (>=1) */
+  int max_batch;      /* frames per orbx_extract_batch call (>=1); the
+                       * pyramid planes of levels >= 1 of all max_batch
+                       * frames must stay below 2 GiB (FAST's cell records
+                       * hold 32-bit plane offsets): about 316 frames at
+                       * 1920x1080 with 8 levels x 1.2, 39 at 4096x4096;
+                       * orbx_create returns EINVAL past it */
   int scale_mode;     /* ORBX_SCALE_*                             */
   int pattern_mode;   /* ORBX_PATTERN_*                           */
   int reserved[5];    /* must be zero                             */
@@ -129,7 +138,8 @@ const char* orbx_version(void);
 int orbx_create(const orbx_config* cfg, orbx_handle* out);
 int orbx_destroy(orbx_handle h);
 
-/* Maximum keypoints one frame can produce (sizes per-frame output slots). */
+/* Maximum keypoints one frame can produce (sizes per-frame output slots);
+ * 0 while a handle created with width/height 0 has seen no image. */
 int orbx_frame_capacity(orbx_handle h);
 
 /* ORBextractor::operator(): host image in, host keypoints/descriptors out.
@@ -190,6 +200,14 @@ int orbx_get_fast_candidates(orbx_handle h, int frame, int level, orbx_kp* out,
  * creation order (the oracle's rule). `kept keypoints` counts the outputs
  * that come from that group. Synchronous (waits for the device). */
 int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out);
+/* Which DistributeOctTree implementation ran per (frame, level) of frames
+ * [frame0, frame0 + nframes) of the last extraction: 1 = the sorted-key path
+ * (node = contiguous range of keys binned by quadtree path code), 0 = the
+ * legacy rounds (levels with more keys than the workgroup's registers hold,
+ * a node to split below the bins' depth, or ORBX_QT_SORTED=0). Both give the
+ * reference's output; this is a diagnostic for tests and profiles.
+ * Synchronous (waits for the device). */
+int orbx_get_quadtree_paths(orbx_handle h, int frame0, int nframes, int* out);
 /* Device status word of the handle's kernels since the last call (0 = ok;
  * bit 1: quadtree round limit, bit 2: quadtree output over capacity, bit 3:
  * a quadtree node without keys, an internal invariant, never expected).
@@ -569,7 +587,12 @@ int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle rig
  * (src/Frame.cc:77-89): keypoints and descriptors are read where those calls
  * left them on the device (no host-to-device copy). nL = the left call's
  * keypoint count (mvKeys.size()); outputs as above. ORBX_EINVAL when either
- * handle's last extraction was a batch call. */
+ * handle's last extraction was a batch call. An empty left or right image
+ * (orbx_extract of 0 x 0) matches nothing: uRight = depth = -1, nkept = 0.
+ * When the extractors' capacity passes the device path's limits (max_kps, or
+ * the stereo kernel's LDS at very large nFeatures) the call copies both
+ * extractions to the host and runs orbm_compute_stereo_matches on their
+ * actual counts instead of failing. */
 int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handle right,
                                      float mb, float mbf, float* uRight, float* depth,
                                      int nL, int* nkept);

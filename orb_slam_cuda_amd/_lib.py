@@ -105,6 +105,7 @@ def lib() -> C.CDLL:
         L.orbx_get_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
         L.orbx_set_stage_events.argtypes = [C.c_void_p, C.c_void_p]
         L.orbx_get_tie_stats.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        L.orbx_get_quadtree_paths.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         L.orbx_get_status.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
         L.orbx_get_pattern.argtypes = [C.c_int, C.c_void_p]
         L.orbm_get_status.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]

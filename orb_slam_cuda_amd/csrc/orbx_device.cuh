@@ -125,6 +125,6 @@ size_t quadtree_lds_bytes(const ExtractParams& P);
 size_t pyr_band_lds_bytes(const ExtractParams& P);
 const void* pyr_band_kernel_ptr();
 size_t fast_lds_bytes(const ExtractParams& P);
-const void* quadtree_kernel_ptr();
+const void* quadtree_kernel_ptr(const ExtractParams& P);
 
 }  // namespace orbx

@@ -44,7 +44,9 @@ __global__ __launch_bounds__(256) void copy2d_kernel(uint8_t* __restrict__ d, si
   }
 }
 size_t quadtree_lds_bytes(const ExtractParams& P);
-extern const void* quadtree_kernel_ptr(int big);
+size_t quadtree_legacy_lds_bytes(const ExtractParams& P);
+size_t quadtree_sorted_lds_bytes(const ExtractParams& P, int big);
+extern const void* quadtree_kernel_ptr(const ExtractParams& P);
 size_t pyr_band_lds_bytes(const ExtractParams& P);
 void blur_tile_dims(int small, int* tw, int* th);
 extern const void* pyr_band_kernel_ptr();
@@ -124,6 +126,7 @@ struct orbx_extractor {
   int graph_w = 0, graph_h = 0;
   bool graph_hp = false;  // the graph holds the host-pyramid copy branch
   bool last_single = false;  // the last extraction was orbx_extract (outputs in d_out)
+  bool last_empty = false;   // ... of an empty image (no outputs, src/ORBextractor.cc:1542-1543)
   int warm_w = 0, warm_h = 0;  // size of the last plain (uncaptured) call: capture from the next one
   int last_batch = 0;
   const uint8_t* last_frames = nullptr;
@@ -467,6 +470,49 @@ static void plan_band_pyramid(ExtractParams& P, std::vector<int2>& rtab) {
   select_pyr_plan(P, 0);  // the default; launch_pyramid picks per launch
 }
 
+// Path codes of the sorted-key quadtree (orbx_quadtree.hip): a node box of
+// DistributeOctTree never depends on the data (roots: nIni columns of width
+// hX, src/ORBextractor.cc:903-914; children: DivideNode's ceil halves,
+// :833-834), so the quadrant of a key at every depth is a function of its x
+// alone (x half) and of its y alone (y half). t = boxW x codes (root index in
+// the top bits, x digit at even bits), then boxH y codes (y digit at odd
+// bits), Dh digits each: xs[x] | ys[y] is the key's bin, its node at depth
+// Dh. bits = 0 (code shift) | Dh << 8 | log2(bins) << 16; bins stay within
+// 4096..8192 so that the bin scan keeps 2..8 words per thread.
+static bool qt_code_tables(const LevelGeom& g, std::vector<uint32_t>& t, int* bits) {
+  int R = 0;
+  while ((1 << R) < g.nIni) ++R;
+  if (R > 5 || g.boxW < 1 || g.boxH < 1 || g.boxW > 0xFFFF || g.boxH > 0xFFFF) return false;
+  const int Dh = (13 - R) / 2;
+  t.assign((size_t)g.boxW + g.boxH, 0u);
+  for (int x = 0; x < g.boxW; ++x) {
+    // vpIniNodes[kp.pt.x/hX] (:920); columns past the last root never hold keys
+    const int r = std::min((int)((float)x / g.hX), g.nIni - 1);
+    int a = (int)(g.hX * (float)r), c = (int)(g.hX * (float)(r + 1));
+    uint32_t code = (uint32_t)r << (2 * Dh);
+    for (int j = 0; j < Dh; ++j) {
+      const int mid = a + (int)std::ceil((float)(c - a) / 2.f);
+      const int bit = x >= mid;
+      if (bit) a = mid; else c = mid;
+      code |= (uint32_t)bit << (2 * (Dh - 1 - j));
+    }
+    t[x] = code;
+  }
+  for (int y = 0; y < g.boxH; ++y) {
+    int a = 0, c = g.boxH;
+    uint32_t code = 0;
+    for (int j = 0; j < Dh; ++j) {
+      const int mid = a + (int)std::ceil((float)(c - a) / 2.f);
+      const int bit = y >= mid;
+      if (bit) a = mid; else c = mid;
+      code |= (uint32_t)bit << (2 * (Dh - 1 - j) + 1);
+    }
+    t[(size_t)g.boxW + y] = code;
+  }
+  *bits = (Dh << 8) | ((R + 2 * Dh) << 16);
+  return true;
+}
+
 static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   Plan& pl = h->plan;
   const orbx_config& c = h->cfg;
@@ -596,6 +642,26 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
       }
     }
   }
+  // sorted-key quadtree: per level, the depth-Dh path code of every column
+  // (root index on top) and of every row (orbx_quadtree.hip), two u32 per
+  // int2 of the resize table
+  P.qt_tabmax = 0;
+  P.qt_nbmax = 0;
+  for (int l = 0; l < L; ++l) {
+    LevelGeom& g = P.lv[l];
+    std::vector<uint32_t> t;
+    int bits = 0;
+    g.qt_tab = -1;
+    if (qt_code_tables(g, t, &bits)) {
+      g.qt_tab = (int)pl.rtab.size() * 2;
+      g.qt_dims = g.boxW | (g.boxH << 16);
+      g.qt_bits = bits;
+      if (t.size() & 1) t.push_back(0u);
+      for (size_t i = 0; i < t.size(); i += 2) pl.rtab.push_back(make_int2((int)t[i], (int)t[i + 1]));
+      P.qt_tabmax = std::max(P.qt_tabmax, g.boxW + g.boxH);
+      P.qt_nbmax = std::max(P.qt_nbmax, 1 << ((bits >> 16) & 0xFF));
+    }
+  }
   if (lvl_off > INT_MAX)  // FAST's cell records hold 32-bit plane offsets
     return fail(ORBX_EINVAL, "max_batch %d: the pyramid planes take %lld bytes, over 2 GiB", B, lvl_off);
   plan_band_pyramid(P, pl.rtab);
@@ -638,6 +704,9 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   {
     const char* e = getenv("ORBX_QT_GENERIC");  // tests: the generic rounds on any plan
     P.qt_lean = maxnodes < 16384 && !(e && e[0] == '1');
+    // the sorted-key path first (ORBX_QT_SORTED=0: the legacy rounds only, for A/B and tests)
+    const char* so = getenv("ORBX_QT_SORTED");
+    P.qt_sorted = P.qt_lean && P.qt_nbmax > 0 && !(so && so[0] == '0');
   }
   {
     // keep the LDS footprint at 80 KiB so two quadtree blocks fit one CU,
@@ -648,11 +717,16 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
 #ifndef ORBX_QT_LDS_KB
 #define ORBX_QT_LDS_KB 80
 #endif
-    const size_t base = quadtree_lds_bytes(P);
+    const size_t base = quadtree_legacy_lds_bytes(P);
     const size_t small = ORBX_QT_LDS_KB * 1024, big = 160 * 1024 - 512;
     P.qt_big = base + 16 * 1024 > small ? 1 : 0;
     const size_t budget = P.qt_big ? big : small;
     P.kcap_lds = base < budget ? (int)((budget - base) / 6) & ~15 : 0;
+    // the sorted path shares the block's LDS (its layout is the legacy one's
+    // alternative, not an addition): on when it fits the same budget
+    if (P.qt_sorted && quadtree_sorted_lds_bytes(P, P.qt_big) > budget) P.qt_sorted = 0;
+    // the sorted path's rounds hold two nodes per thread
+    if (maxnodes > 2 * (P.qt_big ? 1024 : kQtThreads)) P.qt_sorted = 0;
   }
   pl.P = P;
   pl.W = W;
@@ -699,7 +773,7 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
         fprintf(stderr, "pyr plan %d: %d workgroups per CU\n", i, pl.P.pyr_plan[i].occ);
     }
   }
-  if (raise_lds_limit(quadtree_kernel_ptr(P.qt_big), quadtree_lds_bytes(P)))
+  if (raise_lds_limit(quadtree_kernel_ptr(P), quadtree_lds_bytes(P)))
     return fail(ORBX_EDEVICE, "LDS limit of quadtree_kernel: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
 }
@@ -757,6 +831,13 @@ int orbx::extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int
 int orbx::extractor_last_output(orbx_handle h, const int** d_count, const orbx_kp** d_kps, const uint8_t** d_desc,
                                 int* cap) {
   if (!h) return fail(ORBX_EINVAL, "null extractor handle");
+  if (h->last_empty) {  // an empty image: no keypoints
+    *d_count = nullptr;
+    *d_kps = nullptr;
+    *d_desc = nullptr;
+    *cap = 0;
+    return ORBX_OK;
+  }
   if (!h->last_single || !h->d_out.p)
     return fail(ORBX_EINVAL, "the extractor's last extraction was not an orbx_extract call");
   const int c = h->plan.P.kp_per_frame;
@@ -808,7 +889,15 @@ int orbx_create(const orbx_config* cfg, orbx_handle* out) {
   if (c.nlevels < 1 || c.nlevels > kMaxLevels) return fail(ORBX_EINVAL, "nlevels must be 1..%d", kMaxLevels);
   if (c.nfeatures < 0) return fail(ORBX_EINVAL, "nfeatures < 0");
   if (!(c.scale_factor > 1.0f)) return fail(ORBX_EINVAL, "scaleFactor must be > 1");
-  if (c.width <= 0 || c.height <= 0) return fail(ORBX_EINVAL, "width/height must be > 0 (Camera.width/height)");
+  // Camera.width/height absent from the yaml (the reference's mono KITTI /
+  // EuRoC settings, src/Tracking.cc:124-133) arrive as 0: mode U's tables do
+  // not depend on the size, so the plan waits for the first image; mode F's
+  // scale override is computed from the width (src/ORBextractor.cc:674-680)
+  const bool deferred = c.width == 0 && c.height == 0 && c.scale_mode == ORBX_SCALE_U;
+  if (!deferred && (c.width <= 0 || c.height <= 0))
+    return fail(ORBX_EINVAL, c.scale_mode == ORBX_SCALE_F && c.width == 0 && c.height == 0
+                                 ? "scale mode F needs width/height (Camera.width/height)"
+                                 : "width/height must be > 0, or both 0 in scale mode U (Camera.width/height)");
   if (c.max_batch < 1) return fail(ORBX_EINVAL, "max_batch must be >= 1");
   if (c.scale_mode != ORBX_SCALE_U && c.scale_mode != ORBX_SCALE_F) return fail(ORBX_EINVAL, "bad scale_mode");
   if (c.pattern_mode != ORBX_PATTERN_FORK && c.pattern_mode != ORBX_PATTERN_UPSTREAM)
@@ -824,7 +913,8 @@ int orbx_create(const orbx_config* cfg, orbx_handle* out) {
   orbx_extractor* h = new orbx_extractor();
   h->cfg = c;
   compute_scales(h);
-  int rc = build_plan(h, c.width, c.height, c.max_batch);
+  h->plan.B = c.max_batch;
+  int rc = deferred ? ORBX_OK : build_plan(h, c.width, c.height, c.max_batch);
   if (rc) { delete h; return rc; }
   // h->stream (the synchronous API's stream) is created on first use: an idle
   // stream would still take one of the process's few hardware queues, and a
@@ -868,6 +958,8 @@ int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch, size_t
                        orbx_kp* d_kps, uint8_t* d_desc, int* d_counts, void* stream) {
   if (!h || !d_frames || !d_kps || !d_desc || !d_counts) return fail(ORBX_EINVAL, "null argument");
   if (batch < 1 || batch > h->plan.B) return fail(ORBX_EINVAL, "batch %d not in 1..max_batch(%d)", batch, h->plan.B);
+  if (h->plan.W == 0)
+    return fail(ORBX_EINVAL, "no frame size yet: the handle was created with width/height 0 and has seen no orbx_extract");
   if (row_stride < (size_t)h->plan.W) return fail(ORBX_EINVAL, "row_stride < width");
   HIP_OK(hipSetDevice(h->cfg.device));
   void** ev = h->has_user_ev ? h->user_ev : (h->timing ? (void**)h->ev : nullptr);
@@ -882,6 +974,7 @@ int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch, size_t
   h->last_rstride = row_stride;
   h->host_pyr_valid = false;  // the pinned host pyramid is of an earlier orbx_extract
   h->last_single = false;
+  h->last_empty = false;
   if (rc) return fail(rc, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
   return ORBX_OK;
 }
@@ -957,7 +1050,17 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   if (!h || !n) return fail(ORBX_EINVAL, "null argument");
   std::lock_guard<std::mutex> lk(h->mu);
   *n = 0;
-  if (w == 0 || hh == 0) return ORBX_OK;  // src/ORBextractor.cc:1542-1543
+  if (w == 0 || hh == 0) {  // src/ORBextractor.cc:1542-1543
+    // no outputs: later readers of "the last extraction" (the stereo matcher
+    // on the device outputs, the host pyramid) see an empty one, as the
+    // reference's Frame sees empty mvKeysRight
+    h->last_single = false;
+    h->last_empty = true;
+    h->host_pyr_valid = false;
+    h->last_batch = 0;
+    return ORBX_OK;
+  }
+  h->last_empty = false;
   if (!img || w < 0 || hh < 0 || stride < (size_t)w) return fail(ORBX_EINVAL, "bad image");
   HIP_OK(hipSetDevice(h->cfg.device));
   if (w != h->plan.W || hh != h->plan.H) {
@@ -1092,10 +1195,11 @@ int orbx_get_scales(orbx_handle h, float* s, float* is, float* s2, float* is2) {
 int orbx_get_levels_info(orbx_handle h, int* nlevels, int* lw, int* lh, int* nf) {
   if (!h) return fail(ORBX_EINVAL, "null handle");
   const ExtractParams& P = h->plan.P;
-  if (nlevels) *nlevels = P.L;
-  for (int l = 0; l < P.L; ++l) {
-    if (lw) lw[l] = P.lv[l].w;
-    if (lh) lh[l] = P.lv[l].h;
+  const int L = h->cfg.nlevels;  // also before a deferred plan (sizes 0 until the first image)
+  if (nlevels) *nlevels = L;
+  for (int l = 0; l < L; ++l) {
+    if (lw) lw[l] = P.L ? P.lv[l].w : 0;
+    if (lh) lh[l] = P.L ? P.lv[l].h : 0;
     if (nf) nf[l] = h->nfeat[l];
   }
   return ORBX_OK;
@@ -1218,6 +1322,20 @@ int orbx_get_status(orbx_handle h, int reset, int* status) {
   return ORBX_OK;
 }
 
+
+int orbx_get_quadtree_paths(orbx_handle h, int frame0, int nframes, int* out) {
+  if (!h || !out) return fail(ORBX_EINVAL, "null argument");
+  const Plan& pl = h->plan;
+  if (frame0 < 0 || nframes < 1 || frame0 + nframes > h->last_batch)
+    return fail(ORBX_EINVAL, "frames [%d, %d) not in the last extraction (%d frames)", frame0, frame0 + nframes,
+                h->last_batch);
+  if (int rc = handle_quiesce(h)) return rc;
+  const int L = pl.P.L;
+  std::vector<int> t((size_t)nframes * L * 4);
+  if (int rc = handle_d2h(h, t.data(), pl.qties.as<int>() + (size_t)frame0 * L * 4, t.size() * 4)) return rc;
+  for (size_t i = 0; i < (size_t)nframes * L; ++i) out[i] = t[i * 4 + 3];
+  return ORBX_OK;
+}
 
 int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out) {
   if (!h || !out) return fail(ORBX_EINVAL, "null argument");

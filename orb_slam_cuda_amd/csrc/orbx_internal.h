@@ -48,6 +48,11 @@ struct LevelGeom {
   float scale;           // mvScaleFactor[l]
   float size;            // (float)(int)(PATCH_SIZE * mvScaleFactor[l])
   int xtab2;             // band pyramid column table: {sx, a0 | a1 << 16}, replicate folded in
+  // sorted-key quadtree (orbx_quadtree.hip): path-code tables of this level
+  // in the resize table (u32 units: x codes, then y codes), their lengths
+  // (tw | th << 16) and the code layout (bin shift | Dh << 8 | log2 bins << 16);
+  // qt_tab < 0: the level's codes do not separate every position (legacy rounds)
+  int qt_tab, qt_dims, qt_bits;
 };
 
 // keypoint slots per orient+BRIEF workgroup; every level's slot range starts
@@ -80,6 +85,8 @@ struct ExtractParams {
   int kcap_lds;                // quadtree keys kept in LDS up to this count
   int qt_lean;                 // quadtree: lean rounds (packed 16-bit key nodes, maxnodes < 16384), else the generic ones
   int qt_big;                  // quadtree: node tables past 64 KB of LDS: 1024-thread blocks, a whole CU's LDS each
+  int qt_sorted;               // quadtree: the sorted-key path first (levels with code tables, K <= threads x 8, maxnodes <= 2 x threads)
+  int qt_tabmax, qt_nbmax;     // largest code-table length (tw + th) and bin count of any level
   int fast_rh_max;             // largest FAST cell ROI height
   int fast_bw_max, fast_bh_max;  // largest FAST detection band
   int pattern_upstream;
@@ -359,6 +366,7 @@ struct StreamMarks {
 WsOrder* extractor_ws(orbx_handle h);
 // orbx_host.hip: where the handle's last orbx_extract left its frame's
 // outputs on the device (count, keypoints at a pitch of `cap`, descriptors);
+// an empty image leaves cap = 0 and null pointers (no keypoints);
 // ORBX_EINVAL when the last extraction was not an orbx_extract call
 int extractor_last_output(orbx_handle h, const int** d_count, const orbx_kp** d_kps, const uint8_t** d_desc,
                           int* cap);

@@ -1964,10 +1964,36 @@ int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handl
   int capL = 0, capR = 0;
   if (extractor_last_output(left, &dnL, &dkl, &ddl, &capL) || extractor_last_output(right, &dnR, &dkr, &ddr, &capR))
     return mfail(ORBX_EINVAL, "stereo (last extraction): %s", orbx_last_error());
+  if (!dnL || !dnR) {
+    // an empty left or right image: no right keypoints to match, every left
+    // keypoint keeps uRight = depth = -1 (src/Frame.cc:465-470)
+    if (!dnL && nL) return mfail(ORBX_EINVAL, "nL %d but the left extraction was of an empty image", nL);
+    for (int i = 0; i < nL; ++i) uRight[i] = depth[i] = -1.f;
+    *nkept = 0;
+    return ORBX_OK;
+  }
   if (capL != capR) return mfail(ORBX_EINVAL, "left and right extractors have different capacities");
   if (nL > capL) return mfail(ORBX_EINVAL, "nL %d above the left extraction's capacity %d", nL, capL);
-  if (capL > m->max_kps) return mfail(ORBX_ECAPACITY, "extractor capacity %d above max_kps %d", capL, m->max_kps);
   MHIP(hipSetDevice(m->device));
+  // the device path sizes its LDS by the extractors' capacity; past the
+  // matcher's limits (max_kps, or the stereo kernel's LDS for large
+  // nFeatures) the keypoints come to the host and take the host-array path,
+  // whose pitch is the actual counts
+  auto host_fallback = [&]() -> int {
+    int cnt[2] = {0, 0};
+    MHIP(hipMemcpy(&cnt[0], dnL, 4, hipMemcpyDeviceToHost));
+    MHIP(hipMemcpy(&cnt[1], dnR, 4, hipMemcpyDeviceToHost));
+    if (nL > cnt[0]) return mfail(ORBX_EINVAL, "nL %d above the left extraction's count %d", nL, cnt[0]);
+    std::vector<orbx_kp> kl(std::max(cnt[0], 1)), kr(std::max(cnt[1], 1));
+    std::vector<uint8_t> dl((size_t)std::max(cnt[0], 1) * 32), dr((size_t)std::max(cnt[1], 1) * 32);
+    MHIP(hipMemcpy(kl.data(), dkl, (size_t)cnt[0] * sizeof(orbx_kp), hipMemcpyDeviceToHost));
+    MHIP(hipMemcpy(kr.data(), dkr, (size_t)cnt[1] * sizeof(orbx_kp), hipMemcpyDeviceToHost));
+    MHIP(hipMemcpy(dl.data(), ddl, (size_t)cnt[0] * 32, hipMemcpyDeviceToHost));
+    MHIP(hipMemcpy(dr.data(), ddr, (size_t)cnt[1] * 32, hipMemcpyDeviceToHost));
+    return orbm_compute_stereo_matches(m, left, right, kl.data(), dl.data(), nL, kr.data(), dr.data(), cnt[1], mb, mbf,
+                                       uRight, depth, nkept);
+  };
+  if (capL > m->max_kps) return host_fallback();
   // outputs {kept, -, -, -, uRight[nL], depth[nL]} in one block: one copy back
   // into the matcher's pinned staging
   const size_t bytes = 16 + (size_t)capL * 8;
@@ -1987,6 +2013,7 @@ int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handl
   hipStream_t st = m->stream;
   rc = orbm_compute_stereo_matches_batch(m, left, 0, right, 0, dkl, ddl, dnL, dkr, ddr, dnR, capL, 1, mb, mbf, du, dd,
                                          dk, st);
+  if (rc == ORBX_ECAPACITY) return host_fallback();  // checked before any launch
   if (rc) return rc;
   uint8_t* h = (uint8_t*)m->h_stage;
   MHIP(hipMemcpyAsync(h, dk, 16 + (size_t)capL * 8, hipMemcpyDeviceToHost, st));

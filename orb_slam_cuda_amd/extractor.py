@@ -76,9 +76,15 @@ class ORBextractor:
         if img.strides[1] != 1:
             img = np.ascontiguousarray(img)
         cap = self.frame_capacity
+        n = C.c_int(0)
+        if cap == 0:
+            # created with width/height 0 (mono yamls without Camera.width/height,
+            # src/Tracking.cc:124-133): this call plans the handle for the image
+            check(lib().orbx_extract(self._h, ptr(img), img.shape[1], img.shape[0], img.strides[0],
+                                     None, 2**31 - 1, None, C.byref(n)))
+            cap = self.frame_capacity
         kps = np.empty(cap, KP_DTYPE)
         desc = np.empty((cap, 32), np.uint8)
-        n = C.c_int(0)
         check(lib().orbx_extract(self._h, ptr(img), img.shape[1], img.shape[0], img.strides[0],
                                  ptr(kps), cap, ptr(desc), C.byref(n)))
         cap = self.frame_capacity  # a new image size re-plans the handle
@@ -174,6 +180,13 @@ class ORBextractor:
         int array (nframes, nlevels, 3) of {events, group nodes, kept keypoints}."""
         out = np.zeros((nframes, self.nlevels, 3), np.int32)
         check(lib().orbx_get_tie_stats(self._h, frame0, nframes, ptr(out)))
+        return out
+
+    def quadtree_paths(self, frame0: int = 0, nframes: int = 1) -> np.ndarray:
+        """DistributeOctTree implementation per (frame, level) of the last extraction
+        (orbx_get_quadtree_paths): 1 = sorted-key path, 0 = legacy rounds."""
+        out = np.zeros((nframes, self.nlevels), np.int32)
+        check(lib().orbx_get_quadtree_paths(self._h, frame0, nframes, ptr(out)))
         return out
 
     def status(self, reset: bool = True) -> int:

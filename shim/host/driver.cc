@@ -296,7 +296,21 @@ int main(int argc, char** argv) {
   try {
     setenv("ORBX_HOST_PYRAMID", "1", 1);  // the test reads mvImagePyramid
     // Tracking's monocular extractors: mpIniORBextractor has 2x nFeatures (src/Tracking.cc:145-150)
-    ORBextractor extractor(2000, 1.2f, 8, 20, 7, W, H);
+    // ORBX_DRIVER_CTOR_WH=0: the ctor gets width/height 0, as Tracking passes
+    // them for the reference's mono yamls (Examples/Monocular/KITTI00-02.yaml
+    // has no Camera.width/height, src/Tracking.cc:124-133); the scale getters
+    // are recorded before the first call
+    const char* wh = getenv("ORBX_DRIVER_CTOR_WH");
+    const bool zero_wh = wh && wh[0] == '0';
+    ORBextractor extractor(2000, 1.2f, 8, 20, 7, zero_wh ? 0 : W, zero_wh ? 0 : H);
+    {
+      std::vector<float> sc = extractor.GetScaleFactors(), isc = extractor.GetInverseScaleFactors(),
+                         s2 = extractor.GetScaleSigmaSquares(), is2 = extractor.GetInverseScaleSigmaSquares();
+      sc.insert(sc.end(), isc.begin(), isc.end());
+      sc.insert(sc.end(), s2.begin(), s2.end());
+      sc.insert(sc.end(), is2.begin(), is2.end());
+      write_file(out + "/scales_pre.bin", sc.data(), sc.size() * 4);
+    }
     std::vector<Frame> frames;
     for (int i = 0; i < nfr; ++i) {
       cv::Mat im(H, W, CV_8U, pix.data() + (size_t)i * W * H, W);

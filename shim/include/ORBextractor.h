@@ -66,11 +66,16 @@ class ORBextractor {
 
   // The pyramid of the last call (src/ORBextractor.cc:1837-1863). Opt-in
   // (ORBX_HOST_PYRAMID=1): headers over the handle's pinned host copy, which
-  // orbx_extract then fills beside the other kernels (orbx_set_host_pyramid),
-  // valid until the next call as the reference's own buffers are. Off by
-  // default the levels stay empty: the reference's only reader,
-  // ComputeStereoMatches (src/Frame.cc:472-579), reads the device pyramids
-  // here, and the copy would cost ~30 us per call.
+  // orbx_extract then fills beside the other kernels (orbx_set_host_pyramid).
+  // Lifetime and aliasing differ from the reference's: the Mats do not own
+  // their data; every level (level 0 is the call's input staging buffer) is
+  // overwritten by the next operator() on this extractor, so a caller that
+  // keeps a level across calls must clone() it (the reference allocates
+  // fresh Mats per call, :1847). Off by default the levels stay empty: the
+  // reference's only reader, ComputeStereoMatches (src/Frame.cc:472-579),
+  // reads the device pyramids here (the Frame.cc body), and
+  // the copy would cost ~30 us per call. A build that keeps the reference's
+  // own Frame.cc body must set ORBX_HOST_PYRAMID=1.
   std::vector<cv::Mat> mvImagePyramid;
 
   // Per-stage device times of the last call, named as the reference's

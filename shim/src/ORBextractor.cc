@@ -62,7 +62,9 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
   int nl = 0;
   orbx_check(orbx_get_levels_info(h_, &nl, lw_.data(), lh_.data(), mnFeaturesPerLevel.data()));
   cap_ = orbx_frame_capacity(h_);
-  if (cap_ <= 0) throw std::runtime_error("liborbx: bad frame capacity");
+  // width/height 0 (a mono yaml without Camera.width/height, src/Tracking.cc:124-133):
+  // the handle plans on the first image, and operator() re-reads the capacity then
+  if (cap_ <= 0 && !(width == 0 && height == 0)) throw std::runtime_error("liborbx: bad frame capacity");
   // ORBX_HOST_PYRAMID=1: mvImagePyramid filled on every call (opt-in: the copy
   // costs ~30 us per call, bench.py shim_latency, and the reference's only
   // reader, ComputeStereoMatches, reads the device pyramids here)

@@ -160,6 +160,57 @@ def test_generic_quadtree_rounds(pkg, O, monkeypatch):
         assert_same(kp, desc, rkp, rdesc)
 
 
+def _clustered_frame(W, H, seed=11, patches=40, side=10):
+    # flat background with small noise patches: few keys per level (K ~ N),
+    # so the quadtree splits nodes far below the sorted path's bin depth
+    rng = np.random.default_rng(seed)
+    img = np.full((H, W), 128, np.uint8)
+    for _ in range(patches):
+        x, y = int(rng.integers(20, W - 30)), int(rng.integers(20, H - 30))
+        img[y:y + side, x:x + side] = rng.integers(0, 256, (side, side))
+    return img
+
+
+@pytest.mark.parametrize("W,H,nf", [(1241, 376, 2000), (752, 480, 1000), (1241, 376, 4000)])
+def test_quadtree_sorted_path(pkg, O, monkeypatch, W, H, nf):
+    """The sorted-key DistributeOctTree (every node a contiguous range of keys
+    binned by quadtree path code, orbx_quadtree.hip) runs on every level of
+    textured frames and equals the oracle, ties and list order included; the
+    legacy rounds (ORBX_QT_SORTED=0) give the same keypoints."""
+    from orb_slam_cuda_amd.synth import synth_frame
+    cfg = oracle_cfg(O, nf, W, H)
+    for seed in (3, 12):
+        img = synth_frame(seed, W, H)
+        ext = pkg.ORBextractor(nf, 1.2, 8, 20, 7, W, H)
+        kp, desc = ext(img)
+        assert (ext.quadtree_paths() == 1).all(), ext.quadtree_paths()
+        rkp, rdesc = O.extract(cfg, img)
+        assert_same(kp, desc, rkp, rdesc)
+        assert np.array_equal(ext.tie_stats(), _tie_stats_legacy(pkg, monkeypatch, nf, W, H, img))
+
+
+def _tie_stats_legacy(pkg, monkeypatch, nf, W, H, img):
+    with monkeypatch.context() as m:
+        m.setenv("ORBX_QT_SORTED", "0")
+        ext = pkg.ORBextractor(nf, 1.2, 8, 20, 7, W, H)
+        ext(img)
+        assert (ext.quadtree_paths() == 0).all()
+        return ext.tie_stats()
+
+
+def test_quadtree_sorted_path_falls_back(pkg, O):
+    """Corners in small scattered patches: some level must split a node below
+    the bins' depth, its workgroup falls back to the legacy rounds, and every
+    level still equals the oracle."""
+    W, H = 1241, 376
+    img = _clustered_frame(W, H)
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H)
+    kp, desc = ext(img)
+    assert (ext.quadtree_paths() == 0).any()
+    rkp, rdesc = O.extract(oracle_cfg(O, 2000, W, H), img)
+    assert_same(kp, desc, rkp, rdesc)
+
+
 def test_edge_images(pkg, O):
     W, H = 640, 360
     ext = pkg.ORBextractor(1000, 1.2, 8, 20, 7, W, H)
@@ -198,6 +249,26 @@ def test_strided_input_and_replan(pkg, O):
     rkp, rdesc = O.extract(oracle_cfg(O, 2000, 800, 600), img2)
     assert_same(kp, desc, rkp, rdesc)
     assert ext.levels_info()["w"][0] == 800
+
+
+def test_deferred_plan_without_camera_size(pkg, O):
+    """width/height 0 x 0 (Tracking's values for the mono yamls without
+    Camera.width/height, src/Tracking.cc:124-133): scale mode U plans on the
+    first image; the scales are there before it; mode F and one-sided zeros are
+    refused (mode F's scale override needs the width, src/ORBextractor.cc:674-680)."""
+    from orb_slam_cuda_amd.synth import synth_frame
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, 0, 0)
+    W, H = 1241, 376
+    cfg = oracle_cfg(O, 2000, W, H)
+    assert np.array_equal(np.asarray(ext.GetScaleFactors(), np.float32), O.level_info(cfg)["scale"])
+    img = synth_frame(17, W, H)
+    kp, desc = ext(img)
+    rkp, rdesc = O.extract(cfg, img)
+    assert_same(kp, desc, rkp, rdesc)
+    with pytest.raises(pkg.OrbxError):
+        pkg.ORBextractor(2000, 1.2, 8, 20, 7, 0, 0, scale_mode="F")
+    with pytest.raises(pkg.OrbxError):
+        pkg.ORBextractor(2000, 1.2, 8, 20, 7, 0, 376)
 
 
 def test_invalid_inputs_raise(pkg):

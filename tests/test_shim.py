@@ -222,6 +222,37 @@ def test_shim_extractor_modes_from_environment(pkg, O, tmp_path, mode, pattern):
         assert lvl.shape != O.pyramid_level(O.config(), frames[0], 1).shape
 
 
+@pytest.mark.gpu
+def test_shim_extractor_without_camera_size(pkg, O, tmp_path):
+    """Tracking passes Camera.width/height = 0 for the reference's mono yamls
+    (Examples/Monocular/KITTI00-02.yaml has neither key, src/Tracking.cc:124-133):
+    the extractor constructs, its scale getters return the 1.2^l tables before
+    the first call (the Frame ctor reads them first, src/Frame.cc:181-190), and
+    the first 1241x376 frame extracts bit-exact against the oracle."""
+    from orb_slam_cuda_amd.synth import SynthSequence
+    W, H, n = 1241, 376, 2
+    frames = SynthSequence(13, W, H).frames(n)
+    fpath = tmp_path / "frames.u8"
+    frames.tofile(fpath)
+    out = tmp_path / "out"
+    out.mkdir()
+    env = dict(os.environ, ORBX_DRIVER_CTOR_WH="0")
+    r = subprocess.run([DRIVER, str(fpath), str(n), str(W), str(H), "-", str(out)], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    cfg = O.config(nfeatures=2000, width=W, height=H)
+    info = O.level_info(cfg)
+    sc = np.fromfile(out / "scales_pre.bin", dtype=np.float32).reshape(4, 8)
+    for row, key in zip(sc, ("scale", "inv_scale", "sigma2", "inv_sigma2")):
+        assert np.array_equal(row, info[key]), key
+    for i in range(n):
+        rkp, rdesc = O.extract(cfg, frames[i])
+        kp = np.fromfile(out / f"kp{i}.bin", dtype=rkp.dtype)
+        desc = np.fromfile(out / f"desc{i}.bin", dtype=np.uint8).reshape(-1, 32)
+        assert len(kp) == len(rkp) > 1000
+        assert np.array_equal(kp.view(np.uint8), rkp.view(np.uint8)) and np.array_equal(desc, rdesc)
+
+
 def test_shim_rejects_unknown_scale_mode(tmp_path):
     _build()
     frames = np.zeros((1, 64, 64), np.uint8)
