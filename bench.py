@@ -793,6 +793,8 @@ def run_mono(args, cfg, rank, world, local, dist):
     ach = hbm_stages[rk] * BS / (st[rk] * 1e-3) / 1e9
     roof = {"kernel": KERNELS[rk], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": "profiles/pmc_traffic.json: committed FETCH_SIZE/WRITE_SIZE passes (tools/pmc_passes.sh),"
+                              " not measured in this run",
             "algorithmic_bytes_per_launch": int(hbm_stages[rk] * BS),
             "avg_launch_ms": round(st[rk], 4)}
     # the same kernel against VALU issue (it is latency / issue bound, not HBM bound):
@@ -801,7 +803,8 @@ def run_mono(args, cfg, rank, world, local, dist):
     if vi and BS == SQ_LAUNCH_FRAMES:
         roof["valu_issue"] = {"wave_instr_per_launch": int(vi), "achieved_T_per_s": round(vi / (st[rk] * 1e-3) / 1e12, 4),
                               "peak_T_per_s": VALU_ISSUE_PEAK_T, "frac": round(vi / (st[rk] * 1e-3) / 1e12 / VALU_ISSUE_PEAK_T, 4),
-                              "source": "profiles/sq_valu.json (tools/pmc_sq.sh, serial run)"}
+                              "source": "profiles/sq_valu.json: committed SQ_INSTS_VALU pass (tools/pmc_sq.sh, serial "
+                                        "run), not measured in this run; the time is this run's"}
     # the dense matcher runs on the matrix cores: algorithmic work = one 256-element +-1 dot
     # product per (query, candidate) pair = 512 FLOP, against the dense FP4 MFMA peak; the
     # per-pair top-2 update (v_min + v_med3) is reported against the VALU lane-op peak
@@ -824,11 +827,13 @@ def run_mono(args, cfg, rank, world, local, dist):
     gc.collect()
     lat = host = cpu = cpu1 = tie_rule = None
     solo = world == 1
-    shim_lat = None
+    shim_lat = shim_match_lat = None
     if rank == 0 and solo and not args.no_latency:
         lat = latency_leg(cfg, local, frames[:32], args.no_match)
         if not args.no_shim_latency and (W, H, NF) == (1241, 376, 2000) and ext_params(cfg)[2] == 8:
             shim_lat = shim_latency_leg(frames[:32], W, H, local)
+            if not args.no_match:
+                shim_match_lat = shim_matcher_latency_leg(local)
     if rank == 0 and solo and not args.no_host_stream and args.host_steps > 0:
         host = host_stream_leg(args, cfg, local, frames)
     if rank == 0 and solo and args.cpu_sample > 0:
@@ -871,11 +876,15 @@ def run_mono(args, cfg, rank, world, local, dist):
             "cpu_baseline_1thread": cpu1,
             "latency": lat,
             "shim_latency": shim_lat,
+            "shim_matcher_latency": shim_match_lat,
             "host_stream": host,
             "quadtree_tie_straddle": tie,
             "tie_rule_disagreement": tie_rule,
             "pyr_fast_pass_hbm_gbs": round(pf_gbs, 1),
             "dominant_kernel": KERNELS[dominant],
+            "dominant_kernel_basis": "HIP-event stage time of the pipelined step (a stage's events also hold its "
+                                     "workgroups' wait for compute units beside the other streams)",
+            "rocprof_ranking": rocprof_ranking(),
             "stage_ms_per_batch": {s: round(v, 4) for s, v in st.items()},
             "extract_only_frames_per_s": round(BS / (extract_ms * 1e-3), 1),
             "host_issue_ms_per_step": round(issue / args.steps * 1e3, 4), "event_ms_per_step": round(ev_ms / args.steps, 4),
@@ -908,6 +917,23 @@ def dump_batch0(args, pipe, rank, block, prev):
 
 SQ_LAUNCH_FRAMES = 32   # frames per extraction launch of the committed SQ counter run
 VALU_ISSUE_PEAK_T = 1.2288  # wave64 VALU instructions/s: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles
+
+
+def rocprof_ranking(top=6):
+    """Kernels of the newest committed pipelined rocprofv3 summary
+    (profiles/rNN_kernel_stats.csv, the default C3 command) by total time:
+    the ranking beside the HIP-event one (dominant_kernel)."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_kernel_stats.csv")))
+    if not files:
+        return None
+    rows = list(csv.DictReader(open(files[-1])))
+    rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
+    return {"source": os.path.relpath(files[-1], ROOT) + " (committed, not measured in this run)",
+            "by_total_time": [{"kernel": r["Name"].split("(")[0].replace("void ", "").replace("orbx::", ""),
+                               "avg_us": round(float(r["AverageNs"]) / 1e3, 1), "pct": float(r["Percentage"])}
+                              for r in rows[:top]]}
 
 
 def sq_valu(kernel):
@@ -1089,6 +1115,66 @@ def shim_latency_leg(frames, W, H, local, n=200, warm=20):
                    "ORBextractor::operator() as shipped (operator_ms: no host mvImagePyramid, the default) and "
                    "with the opt-in pinned host copy (operator_ms_host_pyramid, ORBX_HOST_PYRAMID=1); "
                    "stereo Frame = two operator() threads + ComputeStereoMatches on the device outputs")
+    return out
+
+
+def shim_matcher_latency_leg(local, n=100, warm=10, cpu_reps=20):
+    """The drop-in ORBmatcher methods per host call as Tracking and LocalMapping
+    make them: SearchByProjection(F, local map points)
+    (src/Tracking.cc:1277), SearchByProjection(CurrentFrame, LastFrame)
+    (:962), SearchByBoW(KF, F) (:842, 1465), SearchForTriangulation
+    (src/LocalMapping.cc:301) and Fuse (:525, 550), each through the compiled
+    shim on reference-typed Frames / KeyFrames / MapPoints at KITTI sizes
+    (2000 keypoints, 2000-3000 map points; tests/shimscene.py builds the
+    scenes, shim/host/scene.cc --scene-latency times the call alone with the
+    state rebuilt outside the clock), and beside each the single-thread CPU
+    restatement (oracle/) on the same inputs, timed in this process after the
+    timed region (the oracle is the CPU baseline here, never the product)."""
+    import subprocess
+    import tempfile
+    import time
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import shimscene
+    from oracle import oracle as O
+    if not os.path.exists(SHIM_DRIVER):
+        return {"error": f"{SHIM_DRIVER} not built (python __graft_entry__.py builds it)"}
+    calls = [("search_by_projection_local_map", "local_map", "src/Tracking.cc:1277"),
+             ("search_by_projection_last_frame", "last_frame", "src/Tracking.cc:962"),
+             ("search_by_bow_kf_f", "bow", "src/Tracking.cc:842"),
+             ("search_for_triangulation", "triangulation", "src/LocalMapping.cc:301"),
+             ("fuse", "fuse", "src/LocalMapping.cc:525")]
+    out = {}
+    env = dict(os.environ, ORBX_DEVICE=str(local))
+    with tempfile.TemporaryDirectory() as d:
+        for key, builder, site in calls:
+            recs, want = getattr(shimscene, builder)(O, 1)
+            cpu_fn = shimscene.LAST_CPU[0]
+            path = os.path.join(d, key + ".bin")
+            shimscene.write_scene(path, recs)
+            try:
+                r = subprocess.run([SHIM_DRIVER, "--scene-latency", path, str(n), str(warm)], capture_output=True,
+                                   text=True, timeout=300, env=env)
+            except subprocess.TimeoutExpired:
+                out[key] = {"error": "shim driver timed out"}
+                continue
+            if r.returncode != 0:
+                out[key] = {"error": f"rc {r.returncode}: {r.stderr.strip()[-200:]}"}
+                continue
+            g = json.loads(r.stdout.strip().splitlines()[-1])
+            cpu_fn()
+            ts = []
+            for _ in range(cpu_reps):
+                t0 = time.perf_counter()
+                cpu_fn()
+                ts.append((time.perf_counter() - t0) * 1e3)
+            cpu_ms = float(np.median(ts))
+            out[key] = {"site": site, "shim_ms": {"median": round(g["median_ms"], 4), "p99": round(g["p99_ms"], 4)},
+                        "cpu_oracle_1thread_ms": round(cpu_ms, 4),
+                        "cpu_over_shim": round(cpu_ms / g["median_ms"], 2) if g["median_ms"] > 0 else None,
+                        "matches": int(g["matches"]), "matches_expected": int(want[0])}
+    out["what"] = ("host clock per call through the drop-in shim (upload, launch, one stream wait, download; the "
+                   "Frame/KeyFrame state rebuilt outside the clock) vs the single-thread oracle on the same scene "
+                   f"(median of {cpu_reps}; ctypes call overhead included); KITTI-sized synthetic scenes")
     return out
 
 

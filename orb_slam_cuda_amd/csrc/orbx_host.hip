@@ -46,6 +46,7 @@ __global__ __launch_bounds__(256) void copy2d_kernel(uint8_t* __restrict__ d, si
 size_t quadtree_lds_bytes(const ExtractParams& P);
 size_t quadtree_legacy_lds_bytes(const ExtractParams& P);
 size_t quadtree_sorted_lds_bytes(const ExtractParams& P, int big);
+int quadtree_sorted_ownmax(const ExtractParams& P, int big, size_t budget);
 extern const void* quadtree_kernel_ptr(const ExtractParams& P);
 size_t pyr_band_lds_bytes(const ExtractParams& P);
 void blur_tile_dims(int small, int* tw, int* th);
@@ -581,8 +582,6 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
           P.fast_bw_max = std::max(P.fast_bw_max, bw);
           P.fast_bh_max = std::max(P.fast_bh_max, bh);
         }
-        cg.slot_off = slot;
-        slot += cg.cap;
         cg.pitch = l == 0 ? 0 : g.pitch;
         cg.row_off = l == 0 ? cg.r0 : (int)(lvl_off + (long long)cg.r0 * g.pitch);
         cg.fstride = l == 0 ? 0 : (int)g.plane;
@@ -591,6 +590,14 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
       }
     }
     g.ncells = (int)pl.cells.size() - g.cell0;
+    // slot ranges at one stride per level (the largest cell's NMS bound):
+    // cell c's keys start at slot0 + c * stride, so the sorted quadtree
+    // finds them without reading the cell records
+    int stride = 1;
+    for (int c = g.cell0; c < (int)pl.cells.size(); ++c) stride = std::max(stride, (int)pl.cells[c].cap);
+    for (int c = g.cell0; c < (int)pl.cells.size(); ++c) pl.cells[c].slot_off = slot + (c - g.cell0) * stride;
+    g.slot_stride = stride;
+    slot += g.ncells * stride;
     g.nslots = slot - g.slot0;
     maxcells = std::max(maxcells, g.ncells);
     // DistributeOctTree (src/ORBextractor.cc:894-898)
@@ -724,7 +731,10 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     P.kcap_lds = base < budget ? (int)((budget - base) / 6) & ~15 : 0;
     // the sorted path shares the block's LDS (its layout is the legacy one's
     // alternative, not an addition): on when it fits the same budget
-    if (P.qt_sorted && quadtree_sorted_lds_bytes(P, P.qt_big) > budget) P.qt_sorted = 0;
+    if (P.qt_sorted) {
+      P.qt_ownmax = quadtree_sorted_ownmax(P, P.qt_big, budget);
+      if (!P.qt_ownmax || quadtree_sorted_lds_bytes(P, P.qt_big) > budget) P.qt_sorted = 0;
+    }
     // the sorted path's rounds hold two nodes per thread
     if (maxnodes > 2 * (P.qt_big ? 1024 : kQtThreads)) P.qt_sorted = 0;
   }
@@ -739,7 +749,7 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
   if ((rc = pl.rtab_d.alloc(std::max<size_t>(pl.rtab.size(), 1) * sizeof(int2)))) return rc;
   if ((rc = pl.cells_d.alloc(pl.cells.size() * sizeof(CellGeom)))) return rc;
   if ((rc = pl.umax_d.alloc(16 * sizeof(int)))) return rc;
-  if ((rc = pl.slots.alloc((size_t)B * slot * 4 + 4))) return rc;
+  if ((rc = pl.slots.alloc((size_t)B * slot * 4 + 4 + 4 * 96))) return rc;  // + the quadtree's prefetch overrun
   if ((rc = pl.cell_counts.alloc((size_t)B * P.ncells_total * 4))) return rc;
   if ((rc = pl.qkeys.alloc((size_t)B * P.kp_per_frame * 4))) return rc;
   if ((rc = pl.qcounts.alloc((size_t)B * L * 4 + 4 * kMaxLevels))) return rc;  // orient_brief reads kMaxLevels counts per frame

@@ -41,6 +41,7 @@ struct LevelGeom {
   int nCols, nRows, wCell, hCell;
   int cell0, ncells;     // range in the cell table
   int slot0, nslots;     // key-slot range of this level inside a frame's slots
+  int slot_stride;       // cell c of the level: slots slot0 + c * slot_stride .. (+ its cap)
   // DistributeOctTree (src/ORBextractor.cc:889-898)
   int N, nIni, boxW, boxH;
   float hX;
@@ -87,6 +88,7 @@ struct ExtractParams {
   int qt_big;                  // quadtree: node tables past 64 KB of LDS: 1024-thread blocks, a whole CU's LDS each
   int qt_sorted;               // quadtree: the sorted-key path first (levels with code tables, K <= threads x 8, maxnodes <= 2 x threads)
   int qt_tabmax, qt_nbmax;     // largest code-table length (tw + th) and bin count of any level
+  int qt_ownmax;               // sorted path: most keys of a level (spill mode past threads x 8: keys in global scratch)
   int fast_rh_max;             // largest FAST cell ROI height
   int fast_bw_max, fast_bh_max;  // largest FAST detection band
   int pattern_upstream;

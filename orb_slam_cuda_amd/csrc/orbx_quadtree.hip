@@ -120,30 +120,34 @@ enum { ST_DONE = 2, ST_FALLBACK = 3 };
 
 template <int NT>
 struct QtSortedLds {
-  int *coff, *soff;
+  int* coff;
   uint32_t *xs, *S32, *bkey;
-  uint16_t* bidx;
+  uint16_t* bidx;  // the keys' cells after the count scan; in register mode the binned keys' original indices
+  int* nodeof;     // spill mode, after the gather: per bin the kept node that holds it (aliases bidx)
   int2 *recA, *recB;
   int *rank, *spos;
   uint32_t* candk;
   int* candn;
   int* s_wave;
-  int* part;     // block scans: two alternating buffers of 4 x 16 wave partials
+  int* part;     // block scans: two alternating buffers of 4 x 16 wave partials, then two of 16 wave maxima
   uint32_t* bm;  // sorted rounds: two alternating [64 sizes][bmw] bitmaps of candidate indices
   int* gw;       // ... per wave: candidates of size > s, s < 64
   uint32_t* bigk;  // ... keys of the candidates of size >= 64 (kQtBig)
   int bmw;       // words per bitmap row (maxnodes / 32)
-  size_t bytes;
+  size_t fixed, bytes;
+  // the key region last: register mode bidx + bkey (6 B per key, NT x kQtKpt
+  // keys), spill mode bidx for qt_ownmax keys, then the bins' node map
+  __host__ __device__ static size_t region(const ExtractParams& P) {
+    const size_t a = 6ull * NT * kQtKpt, b = 2ull * P.qt_ownmax, c = 4ull * P.qt_nbmax;
+    return a > b ? (a > c ? a : c) : (b > c ? b : c);
+  }
   __host__ __device__ QtSortedLds(const ExtractParams& P, unsigned char* base) {
     unsigned char* p = base + kQtHeader;
     auto take = [&](size_t b) { unsigned char* r = p; p += (b + 15) & ~(size_t)15; return r; };
     const size_t MN = P.maxnodes;
     coff = (int*)take(4ull * (P.max_cells_level + 1));
-    soff = (int*)take(4ull * (P.max_cells_level + 1));
     xs = (uint32_t*)take(4ull * P.qt_tabmax);
     S32 = (uint32_t*)take(4ull * (P.qt_nbmax / 2 + 1));
-    bkey = (uint32_t*)take(4ull * NT * kQtKpt);
-    bidx = (uint16_t*)take(2ull * NT * kQtKpt);
     recA = (int2*)take(8 * MN);
     recB = (int2*)take(8 * MN);
     rank = (int*)take(4 * MN);
@@ -151,11 +155,16 @@ struct QtSortedLds {
     candk = (uint32_t*)take(4 * MN);
     candn = (int*)take(4 * MN);
     s_wave = (int*)take(4 * 64);
-    part = (int*)take(4 * 2 * 64);
+    part = (int*)take(4 * (2 * 64 + 2 * 16));
     bmw = (int)((MN + 31) / 32);
     bm = (uint32_t*)take(4ull * 2 * 64 * bmw);
     gw = (int*)take(4ull * NT);
     bigk = (uint32_t*)take(4ull * kQtBig);
+    fixed = (size_t)(p - base);
+    unsigned char* kb = take(region(P));
+    bidx = (uint16_t*)kb;
+    bkey = (uint32_t*)(kb + 2ull * NT * kQtKpt);
+    nodeof = (int*)kb;
     bytes = (size_t)(p - base);
   }
 };
@@ -166,9 +175,9 @@ struct QtSortedLds {
 template <int NT, bool PROF>
 __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int* __restrict__ cell_counts,
                                const uint32_t* __restrict__ slots, const CellGeom* __restrict__ cells,
-                               const uint32_t* __restrict__ qtab, uint32_t* __restrict__ qkeys,
-                               int* __restrict__ qcounts, int* __restrict__ qties, int* err, int* dbg,
-                               unsigned char* smem, const unsigned long long t_begin) {
+                               const uint32_t* __restrict__ qtab, uint32_t* __restrict__ qscratch,
+                               uint32_t* __restrict__ qkeys, int* __restrict__ qcounts, int* __restrict__ qties,
+                               int* err, int* dbg, unsigned char* smem, const unsigned long long t_begin) {
   using namespace qts;
   constexpr int NW = NT / 64;
   constexpr int kIt = 2;  // nodes (and candidate ranks) per thread: the plan keeps maxnodes <= 2 NT
@@ -184,19 +193,19 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
   const uint16_t* S = (const uint16_t*)M.S32;
   unsigned long long t_scan = 0, t_own = 0, t_gather = 0, t_bins = 0, t_scatter = 0, t_rounds = 0;
 
-  // ---- cell counts, slot offsets and the level's code tables (loads in
-  // flight together); bins cleared
+  // ---- cell counts and the level's code tables (loads in flight
+  // together); bins cleared. A thread takes the cells [cb, ce) (one at KITTI
+  // sizes). (Touching each cell's first slot lines here, so that the gather
+  // would hit L2, was measured: the untargeted lines cost more bandwidth than
+  // the gather's round trip)
+  const int stride = g.slot_stride;
+  const uint32_t* fslots = slots + (long long)f * P.slots_per_frame + g.slot0;
+  const int cper = (ncells + NT - 1) / NT, cb = min(tid * cper, ncells), ce = min(cb + cper, ncells);
   {
     const int* cntp = cell_counts + (long long)f * P.ncells_total + g.cell0;
     const uint32_t* tab = qtab + g.qt_tab;
     const int nt = tw + th;
-    for (int c0 = 0; c0 < ncells; c0 += NT) {
-      const int c = c0 + tid;
-      if (c < ncells) {
-        M.coff[c] = cntp[c];
-        M.soff[c] = cells[g.cell0 + c].slot_off;
-      }
-    }
+    for (int c = cb; c < ce; ++c) M.coff[c] = cntp[c];
     for (int i0 = 0; i0 < nt; i0 += 4 * NT) {
       uint32_t v[4];
 #pragma unroll
@@ -209,37 +218,85 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
     for (int i = tid; i < 2 * 64 * M.bmw; i += NT) M.bm[i] = 0u;
     if (tid < 4) s_var[V_TRANK + tid] = 0;  // V_TRANK, -, V_BIG (two)
   }
-  lds_sync();
-  const int K = block_scan_excl<NT, true>(M.coff, ncells, M.s_wave);
-  if (PROF) t_scan = __builtin_amdgcn_s_memtime();
-  if (K > NT * kQtKpt) return false;  // uniform: every thread holds K
-
-  // ---- key -> cell (cells row-major, FAST order inside: the reference's key order)
-  for (int c = tid; c < ncells; c += NT) {
-    const int b = M.coff[c], e = c + 1 < ncells ? M.coff[c + 1] : K;
-    for (int i = b; i < e; ++i) M.bidx[i] = (uint16_t)c;
+  // ---- exclusive scan of the counts; the scan's write-back also lists each
+  // key's cell (cells row-major, FAST order inside: the reference's key order)
+  int K;
+  {
+    int sum = 0;
+    for (int c = cb; c < ce; ++c) sum += M.coff[c];
+    const int x = wave_incl_scan_dpp(sum);
+    if (lane == 63) M.s_wave[wv] = x;
+    lds_sync();
+    int run = x - sum;
+    K = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int v = M.s_wave[i];
+      if (i < wv) run += v;
+      K += v;
+    }
+    if (K <= P.qt_ownmax)
+      for (int c = cb; c < ce; ++c) {
+        const int n = M.coff[c];
+        M.coff[c] = run;
+        for (int i = 0; i < n; ++i) M.bidx[run + i] = (uint16_t)c;
+        run += n;
+      }
   }
+  if (PROF) t_scan = __builtin_amdgcn_s_memtime();
+  if (K > P.qt_ownmax) return false;  // uniform: every thread holds K
+  // register mode: a thread's keys stay in registers from the gather to the
+  // scatter; spill mode (more keys): the keys go to a compact global copy
+  // (this level's slot range of qscratch), the bins are counted but not
+  // scattered, and each key finds its kept node through a per-bin node map
+  const bool spill = K > NT * kQtKpt;
+  uint32_t* cs = qscratch + (long long)f * P.slots_per_frame + g.slot0;
   lds_sync();
   if (PROF) t_own = __builtin_amdgcn_s_memtime();
 
   // ---- gather (one memory round trip for all keys), code, bin, rank in bin.
   // Branch-free: keys past K read key K - 1's slot and are dropped later.
-  const uint32_t* fslots = slots + (long long)f * P.slots_per_frame;
   uint32_t kv[kQtKpt];
   int kb[kQtKpt], kr[kQtKpt];
-  if (K > 0) {
-    int kc[kQtKpt], sl[kQtKpt];
+  if (spill) {
+    for (int k0 = 0; k0 < K; k0 += 4 * NT) {
+      uint32_t kk[4];
 #pragma unroll
-    for (int u = 0; u < kQtKpt; ++u) kc[u] = M.bidx[min(tid + u * NT, K - 1)];
+      for (int u = 0; u < 4; ++u) {
+        const int kc = min(k0 + u * NT + tid, K - 1), c = M.bidx[kc];
+        kk[u] = fslots[c * stride + kc - M.coff[c]];
+      }
 #pragma unroll
-    for (int u = 0; u < kQtKpt; ++u) sl[u] = M.soff[kc[u]] + min(tid + u * NT, K - 1) - M.coff[kc[u]];
-#pragma unroll
-    for (int u = 0; u < kQtKpt; ++u) kv[u] = fslots[sl[u]];
-#pragma unroll
-    for (int u = 0; u < kQtKpt; ++u)
-      kb[u] = (int)((M.xs[min(key_x(kv[u]), tw - 1)] | ys[min(key_y(kv[u]), th - 1)]) >> shB);
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * NT + tid;
+        if (k < K) {
+          const int bn = (int)((M.xs[min(key_x(kk[u]), tw - 1)] | ys[min(key_y(kk[u]), th - 1)]) >> shB);
+          atomicAdd(&M.S32[bn >> 1], 1u << ((bn & 1) << 4));
+          cs[k] = kk[u];
+        }
+      }
+    }
+  } else if (K > 0) {
+    int sl[kQtKpt];
 #pragma unroll
     for (int u = 0; u < kQtKpt; ++u) {
+      if (u * NT >= K) break;  // wave-uniform
+      const int k = min(tid + u * NT, K - 1), c = M.bidx[k];
+      sl[u] = c * stride + k - M.coff[c];
+    }
+#pragma unroll
+    for (int u = 0; u < kQtKpt; ++u) {
+      if (u * NT >= K) break;
+      kv[u] = fslots[sl[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < kQtKpt; ++u) {
+      if (u * NT >= K) break;
+      kb[u] = (int)((M.xs[min(key_x(kv[u]), tw - 1)] | ys[min(key_y(kv[u]), th - 1)]) >> shB);
+    }
+#pragma unroll
+    for (int u = 0; u < kQtKpt; ++u) {
+      if (u * NT >= K) break;
       kr[u] = 0;
       if (tid + u * NT < K) {
         const uint32_t sh = (uint32_t)(kb[u] & 1) << 4;
@@ -283,6 +340,7 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
   // ---- scatter: every depth <= Dh node is now a contiguous range of bkey
 #pragma unroll
   for (int u = 0; u < kQtKpt; ++u) {
+    if (spill || u * NT >= K) break;  // wave-uniform
     const int k = tid + u * NT;
     if (k < K) {
       const int pos = (int)S[kb[u]] + kr[u];
@@ -370,27 +428,60 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
     }
   };
 
+  // roots: nIni columns (src/ORBextractor.cc:903-936), empty ones erased,
+  // and the first breadth round over them folded in when it splits every
+  // multi-key root (it does unless N is about nIni): every wave computes
+  // them on its lanes (lane = root column), wave 0 writes them
+  bool sorted = false, finished = false;
+  int state = ST_DONE, rounds = 0, srounds = 0, tie_ev = 0, tie_nodes = 0, tie_keys = 0, ncand = 0, pbm = 0;
   int size;
   {
-    // roots: nIni columns (src/ORBextractor.cc:903-936), empty ones erased;
-    // every wave counts them, wave 0 writes them
-    int b = 0, e = 0;
+    int B[5] = {0, 0, 0, 0, 0};
     if (lane < nIni) {
-      b = S[lane << (2 * Dh)];
-      e = S[(lane + 1) << (2 * Dh)];
+      B[0] = S[lane << (2 * Dh)];
+      B[4] = S[(lane + 1) << (2 * Dh)];
     }
-    const uint64_t mk = __ballot(e > b);
-    size = __popcll(mk);
-    if (wv == 0 && e > b) {
-      nA[mbcnt64(mk)] = mkrec(b, e, lane, 0, 0);
-      M.rank[mbcnt64(mk)] = -1;
+    const int2 r = mkrec(B[0], B[4], lane, 0, 0);
+    bounds(r, B);
+    const uint64_t mk = __ballot(B[4] > B[0]);
+    const int size0 = __popcll(mk), pos = mbcnt64(mk);
+    const int v = rcnt(r) > 1 ? ((nonempty5(B) - 1) << 16) | 1 : 0, nm = v ? multi5(B) : 0;
+    const int x = wave_incl_scan_dpp(v), cx = wave_incl_scan_dpp(nm);
+    const int tot = __builtin_amdgcn_readlane(x, 63), nnext = __builtin_amdgcn_readlane(cx, 63);
+    const int last = wave_max_dpp(v ? (lane << 2) | (nonempty5(B) - 1) : -1);
+    const int Ctot = tot & 0xFFFF, Etot = (int)((uint32_t)tot >> 16);
+    if (Ctot > 0 && size0 + Etot - (last & 3) < N) {
+      const int m = Ctot, T = Etot + Ctot, run = x - v, E = (int)((uint32_t)run >> 16), C = run & 0xFFFF;
+      int cpos = cx - nm;
+      if (wv == 0 && B[4] > B[0]) {
+        if (v) {
+          place_split(r, B, C, T - (E + C + nonempty5(B)), &cpos);
+        } else {
+          nB[T + pos - min(C, m)] = r;
+          M.rank[T + pos - min(C, m)] = -1;
+        }
+      }
+      {
+        int2* t = nA;
+        nA = nB;
+        nB = t;
+      }
+      size = T + (size0 - m);
+      ncand = nnext;
+      rounds = 1;
+      finished = size >= N || size == size0;
+      sorted = !finished && size + 3 * nnext > N;
+    } else {
+      size = size0;
+      if (wv == 0 && B[4] > B[0]) {
+        nA[pos] = r;
+        M.rank[pos] = -1;
+      }
     }
   }
-  bool sorted = false;
-  int state = ST_DONE, rounds = 0, srounds = 0, tie_ev = 0, tie_nodes = 0, tie_keys = 0, ncand = 0, pbm = 0;
   unsigned long long pr_b = 0, pr_s = 0;  // PROF: clocks of the breadth rounds, of the sorted rounds
   lds_sync();
-  for (;;) {
+  while (!finished) {
     const unsigned long long tr0 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     const bool was_sorted = sorted;
     if (rounds == 64) {
@@ -407,45 +498,89 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
       int2 r[kIt];
       int B[kIt][5];
       int v[kIt];
-      int s1[1] = {0};
+      // one scan: the packed values, the multi-key children and the deep
+      // candidates as if every candidate were split, and (max) the last
+      // candidate's children - 1. Every round but a breadth phase's last one
+      // splits all its candidates, and that is decided from the totals alone
+      // (size + E of the last candidate < N); the cut-off round takes a
+      // second scan
+      int s3[3] = {0, 0, 0}, last = -1;
 #pragma unroll
       for (int i = 0; i < kIt; ++i) {
+        if (i >= per) break;  // wave-uniform
         r[i] = nb + i < ne ? nA[nb + i] : make_int2(0, 0);
         bounds(r[i], B[i]);
         v[i] = rcnt(r[i]) > 1 ? ((nonempty5(B[i]) - 1) << 16) | 1 : 0;
-        s1[0] += v[i];
-      }
-      int ex1[1], tot1[1];
-      bscan(s1, ex1, tot1);
-      // split decisions; totals: candidates of the next round (and this
-      // thread's first slot), splits, children of the split nodes, deep
-      int run = ex1[0];
-      int s4[4] = {0, 0, 0, 0}, rn[kIt];
-#pragma unroll
-      for (int i = 0; i < kIt; ++i) {
-        rn[i] = run;
-        if (v[i] && size + (int)((uint32_t)run >> 16) < N) {
-          s4[0] += multi5(B[i]);
-          s4[1] += 1;
-          s4[2] += nonempty5(B[i]);
-          s4[3] |= rdepth(r[i]) >= Dh;  // its children are not in the bins
-        } else {
-          v[i] = -v[i] - 1;  // kept (the scan value is still needed below)
+        s3[0] += v[i];
+        if (v[i]) {
+          s3[1] += multi5(B[i]);
+          s3[2] += rdepth(r[i]) >= Dh;  // its children are not in the bins
+          last = ((nb + i) << 2) | (nonempty5(B[i]) - 1);
         }
-        run += v[i] >= 0 ? v[i] : -v[i] - 1;
       }
-      int ex4[4], tot4[4];
-      bscan(s4, ex4, tot4);
-      nnext = tot4[0];
-      m = tot4[1];
-      T = tot4[2];
-      if (tot4[3]) {  // a node to split below the bins' depth: the legacy rounds take the level
-        state = ST_FALLBACK;
-        break;
+      int ex3[3], tot3[3];
+      const int lmax = wave_max_dpp(last);
+      if (lane == 63) M.part[128 + pb * 16 + wv] = lmax;
+      const int pbl = pb;
+      bscan(s3, ex3, tot3);
+      int lastall = -1;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) lastall = max(lastall, M.part[128 + pbl * 16 + i]);
+      const int Ctot = tot3[0] & 0xFFFF, Etot = (int)((uint32_t)tot3[0] >> 16);
+      int rn[kIt];
+      int cpos = 0;
+      if (Ctot == 0 || size + Etot - (lastall & 3) < N) {
+        // a full round: every candidate splits
+        if (tot3[2]) {  // a node to split below the bins' depth: the legacy rounds take the level
+          state = ST_FALLBACK;
+          break;
+        }
+        nnext = tot3[1];
+        m = Ctot;
+        T = Etot + Ctot;
+        cpos = ex3[1];
+        int run = ex3[0];
+#pragma unroll
+        for (int i = 0; i < kIt; ++i) {
+          if (i >= per) break;  // wave-uniform
+          rn[i] = run;
+          run += v[i];
+          if (!v[i]) v[i] = -1;  // kept
+        }
+      } else {
+        // the cut-off round: split decisions; totals: candidates of the next
+        // round (and this thread's first slot), splits, children of the
+        // split nodes, deep
+        int run = ex3[0];
+        int s4[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < kIt; ++i) {
+          if (i >= per) break;  // wave-uniform
+          rn[i] = run;
+          if (v[i] && size + (int)((uint32_t)run >> 16) < N) {
+            s4[0] += multi5(B[i]);
+            s4[1] += 1;
+            s4[2] += nonempty5(B[i]);
+            s4[3] |= rdepth(r[i]) >= Dh;
+          } else {
+            v[i] = -v[i] - 1;  // kept (the scan value is still needed below)
+          }
+          run += v[i] >= 0 ? v[i] : -v[i] - 1;
+        }
+        int ex4[4], tot4[4];
+        bscan(s4, ex4, tot4);
+        nnext = tot4[0];
+        m = tot4[1];
+        T = tot4[2];
+        if (tot4[3]) {
+          state = ST_FALLBACK;
+          break;
+        }
+        cpos = ex4[0];
       }
-      int cpos = ex4[0];
 #pragma unroll
       for (int i = 0; i < kIt; ++i) {
+        if (i >= per) break;  // wave-uniform
         const int n = nb + i;
         if (n < ne) {
           const int E = (int)((uint32_t)rn[i] >> 16), C = rn[i] & 0xFFFF;
@@ -520,6 +655,7 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
       int s1[1] = {0};
 #pragma unroll
       for (int i = 0; i < kIt; ++i) {
+        if (i >= cper) break;  // wave-uniform
         r[i] = cb + i < ce ? nA[M.spos[cb + i]] : make_int2(0, 0);
         bounds(r[i], B[i]);
         s1[0] += cb + i < ce ? nonempty5(B[i]) - 1 : 0;
@@ -530,6 +666,7 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
       int s4[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int i = 0; i < kIt; ++i) {
+        if (i >= cper) break;  // wave-uniform
         rn[i] = run;
         if (cb + i < ce) {
           if (size + run < N) {
@@ -564,10 +701,11 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
             s3[1] += cb + i < m ? nonempty5(B[i]) : 1;
           }
       }
-      bool kp[kIt];
+      bool kp[kIt] = {};
       int2 k2[kIt];
 #pragma unroll
       for (int i = 0; i < kIt; ++i) {
+        if (i >= per) break;  // wave-uniform
         const int n = nb + i;
         const int j = n < ne ? M.rank[n] : 0;
         kp[i] = n < ne && !(j >= 0 && j < m);
@@ -584,13 +722,14 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
       // children blocks of the split ranks, then the kept nodes in list order
 #pragma unroll
       for (int i = 0; i < kIt; ++i) {
+        if (i >= cper) break;  // wave-uniform
         const int j = cb + i;
         if (j < ce && j < m) place_split(r[i], B[i], j, T - (rn[i] + j + nonempty5(B[i])), &cpos);
       }
       int kpos = T + ex3[2];
 #pragma unroll
       for (int i = 0; i < kIt; ++i)
-        if (kp[i]) {
+        if (i < per && kp[i]) {
           nB[kpos] = k2[i];
           M.rank[kpos] = -1;
           ++kpos;
@@ -621,7 +760,75 @@ __device__ __forceinline__ bool qt_sorted_path(const ExtractParams& P, const int
   // ---- keep the best key per node: max FAST score, first original index on ties
   const int2* fin = nA;
   uint32_t* out = qkeys + (long long)f * P.kp_per_frame + g.kbase;
-  for (int n = tid; n < size && n < g.kcap; n += NT) {
+  if (spill) {
+    // every bin holding keys lies in exactly one kept node: mark each node at
+    // its first bin, fill forward (max scan of (bin + 1) << 16 | node), then
+    // every key takes the max of (score, first index) into its node
+    __syncthreads();  // the compact keys (global) of the gather, written by other threads
+    int* nodeof = M.nodeof;
+    int* best = M.rank;
+    for (int i = tid; i < NB; i += NT) nodeof[i] = 0;
+    for (int n = tid; n < size; n += NT) best[n] = 0;
+    lds_sync();
+    for (int n = tid; n < size; n += NT) {
+      const int2 r = fin[n];
+      const int lo = rpre(r) << (2 * (Dh - rdepth(r)));
+      nodeof[lo] = ((lo + 1) << 16) | n;
+    }
+    lds_sync();
+    {
+      const int per = NB / NT;  // 4 .. 16
+      int w[16], mx = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (i < per) {
+          w[i] = nodeof[tid * per + i];
+          mx = max(mx, w[i]);
+        }
+      int x = mx;  // inclusive max over the lanes
+      x = max(x, dpp_i<kDppShr1>(0, x));
+      x = max(x, dpp_i<kDppShr2>(0, x));
+      x = max(x, dpp_i<kDppShr4>(0, x));
+      x = max(x, dpp_i<kDppShr8>(0, x));
+      x = max(x, dpp_i<kDppBcast15, 0xa>(0, x));
+      x = max(x, dpp_i<kDppBcast31, 0xc>(0, x));
+      if (lane == 63) M.s_wave[32 + wv] = x;
+      const int prev = __shfl_up(x, 1);  // this lane's carry: the lanes before it
+      lds_sync();
+      int run = lane ? prev : 0;
+#pragma unroll
+      for (int i = 0; i < NW; ++i)
+        if (i < wv) run = max(run, M.s_wave[32 + i]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (i < per) {
+          run = max(run, w[i]);
+          nodeof[tid * per + i] = run;
+        }
+    }
+    lds_sync();
+    for (int k0 = 0; k0 < K; k0 += 4 * NT) {
+      uint32_t kk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) kk[u] = cs[min(k0 + u * NT + tid, K - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * NT + tid;
+        if (k < K) {
+          const int bn = (int)((M.xs[min(key_x(kk[u]), tw - 1)] | ys[min(key_y(kk[u]), th - 1)]) >> shB);
+          const int n = nodeof[bn] & 0xFFFF;
+          atomicMax(&best[n], ((key_score(kk[u]) + 1) << 16) | (0xFFFF - k));
+        }
+      }
+    }
+    lds_sync();
+    for (int n = tid; n < size && n < g.kcap; n += NT) {
+      const int v = best[n];
+      if (!v) atomicOr(err, 8);  // a node without keys: a broken list
+      else out[n] = cs[0xFFFF - (v & 0xFFFF)];
+    }
+  }
+  for (int n = tid; n < size && n < g.kcap && !spill; n += NT) {
     const int2 r = fin[n];
     const int b = rb(r), e = re(r);
     if (e <= b) {
@@ -1489,7 +1696,8 @@ __global__ __launch_bounds__(NT, ORBX_QT_MINW) void quadtree_kernel(ExtractParam
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const unsigned long long t_begin = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
   if (P.qt_sorted && P.lv[blockIdx.x].qt_tab >= 0 &&
-      qt_sorted_path<NT, PROF>(P, cell_counts, slots, cells, qtab, qkeys, qcounts, qties, err, dbg, smem, t_begin))
+      qt_sorted_path<NT, PROF>(P, cell_counts, slots, cells, qtab, qscratch, qkeys, qcounts, qties, err, dbg, smem,
+                               t_begin))
     return;
   qt_legacy<NT, PROF>(P, cell_counts, slots, cells, qscratch, qnscratch, qkeys, qcounts, qties, err, dbg, smem, t_begin);
 }
@@ -1505,6 +1713,15 @@ size_t quadtree_legacy_lds_bytes(const ExtractParams& P) {
 
 size_t quadtree_sorted_lds_bytes(const ExtractParams& P, int big) {
   return big ? QtSortedLds<1024>(P, nullptr).bytes : QtSortedLds<kQtThreads>(P, nullptr).bytes;
+}
+// the sorted path's largest spill-mode key count for an LDS budget (0: the
+// register mode's region does not fit)
+int quadtree_sorted_ownmax(const ExtractParams& P, int big, size_t budget) {
+  const size_t fixed = big ? QtSortedLds<1024>(P, nullptr).fixed : QtSortedLds<kQtThreads>(P, nullptr).fixed;
+  const size_t nt = big ? 1024 : kQtThreads;
+  const size_t need = std::max<size_t>(6 * nt * kQtKpt, 4ull * P.qt_nbmax) + 16;
+  if (fixed + need > budget) return 0;
+  return (int)std::min<size_t>(32767, std::max<size_t>(nt * kQtKpt, (budget - fixed - 16) / 2) & ~(size_t)7);
 }
 
 size_t quadtree_lds_bytes(const ExtractParams& P) {

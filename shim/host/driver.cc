@@ -49,6 +49,7 @@ static std::vector<int> ids(const std::vector<MapPoint*>& v) {
 }
 
 int run_scene(const std::string& in, const std::string& out);  // scene.cc
+int run_scene_latency(const std::string& in, int ncalls, int warm);  // scene.cc
 
 // The stereo Frame constructor (src/Frame.cc:60-128) over NPAIRS stereo
 // pairs: two extractors, left and right extraction on two std::threads
@@ -263,6 +264,7 @@ int main(int argc, char** argv) {
   }
   try {
     if (argc == 4 && std::string(argv[1]) == "--scene") return run_scene(argv[2], argv[3]);
+    if (argc == 5 && std::string(argv[1]) == "--scene-latency") return run_scene_latency(argv[2], atoi(argv[3]), atoi(argv[4]));
     if (argc == 10 && std::string(argv[1]) == "--latency")
       return run_latency(argv[2], argv[3], argv[4], atoi(argv[5]), atoi(argv[6]), atoi(argv[7]), atoi(argv[8]),
                          atoi(argv[9]));

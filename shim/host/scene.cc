@@ -11,8 +11,13 @@
 //   op 6 Fuse(pKF, Scw, vpPoints, th, vpReplacePoint)     LoopClosing.cc:654
 //   op 7 SearchBySim3(pKF1, pKF2, vpMatches12, ...)        LoopClosing.cc:362
 //   op 8 SearchForTriangulation(pKF1, pKF2, F12, ...)      LocalMapping.cc:301
+//   op 9 SearchByBoW(pKF, F, vpMapPointMatches)            Tracking.cc:842, 1465
+// --scene-latency: the same scene rebuilt per call, only the method call on
+// the host clock (median / p99 over the calls after the warm ones).
 // Scene file: records of [u32 name length][name][u32 dtype 0 u8 / 1 i32 /
 // 2 f32][u32 count][count elements].
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -161,6 +166,13 @@ std::unique_ptr<Frame> frame(const Scene& s, const std::string& X, const std::ve
     const auto m = s.vec<int>(X + "_mps");
     for (int i = 0; i < F->N; ++i) F->mvpMapPoints[i] = ptr_of(pool, m[i]);
   }
+  if (s.has(X + "_fv_nodes")) {
+    const auto nodes = s.vec<int>(X + "_fv_nodes");
+    const auto off = s.vec<int>(X + "_fv_off");
+    const auto idx = s.vec<int>(X + "_fv_idx");
+    for (size_t j = 0; j < nodes.size(); ++j)
+      F->mFeatVec[(unsigned)nodes[j]] = std::vector<unsigned>(idx.begin() + off[j], idx.begin() + off[j + 1]);
+  }
   F->mvbOutlier.assign(F->N, false);
   if (s.has(X + "_outlier")) {
     const auto o = s.vec<uint8_t>(X + "_outlier");
@@ -230,18 +242,24 @@ void write_ints(const std::string& path, const std::vector<int>& v) {
 }
 }  // namespace
 
-// Returns 0 on success; results in OUT as int32 arrays (see each op).
-int run_scene(const std::string& in, const std::string& out) {
-  const Scene s = load(in);
+// One method call on the scene's state (built here), its results as int32
+// arrays (see each op) and its host time in *ms (the call alone).
+static void run_op(const Scene& s, std::vector<int>& res, double* ms) {
   const int op = s.i("op");
   auto pool = map_points(s);
   ORBmatcher matcher(s.has("nnratio") ? s.f("nnratio") : 0.6f, s.has("check_ori") ? s.i("check_ori") != 0 : true);
-  std::vector<int> res;
+  using clk = std::chrono::steady_clock;
+  clk::time_point t0;
+  auto tic = [&]() { t0 = clk::now(); };
+  auto toc = [&]() { *ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count(); };
   switch (op) {
     case 1: {  // -> [n, F.mvpMapPoints...]
       auto F = frame(s, "A", pool);
       set_nobs(s, pool);
-      const int n = matcher.SearchByProjection(*F, pointers(s, "vp", pool), s.f("th"));
+      const std::vector<MapPoint*> vp = pointers(s, "vp", pool);
+      tic();
+      const int n = matcher.SearchByProjection(*F, vp, s.f("th"));
+      toc();
       res.push_back(n);
       for (MapPoint* p : F->mvpMapPoints) res.push_back(id_of(p));
       break;
@@ -250,7 +268,9 @@ int run_scene(const std::string& in, const std::string& out) {
       auto Last = frame(s, "B", pool);
       auto Cur = frame(s, "A", pool);  // A last: the Frame statics are the current frame's
       set_nobs(s, pool);
+      tic();
       const int n = matcher.SearchByProjection(*Cur, *Last, s.f("th"), s.i("mono") != 0);
+      toc();
       res.push_back(n);
       for (MapPoint* p : Cur->mvpMapPoints) res.push_back(id_of(p));
       break;
@@ -261,7 +281,9 @@ int run_scene(const std::string& in, const std::string& out) {
       set_nobs(s, pool);
       std::set<MapPoint*> found;
       for (MapPoint* p : pointers(s, "already", pool)) found.insert(p);
+      tic();
       const int n = matcher.SearchByProjection(*Cur, K.get(), found, s.f("th"), s.i("orb_dist"));
+      toc();
       res.push_back(n);
       for (MapPoint* p : Cur->mvpMapPoints) res.push_back(id_of(p));
       break;
@@ -270,7 +292,11 @@ int run_scene(const std::string& in, const std::string& out) {
       auto K = keyframe(s, "A", pool);
       set_nobs(s, pool);
       std::vector<MapPoint*> matched = pointers(s, "matched", pool);
-      const int n = matcher.SearchByProjection(K.get(), pose4(s, "Scw"), pointers(s, "vp", pool), matched, s.i("thi"));
+      const cv::Mat Scw = pose4(s, "Scw");
+      const std::vector<MapPoint*> vp = pointers(s, "vp", pool);
+      tic();
+      const int n = matcher.SearchByProjection(K.get(), Scw, vp, matched, s.i("thi"));
+      toc();
       res.push_back(n);
       for (MapPoint* p : matched) res.push_back(id_of(p));
       break;
@@ -279,7 +305,10 @@ int run_scene(const std::string& in, const std::string& out) {
       auto K = keyframe(s, "A", pool);
       observe(K.get(), s, pool);
       set_nobs(s, pool);
-      const int n = matcher.Fuse(K.get(), pointers(s, "vp", pool), s.f("th"));
+      const std::vector<MapPoint*> vp = pointers(s, "vp", pool);
+      tic();
+      const int n = matcher.Fuse(K.get(), vp, s.f("th"));
+      toc();
       res.push_back(n);
       for (MapPoint* p : K->mvpMapPoints) res.push_back(id_of(p));
       for (auto& p : pool) res.push_back(p->isBad() ? 1 : 0);
@@ -292,7 +321,10 @@ int run_scene(const std::string& in, const std::string& out) {
       set_nobs(s, pool);
       const std::vector<MapPoint*> vp = pointers(s, "vp", pool);
       std::vector<MapPoint*> replace(vp.size(), nullptr);
-      const int n = matcher.Fuse(K.get(), pose4(s, "Scw"), vp, s.f("th"), replace);
+      const cv::Mat Scw = pose4(s, "Scw");
+      tic();
+      const int n = matcher.Fuse(K.get(), Scw, vp, s.f("th"), replace);
+      toc();
       res.push_back(n);
       for (MapPoint* p : K->mvpMapPoints) res.push_back(id_of(p));
       for (MapPoint* p : replace) res.push_back(id_of(p));
@@ -310,7 +342,9 @@ int run_scene(const std::string& in, const std::string& out) {
       for (int k = 0; k < 9; ++k) R12.at<float>(k / 3, k % 3) = R[k];
       for (int k = 0; k < 3; ++k) t12.at<float>(k) = t[k];
       const float s12 = s.f("s12");
+      tic();
       const int n = matcher.SearchBySim3(K1.get(), K2.get(), m12, s12, R12, t12, s.f("th"));
+      toc();
       res.push_back(n);
       for (MapPoint* p : m12) res.push_back(id_of(p));
       break;
@@ -322,7 +356,9 @@ int run_scene(const std::string& in, const std::string& out) {
       cv::Mat F12(3, 3, CV_32F);
       for (int k = 0; k < 9; ++k) F12.at<float>(k / 3, k % 3) = Fv[k];
       std::vector<std::pair<size_t, size_t>> pairs;
+      tic();
       const int n = matcher.SearchForTriangulation(K1.get(), K2.get(), F12, pairs, s.i("only_stereo") != 0);
+      toc();
       res.push_back(n);
       for (auto& pr : pairs) {
         res.push_back((int)pr.first);
@@ -330,9 +366,48 @@ int run_scene(const std::string& in, const std::string& out) {
       }
       break;
     }
+    case 9: {  // -> [n, vpMapPointMatches...]
+      auto K = keyframe(s, "B", pool);
+      auto F = frame(s, "A", pool);
+      std::vector<MapPoint*> matches;
+      tic();
+      const int n = matcher.SearchByBoW(K.get(), *F, matches);
+      toc();
+      res.push_back(n);
+      for (MapPoint* p : matches) res.push_back(id_of(p));
+      break;
+    }
     default:
       throw std::runtime_error("unknown scene op " + std::to_string(op));
   }
+}
+
+// Returns 0 on success; results in OUT as int32 arrays (see each op).
+int run_scene(const std::string& in, const std::string& out) {
+  const Scene s = load(in);
+  std::vector<int> res;
+  double ms = 0;
+  run_op(s, res, &ms);
   write_ints(out, res);
+  return 0;
+}
+
+// Per-call host time of the scene's method (the state rebuilt before every
+// call, outside the clock): one JSON object on stdout.
+int run_scene_latency(const std::string& in, int ncalls, int warm) {
+  const Scene s = load(in);
+  std::vector<double> t;
+  int n = 0;
+  for (int i = 0; i < warm + ncalls; ++i) {
+    std::vector<int> res;
+    double ms = 0;
+    run_op(s, res, &ms);
+    if (i >= warm) t.push_back(ms);
+    n = res.empty() ? 0 : res[0];
+  }
+  std::sort(t.begin(), t.end());
+  const double med = t[t.size() / 2], p99 = t[std::min(t.size() - 1, (size_t)(0.99 * (double)t.size()))];
+  printf("{\"op\": %d, \"calls\": %d, \"median_ms\": %.4f, \"p99_ms\": %.4f, \"matches\": %d}\n", s.i("op"), ncalls,
+         med, p99, n);
   return 0;
 }

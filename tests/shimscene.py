@@ -11,7 +11,17 @@ from posecase import CX, CY, FX, FY, MB, fuse_case, keyframe_case, last_frame_ca
     triangulation_case
 from projcase import projection_case
 
-OPS = dict(local_map=1, last_frame=2, keyframe=3, sim3=4, fuse=5, fuse_sim3=6, sim3_match=7, triangulation=8)
+OPS = dict(local_map=1, last_frame=2, keyframe=3, sim3=4, fuse=5, fuse_sim3=6, sim3_match=7, triangulation=8,
+           bow=9)
+
+# the oracle call of the last scene built, as a zero-argument callable
+# (bench.py times the single-thread CPU restatement on the scene's own inputs)
+LAST_CPU = [None]
+
+
+def _cpu(fn):
+    LAST_CPU[0] = fn
+    return fn()
 
 
 def write_scene(path, recs):
@@ -65,7 +75,7 @@ def local_map(O, seed, th=3.0, ratio=0.8, stereo=True, nmp=3000):
                 vp=np.arange(M, dtype=np.int32))
     cur = np.where(blocked == 1, holder, -1).astype(np.int32)
     recs.update(_side("A", kps, desc, bounds, scale, uright=ur, mps=cur))
-    eout, enm = O.search_by_projection(kps, desc, ur, bounds, scale, blocked, mps, mpd, th, ratio)
+    eout, enm = _cpu(lambda: O.search_by_projection(kps, desc, ur, bounds, scale, blocked, mps, mpd, th, ratio))
     want = cur.copy()
     want[eout >= 0] = eout[eout >= 0]
     return recs, np.concatenate([[enm], want]).astype(np.int32)
@@ -88,8 +98,9 @@ def last_frame(O, seed, th=7.0, stereo=True, motion="forward"):
                       mps=np.arange(M), outlier=(~mps["valid"].astype(bool)).astype(np.uint8)))
     recs.update(_side("A", c["kps"], c["desc"], c["bounds"], c["scale"], T=np.float32(list(cam.Tcw)),
                       uright=c["uright"], mps=cur, cam=_cam(cam.fx, cam.fy, cam.cx, cam.cy, cam.mb, cam.mbf)))
-    eout, enm = O.search_by_projection_last_frame(c["kps"], c["desc"], c["uright"], c["bounds"], c["scale"],
-                                                  c["blocked"], c["cam"], c["Tlw"], mps, c["mpdesc"], th, c["mono"])
+    eout, enm = _cpu(lambda: O.search_by_projection_last_frame(c["kps"], c["desc"], c["uright"], c["bounds"],
+                                                               c["scale"], c["blocked"], c["cam"], c["Tlw"], mps,
+                                                               c["mpdesc"], th, c["mono"]))
     want = cur.copy()
     want[eout >= 0] = eout[eout >= 0]
     want[eout == -2] = -1
@@ -183,8 +194,8 @@ def fuse(O, seed, th=3.0):
     recs.update(_side("A", c["kps"], c["desc"], c["bounds"], c["scale"], T=np.float32(list(cam.Tcw)),
                       uright=c["uright"], mps=kmp, invsigma2=np.float32(c["inv_sigma2"]),
                       cam=_cam(cam.fx, cam.fy, cam.cx, cam.cy, cam.mb, cam.mbf)))
-    eout, _ = O.fuse(c["kps"], c["desc"], c["uright"], c["bounds"], c["scale"], c["inv_sigma2"], 1.2, cam, mps,
-                     c["mpdesc"], th)
+    eout, _ = _cpu(lambda: O.fuse(c["kps"], c["desc"], c["uright"], c["bounds"], c["scale"], c["inv_sigma2"], 1.2,
+                                  cam, mps, c["mpdesc"], th))
     # the reference's tail on a model of the map: observations in this keyframe only
     kmp_now = kmp.copy()
     bad_now = bad.copy()
@@ -295,6 +306,52 @@ def triangulation(O, seed, only_stereo=False):
                       uright=kf1["uright"], mps=held(kf1), cam=cam, **fv(kf1)))
     recs.update(_side("B", kf2["kps"], kf2["desc"], (0.0, 1241.0, 0.0, 376.0), kf2["scale"], T=T2w,
                       uright=kf2["uright"], mps=held(kf2), cam=cam, sigma2=np.float32(sig2), **fv(kf2)))
-    e, enm = O.search_for_triangulation(kf1, kf2, cw1, T2w, cam2, sig2, F12, only_stereo, True)
+    e, enm = _cpu(lambda: O.search_for_triangulation(kf1, kf2, cw1, T2w, cam2, sig2, F12, only_stereo, True))
     pairs = [(i, int(j)) for i, j in enumerate(e) if j >= 0]
     return recs, np.array([enm] + [v for p in pairs for v in p], np.int32)
+
+
+def _featvec_csr(desc, seed, nodes=100):
+    """A stand-in DBoW2 FeatureVector at the reference's level (Frame::ComputeBoW
+    levelsup 4 on the 10^6-word vocabulary: ~100 nodes): node = a hash of 7
+    descriptor bits, so near descriptors tend to share a node."""
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(256)[:7]
+    bits = np.unpackbits(np.ascontiguousarray(desc, np.uint8), axis=1)[:, perm]
+    node = (bits * (1 << np.arange(7))).sum(1) % nodes
+    ids = np.unique(node)
+    off = np.zeros(len(ids) + 1, np.int32)
+    idx = []
+    for k, v in enumerate(ids):
+        idx += np.nonzero(node == v)[0].tolist()
+        off[k + 1] = len(idx)
+    return (ids * 11 + 5).astype(np.int32), off, np.array(idx, np.int32)
+
+
+def bow(O, seed, ratio=0.7, W=1241, H=376, nf=2000):
+    """SearchByBoW(pKF, F, vpMapPointMatches) (Tracking::TrackReferenceKeyFrame,
+    src/Tracking.cc:839-842): the reference keyframe is frame t of a synthetic
+    sequence, the current frame t + 1; every 4th keyframe keypoint has no
+    MapPoint and every 9th is bad."""
+    from orb_slam_cuda_amd.synth import SynthSequence
+    fr = SynthSequence(seed, W, H).frames(2)
+    cfg = O.config(nfeatures=nf, width=W, height=H)
+    (k1, d1), (k2, d2) = O.extract(cfg, fr[0]), O.extract(cfg, fr[1])
+    n1 = len(k1)
+    kmp = np.where(np.arange(n1) % 4 == 3, -1, np.arange(n1)).astype(np.int32)
+    bad = (np.arange(n1) % 9 == 4).astype(np.uint8)
+    good = ((kmp >= 0) & (bad[np.maximum(kmp, 0)] == 0)).astype(np.uint8)
+    fa, fb = _featvec_csr(d1, seed), _featvec_csr(d2, seed)
+    info = O.level_info(cfg)
+    recs = dict(op=np.int32([OPS["bow"]]), nnratio=np.float32([ratio]), check_ori=np.int32([1]),
+                mp_desc=np.ascontiguousarray(d1, np.uint8), mp_bad=bad)
+    recs.update(_side("B", k1, d1, (0, W, 0, H), info["scale"], mps=kmp, fv_nodes=fa[0], fv_off=fa[1],
+                      fv_idx=fa[2]))
+    recs.update(_side("A", k2, d2, (0, W, 0, H), info["scale"], fv_nodes=fb[0], fv_off=fb[1], fv_idx=fb[2]))
+    out, nm = _cpu(lambda: O.search_by_bow(d1, k1["angle"], good, tuple(x.astype(np.uint32) if i == 0 else x
+                                                                        for i, x in enumerate(fa)),
+                                           d2, k2["angle"], np.ones(len(d2), np.uint8),
+                                           tuple(x.astype(np.uint32) if i == 0 else x for i, x in enumerate(fb)),
+                                           ratio, True, False))
+    want = np.where(out >= 0, kmp[np.maximum(out, 0)], -1)
+    return recs, np.concatenate([[nm], want]).astype(np.int32)

@@ -198,6 +198,24 @@ def _tie_stats_legacy(pkg, monkeypatch, nf, W, H, img):
         return ext.tie_stats()
 
 
+@pytest.mark.parametrize("W,H,nf,nl,ini,mn", [(1241, 376, 2000, 8, 20, 7), (1920, 1080, 2000, 3, 10, 4)])
+def test_quadtree_spill_mode(pkg, O, W, H, nf, nl, ini, mn):
+    """Levels with more keys than the workgroup holds in registers (dense noise
+    at KITTI size; intcatch-1080p's yaml, 1920x1080, 3 levels, thresholds
+    10/4): the sorted path keeps the keys in a compact global copy and finds
+    each key's kept node through the per-bin node map; bit-exact, and at least
+    one such level runs the sorted path."""
+    from orb_slam_cuda_amd.synth import synth_frame
+    rng = np.random.default_rng(8)
+    img = (rng.integers(0, 256, size=(H, W), dtype=np.uint8) if W == 1241 else synth_frame(91, W, H))
+    ext = pkg.ORBextractor(nf, 1.2, nl, ini, mn, W, H)
+    kp, desc = ext(img)
+    big = [l for l in range(nl) if len(ext.fast_candidates(l)) > (4096 if W == 1241 else 8192)]
+    assert big and (ext.quadtree_paths()[0][big] == 1).any(), (big, ext.quadtree_paths())
+    rkp, rdesc = O.extract(oracle_cfg(O, nf, W, H, nlevels=nl, ini=ini, mn=mn), img)
+    assert_same(kp, desc, rkp, rdesc)
+
+
 def test_quadtree_sorted_path_falls_back(pkg, O):
     """Corners in small scattered patches: some level must split a node below
     the bins' depth, its workgroup falls back to the legacy rounds, and every

@@ -110,7 +110,8 @@ SCENES = [("local_map", dict(seed=1)), ("local_map", dict(seed=2, th=1.0, ratio=
           ("sim3", dict(seed=1)), ("sim3", dict(seed=2, th=5, s=0.7)),
           ("fuse", dict(seed=1)), ("fuse", dict(seed=2, th=5.0)),
           ("fuse_sim3", dict(seed=1)), ("sim3_match", dict(seed=1)), ("sim3_match", dict(seed=2, s12=1.08)),
-          ("triangulation", dict(seed=1)), ("triangulation", dict(seed=2, only_stereo=True))]
+          ("triangulation", dict(seed=1)), ("triangulation", dict(seed=2, only_stereo=True)),
+          ("bow", dict(seed=1)), ("bow", dict(seed=3, ratio=0.75))]
 
 
 @pytest.mark.gpu
