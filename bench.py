@@ -153,6 +153,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-match-priority", dest="match_priority", action="store_false",
                     help="matching stream(s) at normal priority (default: high, so the matcher's "
                          "one-workgroup-per-pair kernels get CUs as the extraction kernels drain them)")
+    ap.add_argument("--match-cus", default="",
+                    help="A/B: the matching stream(s) on a compute-unit subset, 'stride:K' (every K-th CU) or "
+                         "'first:N'; with --cu-exclusive the extraction streams get the other CUs")
+    ap.add_argument("--cu-exclusive", action="store_true", help="with --match-cus: extraction on the complement")
     ap.add_argument("--bow", action="store_true",
                     help="also Frame::ComputeBoW every frame (synthetic ORBvoc-shaped vocabulary, k 10 L 6)")
     ap.add_argument("--bow-match", action="store_true",
@@ -448,15 +452,18 @@ class MonoPipeline:
                 raise SystemExit(f"bench.py: --h2d-split {nparts} must divide the batch and be a multiple of --split")
             self.s_h2ds = [self.s_h2d] + [_lib.Stream(hp) for _ in range(nparts - 1)]
         prio = 1 if args.priority else None
-        self.s_exts = [_lib.Stream(prio) for _ in range(S)]
+        mmask = emask = None
+        if args.match_cus and not args.serial:
+            mmask, emask = cu_masks(args.match_cus, args.cu_exclusive)
+        self.s_exts = [_lib.Stream(prio, emask) for _ in range(S)]
         self.s_ext = self.s_exts[0]
         # the host-streamed leg keeps normal priority: there the high-priority
         # matcher starves the copy streams (32.6 k vs 46.1 k frames/s)
         mprio = 0 if args.priority else (1 if args.match_priority and not host else None)
-        self.s_match = _lib.Stream(mprio) if not args.serial else self.s_ext
+        self.s_match = _lib.Stream(mprio, mmask) if not args.serial else self.s_ext
         self.two_match = (args.match_streams == 2 and not args.serial and not args.no_match
                           and args.carry == "match" and not host)
-        self.s_init = _lib.Stream(mprio) if self.two_match else self.s_match
+        self.s_init = _lib.Stream(mprio, mmask) if self.two_match else self.s_match
         self.bounds = _lib.GridBounds(0.0, float(W), 0.0, float(H))
         self.voc = None
         self.bow_match = args.bow_match and not host
@@ -917,6 +924,18 @@ def dump_batch0(args, pipe, rank, block, prev):
 
 SQ_LAUNCH_FRAMES = 32   # frames per extraction launch of the committed SQ counter run
 VALU_ISSUE_PEAK_T = 1.2288  # wave64 VALU instructions/s: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles
+
+
+def cu_masks(spec, exclusive, ncu=None):
+    """CU masks (lists of u32 words) for --match-cus: the matching stream's and
+    (exclusive) the extraction streams' complement, or None for the latter."""
+    ncu = ncu or 256  # MI355X: 8 XCDs x 32 CUs
+    kind, _, val = spec.partition(":")
+    k = int(val)
+    sel = [(i % k == 0) if kind == "stride" else (i < k) for i in range(ncu)]
+    words = lambda bits: [sum(1 << b for b in range(32) if w * 32 + b < ncu and bits[w * 32 + b])
+                          for w in range((ncu + 31) // 32)]
+    return words(sel), (words([not x for x in sel]) if exclusive else None)
 
 
 def rocprof_ranking(top=6):

@@ -37,6 +37,8 @@
  *                          matcher (dense, device-resident, batched)
  *   orbm_compute_stereo_matches  Frame::ComputeStereoMatches (mvuRight, mvDepth)
  *                          include/Frame.h:82, src/Frame.cc:465-639
+ *   orbm_stereo_frame      the stereo Frame constructor's two ExtractORB
+ *                          threads + ComputeStereoMatches, src/Frame.cc:77-89
  *   orbm_search_by_projection  ORBmatcher::SearchByProjection(Frame&,
  *                          const vector<MapPoint*>&, th)  include/ORBmatcher.h:48,
  *                          src/ORBmatcher.cc:45-126 (Tracking::SearchLocalPoints)
@@ -596,6 +598,23 @@ int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle rig
 int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handle right,
                                      float mb, float mbf, float* uRight, float* depth,
                                      int nL, int* nkept);
+/* The stereo Frame constructor's extraction and matching steps
+ * (src/Frame.cc:77-89: ExtractORB on threadLeft / threadRight, then
+ * ComputeStereoMatches) from the calling thread with one device round trip.
+ * Outputs equal orbx_extract(left, img_left ...), orbx_extract(right,
+ * img_right ...) and orbm_compute_stereo_matches_last(m, left, right, mb, mbf,
+ * uRight, depth, *n_left, nkept) made in that order; the two extraction chains
+ * run concurrently on the handles' streams and the stereo kernel follows on
+ * the device. Both images are w x h (their own row strides); uRight and depth
+ * hold cap_left floats. `left` and `right` are two distinct handles. Empty
+ * images (w or h 0) take the three calls' own path. */
+int orbm_stereo_frame(orbm_handle m, orbx_handle left, orbx_handle right,
+                      const uint8_t* img_left, size_t stride_left,
+                      const uint8_t* img_right, size_t stride_right, int w, int h,
+                      float mb, float mbf, orbx_kp* kps_left, int cap_left,
+                      uint8_t* desc_left, int* n_left, orbx_kp* kps_right,
+                      int cap_right, uint8_t* desc_right, int* n_right,
+                      float* uRight, float* depth, int* nkept);
 
 /* Batched device-resident variant: pair p = left frame (left_frame0 + p) of
  * `left`'s last orbx_extract_batch and right frame (right_frame0 + p) of
@@ -735,6 +754,11 @@ int orbx_stream_create(void** stream);
 /* A stream whose work the dispatcher prefers (high = 1) or defers (high = 0)
  * when both compete for compute units (hipStreamCreateWithPriority). */
 int orbx_stream_create_priority(void** stream, int high);
+/* A stream whose kernels run only on the compute units whose bits are set in
+ * mask[0 .. nwords) (hipExtStreamCreateWithCUMask; bit i = CU i in the
+ * runtime's order): partitions the chip between concurrent pipelines
+ * (bench.py --match-cus). */
+int orbx_stream_create_cumask(void** stream, const uint32_t* mask, int nwords);
 int orbx_stream_destroy(void* stream);
 int orbx_stream_synchronize(void* stream);
 int orbx_event_create(void** ev);

@@ -7,9 +7,9 @@ host-side mirror of the reference classes in Python.
 """
 from ._lib import KP_DTYPE, OrbxError, device_count, header_functions, lib  # noqa: F401
 from .extractor import ORBextractor  # noqa: F401
-from .matcher import ComputeStereoMatches, ComputeStereoMatchesLast, Frame, KeyFrame, MapPoints, ORBmatcher  # noqa: F401
+from .matcher import ComputeStereoMatches, ComputeStereoMatchesLast, ExtractStereo, Frame, KeyFrame, MapPoints, ORBmatcher  # noqa: F401
 from .vocabulary import ComputeBoW, ORBVocabulary  # noqa: F401
 
 __all__ = ["ORBextractor", "ORBmatcher", "ORBVocabulary", "Frame", "KeyFrame", "ComputeBoW",
-           "ComputeStereoMatches", "ComputeStereoMatchesLast", "MapPoints", "KP_DTYPE", "OrbxError",
+           "ComputeStereoMatches", "ComputeStereoMatchesLast", "ExtractStereo", "MapPoints", "KP_DTYPE", "OrbxError",
            "device_count", "header_functions", "lib"]

@@ -134,6 +134,10 @@ def lib() -> C.CDLL:
         L.orbm_compute_stereo_matches_last.argtypes = [
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_int,
             C.POINTER(C.c_int)]
+        L.orbm_stereo_frame.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int, C.c_int,
+            C.c_float, C.c_float, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int), C.c_void_p, C.c_int,
+            C.c_void_p, C.POINTER(C.c_int), C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
         L.orbm_compute_stereo_matches_batch.argtypes = [
             C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_void_p,
@@ -313,10 +317,14 @@ class HostArray:
 
 
 class Stream:
-    def __init__(self, priority: int | None = None):
-        """priority None: default; 1: preferred by the dispatcher; 0: deferred."""
+    def __init__(self, priority: int | None = None, cu_mask: list | None = None):
+        """priority None: default; 1: preferred by the dispatcher; 0: deferred.
+        cu_mask: list of u32 words, the compute units the stream may use."""
         self.s = C.c_void_p(0)
-        if priority is None:
+        if cu_mask is not None:
+            m = (C.c_uint32 * len(cu_mask))(*cu_mask)
+            check(lib().orbx_stream_create_cumask(C.byref(self.s), m, len(cu_mask)))
+        elif priority is None:
             check(lib().orbx_stream_create(C.byref(self.s)))
         else:
             check(lib().orbx_stream_create_priority(C.byref(self.s), int(priority)))

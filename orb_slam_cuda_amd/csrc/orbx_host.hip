@@ -725,7 +725,8 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
 #define ORBX_QT_LDS_KB 80
 #endif
     const size_t base = quadtree_legacy_lds_bytes(P);
-    const size_t small = ORBX_QT_LDS_KB * 1024, big = 160 * 1024 - 512;
+    size_t small = ORBX_QT_LDS_KB * 1024, big = 160 * 1024 - 512;
+    if (const char* e = getenv("ORBX_QT_LDS_KB")) small = (size_t)std::max(32, atoi(e)) * 1024;  // A/B: blocks per CU
     P.qt_big = base + 16 * 1024 > small ? 1 : 0;
     const size_t budget = P.qt_big ? big : small;
     P.kcap_lds = base < budget ? (int)((budget - base) / 6) & ~15 : 0;
@@ -1055,21 +1056,12 @@ static int issue_one_frame(orbx_extractor* h, size_t pitch, int hh, int cap_fram
   return ORBX_OK;
 }
 
-int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride, orbx_kp* kps, int cap,
-                 uint8_t* desc, int* n) {
-  if (!h || !n) return fail(ORBX_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
-  *n = 0;
-  if (w == 0 || hh == 0) {  // src/ORBextractor.cc:1542-1543
-    // no outputs: later readers of "the last extraction" (the stereo matcher
-    // on the device outputs, the host pyramid) see an empty one, as the
-    // reference's Frame sees empty mvKeysRight
-    h->last_single = false;
-    h->last_empty = true;
-    h->host_pyr_valid = false;
-    h->last_batch = 0;
-    return ORBX_OK;
-  }
+// orbx_extract's halves. extract_submit: the image staged in the handle's
+// pinned buffer and the call's chain (H2D, the five launches, one D2H of
+// {count, status, keypoints, descriptors}) issued on its stream; the handle's
+// lock is held, the image is not empty. extract_finish: after that stream was
+// waited for, the outputs copied out of the pinned block.
+static int extract_submit(orbx_extractor* h, const uint8_t* img, int w, int hh, size_t stride, double* t_staged) {
   h->last_empty = false;
   if (!img || w < 0 || hh < 0 || stride < (size_t)w) return fail(ORBX_EINVAL, "bad image");
   HIP_OK(hipSetDevice(h->cfg.device));
@@ -1114,11 +1106,9 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
     for (auto& e : h->pev)
       if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
-  static const bool prof = getenv("ORBX_EXTRACT_PROF") && getenv("ORBX_EXTRACT_PROF")[0] == '1';
-  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  const double t0 = prof ? now() : 0;
+  // the pinned staging buffer is free: every call waits for its chain before it returns
   for (int y = 0; y < hh; ++y) memcpy((uint8_t*)h->h_in + (size_t)y * pitch, img + (size_t)y * stride, w);
-  const double t1 = prof ? now() : 0;
+  if (t_staged) *t_staged = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   // the plan buffers may still be in use by a batch call on another stream
   if (h->ws.before(h->stream)) return fail(ORBX_EDEVICE, "stream wait on the handle's last use failed");
   static const bool use_graph = !(getenv("ORBX_EXTRACT_GRAPH") && getenv("ORBX_EXTRACT_GRAPH")[0] == '0');
@@ -1159,10 +1149,12 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   h->last_frames = h->d_in.as<uint8_t>();
   h->last_fpitch = pitch * hh;
   h->last_rstride = pitch;
-  const double t2 = prof ? now() : 0;
-  HIP_OK(hipStreamSynchronize(h->stream));
-  const double t3 = prof ? now() : 0;
+  return ORBX_OK;
+}
+
+static int extract_finish(orbx_extractor* h, orbx_kp* kps, int cap, uint8_t* desc, int* n) {
   h->host_pyr_valid = h->host_pyr;
+  const int cap_frame = h->plan.P.kp_per_frame;
   const int* head = (const int*)h->h_out;
   const int cnt = head[0], err = head[1];
   if (err) {
@@ -1179,6 +1171,38 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride
   const uint8_t* o = (const uint8_t*)h->h_out + 16;
   if (kps) memcpy(kps, o, (size_t)cnt * sizeof(orbx_kp));
   if (desc) memcpy(desc, (const uint8_t*)h->h_out + out_desc_off(cap_frame), (size_t)cnt * 32);
+  return ORBX_OK;
+}
+
+static void extract_empty(orbx_extractor* h) {
+  // src/ORBextractor.cc:1542-1543: no outputs. Later readers of "the last
+  // extraction" (the stereo matcher on the device outputs, the host pyramid)
+  // see an empty one, as the reference's Frame sees empty mvKeysRight
+  h->last_single = false;
+  h->last_empty = true;
+  h->host_pyr_valid = false;
+  h->last_batch = 0;
+}
+
+int orbx_extract(orbx_handle h, const uint8_t* img, int w, int hh, size_t stride, orbx_kp* kps, int cap,
+                 uint8_t* desc, int* n) {
+  if (!h || !n) return fail(ORBX_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  *n = 0;
+  if (w == 0 || hh == 0) {
+    extract_empty(h);
+    return ORBX_OK;
+  }
+  static const bool prof = getenv("ORBX_EXTRACT_PROF") && getenv("ORBX_EXTRACT_PROF")[0] == '1';
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t0 = prof ? now() : 0;
+  double t1 = 0;
+  int rc = extract_submit(h, img, w, hh, stride, prof ? &t1 : nullptr);
+  if (rc) return rc;
+  const double t2 = prof ? now() : 0;
+  HIP_OK(hipStreamSynchronize(h->stream));
+  const double t3 = prof ? now() : 0;
+  if ((rc = extract_finish(h, kps, cap, desc, n))) return rc;
   if (prof) {
     const double t4 = now();
     h->prof_s[0] += t1 - t0;
@@ -1433,6 +1457,11 @@ int orbx_stream_create_priority(void** s, int high) {
   HIP_OK(hipStreamCreateWithPriority((hipStream_t*)s, hipStreamNonBlocking, high ? greatest : least));
   return ORBX_OK;
 }
+int orbx_stream_create_cumask(void** s, const uint32_t* mask, int nwords) {
+  if (!s || !mask || nwords < 1) return fail(ORBX_EINVAL, "bad argument");
+  HIP_OK(hipExtStreamCreateWithCUMask((hipStream_t*)s, (uint32_t)nwords, mask));
+  return ORBX_OK;
+}
 int orbx_stream_destroy(void* s) { HIP_OK(hipStreamDestroy((hipStream_t)s)); return ORBX_OK; }
 int orbx_stream_synchronize(void* s) { HIP_OK(hipStreamSynchronize((hipStream_t)s)); return ORBX_OK; }
 int orbx_event_create(void** e) { HIP_OK(hipEventCreate((hipEvent_t*)e)); return ORBX_OK; }
@@ -1453,3 +1482,26 @@ int orbx_event_elapsed_ms(void* a, void* b, float* ms) {
 }
 
 }  // extern "C"
+
+int orbx::extract_pair(orbx_handle L, orbx_handle R, const uint8_t* imL, size_t strideL, const uint8_t* imR,
+                       size_t strideR, int w, int hh, const std::function<int(hipStream_t)>& between,
+                       orbx_kp* kpsL, int capL, uint8_t* descL, int* nL, orbx_kp* kpsR, int capR, uint8_t* descR,
+                       int* nR) {
+  if (!L || !R || !nL || !nR) return fail(ORBX_EINVAL, "null argument");
+  if (L == R) return fail(ORBX_EINVAL, "left and right need two extractor handles");
+  if (w <= 0 || hh <= 0) return fail(ORBX_EINVAL, "empty image");
+  if (L->cfg.device != R->cfg.device) return fail(ORBX_EINVAL, "left and right extractors on different devices");
+  std::unique_lock<std::mutex> lkL(L->mu, std::defer_lock), lkR(R->mu, std::defer_lock);
+  std::lock(lkL, lkR);
+  *nL = *nR = 0;
+  // left first: its chain runs while the right image is staged
+  int rc;
+  if ((rc = extract_submit(L, imL, w, hh, strideL, nullptr)) || (rc = extract_submit(R, imR, w, hh, strideR, nullptr)))
+    return rc;
+  const int rb = between(L->stream);
+  // both streams: `between` may have failed before it ordered anything after the right chain
+  HIP_OK(hipStreamSynchronize(L->stream));
+  HIP_OK(hipStreamSynchronize(R->stream));
+  if ((rc = extract_finish(L, kpsL, capL, descL, nL)) || (rc = extract_finish(R, kpsR, capR, descR, nR))) return rc;
+  return rb;
+}

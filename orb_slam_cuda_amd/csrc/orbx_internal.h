@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
+
 #include "../../include/orbx_c.h"
 
 namespace orbx {
@@ -378,5 +380,15 @@ int raise_lds_limit(const void* fn, size_t bytes);
 // orbx_host.hip: the pyramid of frames [frame0, frame0 + n) of an extractor's last extraction
 int extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int* w, int* hgt, float* scale,
                       float* inv_scale, int* L);
+// orbx_host.hip: the stereo Frame's two extractions (src/Frame.cc:77-80) as two
+// orbx_extract calls make them, from one thread and with one wait: left staged
+// and launched on its handle's stream, right on its own (the two run
+// concurrently), then `between(left's stream)` enqueues the work that reads
+// both outputs on the device (ComputeStereoMatches), then both streams are
+// waited for and the outputs copied out. Two distinct handles, non-empty
+// images of one size.
+int extract_pair(orbx_handle L, orbx_handle R, const uint8_t* imL, size_t strideL, const uint8_t* imR,
+                 size_t strideR, int w, int h, const std::function<int(hipStream_t)>& between, orbx_kp* kpsL,
+                 int capL, uint8_t* descL, int* nL, orbx_kp* kpsR, int capR, uint8_t* descR, int* nR);
 
 }  // namespace orbx

@@ -1529,6 +1529,16 @@ static int stage_reserve(orbx_matcher* m, size_t bytes) {
   return ORBX_OK;
 }
 
+static int host_stage_reserve(orbx_matcher* m, size_t bytes) {
+  if (m->h_stage_bytes >= bytes) return ORBX_OK;
+  if (m->h_stage) (void)hipHostFree(m->h_stage);
+  m->h_stage = nullptr;
+  m->h_stage_bytes = 0;
+  MHIP(hipHostMalloc(&m->h_stage, bytes, hipHostMallocDefault));
+  m->h_stage_bytes = bytes;
+  return ORBX_OK;
+}
+
 static int search_init_launch(orbx_matcher* m, const orbx_kp* d_kp1, const uint8_t* d_desc1, const int* d_n1,
                               const orbx_kp* d_kp2, const uint8_t* d_desc2, const int* d_n2, int kp_pitch, int pairs,
                               orbm_grid_bounds b, float* d_prev_xy, int window, float nnratio, int check_ori,
@@ -1998,14 +2008,7 @@ int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handl
   // into the matcher's pinned staging
   const size_t bytes = 16 + (size_t)capL * 8;
   int rc;
-  if ((rc = stage_reserve(m, bytes))) return rc;
-  if (m->h_stage_bytes < bytes) {
-    if (m->h_stage) (void)hipHostFree(m->h_stage);
-    m->h_stage = nullptr;
-    m->h_stage_bytes = 0;
-    MHIP(hipHostMalloc(&m->h_stage, bytes, hipHostMallocDefault));
-    m->h_stage_bytes = bytes;
-  }
+  if ((rc = stage_reserve(m, bytes)) || (rc = host_stage_reserve(m, bytes))) return rc;
   int* dk = (int*)m->stage;
   float* du = (float*)m->stage + 4;  // uRight: capL floats (the kernels' pitch), then depth
   float* dd = du + capL;
@@ -2022,6 +2025,72 @@ int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handl
   if (nL) {
     memcpy(uRight, h + 16, (size_t)nL * 4);
     memcpy(depth, h + 16 + (size_t)capL * 4, (size_t)nL * 4);
+  }
+  return ORBX_OK;
+}
+
+// The stereo Frame's construction steps (src/Frame.cc:77-89: ExtractORB on
+// threadLeft / threadRight, then ComputeStereoMatches :465-639) with one
+// device round trip: both extraction chains are issued from the calling
+// thread on the two handles' streams (they run concurrently), the stereo
+// kernel follows on the left stream once both are done, and its {kept,
+// uRight, depth} block comes back in the same wait as the two extractions'
+// outputs. Results are those of orbx_extract x2 + orbm_compute_stereo_matches_last.
+int orbm_stereo_frame(orbm_handle m, orbx_handle left, orbx_handle right, const uint8_t* img_left,
+                      size_t stride_left, const uint8_t* img_right, size_t stride_right, int w, int h, float mb,
+                      float mbf, orbx_kp* kps_left, int cap_left, uint8_t* desc_left, int* n_left,
+                      orbx_kp* kps_right, int cap_right, uint8_t* desc_right, int* n_right, float* uRight,
+                      float* depth, int* nkept) {
+  if (!m || !left || !right || !n_left || !n_right || !nkept || w < 0 || h < 0) return mfail(ORBX_EINVAL, "bad argument");
+  if (left == right) return mfail(ORBX_EINVAL, "left and right need two extractor handles");
+  if (!(mb > 0.f)) return mfail(ORBX_EINVAL, "baseline mb must be positive");
+  *nkept = 0;
+  if (w == 0 || h == 0) {
+    // empty images: the two calls' own semantics (no outputs, uRight = -1)
+    if (orbx_extract(left, img_left, w, h, stride_left, kps_left, cap_left, desc_left, n_left) ||
+        orbx_extract(right, img_right, w, h, stride_right, kps_right, cap_right, desc_right, n_right))
+      return mfail(ORBX_EINVAL, "stereo frame: %s", orbx_last_error());
+    return orbm_compute_stereo_matches_last(m, left, right, mb, mbf, uRight, depth, *n_left, nkept);
+  }
+  MHIP(hipSetDevice(m->device));
+  int brc = ORBX_OK, cap = 0;
+  auto between = [&](hipStream_t st) -> int {
+    const int* dnL = nullptr;
+    const int* dnR = nullptr;
+    const orbx_kp *dkl = nullptr, *dkr = nullptr;
+    const uint8_t *ddl = nullptr, *ddr = nullptr;
+    int capR = 0;
+    if (extractor_last_output(left, &dnL, &dkl, &ddl, &cap) || extractor_last_output(right, &dnR, &dkr, &ddr, &capR))
+      return brc = mfail(ORBX_EINVAL, "stereo frame: %s", orbx_last_error());
+    if (cap != capR) return brc = mfail(ORBX_EINVAL, "left and right extractors have different capacities");
+    // past the matcher's limits: the host-array path after the extractions
+    if (cap > m->max_kps) return (brc = ORBX_ECAPACITY), ORBX_OK;
+    const size_t bytes = 16 + (size_t)cap * 8;
+    int rc;
+    if ((rc = stage_reserve(m, bytes)) || (rc = host_stage_reserve(m, bytes))) return brc = rc;
+    int* dk = (int*)m->stage;
+    float* du = (float*)m->stage + 4;
+    float* dd = du + cap;
+    rc = orbm_compute_stereo_matches_batch(m, left, 0, right, 0, dkl, ddl, dnL, dkr, ddr, dnR, cap, 1, mb, mbf, du,
+                                           dd, dk, st);
+    if (rc == ORBX_ECAPACITY) return (brc = ORBX_ECAPACITY), ORBX_OK;  // checked before any launch
+    if (rc) return brc = rc;
+    MHIP(hipMemcpyAsync(m->h_stage, dk, bytes, hipMemcpyDeviceToHost, st));
+    return ORBX_OK;
+  };
+  int rc = extract_pair(left, right, img_left, stride_left, img_right, stride_right, w, h, between, kps_left, cap_left,
+                        desc_left, n_left, kps_right, cap_right, desc_right, n_right);
+  if (rc) return brc ? brc : mfail(rc, "stereo frame: %s", orbx_last_error());
+  if (brc == ORBX_ECAPACITY)
+    return orbm_compute_stereo_matches_last(m, left, right, mb, mbf, uRight, depth, *n_left, nkept);
+  if (brc) return brc;
+  const uint8_t* hs = (const uint8_t*)m->h_stage;
+  *nkept = ((const int*)hs)[0];
+  const int nL = *n_left;
+  if (nL && (!uRight || !depth)) return mfail(ORBX_EINVAL, "null uRight/depth");
+  if (nL) {
+    memcpy(uRight, hs + 16, (size_t)nL * 4);
+    memcpy(depth, hs + 16 + (size_t)cap * 4, (size_t)nL * 4);
   }
   return ORBX_OK;
 }

@@ -70,25 +70,36 @@ class ORBextractor:
         like the reference (include/ORBextractor.h:89)."""
         img = np.asarray(image)
         if img.size == 0:
+            # no outputs (src/ORBextractor.cc:1542-1543); the handle's last
+            # extraction becomes an empty one (what the stereo matcher then reads)
+            check(lib().orbx_extract(self._h, None, 0, 0, 0, None, 0, None, C.byref(C.c_int(0))))
             return np.zeros(0, KP_DTYPE), np.zeros((0, 32), np.uint8)
         if img.dtype != np.uint8 or img.ndim != 2:
             raise _lib.OrbxError(_lib.ORBX_EINVAL, "image must be CV_8UC1 (2-D uint8)")  # :1546 assert
         if img.strides[1] != 1:
             img = np.ascontiguousarray(img)
-        cap = self.frame_capacity
+        cap = self._begin(img)
         n = C.c_int(0)
-        if cap == 0:
-            # created with width/height 0 (mono yamls without Camera.width/height,
-            # src/Tracking.cc:124-133): this call plans the handle for the image
-            check(lib().orbx_extract(self._h, ptr(img), img.shape[1], img.shape[0], img.strides[0],
-                                     None, 2**31 - 1, None, C.byref(n)))
-            cap = self.frame_capacity
         kps = np.empty(cap, KP_DTYPE)
         desc = np.empty((cap, 32), np.uint8)
         check(lib().orbx_extract(self._h, ptr(img), img.shape[1], img.shape[0], img.strides[0],
                                  ptr(kps), cap, ptr(desc), C.byref(n)))
-        cap = self.frame_capacity  # a new image size re-plans the handle
         return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def _begin(self, img: np.ndarray) -> int:
+        """Plan the handle for the image's size (created with width/height 0, as mono
+        yamls without Camera.width/height leave it, src/Tracking.cc:124-133, or a new
+        size: the reference accepts any size per call) with one call that has no
+        outputs; returns the frame capacity the outputs are sized to."""
+        lw = (C.c_int * self.nlevels)()
+        lh = (C.c_int * self.nlevels)()
+        nl = C.c_int(0)
+        check(lib().orbx_get_levels_info(self._h, C.byref(nl), lw, lh, None))
+        if (lw[0], lh[0]) != (img.shape[1], img.shape[0]):
+            n = C.c_int(0)
+            check(lib().orbx_extract(self._h, ptr(img), img.shape[1], img.shape[0], img.strides[0],
+                                     None, 2**31 - 1, None, C.byref(n)))
+        return self.frame_capacity
 
     def extract_batch_device(self, d_frames: int, batch: int, frame_pitch: int, row_stride: int,
                              d_kps: int, d_desc: int, d_counts: int, stream=None) -> None:

@@ -29,6 +29,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
+from . import _lib
 from ._lib import (KP_DTYPE, MAP_POINT_PROJ_DTYPE, MAP_POINT_WORLD_DTYPE, FeatureVectorC, GridBounds, camera, check,
                    lib, ptr)
 
@@ -164,6 +165,41 @@ def ComputeStereoMatchesLast(F: Frame, extractorLeft, extractorRight, matcher: "
         ptr(uR), ptr(dep), n, C.byref(kept)), matcher=True)
     F.mvuRight, F.mvDepth = uR, dep
     return kept.value
+
+
+def ExtractStereo(extractorLeft, extractorRight, imLeft, imRight, matcher: "ORBmatcher", mb: float,
+                  mbf: float):
+    """The stereo Frame constructor's extraction and matching steps (src/Frame.cc:77-89:
+    ExtractORB on threadLeft / threadRight, then ComputeStereoMatches) with one device round
+    trip (orbm_stereo_frame). Returns (keysLeft, descLeft, keysRight, descRight, mvuRight,
+    mvDepth, kept), equal to the two extractor calls followed by ComputeStereoMatchesLast."""
+    imgs = []
+    for im in (imLeft, imRight):
+        im = np.asarray(im)
+        if im.size and (im.dtype != np.uint8 or im.ndim != 2):
+            raise _lib.OrbxError(_lib.ORBX_EINVAL, "image must be CV_8UC1 (2-D uint8)")
+        imgs.append(np.ascontiguousarray(im) if im.size and im.strides[1] != 1 else im)
+    L, R = imgs
+    if L.size == 0 or R.size == 0 or L.shape != R.shape:
+        kL, dL = extractorLeft(L)
+        kR, dR = extractorRight(R)
+        F = Frame.from_extraction(kL, dL, 0, 0)
+        F.mb, F.mbf = mb, mbf
+        kept = ComputeStereoMatchesLast(F, extractorLeft, extractorRight, matcher)
+        return kL, dL, kR, dR, F.mvuRight, F.mvDepth, kept
+    capL, capR = extractorLeft._begin(L), extractorRight._begin(R)
+    kL, kR = np.empty(capL, KP_DTYPE), np.empty(capR, KP_DTYPE)
+    dL, dR = np.empty((capL, 32), np.uint8), np.empty((capR, 32), np.uint8)
+    uR = np.full(capL, -1.0, np.float32)
+    dep = np.full(capL, -1.0, np.float32)
+    nL, nR, kept = C.c_int(0), C.c_int(0), C.c_int(0)
+    check(lib().orbm_stereo_frame(
+        matcher.handle, extractorLeft.handle, extractorRight.handle, ptr(L), L.strides[0], ptr(R), R.strides[0],
+        L.shape[1], L.shape[0], C.c_float(mb), C.c_float(mbf), ptr(kL), capL, ptr(dL), C.byref(nL), ptr(kR),
+        capR, ptr(dR), C.byref(nR), ptr(uR), ptr(dep), C.byref(kept)), matcher=True)
+    n, m = nL.value, nR.value
+    return (kL[:n].copy(), dL[:n].copy(), kR[:m].copy(), dR[:m].copy(), uR[:n].copy(), dep[:n].copy(),
+            kept.value)
 
 
 @dataclass

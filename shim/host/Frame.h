@@ -10,6 +10,7 @@
 #ifndef ORBX_SHIM_FRAME_H
 #define ORBX_SHIM_FRAME_H
 #include <cmath>
+#include <cstdlib>
 #include <exception>
 #include <thread>
 #include <vector>
@@ -39,39 +40,46 @@ class Frame {
     mvbOutlier.assign(N, false);
     image_bounds(imGray);
   }
-  // The stereo constructor (src/Frame.cc:60-128): left and right extraction
-  // on two std::threads, as the reference does (:77-80, threadLeft /
-  // threadRight over ExtractORB), then ComputeStereoMatches(); bf = baseline
-  // x fx, mb = bf / fx. The two extractor handles are independent; an
-  // exception on either thread is rethrown here after both joined.
+  // The stereo constructor (src/Frame.cc:60-128); bf = baseline x fx, mb =
+  // bf / fx. Its extraction and matching steps (:77-89) are the drop-in body
+  // ExtractStereo (shim/src/Frame.cc: both extractions and ComputeStereoMatches
+  // in one device round trip). ORBX_STEREO_THREADS=1 runs the reference's own
+  // structure instead, for comparison: ExtractORB on two std::threads
+  // (threadLeft / threadRight), an exception on either rethrown here after
+  // both joined, then ComputeStereoMatches().
   Frame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* extractorLeft, ORBextractor* extractorRight,
         ORBVocabulary* voc, float bf)
       : mpORBvocabulary(voc), mpORBextractorLeft(extractorLeft), mpORBextractorRight(extractorRight), mbf(bf) {
     scale_info();
-    std::exception_ptr errL, errR;
-    std::thread threadLeft([&] {
-      try {
-        (*mpORBextractorLeft)(imLeft, cv::noArray(), mvKeys, mDescriptors);
-      } catch (...) {
-        errL = std::current_exception();
-      }
-    });
-    std::thread threadRight([&] {
-      try {
-        (*mpORBextractorRight)(imRight, cv::noArray(), mvKeysRight, mDescriptorsRight);
-      } catch (...) {
-        errR = std::current_exception();
-      }
-    });
-    threadLeft.join();
-    threadRight.join();
-    if (errL) std::rethrow_exception(errL);
-    if (errR) std::rethrow_exception(errR);
-    N = (int)mvKeys.size();
+    mb = mbf / fx;
+    const char* th = std::getenv("ORBX_STEREO_THREADS");
+    if (th && th[0] == '1') {
+      std::exception_ptr errL, errR;
+      std::thread threadLeft([&] {
+        try {
+          (*mpORBextractorLeft)(imLeft, cv::noArray(), mvKeys, mDescriptors);
+        } catch (...) {
+          errL = std::current_exception();
+        }
+      });
+      std::thread threadRight([&] {
+        try {
+          (*mpORBextractorRight)(imRight, cv::noArray(), mvKeysRight, mDescriptorsRight);
+        } catch (...) {
+          errR = std::current_exception();
+        }
+      });
+      threadLeft.join();
+      threadRight.join();
+      if (errL) std::rethrow_exception(errL);
+      if (errR) std::rethrow_exception(errR);
+      N = (int)mvKeys.size();
+      ComputeStereoMatches();
+    } else {
+      ExtractStereo(imLeft, imRight);
+    }
     mvKeysUn = mvKeys;
     image_bounds(imLeft);
-    mb = mbf / fx;
-    ComputeStereoMatches();
     mvpMapPoints.assign(N, static_cast<MapPoint*>(nullptr));
     mvbOutlier.assign(N, false);
   }
@@ -86,6 +94,10 @@ class Frame {
   // Search a match for each keypoint in the left image to a keypoint in the
   // right image (shim/src/Frame.cc, over orbm_compute_stereo_matches)
   void ComputeStereoMatches();
+  // The stereo constructor's ExtractORB threads and ComputeStereoMatches
+  // (src/Frame.cc:77-89) in one call (shim/src/Frame.cc): mvKeys, mDescriptors,
+  // mvKeysRight, mDescriptorsRight, N, mvuRight, mvDepth
+  void ExtractStereo(const cv::Mat& imLeft, const cv::Mat& imRight);
 
   ORBVocabulary* mpORBvocabulary = nullptr;
   ORBextractor* mpORBextractorLeft = nullptr;

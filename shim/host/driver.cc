@@ -52,8 +52,9 @@ int run_scene(const std::string& in, const std::string& out);  // scene.cc
 int run_scene_latency(const std::string& in, int ncalls, int warm);  // scene.cc
 
 // The stereo Frame constructor (src/Frame.cc:60-128) over NPAIRS stereo
-// pairs: two extractors, left and right extraction on two std::threads
-// (Frame.h, as the reference's :77-80), ComputeStereoMatches; writes each
+// pairs: two extractors, Frame::ExtractStereo (or, ORBX_STEREO_THREADS=1, left
+// and right extraction on two std::threads as the reference's :77-80, then
+// ComputeStereoMatches); writes each
 // pair's left / right keypoints, mvuRight and mvDepth.
 static int run_stereo(const char* left, const char* right, int npairs, int W, int H, float bf,
                       const std::string& out) {
@@ -114,8 +115,10 @@ static std::string stats(std::vector<double> t) {
 //   orbx_extract        the C-ABI call alone (its own handle, host buffers)
 //   operator()          ORBextractor::operator() (src/Frame.cc:246-252), with
 //                       and without the pinned host pyramid (ORBX_HOST_PYRAMID)
-//   stereo Frame        the stereo constructor: left and right operator() on two
-//                       std::threads + ComputeStereoMatches (src/Frame.cc:60-128)
+//   stereo Frame        the stereo constructor (src/Frame.cc:60-128): its drop-in
+//                       body (Frame::ExtractStereo, one device round trip) and the
+//                       reference's structure (left and right operator() on two
+//                       std::threads + ComputeStereoMatches, ORBX_STEREO_THREADS=1)
 // Prints one JSON object.
 static int run_latency(const char* mono, const char* left, const char* right, int nfr, int W, int H, int ncalls,
                        int warm) {
@@ -172,8 +175,12 @@ static int run_latency(const char* mono, const char* left, const char* right, in
   Frame::cy = 185.2157f;
   Frame::invfx = Frame::invfy = 1.0f / 718.856f;
   const float bf = 0.54f * 718.856f;
-  for (int hp = 0; hp <= 1; ++hp) {
+  // the stereo constructor: the drop-in body (one device round trip), with and
+  // without the host pyramid, then the reference's two-thread structure
+  for (int v = 0; v < 3; ++v) {
+    const int hp = v == 1;
     setenv("ORBX_HOST_PYRAMID", hp ? "1" : "0", 1);
+    setenv("ORBX_STEREO_THREADS", v == 2 ? "1" : "0", 1);
     ORBextractor le(2000, 1.2f, 8, 20, 7, W, H), re(2000, 1.2f, 8, 20, 7, W, H);
     std::vector<double> t;
     size_t kept = 0;
@@ -189,8 +196,10 @@ static int run_latency(const char* mono, const char* left, const char* right, in
     }
     char buf[96];
     snprintf(buf, sizeof buf, "\"stereo_matches_per_frame\": %.1f, ", (double)kept / ncalls);
-    out += std::string(", ") + (hp ? "" : buf) + "\"stereo_frame_ms" + (hp ? "_host_pyramid" : "") + "\": " + stats(t);
+    const char* key = v == 0 ? "stereo_frame_ms" : v == 1 ? "stereo_frame_ms_host_pyramid" : "stereo_frame_threads_ms";
+    out += std::string(", ") + (v == 0 ? buf : "") + "\"" + key + "\": " + stats(t);
   }
+  unsetenv("ORBX_STEREO_THREADS");
   {
     // the stereo constructor's parts (no host pyramid): the two extraction
     // threads alone, the two extractions on one thread, ComputeStereoMatches alone

@@ -57,6 +57,17 @@ class ORBextractor {
   void operator()(cv::InputArray image, cv::InputArray mask, std::vector<cv::KeyPoint>& keypoints,
                   cv::OutputArray descriptors);
 
+  // The stereo Frame's two calls (src/Frame.cc:77-80, operator() on threadLeft
+  // and threadRight) and ComputeStereoMatches (:89) with one device round trip
+  // (orbm_stereo_frame): the same keypoints, descriptors, mvImagePyramid and
+  // uRight / depth (mvuRight, mvDepth: one entry per left keypoint) as those
+  // three steps. Images of different sizes or an empty one take the steps one
+  // after the other. mb, mbf as Frame's.
+  static void ExtractStereo(ORBextractor& left, ORBextractor& right, const cv::Mat& imLeft, const cv::Mat& imRight,
+                            orbm_handle matcher, float mb, float mbf, std::vector<cv::KeyPoint>& keysLeft,
+                            cv::OutputArray descLeft, std::vector<cv::KeyPoint>& keysRight, cv::OutputArray descRight,
+                            std::vector<float>& uRight, std::vector<float>& depth);
+
   int inline GetLevels() { return nlevels; }
   float inline GetScaleFactor() { return (float)scaleFactor; }
   std::vector<float> inline GetScaleFactors() { return mvScaleFactor; }
@@ -105,6 +116,9 @@ class ORBextractor {
   long long totalTime = 0;
   unsigned int nFrame = 0;
   std::vector<times_t> times;
+
+  void BeginCall(const cv::Mat& image, std::vector<cv::KeyPoint>& keypoints, cv::OutputArray descriptors);
+  void EndCall(int n, std::vector<cv::KeyPoint>& keypoints, cv::OutputArray descriptors);
 
   orbx_handle h_ = nullptr;
   int cap_ = 0;

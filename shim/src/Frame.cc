@@ -27,4 +27,17 @@ void Frame::ComputeStereoMatches() {
                                                   mvDepth.data(), N, &kept);
   if (rc != ORBX_OK) throw std::runtime_error(std::string("liborbx: ") + orbm_last_error());
 }
+
+// The stereo constructor's extraction and matching steps (src/Frame.cc:77-89:
+// ExtractORB on threadLeft / threadRight, N = mvKeys.size(), then
+// ComputeStereoMatches) as one call with one device round trip: both
+// extraction chains are issued from this thread and run concurrently on the
+// device, the stereo kernel follows them there, and the keypoints,
+// descriptors, mvuRight and mvDepth come back together (orbm_stereo_frame).
+// Same results as those steps.
+void Frame::ExtractStereo(const cv::Mat& imLeft, const cv::Mat& imRight) {
+  ORBextractor::ExtractStereo(*mpORBextractorLeft, *mpORBextractorRight, imLeft, imRight, ORBmatcher::Handle(), mb, mbf,
+                              mvKeys, mDescriptors, mvKeysRight, mDescriptorsRight, mvuRight, mvDepth);
+  N = (int)mvKeys.size();
+}
 }  // namespace ORB_SLAM2

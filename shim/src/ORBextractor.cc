@@ -94,35 +94,29 @@ ORBextractor::~ORBextractor() {
   if (h_) orbx_destroy(h_);
 }
 
-void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask*/, std::vector<cv::KeyPoint>& _keypoints,
-                              cv::OutputArray _descriptors) {
-  if (_image.empty()) return;  // :1542-1543
-  cv::Mat image = _image.getMat();
-  assert(image.type() == CV_8UC1);  // :1546
-  const auto start = std::chrono::steady_clock::now();
-  {
-  GetTime total(this, "Total Time ORB extraction", -1);  // :1548 (recorded only with ORBX_TIMING=1)
-  // keypoints and descriptors are written straight into the outputs at their
-  // capacity and trimmed to the count (no staging copy)
-  _keypoints.resize(cap_);
-  _descriptors.create(cap_, 32, CV_8U);
-  cv::Mat& desc = _descriptors.getMatRef();
-  int n = 0;
+// Before a call: outputs sized to the capacity (keypoints and descriptors are
+// written straight into them and trimmed to the count, no staging copy); a
+// new image size re-plans the handle (the reference accepts any size per
+// call): one call with no outputs plans it, then the capacity is known.
+void ORBextractor::BeginCall(const cv::Mat& image, std::vector<cv::KeyPoint>& keypoints, cv::OutputArray descriptors) {
   if (image.cols != lw_[0] || image.rows != lh_[0]) {
-    // a new image size re-plans the handle (the reference accepts any size per
-    // call): one call with no outputs plans it, then the capacity is known
+    int n = 0;
     orbx_check(orbx_extract(h_, image.data, image.cols, image.rows, image.step, nullptr, INT_MAX, nullptr, &n));
     cap_ = orbx_frame_capacity(h_);
     int nl = 0;
     orbx_check(orbx_get_levels_info(h_, &nl, lw_.data(), lh_.data(), mnFeaturesPerLevel.data()));
-    _keypoints.resize(cap_);
-    _descriptors.create(cap_, 32, CV_8U);
   }
-  orbx_check(orbx_extract(h_, image.data, image.cols, image.rows, image.step,
-                          reinterpret_cast<orbx_kp*>(_keypoints.data()), cap_, desc.data, &n));
-  _keypoints.resize(n);
+  keypoints.resize(cap_);
+  descriptors.create(cap_, 32, CV_8U);
+}
+
+// After a call that left n keypoints: outputs trimmed, mvImagePyramid and the
+// time records of the call.
+void ORBextractor::EndCall(int n, std::vector<cv::KeyPoint>& keypoints, cv::OutputArray descriptors) {
+  cv::Mat& desc = descriptors.getMatRef();
+  keypoints.resize(n);
   if (n == 0)
-    _descriptors.release();  // :1716-1717
+    descriptors.release();  // :1716-1717
   else
     desc = desc.rowRange(0, n);  // _descriptors.create(nkeypoints, 32, CV_8U) :1719
   // mvImagePyramid: headers over the pinned host copy of this call's pyramid
@@ -142,9 +136,77 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask*/, s
     const int n_st = GetStageTimes(ms, names);
     for (int i = 0; i < n_st; ++i) times.push_back(times_t{(int)nFrame, names[i], -1, (long long)(ms[i] * 1e6)});
   }
+}
+
+void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask*/, std::vector<cv::KeyPoint>& _keypoints,
+                              cv::OutputArray _descriptors) {
+  if (_image.empty()) {  // :1542-1543, no outputs
+    // the handle's last extraction becomes an empty one, so ComputeStereoMatches
+    // after an empty right image matches nothing (the reference's empty mvKeysRight)
+    int n = 0;
+    orbx_check(orbx_extract(h_, nullptr, 0, 0, 0, nullptr, 0, nullptr, &n));
+    return;
+  }
+  cv::Mat image = _image.getMat();
+  assert(image.type() == CV_8UC1);  // :1546
+  const auto start = std::chrono::steady_clock::now();
+  {
+    GetTime total(this, "Total Time ORB extraction", -1);  // :1548 (recorded only with ORBX_TIMING=1)
+    BeginCall(image, _keypoints, _descriptors);
+    int n = 0;
+    orbx_check(orbx_extract(h_, image.data, image.cols, image.rows, image.step,
+                            reinterpret_cast<orbx_kp*>(_keypoints.data()), cap_, _descriptors.getMatRef().data, &n));
+    EndCall(n, _keypoints, _descriptors);
   }
   totalTime += std::chrono::duration<long long, std::nano>(std::chrono::steady_clock::now() - start).count();  // :1810-1814
   nFrame++;
+}
+
+void ORBextractor::ExtractStereo(ORBextractor& left, ORBextractor& right, const cv::Mat& imLeft, const cv::Mat& imRight,
+                                 orbm_handle matcher, float mb, float mbf, std::vector<cv::KeyPoint>& keysLeft,
+                                 cv::OutputArray descLeft, std::vector<cv::KeyPoint>& keysRight,
+                                 cv::OutputArray descRight, std::vector<float>& uRight, std::vector<float>& depth) {
+  auto matcher_check = [](int rc) {
+    if (rc != ORBX_OK) throw std::runtime_error(std::string("liborbx: ") + orbm_last_error());
+  };
+  if (imLeft.empty() || imRight.empty() || imLeft.rows != imRight.rows || imLeft.cols != imRight.cols ||
+      &left == &right) {
+    // the two operator() calls one after the other, then the matching
+    left(imLeft, cv::noArray(), keysLeft, descLeft);
+    right(imRight, cv::noArray(), keysRight, descRight);
+    uRight.assign(keysLeft.size(), -1.0f);
+    depth.assign(keysLeft.size(), -1.0f);
+    if (keysLeft.empty()) return;
+    int kept = 0;
+    matcher_check(orbm_compute_stereo_matches_last(matcher, left.h_, right.h_, mb, mbf, uRight.data(), depth.data(),
+                                                   (int)keysLeft.size(), &kept));
+    return;
+  }
+  assert(imLeft.type() == CV_8UC1 && imRight.type() == CV_8UC1);
+  const auto start = std::chrono::steady_clock::now();
+  {
+    // both extractors record the pair's time as their total (ORBX_TIMING=1)
+    GetTime totalL(&left, "Total Time ORB extraction", -1), totalR(&right, "Total Time ORB extraction", -1);
+    left.BeginCall(imLeft, keysLeft, descLeft);
+    right.BeginCall(imRight, keysRight, descRight);
+    uRight.assign(left.cap_, -1.0f);
+    depth.assign(left.cap_, -1.0f);
+    int nL = 0, nR = 0, kept = 0;
+    matcher_check(orbm_stereo_frame(matcher, left.h_, right.h_, imLeft.data, imLeft.step, imRight.data, imRight.step,
+                                    imLeft.cols, imLeft.rows, mb, mbf, reinterpret_cast<orbx_kp*>(keysLeft.data()),
+                                    left.cap_, descLeft.getMatRef().data, &nL,
+                                    reinterpret_cast<orbx_kp*>(keysRight.data()), right.cap_,
+                                    descRight.getMatRef().data, &nR, uRight.data(), depth.data(), &kept));
+    uRight.resize(nL);
+    depth.resize(nL);
+    left.EndCall(nL, keysLeft, descLeft);
+    right.EndCall(nR, keysRight, descRight);
+  }
+  const long long ns = std::chrono::duration<long long, std::nano>(std::chrono::steady_clock::now() - start).count();
+  for (ORBextractor* e : {&left, &right}) {
+    e->totalTime += ns;
+    e->nFrame++;
+  }
 }
 
 GetTime::GetTime(std::vector<times_t>& times, int nFrame, std::string name, int level) : o(nullptr), times(times) {

@@ -121,3 +121,54 @@ def test_stereo_last_refuses_batch_extraction(pkg):
         pkg.ComputeStereoMatchesLast(F, eL, eR, m)
     n = C.c_int(0)
     assert _lib.lib().orbx_get_status(eL.handle, 1, C.byref(n)) == 0 and n.value == 0
+
+
+def test_stereo_frame_one_round_trip_equals_oracle(pkg, O):
+    """orbm_stereo_frame (the stereo Frame's two extractions + ComputeStereoMatches
+    issued from one thread with one wait) gives the oracle's keypoints, descriptors,
+    mvuRight and mvDepth: first call (plain launches), graph replays, a new image size
+    (re-plan of both handles), an empty right image and images of different sizes (the
+    steps one after the other)."""
+    from orb_slam_cuda_amd.synth import stereo_pair
+    eL = pkg.ORBextractor(2000, 1.2, 8, 20, 7, 1241, 376)
+    eR = pkg.ORBextractor(2000, 1.2, 8, 20, 7, 1241, 376)
+    m = pkg.ORBmatcher(max_kps=4096)
+
+    def oracle(imL, imR):
+        W, H = imL.shape[1], imL.shape[0]
+        cfg = O.config(nfeatures=2000, width=W, height=H)
+        li = O.level_info(cfg)
+        kL, dL = O.extract(cfg, imL)
+        kR, dR = O.extract(cfg, imR)
+        uR, dep, kept = O.compute_stereo_matches(kL, dL, kR, dR, O.pyramid(cfg, imL), O.pyramid(cfg, imR),
+                                                 li["scale"], li["inv_scale"], MB, MBF)
+        return kL, dL, kR, dR, uR, dep, kept
+
+    cases = [(3, 1241, 376), (4, 1241, 376), (5, 1241, 376), (6, 752, 480), (7, 1241, 376)]
+    for seed, W, H in cases:
+        imL, imR = stereo_pair(seed, W, H)
+        got = pkg.ExtractStereo(eL, eR, imL, imR, m, MB, float(MBF))
+        want = oracle(imL, imR)
+        for g, w, name in zip(got[:4], want[:4], ("kL", "dL", "kR", "dR")):
+            assert np.array_equal(np.asarray(g).view(np.uint8), np.asarray(w).view(np.uint8)), (seed, name)
+        assert np.array_equal(got[4], want[4]) and np.array_equal(got[5], want[5]), seed
+        assert got[6] == want[6] > 0.3 * len(want[0]), seed
+        # the same handles then serve the separate calls (the pyramids are the pair's)
+        n = C.c_int(0)
+        assert pkg.lib().orbx_get_status(eL.handle, 1, C.byref(n)) == 0 and n.value == 0
+    # an empty right image: the left keypoints match nothing
+    imL, _ = stereo_pair(9, 1241, 376)
+    kL, dL, kR, dR, uR, dep, kept = pkg.ExtractStereo(eL, eR, imL, np.zeros((0, 0), np.uint8), m, MB, float(MBF))
+    cfg = O.config(nfeatures=2000, width=1241, height=376)
+    rkL, rdL = O.extract(cfg, imL)
+    assert np.array_equal(kL.view(np.uint8), rkL.view(np.uint8)) and len(kR) == 0
+    assert kept == 0 and np.all(uR == -1) and np.all(dep == -1) and len(uR) == len(kL)
+    # different sizes: the steps one after the other; the stereo matcher refuses the pair
+    imR2, _ = stereo_pair(10, 752, 480)
+    with pytest.raises(pkg.OrbxError):
+        pkg.ExtractStereo(eL, eR, imL, imR2, m, MB, float(MBF))
+    # and the pair path again after all that
+    imL, imR = stereo_pair(11, 1241, 376)
+    got = pkg.ExtractStereo(eL, eR, imL, imR, m, MB, float(MBF))
+    want = oracle(imL, imR)
+    assert np.array_equal(got[4], want[4]) and got[6] == want[6]

@@ -134,14 +134,20 @@ def test_shim_matcher_methods_match_oracle(pkg, O, tmp_path, op, kw):
     assert want[0] > 20  # the scene exercises the method
 
 
+_STEREO_REFS = {}
+
+
 @pytest.mark.gpu
-def test_shim_stereo_frame_matches_oracle(pkg, O, tmp_path):
-    """The stereo Frame constructor through the shim over 16 stereo pairs: two
-    ORBextractors driven from two std::threads per Frame, as the reference does
-    (src/Frame.cc:77-80), then Frame::ComputeStereoMatches (:465-639) over
-    orbm_compute_stereo_matches, against the oracle's extraction + stereo
-    matching. The first Frame of the process also races the two handles'
-    first launches (the per-device BRIEF table upload)."""
+@pytest.mark.parametrize("threads", [0, 1])
+def test_shim_stereo_frame_matches_oracle(pkg, O, tmp_path, threads):
+    """The stereo Frame constructor through the shim over 16 stereo pairs, against
+    the oracle's extraction + stereo matching. threads=0: the drop-in body
+    Frame::ExtractStereo (both extractions and ComputeStereoMatches with one
+    device round trip, orbm_stereo_frame). threads=1 (ORBX_STEREO_THREADS=1): the
+    reference's structure, two ORBextractors driven from two std::threads per
+    Frame (src/Frame.cc:77-80), then Frame::ComputeStereoMatches (:465-639) over
+    orbm_compute_stereo_matches_last; its first Frame also races the two
+    handles' first launches (the per-device BRIEF table upload)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from orb_slam_cuda_amd.synth import stereo_pair
@@ -151,8 +157,9 @@ def test_shim_stereo_frame_matches_oracle(pkg, O, tmp_path):
     lp, rp = tmp_path / "l.u8", tmp_path / "r.u8"
     np.ascontiguousarray(np.stack([p[0] for p in pairs])).tofile(lp)
     np.ascontiguousarray(np.stack([p[1] for p in pairs])).tofile(rp)
+    env = dict(os.environ, ORBX_STEREO_THREADS=str(threads))
     r = subprocess.run([DRIVER, "--stereo", str(lp), str(rp), str(n), str(W), str(H), repr(bf), str(tmp_path)],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
     cfg = O.config(nfeatures=2000, width=W, height=H)
     info = O.level_info(cfg)
@@ -160,12 +167,15 @@ def test_shim_stereo_frame_matches_oracle(pkg, O, tmp_path):
     assert mb == np.float32(bf) / np.float32(718.856)
 
     def ref(i):
+        if i in _STEREO_REFS:
+            return _STEREO_REFS[i]
         L, R = pairs[i]
         kl, dl = O.extract(cfg, L)
         kr, dr = O.extract(cfg, R)
         ru, rd, rk = O.compute_stereo_matches(kl, dl, kr, dr, O.pyramid(cfg, L), O.pyramid(cfg, R), info["scale"],
                                               info["inv_scale"], mb, np.float32(bf))
-        return kl, dl, kr, dr, ru, rd, rk
+        _STEREO_REFS[i] = (kl, dl, kr, dr, ru, rd, rk)
+        return _STEREO_REFS[i]
 
     with ThreadPoolExecutor(8) as ex:
         refs = list(ex.map(ref, range(n)))
