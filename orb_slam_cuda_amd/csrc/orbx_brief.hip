@@ -133,7 +133,12 @@ __global__ __launch_bounds__(kObThreads) void orient_brief_kernel(ExtractParams 
     if (i < l) before += ci;
     tot += ci;
   }
-  if (bx == 0 && tid == 0) out_counts[f] = tot;
+  if (bx == 0 && tid == 0) {
+    out_counts[f] = tot;
+    // the earlier stages' status word beside the count (single-frame calls:
+    // one read-back carries both; they finished before this launch began)
+    if (P.status_dst && f == 0) *P.status_dst = *P.status_src;
+  }
 
   // ---- the keypoint of this half-wave
   const int idx = slot - g_kbase;

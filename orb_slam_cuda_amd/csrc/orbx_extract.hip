@@ -17,10 +17,12 @@ namespace orbx {
 
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames, int batch,
                    size_t frame_pitch, size_t row_stride, orbx_kp* d_kps, uint8_t* d_desc, int* d_counts,
-                   void* stream_, void** ev, void* pyr_event) {
+                   void* stream_, void** ev, void* pyr_event, int* status_dst) {
   hipStream_t stream = (hipStream_t)stream_;
   ExtractParams Q = P;
   Q.B = batch;
+  Q.status_src = status_dst ? X.err : nullptr;
+  Q.status_dst = status_dst;
   LevelPtrs lp;
   lp.base[0] = d_frames;
   lp.fstride[0] = (long long)frame_pitch;

@@ -118,6 +118,11 @@ struct ExtractParams {
   int blur_tiles[2], blur_ntiles[2];
   unsigned blur_magic[2];
   LevelGeom lv[kMaxLevels];
+  // single-frame calls: the device status word copied to status_dst by the
+  // last stage (orient_brief_kernel), so the output block carries it and one
+  // read-back serves both (null otherwise)
+  const int* status_src;
+  int* status_dst;
 };
 
 inline void select_pyr_plan(ExtractParams& P, int i) {
@@ -213,7 +218,7 @@ struct ExtractBuffers {
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames,
                    int batch, size_t frame_pitch, size_t row_stride, orbx_kp* d_kps,
                    uint8_t* d_desc, int* d_counts, void* stream, void** stage_events,
-                   void* pyr_event = nullptr);
+                   void* pyr_event = nullptr, int* status_dst = nullptr);
 
 // orbx_match.hip
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap,
