@@ -1490,10 +1490,22 @@ int orbx_event_elapsed_ms(void* a, void* b, float* ms) {
 
 }  // extern "C"
 
+int orbx::copy_to_host_async(void* host_dst, const void* dev_src, size_t bytes, hipStream_t stream) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, host_dst, 0) != hipSuccess) return fail(ORBX_EDEVICE, "hipHostGetDevicePointer failed");
+  const int blocks = (int)std::min<size_t>(64, (bytes + 4095) / 4096);
+  hipLaunchKernelGGL(orbx::copy2d_kernel, dim3(std::max(blocks, 1)), dim3(256), 0, stream, (uint8_t*)d, bytes,
+                     (const uint8_t*)dev_src, bytes, bytes, (size_t)1);
+  return hipGetLastError() == hipSuccess ? ORBX_OK : fail(ORBX_EDEVICE, "copy kernel launch failed");
+}
+
 int orbx::extract_pair(orbx_handle L, orbx_handle R, const uint8_t* imL, size_t strideL, const uint8_t* imR,
                        size_t strideR, int w, int hh, const std::function<int(hipStream_t)>& between,
                        orbx_kp* kpsL, int capL, uint8_t* descL, int* nL, orbx_kp* kpsR, int capR, uint8_t* descR,
-                       int* nR) {
+                       int* nR, double* stamps) {
+  auto stamp = [stamps](int i) {
+    if (stamps) stamps[i] = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
   if (!L || !R || !nL || !nR) return fail(ORBX_EINVAL, "null argument");
   if (L == R) return fail(ORBX_EINVAL, "left and right need two extractor handles");
   if (w <= 0 || hh <= 0) return fail(ORBX_EINVAL, "empty image");
@@ -1503,12 +1515,17 @@ int orbx::extract_pair(orbx_handle L, orbx_handle R, const uint8_t* imL, size_t 
   *nL = *nR = 0;
   // left first: its chain runs while the right image is staged
   int rc;
-  if ((rc = extract_submit(L, imL, w, hh, strideL, nullptr)) || (rc = extract_submit(R, imR, w, hh, strideR, nullptr)))
-    return rc;
-  const int rb = between(L->stream);
+  if ((rc = extract_submit(L, imL, w, hh, strideL, nullptr))) return rc;
+  stamp(0);
+  if ((rc = extract_submit(R, imR, w, hh, strideR, nullptr))) return rc;
+  stamp(1);
+  const int rb = between(R->stream);
+  stamp(2);
   // both streams: `between` may have failed before it ordered anything after the right chain
   HIP_OK(hipStreamSynchronize(L->stream));
   HIP_OK(hipStreamSynchronize(R->stream));
+  stamp(3);
   if ((rc = extract_finish(L, kpsL, capL, descL, nL)) || (rc = extract_finish(R, kpsR, capR, descR, nR))) return rc;
+  stamp(4);
   return rb;
 }

@@ -385,15 +385,21 @@ int raise_lds_limit(const void* fn, size_t bytes);
 // orbx_host.hip: the pyramid of frames [frame0, frame0 + n) of an extractor's last extraction
 int extractor_pyramid(orbx_handle h, int frame0, int n, LevelPtrs* lp, int* w, int* hgt, float* scale,
                       float* inv_scale, int* L);
+// orbx_host.hip: `bytes` from device memory to pinned host memory by a copy
+// kernel on `stream` (a blit launch, as a graph's memcpy node runs, instead of
+// a copy-engine transfer and its start-up latency)
+int copy_to_host_async(void* host_dst, const void* dev_src, size_t bytes, hipStream_t stream);
 // orbx_host.hip: the stereo Frame's two extractions (src/Frame.cc:77-80) as two
 // orbx_extract calls make them, from one thread and with one wait: left staged
 // and launched on its handle's stream, right on its own (the two run
-// concurrently), then `between(left's stream)` enqueues the work that reads
-// both outputs on the device (ComputeStereoMatches), then both streams are
-// waited for and the outputs copied out. Two distinct handles, non-empty
-// images of one size.
+// concurrently), then `between(right's stream)` enqueues the work that reads
+// both outputs on the device (ComputeStereoMatches; the left chain, started
+// first, has normally finished by then, so its wait costs nothing on the
+// critical path), then both streams are waited for and the outputs copied
+// out. Two distinct handles, non-empty images of one size.
 int extract_pair(orbx_handle L, orbx_handle R, const uint8_t* imL, size_t strideL, const uint8_t* imR,
                  size_t strideR, int w, int h, const std::function<int(hipStream_t)>& between, orbx_kp* kpsL,
-                 int capL, uint8_t* descL, int* nL, orbx_kp* kpsR, int capR, uint8_t* descR, int* nR);
+                 int capL, uint8_t* descL, int* nL, orbx_kp* kpsR, int capR, uint8_t* descR, int* nR,
+                 double* stamps = nullptr);  // diagnostics: host clock after each of its 5 phases
 
 }  // namespace orbx

@@ -21,12 +21,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -2029,13 +2031,41 @@ int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handl
   return ORBX_OK;
 }
 
+// orbm_stereo_frame's host phases (ORBX_STEREO_PROF=1): left staged + issued,
+// right staged + issued, stereo issued, waited, copied out; medians of the
+// calls after the first 20, printed at exit
+struct StereoProf {
+  std::mutex mu;
+  std::vector<double> t[5];
+  void add(const double* st) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (int k = 0; k < 5; ++k) t[k].push_back(st[k + 1] - st[k]);
+  }
+  ~StereoProf() {
+    if (t[0].size() <= 20) return;
+    const char* names[5] = {"left staged+issued", "right staged+issued", "stereo issued", "wait", "copy-out"};
+    fprintf(stderr, "orbm_stereo_frame host phases, median of %zu calls (us):", t[0].size() - 20);
+    for (int k = 0; k < 5; ++k) {
+      std::vector<double> v(t[k].begin() + 20, t[k].end());
+      std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+      fprintf(stderr, " %s %.1f", names[k], v[v.size() / 2] * 1e6);
+    }
+    fprintf(stderr, "\n");
+  }
+};
+static StereoProf& stereo_prof() {
+  static StereoProf p;
+  return p;
+}
+
 // The stereo Frame's construction steps (src/Frame.cc:77-89: ExtractORB on
 // threadLeft / threadRight, then ComputeStereoMatches :465-639) with one
 // device round trip: both extraction chains are issued from the calling
 // thread on the two handles' streams (they run concurrently), the stereo
-// kernel follows on the left stream once both are done, and its {kept,
-// uRight, depth} block comes back in the same wait as the two extractions'
-// outputs. Results are those of orbx_extract x2 + orbm_compute_stereo_matches_last.
+// kernels follow on the right stream once both are done, and their {kept,
+// uRight, depth} block comes back (a copy kernel into pinned memory) in the
+// same wait as the two extractions' outputs. Results are those of
+// orbx_extract x2 + orbm_compute_stereo_matches_last.
 int orbm_stereo_frame(orbm_handle m, orbx_handle left, orbx_handle right, const uint8_t* img_left,
                       size_t stride_left, const uint8_t* img_right, size_t stride_right, int w, int h, float mb,
                       float mbf, orbx_kp* kps_left, int cap_left, uint8_t* desc_left, int* n_left,
@@ -2075,11 +2105,16 @@ int orbm_stereo_frame(orbm_handle m, orbx_handle left, orbx_handle right, const 
                                            dd, dk, st);
     if (rc == ORBX_ECAPACITY) return (brc = ORBX_ECAPACITY), ORBX_OK;  // checked before any launch
     if (rc) return brc = rc;
-    MHIP(hipMemcpyAsync(m->h_stage, dk, bytes, hipMemcpyDeviceToHost, st));
+    if ((rc = copy_to_host_async(m->h_stage, dk, bytes, st))) return brc = mfail(rc, "%s", orbx_last_error());
     return ORBX_OK;
   };
+  // ORBX_STEREO_PROF=1 (diagnostics): host phases per call, medians printed at exit
+  static const bool prof = getenv("ORBX_STEREO_PROF") && getenv("ORBX_STEREO_PROF")[0] == '1';
+  double st[6];
+  if (prof) st[0] = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   int rc = extract_pair(left, right, img_left, stride_left, img_right, stride_right, w, h, between, kps_left, cap_left,
-                        desc_left, n_left, kps_right, cap_right, desc_right, n_right);
+                        desc_left, n_left, kps_right, cap_right, desc_right, n_right, prof ? st + 1 : nullptr);
+  if (prof && !rc) stereo_prof().add(st);
   if (rc) return brc ? brc : mfail(rc, "stereo frame: %s", orbx_last_error());
   if (brc == ORBX_ECAPACITY)
     return orbm_compute_stereo_matches_last(m, left, right, mb, mbf, uRight, depth, *n_left, nkept);
