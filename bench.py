@@ -204,16 +204,17 @@ def parse_args(argv=None):
 # Tuning: select among bit-exact code paths; allowed, and stamped into the line.
 ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_EXTRACT_ORDER", "ORBX_PYR_PLAN", "ORBX_QT_GENERIC",
               "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS",
-              "ORBX_BOW_ROUNDS", "ORBX_PYR_KEEP",
+              "ORBX_BOW_ROUNDS", "ORBX_PYR_KEEP", "ORBX_QT_SORTED", "ORBX_QT_LDS_KB",
               # the C++ shim's configuration (shim/src/ORBextractor.cc); bench.py does not read them
-              "ORBX_DEVICE", "ORBX_SCALE_MODE", "ORBX_PATTERN", "ORBX_HOST_PYRAMID"}
+              "ORBX_DEVICE", "ORBX_SCALE_MODE", "ORBX_PATTERN", "ORBX_HOST_PYRAMID",
+              "ORBX_STEREO_THREADS"}
 # Diagnostics: phase clocks synchronise after every launch, *_STOP / FAST_TWICE
 # skip or repeat work (they only act in -DORBX_DIAG builds), ORBX_LIB_VARIANT
 # loads an A/B build of the library. A timed region under any of them is not
 # the product's: refused unless --allow-diag.
 ENV_DIAG = {"ORBX_LIB_VARIANT", "ORBX_FAST_TWICE", "ORBX_INIT_STOP", "ORBX_STEREO_STOP", "ORBX_VOC_STOP",
             "ORBX_FAST_PROF", "ORBX_PYR_PROF", "ORBX_QT_PROF", "ORBX_INIT_PROF", "ORBX_BOW_PROF", "ORBX_PROJ_PROF",
-            "ORBX_EXTRACT_PROF", "ORBX_PYR_PADMOD",
+            "ORBX_EXTRACT_PROF", "ORBX_PYR_PADMOD", "ORBX_STEREO_PROF",
             }
 
 
