@@ -9,7 +9,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cfloat>
 #include <cstdarg>
 #include <climits>
@@ -19,6 +21,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "orbx_internal.h"
@@ -148,6 +151,8 @@ struct orbx_extractor {
   long long h_pyr_off[kMaxLevels] = {};  // level l's offset in h_pyr (l >= 1)
   hipStream_t pstream = nullptr;         // the copy branch's stream (capture fork)
   hipEvent_t pev[2] = {};                // pyramid done, copy done
+  hipStream_t bstream = nullptr;         // the blur branch's stream (ORBX_BLUR_FORK=1)
+  hipEvent_t bev[2] = {};                // pyramid done, blur done
   // ORBX_EXTRACT_PROF=1 (diagnostics): orbx_extract's host phases per call
   // (s), their medians printed by orbx_destroy: staging copy, issue, wait, copy-out
   std::vector<float> prof_t[4];
@@ -964,6 +969,10 @@ int orbx_destroy(orbx_handle h) {
   for (auto& e : h->pev)
     if (e) (void)hipEventDestroy(e);
   if (h->pstream) (void)hipStreamDestroy(h->pstream);
+  if (h->bstream) (void)hipStreamSynchronize(h->bstream);
+  for (auto& e : h->bev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->bstream) (void)hipStreamDestroy(h->bstream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return ORBX_OK;
@@ -1034,9 +1043,11 @@ static int issue_one_frame(orbx_extractor* h, size_t pitch, int hh, int cap_fram
   uint8_t* d = h->d_out.as<uint8_t>();
   const size_t doff = out_desc_off(cap_frame);
   const bool hp = h->host_pyr && P.L > 1;
+  const BlurFork fork{h->bstream, h->bev[0], h->bev[1]};
   const int rc = launch_extract(P, buffers_of(h->plan), h->d_in.as<uint8_t>(), 1, pitch * hh, pitch,
                                 (orbx_kp*)(d + 16), d + doff, (int*)d, s, h->timing ? (void**)h->ev : nullptr,
-                                hp ? (void*)h->pev[0] : nullptr, (int*)d + 1);
+                                hp ? (void*)h->pev[0] : nullptr, (int*)d + 1,
+                                h->bstream ? &fork : nullptr);
   if (rc) return fail(rc, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (hp) {
     // fork: the pyramid levels go to pinned host memory beside FAST .. BRIEF
@@ -1066,7 +1077,10 @@ static int issue_one_frame(orbx_extractor* h, size_t pitch, int hh, int cap_fram
 // {count, status, keypoints, descriptors}) issued on its stream; the handle's
 // lock is held, the image is not empty. extract_finish: after that stream was
 // waited for, the outputs copied out of the pinned block.
-static int extract_submit(orbx_extractor* h, const uint8_t* img, int w, int hh, size_t stride, double* t_staged) {
+// extract_submit = extract_prepare (plan and buffers for the image size),
+// extract_stage (the copy into the pinned staging; no HIP call, so another
+// thread may run it) and extract_issue (the chain on the handle's stream).
+static int extract_prepare(orbx_extractor* h, const uint8_t* img, int w, int hh, size_t stride) {
   h->last_empty = false;
   if (!img || w < 0 || hh < 0 || stride < (size_t)w) return fail(ORBX_EINVAL, "bad image");
   HIP_OK(hipSetDevice(h->cfg.device));
@@ -1103,6 +1117,13 @@ static int extract_submit(orbx_extractor* h, const uint8_t* img, int w, int hh, 
   if (!h->stream) HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   h->host_pyr_valid = false;
   if (h->graph && h->graph_hp != h->host_pyr) drop_graph();  // captured with / without the copy branch
+  // ORBX_BLUR_FORK=1: the blur on a branch beside FAST and the quadtree (A/B)
+  static const bool blur_fork = getenv("ORBX_BLUR_FORK") && getenv("ORBX_BLUR_FORK")[0] == '1';
+  if (blur_fork && !h->bstream) {
+    drop_graph();
+    HIP_OK(hipStreamCreateWithFlags(&h->bstream, hipStreamNonBlocking));
+    for (auto& e : h->bev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   if (h->host_pyr) {
     const size_t pb = host_pyr_layout(h);
     if (h->h_pyr_bytes < pb) drop_graph();
@@ -1111,12 +1132,30 @@ static int extract_submit(orbx_extractor* h, const uint8_t* img, int w, int hh, 
     for (auto& e : h->pev)
       if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
+  return ORBX_OK;
+}
+
+static void extract_stage(orbx_extractor* h, const uint8_t* img, int w, int hh, size_t stride) {
   // the pinned staging buffer is free: every call waits for its chain before it returns
   // (plain stores: streaming ones that skip the destination's read-for-ownership
   // measured slower, 0.108 vs 0.100 ms per call: the copy engine then reads DRAM
   // instead of lines still in the host's caches)
-  for (int y = 0; y < hh; ++y) memcpy((uint8_t*)h->h_in + (size_t)y * pitch, img + (size_t)y * stride, w);
-  if (t_staged) *t_staged = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  const size_t pitch = ((size_t)w + 63) & ~(size_t)63;
+  if (stride == pitch) {
+    memcpy(h->h_in, img, pitch * hh);
+  } else {
+    for (int y = 0; y < hh; ++y) memcpy((uint8_t*)h->h_in + (size_t)y * pitch, img + (size_t)y * stride, w);
+  }
+}
+
+static int extract_issue(orbx_extractor* h, int w, int hh) {
+  const int cap_frame = h->plan.P.kp_per_frame;
+  const size_t pitch = ((size_t)w + 63) & ~(size_t)63;
+  int rc;
+  auto drop_graph = [&]() {
+    if (h->graph) (void)hipGraphExecDestroy(h->graph);
+    h->graph = nullptr;
+  };
   // the plan buffers may still be in use by a batch call on another stream
   if (h->ws.before(h->stream)) return fail(ORBX_EDEVICE, "stream wait on the handle's last use failed");
   static const bool use_graph = !(getenv("ORBX_EXTRACT_GRAPH") && getenv("ORBX_EXTRACT_GRAPH")[0] == '0');
@@ -1158,6 +1197,14 @@ static int extract_submit(orbx_extractor* h, const uint8_t* img, int w, int hh, 
   h->last_fpitch = pitch * hh;
   h->last_rstride = pitch;
   return ORBX_OK;
+}
+
+static int extract_submit(orbx_extractor* h, const uint8_t* img, int w, int hh, size_t stride, double* t_staged) {
+  const int rc = extract_prepare(h, img, w, hh, stride);
+  if (rc) return rc;
+  extract_stage(h, img, w, hh, stride);
+  if (t_staged) *t_staged = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  return extract_issue(h, w, hh);
 }
 
 static int extract_finish(orbx_extractor* h, orbx_kp* kps, int cap, uint8_t* desc, int* n) {
@@ -1499,6 +1546,76 @@ int orbx::copy_to_host_async(void* host_dst, const void* dev_src, size_t bytes, 
   return hipGetLastError() == hipSuccess ? ORBX_OK : fail(ORBX_EDEVICE, "copy kernel launch failed");
 }
 
+// A process-wide helper thread for orbm_stereo_frame: it copies the right
+// image into its handle's pinned staging while the calling thread stages and
+// issues the left one, so the two copies take two host cores as the
+// reference's two extraction threads do, without spawning threads per frame.
+// One job at a time: a caller that finds it busy copies inline. The worker
+// makes no HIP call. ORBX_STAGE_THREAD=0: both copies on the calling thread.
+namespace {
+class StageHelper {
+ public:
+  static StageHelper& get() {
+    static StageHelper s;
+    return s;
+  }
+  bool try_post(orbx_extractor* h, const uint8_t* img, int w, int hh, size_t stride) {
+    if (busy_.test_and_set(std::memory_order_acquire)) return false;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+      h_ = h;
+      img_ = img;
+      w_ = w;
+      hh_ = hh;
+      stride_ = stride;
+      state_.store(1, std::memory_order_relaxed);
+    }
+    cv_.notify_one();
+    return true;
+  }
+  void wait() {  // the posted copy is done (spin briefly, then yield)
+    for (int i = 0; state_.load(std::memory_order_acquire) != 2; ++i) {
+      if (i < 2000) __builtin_ia32_pause();
+      else std::this_thread::yield();
+    }
+    state_.store(0, std::memory_order_relaxed);
+    busy_.clear(std::memory_order_release);
+  }
+  ~StageHelper() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_ = true;
+    }
+    cv_.notify_one();
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [this] { return quit_ || state_.load(std::memory_order_relaxed) == 1; });
+      if (quit_) return;
+      lk.unlock();
+      extract_stage(h_, img_, w_, hh_, stride_);
+      state_.store(2, std::memory_order_release);
+      lk.lock();
+    }
+  }
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::atomic_flag busy_ = ATOMIC_FLAG_INIT;
+  std::atomic<int> state_{0};  // 0 idle, 1 posted, 2 done
+  bool quit_ = false;
+  orbx_extractor* h_ = nullptr;
+  const uint8_t* img_ = nullptr;
+  int w_ = 0, hh_ = 0;
+  size_t stride_ = 0;
+};
+}  // namespace
+
 int orbx::extract_pair(orbx_handle L, orbx_handle R, const uint8_t* imL, size_t strideL, const uint8_t* imR,
                        size_t strideR, int w, int hh, const std::function<int(hipStream_t)>& between,
                        orbx_kp* kpsL, int capL, uint8_t* descL, int* nL, orbx_kp* kpsR, int capR, uint8_t* descR,
@@ -1515,17 +1632,28 @@ int orbx::extract_pair(orbx_handle L, orbx_handle R, const uint8_t* imL, size_t 
   *nL = *nR = 0;
   // left first: its chain runs while the right image is staged
   int rc;
-  if ((rc = extract_submit(L, imL, w, hh, strideL, nullptr))) return rc;
+  if ((rc = extract_prepare(L, imL, w, hh, strideL)) || (rc = extract_prepare(R, imR, w, hh, strideR))) return rc;
+  static const bool use_helper = !(getenv("ORBX_STAGE_THREAD") && getenv("ORBX_STAGE_THREAD")[0] == '0');
+  const bool posted = use_helper && StageHelper::get().try_post(R, imR, w, hh, strideR);
+  extract_stage(L, imL, w, hh, strideL);
   stamp(0);
-  if ((rc = extract_submit(R, imR, w, hh, strideR, nullptr))) return rc;
+  if ((rc = extract_issue(L, w, hh))) {
+    if (posted) StageHelper::get().wait();
+    return rc;
+  }
   stamp(1);
-  const int rb = between(R->stream);
+  if (posted) StageHelper::get().wait();
+  else extract_stage(R, imR, w, hh, strideR);
   stamp(2);
+  if ((rc = extract_issue(R, w, hh))) return rc;
+  stamp(3);
+  const int rb = between(R->stream);
+  stamp(4);
   // both streams: `between` may have failed before it ordered anything after the right chain
   HIP_OK(hipStreamSynchronize(L->stream));
   HIP_OK(hipStreamSynchronize(R->stream));
-  stamp(3);
+  stamp(5);
   if ((rc = extract_finish(L, kpsL, capL, descL, nL)) || (rc = extract_finish(R, kpsR, capR, descR, nR))) return rc;
-  stamp(4);
+  stamp(6);
   return rb;
 }

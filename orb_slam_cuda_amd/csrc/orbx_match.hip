@@ -2031,26 +2031,33 @@ int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handl
   return ORBX_OK;
 }
 
-// orbm_stereo_frame's host phases (ORBX_STEREO_PROF=1): left staged + issued,
-// right staged + issued, stereo issued, waited, copied out; medians of the
-// calls after the first 20, printed at exit
+// orbm_stereo_frame's host phases (ORBX_STEREO_PROF=1): left staged, issued,
+// right staged, issued, stereo issued, waited, copied out; medians of the
+// calls after the first 20 per left handle, printed at exit
 struct StereoProf {
   std::mutex mu;
-  std::vector<double> t[5];
-  void add(const double* st) {
+  std::vector<std::pair<const void*, std::vector<double>>> per;  // per left handle: 7 phases per call
+  void add(const void* key, const double* st) {
     std::lock_guard<std::mutex> lk(mu);
-    for (int k = 0; k < 5; ++k) t[k].push_back(st[k + 1] - st[k]);
+    size_t i = 0;
+    while (i < per.size() && per[i].first != key) ++i;
+    if (i == per.size()) per.push_back({key, {}});
+    for (int k = 0; k < 7; ++k) per[i].second.push_back(st[k + 1] - st[k]);
   }
   ~StereoProf() {
-    if (t[0].size() <= 20) return;
-    const char* names[5] = {"left staged+issued", "right staged+issued", "stereo issued", "wait", "copy-out"};
-    fprintf(stderr, "orbm_stereo_frame host phases, median of %zu calls (us):", t[0].size() - 20);
-    for (int k = 0; k < 5; ++k) {
-      std::vector<double> v(t[k].begin() + 20, t[k].end());
-      std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
-      fprintf(stderr, " %s %.1f", names[k], v[v.size() / 2] * 1e6);
+    const char* names[7] = {"left staged", "issued", "right staged", "issued", "stereo issued", "wait", "copy-out"};
+    for (auto& e : per) {
+      const size_t n = e.second.size() / 7;
+      if (n <= 20) continue;
+      fprintf(stderr, "orbm_stereo_frame host phases, median of %zu calls (us):", n - 20);
+      for (int k = 0; k < 7; ++k) {
+        std::vector<double> v;
+        for (size_t c = 20; c < n; ++c) v.push_back(e.second[c * 7 + k]);
+        std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+        fprintf(stderr, " %s %.1f", names[k], v[v.size() / 2] * 1e6);
+      }
+      fprintf(stderr, "\n");
     }
-    fprintf(stderr, "\n");
   }
 };
 static StereoProf& stereo_prof() {
@@ -2110,11 +2117,11 @@ int orbm_stereo_frame(orbm_handle m, orbx_handle left, orbx_handle right, const 
   };
   // ORBX_STEREO_PROF=1 (diagnostics): host phases per call, medians printed at exit
   static const bool prof = getenv("ORBX_STEREO_PROF") && getenv("ORBX_STEREO_PROF")[0] == '1';
-  double st[6];
+  double st[8];
   if (prof) st[0] = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   int rc = extract_pair(left, right, img_left, stride_left, img_right, stride_right, w, h, between, kps_left, cap_left,
                         desc_left, n_left, kps_right, cap_right, desc_right, n_right, prof ? st + 1 : nullptr);
-  if (prof && !rc) stereo_prof().add(st);
+  if (prof && !rc) stereo_prof().add(left, st);
   if (rc) return brc ? brc : mfail(rc, "stereo frame: %s", orbx_last_error());
   if (brc == ORBX_ECAPACITY)
     return orbm_compute_stereo_matches_last(m, left, right, mb, mbf, uRight, depth, *n_left, nkept);
