@@ -205,6 +205,7 @@ def parse_args(argv=None):
 ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_EXTRACT_ORDER", "ORBX_PYR_PLAN", "ORBX_QT_GENERIC",
               "ORBX_PROJ_ROUNDS", "ORBX_TOP2_VALU", "ORBX_VOC_GL", "ORBX_STEREO_GROUPS",
               "ORBX_BOW_ROUNDS", "ORBX_PYR_KEEP", "ORBX_QT_SORTED", "ORBX_QT_LDS_KB",
+              "ORBX_STAGE_THREAD",
               # the C++ shim's configuration (shim/src/ORBextractor.cc); bench.py does not read them
               "ORBX_DEVICE", "ORBX_SCALE_MODE", "ORBX_PATTERN", "ORBX_HOST_PYRAMID",
               "ORBX_STEREO_THREADS"}

@@ -17,7 +17,7 @@ namespace orbx {
 
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames, int batch,
                    size_t frame_pitch, size_t row_stride, orbx_kp* d_kps, uint8_t* d_desc, int* d_counts,
-                   void* stream_, void** ev, void* pyr_event, int* status_dst, const BlurFork* fork) {
+                   void* stream_, void** ev, void* pyr_event, int* status_dst) {
   hipStream_t stream = (hipStream_t)stream_;
   ExtractParams Q = P;
   Q.B = batch;
@@ -49,29 +49,14 @@ int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_
     return e;
   }();
   int rc;
-  // the blur branch needs the default order (and no stage events, which time one stream)
-  if (fork && (ev || strcmp(order, "pbfqo") != 0)) fork = nullptr;
   rec(0);
   for (int i = 0; i < 5; ++i) {
     switch (order[i]) {
       case 'p': rc = launch_pyramid(Q, lp, X.rtab, batch, stream); break;
-      case 'b':
-        if (fork) {
-          if (hipEventRecord(fork->after_pyr, stream) != hipSuccess ||
-              hipStreamWaitEvent(fork->s, fork->after_pyr, 0) != hipSuccess)
-            return ORBX_EDEVICE;
-          rc = launch_blur(Q, lp, X.rtab, X.blur, batch, fork->s);
-          if (!rc && hipEventRecord(fork->after_blur, fork->s) != hipSuccess) return ORBX_EDEVICE;
-        } else {
-          rc = launch_blur(Q, lp, X.rtab, X.blur, batch, stream);
-        }
-        break;
+      case 'b': rc = launch_blur(Q, lp, X.rtab, X.blur, batch, stream); break;
       case 'f': rc = launch_fast(Q, lp, X.cells, X.slots, X.cell_counts, batch, stream); break;
       case 'q': rc = launch_quadtree(Q, X, batch, stream); break;
-      default:
-        if (fork && hipStreamWaitEvent(stream, fork->after_blur, 0) != hipSuccess) return ORBX_EDEVICE;
-        rc = launch_orient_brief(Q, lp, X, d_kps, d_desc, d_counts, batch, stream);
-        break;
+      default: rc = launch_orient_brief(Q, lp, X, d_kps, d_desc, d_counts, batch, stream); break;
     }
     if (rc) return rc;
     if (order[i] == 'p' && pyr_event && hipEventRecord((hipEvent_t)pyr_event, stream) != hipSuccess)

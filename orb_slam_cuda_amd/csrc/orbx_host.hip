@@ -151,8 +151,6 @@ struct orbx_extractor {
   long long h_pyr_off[kMaxLevels] = {};  // level l's offset in h_pyr (l >= 1)
   hipStream_t pstream = nullptr;         // the copy branch's stream (capture fork)
   hipEvent_t pev[2] = {};                // pyramid done, copy done
-  hipStream_t bstream = nullptr;         // the blur branch's stream (ORBX_BLUR_FORK=1)
-  hipEvent_t bev[2] = {};                // pyramid done, blur done
   // ORBX_EXTRACT_PROF=1 (diagnostics): orbx_extract's host phases per call
   // (s), their medians printed by orbx_destroy: staging copy, issue, wait, copy-out
   std::vector<float> prof_t[4];
@@ -969,10 +967,6 @@ int orbx_destroy(orbx_handle h) {
   for (auto& e : h->pev)
     if (e) (void)hipEventDestroy(e);
   if (h->pstream) (void)hipStreamDestroy(h->pstream);
-  if (h->bstream) (void)hipStreamSynchronize(h->bstream);
-  for (auto& e : h->bev)
-    if (e) (void)hipEventDestroy(e);
-  if (h->bstream) (void)hipStreamDestroy(h->bstream);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return ORBX_OK;
@@ -1043,11 +1037,9 @@ static int issue_one_frame(orbx_extractor* h, size_t pitch, int hh, int cap_fram
   uint8_t* d = h->d_out.as<uint8_t>();
   const size_t doff = out_desc_off(cap_frame);
   const bool hp = h->host_pyr && P.L > 1;
-  const BlurFork fork{h->bstream, h->bev[0], h->bev[1]};
   const int rc = launch_extract(P, buffers_of(h->plan), h->d_in.as<uint8_t>(), 1, pitch * hh, pitch,
                                 (orbx_kp*)(d + 16), d + doff, (int*)d, s, h->timing ? (void**)h->ev : nullptr,
-                                hp ? (void*)h->pev[0] : nullptr, (int*)d + 1,
-                                h->bstream ? &fork : nullptr);
+                                hp ? (void*)h->pev[0] : nullptr, (int*)d + 1);
   if (rc) return fail(rc, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (hp) {
     // fork: the pyramid levels go to pinned host memory beside FAST .. BRIEF
@@ -1117,13 +1109,6 @@ static int extract_prepare(orbx_extractor* h, const uint8_t* img, int w, int hh,
   if (!h->stream) HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   h->host_pyr_valid = false;
   if (h->graph && h->graph_hp != h->host_pyr) drop_graph();  // captured with / without the copy branch
-  // ORBX_BLUR_FORK=1: the blur on a branch beside FAST and the quadtree (A/B)
-  static const bool blur_fork = getenv("ORBX_BLUR_FORK") && getenv("ORBX_BLUR_FORK")[0] == '1';
-  if (blur_fork && !h->bstream) {
-    drop_graph();
-    HIP_OK(hipStreamCreateWithFlags(&h->bstream, hipStreamNonBlocking));
-    for (auto& e : h->bev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
   if (h->host_pyr) {
     const size_t pb = host_pyr_layout(h);
     if (h->h_pyr_bytes < pb) drop_graph();

@@ -213,19 +213,12 @@ struct ExtractBuffers {
   int* err;            // device error word
 };
 
-// The blur on a branch of its own (single-frame calls): forked after the
-// pyramid on `s`, joined before orient+BRIEF, so it runs beside FAST and the
-// quadtree instead of ahead of them (it feeds only the descriptors)
-struct BlurFork {
-  hipStream_t s;
-  hipEvent_t after_pyr, after_blur;
-};
 // pyr_event (optional): recorded on `stream` right after the pyramid stage, so
 // a caller can fork work that only needs the pyramid (orbx_extract's host copy)
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames,
                    int batch, size_t frame_pitch, size_t row_stride, orbx_kp* d_kps,
                    uint8_t* d_desc, int* d_counts, void* stream, void** stage_events,
-                   void* pyr_event = nullptr, int* status_dst = nullptr, const BlurFork* fork = nullptr);
+                   void* pyr_event = nullptr, int* status_dst = nullptr);
 
 // orbx_match.hip
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap,
