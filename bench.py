@@ -215,7 +215,7 @@ ENV_TUNING = {"ORBX_TIMING", "ORBX_EXTRACT_GRAPH", "ORBX_EXTRACT_ORDER", "ORBX_P
 # the product's: refused unless --allow-diag.
 ENV_DIAG = {"ORBX_LIB_VARIANT", "ORBX_FAST_TWICE", "ORBX_INIT_STOP", "ORBX_STEREO_STOP", "ORBX_VOC_STOP",
             "ORBX_FAST_PROF", "ORBX_PYR_PROF", "ORBX_QT_PROF", "ORBX_INIT_PROF", "ORBX_BOW_PROF", "ORBX_PROJ_PROF",
-            "ORBX_EXTRACT_PROF", "ORBX_PYR_PADMOD", "ORBX_STEREO_PROF",
+            "ORBX_EXTRACT_PROF", "ORBX_PYR_PADMOD", "ORBX_STEREO_PROF", "ORBX_PLAN_INFO",
             }
 
 

@@ -79,12 +79,30 @@ class OrbxError(RuntimeError):
 _lib = None
 
 
+class _Tolerant:
+    """A loaded library whose missing symbols read as throwaway objects, so the
+    signature table below can be applied to an older variant build."""
+
+    def __init__(self, L):
+        self.__dict__["_L"] = L
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._L, name)
+        except AttributeError:
+            return type("Missing", (), {})()
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise OrbxError(ORBX_EDEVICE, f"{LIB_PATH} not built; run __graft_entry__.build()")
         L = C.CDLL(LIB_PATH)
+        if os.environ.get("ORBX_LIB_VARIANT"):
+            # A/B builds of other revisions may lack newer entry points: their
+            # signatures are skipped here (a call to one fails when made)
+            L = _Tolerant(L)
         L.orbx_last_error.restype = C.c_char_p
         L.orbm_last_error.restype = C.c_char_p
         L.orbx_version.restype = C.c_char_p

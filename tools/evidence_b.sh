@@ -1,5 +1,5 @@
 #!/bin/bash
-# A round's evidence, part B (ROUND=rNN; run after part A and tools/collect.sh): per-config bench lines + rocprofv3 stats (C2, C4,
+# A round's evidence, part B (ROUND=rNN, PART=1|2|all; run after part A and tools/collect.sh): per-config bench lines + rocprofv3 stats (C2, C4,
 # C5, C3 + BoW, the KITTI14 / intcatch-1080p settings), SQ counters of the
 # serial C3 bench, FAST and search_init phase clocks, the link microbench.
 set -e
@@ -14,6 +14,8 @@ run() {  # name, bench args
     python3 bench.py --cpu-sample 0 --no-latency --no-host-stream --steps 30 --warmup 5 "$@" > $O/${name}_prof.log 2>&1
   python3 -c "import json;d=json.loads(open('$O/$name.log').read().strip().splitlines()[-1]);print('$name',d['value'],d['unit'])"
 }
+PART=${PART:-all}  # 1: the config lines and their stats, 2: counters, phases, link, final line
+if [ $PART != 2 ]; then
 run c2 --no-match
 run c4 --config stereo
 run c5 --config euroc
@@ -24,6 +26,8 @@ run intcatch1080 --config intcatch1080
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/intcatch1080_serial -o run -- \
   python3 bench.py --cpu-sample 0 --no-latency --no-host-stream --steps 30 --warmup 5 --serial --config intcatch1080 \
   > $O/intcatch1080_serial.log 2>&1
+fi
+[ $PART = 1 ] && { echo part-1-done; exit 0; }
 bash tools/qt_prof.sh > $O/qt_phases.txt 2>&1
 bash tools/pmc_sq.sh $O/sq > $O/sq.log 2>&1
 python3 tools/sq_valu.py $O/sq/summary.txt $O/sq_valu.json
