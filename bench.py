@@ -758,15 +758,17 @@ def run_mono(args, cfg, rank, world, local, dist):
     BS, S, cap = pipe.BS, pipe.S, pipe.cap
     timed = pipe.evsets[args.warmup * SUB:]
     ev_ms = timed[0][0].elapsed_ms(timed[-1][8])
+    from orb_slam_cuda_amd import _lib as _stage_lib
     names = STAGES
     ext_stages = names[:5]
+    launch_order = _stage_lib.stage_order()  # stage event i + 1 closes launch_order[i]
     STAGES_RUN = ext_stages + (["hamming_top2", "search_init"] if not args.no_match else []) \
         + (["bow_transform"] if (args.bow or args.bow_match) else []) + (["bow_match"] if args.bow_match else [])
     # per-stage average durations over the timed steps (ms per launch-group, BS frames),
     # each bracketed by events on the stream its kernels run on
     st = {s: 0.0 for s in STAGES_RUN}
     for evs in timed:
-        for i, s in enumerate(names[:5]):
+        for i, s in enumerate(launch_order):
             st[s] += evs[i].elapsed_ms(evs[i + 1])
         if args.bow or args.bow_match:
             st["bow_transform"] += evs[9].elapsed_ms(evs[10])
@@ -1353,11 +1355,12 @@ def run_stereo(args, cfg, rank, world, local, dist):
         if st["m"].status():
             raise RuntimeError("matcher device status word set")
     timed = evs[args.warmup:]
-    names = STAGES
-    stages = names[:5] + ["stereo"]
+    from orb_slam_cuda_amd import _lib as _stage_lib
+    launch_order = _stage_lib.stage_order()  # stage event i + 1 closes launch_order[i]
+    stages = STAGES[:5] + ["stereo"]
     sm = {s: 0.0 for s in stages}
     for ev in timed:
-        for i, s in enumerate(names[:5]):
+        for i, s in enumerate(launch_order):
             sm[s] += ev[i].elapsed_ms(ev[i + 1])
         sm["stereo"] += ev[6].elapsed_ms(ev[7])
     sm = {s: v / args.steps for s, v in sm.items()}

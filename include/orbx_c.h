@@ -222,16 +222,21 @@ int orbx_get_status(orbx_handle h, int reset, int* status);
  * ORBX_PATTERN_FORK (entry 96 = VX_FAILURE-2 = -3, :261-262) or
  * ORBX_PATTERN_UPSTREAM (-2). Host only, no device needed. */
 int orbx_get_pattern(int pattern_mode, int* out1024);
-/* Per-stage device time (ms) of the last extraction, stage names as the
- * reference's GetTime labels (src/ORBextractor.cc:1131,1331,1737,1753,1841).
- * Filled only when the handle was created with timing enabled
- * (ORBX_TIMING=1 in the environment). */
+/* Per-stage device time (ms) of the last extraction, in launch order
+ * (orbx_get_stage_order), stage names as the reference's GetTime labels
+ * (src/ORBextractor.cc:1131,1331,1737,1753,1841). Filled only when the handle
+ * was created with timing enabled (ORBX_TIMING=1 in the environment). */
 int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap,
                          int* n);
+/* The extraction stages' launch order as 5 letters + NUL into out[6]: p
+ * pyramid, b Gaussian blur, f FAST + grid, q quadtree, o angle + descriptor
+ * (default "pfqbo"; the pyramid first, FAST before the quadtree, the blur
+ * and the quadtree before the descriptors). Host only. */
+int orbx_get_stage_order(char* out);
 /* Record caller-owned HIP events (ORBX_STAGE_EVENTS of them, hipEvent_t as
  * void*) between the stages of the NEXT orbx_extract_batch call on its
- * stream: ev[0] before the pyramid, ev[1] after it, then after blur, FAST,
- * quadtree and angle/descriptor. Lets a caller time every kernel of every
+ * stream: ev[0] before the first stage, ev[i + 1] after the i-th stage
+ * launched (orbx_get_stage_order). Lets a caller time every kernel of every
  * call without a host synchronisation. One-shot. */
 #define ORBX_STAGE_EVENTS 6
 int orbx_set_stage_events(orbx_handle h, void** events);

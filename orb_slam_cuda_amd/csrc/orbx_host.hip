@@ -1429,9 +1429,23 @@ int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out) {
   return ORBX_OK;
 }
 
+int orbx_get_stage_order(char* out) {
+  if (!out) return fail(ORBX_EINVAL, "null argument");
+  memcpy(out, extract_stage_order(), 6);
+  return ORBX_OK;
+}
+
 int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap, int* n) {
-  static const char* kNames[5] = {"Pyramid/Resize", "Gaussian Blur", "FAST+Grid", "Make quadtree",
-                                  "Compute angle+ORB descriptor+scale"};
+  auto name_of = [](char c) -> const char* {
+    switch (c) {
+      case 'p': return "Pyramid/Resize";
+      case 'b': return "Gaussian Blur";
+      case 'f': return "FAST+Grid";
+      case 'q': return "Make quadtree";
+      default: return "Compute angle+ORB descriptor+scale";
+    }
+  };
+  const char* order = extract_stage_order();
   if (!h || !n) return fail(ORBX_EINVAL, "null argument");
   *n = 0;
   if (!h->timing) return ORBX_OK;
@@ -1440,7 +1454,7 @@ int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap, 
     float t = 0;
     HIP_OK(hipEventElapsedTime(&t, h->ev[i], h->ev[i + 1]));
     if (ms) ms[i] = t;
-    if (names) names[i] = kNames[i];
+    if (names) names[i] = name_of(order[i]);
     *n = i + 1;
   }
   return ORBX_OK;

@@ -213,6 +213,9 @@ struct ExtractBuffers {
   int* err;            // device error word
 };
 
+// orbx_extract.hip: the stages' launch order, one letter each (p pyramid, b
+// blur, f FAST, q quadtree, o orient+BRIEF)
+const char* extract_stage_order();
 // pyr_event (optional): recorded on `stream` right after the pyramid stage, so
 // a caller can fork work that only needs the pyramid (orbx_extract's host copy)
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames,

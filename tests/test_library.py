@@ -50,6 +50,19 @@ def test_descriptor_distance_is_host_exact():
         assert pkg.ORBmatcher.DescriptorDistance(D[i], D[j]) == int(np.unpackbits(D[i] ^ D[j]).sum())
 
 
+def test_stage_order_is_a_valid_launch_order():
+    """orbx_get_stage_order (host only): the five stages once each, the
+    pyramid first, FAST before the quadtree, orient+BRIEF last (after the blur
+    and the quadtree it reads); the default is pyramid, FAST, quadtree, blur."""
+    from orb_slam_cuda_amd import _lib
+    order = _lib.stage_order()
+    assert sorted(order) == sorted(["pyramid", "blur", "fast_grid", "quadtree", "orient_brief"])
+    assert order[0] == "pyramid" and order[-1] == "orient_brief"
+    assert order.index("fast_grid") < order.index("quadtree")
+    if "ORBX_EXTRACT_ORDER" not in os.environ:
+        assert order == ["pyramid", "fast_grid", "quadtree", "blur", "orient_brief"]
+
+
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="only meaningful without a GPU")
 def test_no_gpu_fails_loudly():
     import orb_slam_cuda_amd as pkg

@@ -300,7 +300,8 @@ def test_shim_gettime_tracking_usage(tmp_path):
 @pytest.mark.gpu
 def test_shim_times_csv(pkg, tmp_path):
     """ORBX_TIMING=1: every operator() call records the device stage times under
-    the reference's GetTime names plus "Total Time ORB extraction", and the
+    the reference's GetTime names (in the stages' launch order) plus "Total
+    Time ORB extraction", and the
     destructor appends them to ./times.csv in the reference's layout
     (src/ORBextractor.cc:800-820): '#Frame;Name Processing function;Level;Time
     spent (ns);Time spent (ms)' then 'frame;name;level;ns;ms;' rows."""
@@ -319,8 +320,11 @@ def test_shim_times_csv(pkg, tmp_path):
     lines = (tmp_path / "times.csv").read_text().splitlines()
     assert lines[0] == "#Frame;Name Processing function;Level;Time spent (ns);Time spent (ms)"
     rows = [l.split(";") for l in lines[1:]]
-    names = ["Pyramid/Resize", "Gaussian Blur", "FAST+Grid", "Make quadtree", "Compute angle+ORB descriptor+scale",
-             "Total Time ORB extraction"]
+    # the stage records in launch order (orbx_get_stage_order), then the total
+    label = {"pyramid": "Pyramid/Resize", "blur": "Gaussian Blur", "fast_grid": "FAST+Grid", "quadtree": "Make quadtree",
+             "orient_brief": "Compute angle+ORB descriptor+scale"}
+    from orb_slam_cuda_amd import _lib
+    names = [label[s] for s in _lib.stage_order()] + ["Total Time ORB extraction"]
     assert len(rows) == n * len(names)
     for k, row in enumerate(rows):
         assert len(row) == 6 and row[5] == ""
