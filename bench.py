@@ -150,9 +150,12 @@ def parse_args(argv=None):
     ap.add_argument("--split", type=int, default=2, help="extraction launches (and streams) per batch")
     ap.add_argument("--priority", action="store_true",
                     help="high-priority extraction streams, low-priority matching stream")
-    ap.add_argument("--no-match-priority", dest="match_priority", action="store_false",
-                    help="matching stream(s) at normal priority (default: high, so the matcher's "
-                         "one-workgroup-per-pair kernels get CUs as the extraction kernels drain them)")
+    ap.add_argument("--match-priority", dest="match_priority", action="store_true", default=False,
+                    help="matching stream(s) at high priority (A/B; default normal: with the pyramid, FAST, "
+                         "quadtree, blur, orient+BRIEF stage order that is 2 %% faster on C3 and EuRoC and "
+                         "equal on the other configs, DESIGN.md section 6)")
+    ap.add_argument("--no-match-priority", dest="match_priority", action="store_false", default=False,
+                    help="matching stream(s) at normal priority (the default)")
     ap.add_argument("--match-cus", default="",
                     help="A/B: the matching stream(s) on a compute-unit subset, 'stride:K' (every K-th CU) or "
                          "'first:N'; with --cu-exclusive the extraction streams get the other CUs")

@@ -39,7 +39,7 @@ def _run_pipeline(argv, batches, host=False):
     W, H, B = cfg["W"], cfg["H"], args.batch
     frames = SynthSequence(sharding.sequence_seed(0), W, H).frames(args.pool)
     pipe = bench.MonoPipeline(args, cfg, 0, frames, host=host)
-    assert pipe.S == 2 and pipe.NS == 3 and not args.serial and args.carry == "match" and args.match_priority
+    assert pipe.S == 2 and pipe.NS == 3 and not args.serial and args.carry == "match" and not args.match_priority
     assert pipe.nbatches > 1  # the pool cycles: level 0 streams from a different slot every batch
     pipe.run(0, batches, None)  # the timed region's issue order, without the warmup split
     pipe.check_status()
