@@ -172,6 +172,9 @@ def parse_args(argv=None):
                          "(SearchForInitialization)")
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
                     help="stream that copies a batch's last frame for the next batch's first pair")
+    ap.add_argument("--stage-order", default="",
+                    help="the extraction stages' launch order (orbx_set_stage_order: p b f q o, e.g. pfqbo); "
+                         "default: the library's, pbfqo with --bow / --bow-match")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency leg")
     ap.add_argument("--no-shim-latency", action="store_true",
                     help="skip the drop-in C++ shim's per-call latency leg (a child process)")
@@ -431,6 +434,14 @@ class MonoPipeline:
             raise SystemExit("--split must divide --batch")
         self.S, self.BS = S, B // S
         self.exts = [pkg.ORBextractor(*ext_params(cfg), W, H, device=local, max_batch=self.BS) for _ in range(S)]
+        # the stages' launch order for this pipeline (results do not depend on
+        # it): the library default, or "pbfqo" when the matching stream also runs
+        # ComputeBoW + SearchByBoW (C3 + BoW 136.1 / 133.3 k vs 123.7 / 123.7 k
+        # with the default); --stage-order overrides
+        self.stage_order = args.stage_order or ("pbfqo" if (args.bow or args.bow_match) else "")
+        if self.stage_order:
+            for ex in self.exts:
+                ex.set_stage_order(self.stage_order)
         self.cap = cap = self.exts[0].frame_capacity
         NS = self.NS
         DA = _lib.DeviceArray
@@ -764,7 +775,7 @@ def run_mono(args, cfg, rank, world, local, dist):
     from orb_slam_cuda_amd import _lib as _stage_lib
     names = STAGES
     ext_stages = names[:5]
-    launch_order = _stage_lib.stage_order()  # stage event i + 1 closes launch_order[i]
+    launch_order = _stage_lib.stage_order(pipe.exts[0].handle)  # stage event i + 1 closes launch_order[i]
     STAGES_RUN = ext_stages + (["hamming_top2", "search_init"] if not args.no_match else []) \
         + (["bow_transform"] if (args.bow or args.bow_match) else []) + (["bow_match"] if args.bow_match else [])
     # per-stage average durations over the timed steps (ms per launch-group, BS frames),
@@ -882,6 +893,7 @@ def run_mono(args, cfg, rank, world, local, dist):
                        "streams": 1 if args.serial else S + 1, "frames_per_extract_launch": BS,
                        "match_stream_priority": ("low" if args.priority else "high" if args.match_priority
                                                  else "normal"),
+                       "stage_order": "".join(c[0] if c != "fast_grid" else "f" for c in launch_order),
                        "match_order": args.match_order},
             "per_rank_frames_per_s": agg["per_rank"],
             "roofline": roof,
@@ -1359,7 +1371,7 @@ def run_stereo(args, cfg, rank, world, local, dist):
             raise RuntimeError("matcher device status word set")
     timed = evs[args.warmup:]
     from orb_slam_cuda_amd import _lib as _stage_lib
-    launch_order = _stage_lib.stage_order()  # stage event i + 1 closes launch_order[i]
+    launch_order = _stage_lib.stage_order(sets[0]["eL"].handle)  # stage event i + 1 closes launch_order[i]
     stages = STAGES[:5] + ["stereo"]
     sm = {s: 0.0 for s in stages}
     for ev in timed:

@@ -228,11 +228,18 @@ int orbx_get_pattern(int pattern_mode, int* out1024);
  * was created with timing enabled (ORBX_TIMING=1 in the environment). */
 int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap,
                          int* n);
-/* The extraction stages' launch order as 5 letters + NUL into out[6]: p
- * pyramid, b Gaussian blur, f FAST + grid, q quadtree, o angle + descriptor
- * (default "pfqbo"; the pyramid first, FAST before the quadtree, the blur
- * and the quadtree before the descriptors). Host only. */
-int orbx_get_stage_order(char* out);
+/* The extraction stages' launch order of handle h (NULL: the default) as 5
+ * letters + NUL into out[6]: p pyramid, b Gaussian blur, f FAST + grid, q
+ * quadtree, o angle + descriptor (default "pfqbo", or ORBX_EXTRACT_ORDER).
+ * Host only. */
+int orbx_get_stage_order(orbx_handle h, char* out);
+/* Set a handle's stage launch order for its later extractions: the pyramid
+ * first, orient+BRIEF last, FAST before the quadtree ("pfqbo", "pbfqo",
+ * "pfbqo"). Results do not depend on it; how the launches interleave with a
+ * caller's other streams does (a pipeline that overlaps ComputeBoW and
+ * SearchByBoW with the next extraction runs faster with "pbfqo", DESIGN.md
+ * section 6). ORBX_EINVAL for any other string. */
+int orbx_set_stage_order(orbx_handle h, const char* order);
 /* Record caller-owned HIP events (ORBX_STAGE_EVENTS of them, hipEvent_t as
  * void*) between the stages of the NEXT orbx_extract_batch call on its
  * stream: ev[0] before the first stage, ev[i + 1] after the i-th stage

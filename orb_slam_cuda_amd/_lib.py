@@ -93,11 +93,12 @@ class _Tolerant:
             return type("Missing", (), {})()
 
 
-def stage_order() -> list:
-    """The extraction stages in launch order, as bench.py's stage names
-    (orbx_get_stage_order): stage event i + 1 closes entry i."""
+def stage_order(handle=None) -> list:
+    """The extraction stages in launch order of an extractor handle (None: the
+    default), as bench.py's stage names (orbx_get_stage_order): stage event
+    i + 1 closes entry i."""
     buf = C.create_string_buffer(6)
-    check(lib().orbx_get_stage_order(buf))
+    check(lib().orbx_get_stage_order(handle, buf))
     names = {"p": "pyramid", "b": "blur", "f": "fast_grid", "q": "quadtree", "o": "orient_brief"}
     return [names[c] for c in buf.value.decode()]
 
@@ -124,7 +125,8 @@ def lib() -> C.CDLL:
                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.orbx_get_scales.argtypes = [C.c_void_p] + [C.c_void_p] * 4
         L.orbx_get_levels_info.argtypes = [C.c_void_p] + [C.c_void_p] * 4
-        L.orbx_get_stage_order.argtypes = [C.c_char_p]
+        L.orbx_get_stage_order.argtypes = [C.c_void_p, C.c_char_p]
+        L.orbx_set_stage_order.argtypes = [C.c_void_p, C.c_char_p]
         L.orbx_get_level.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t]
         L.orbx_set_host_pyramid.argtypes = [C.c_void_p, C.c_int]
         L.orbx_get_host_pyramid.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]

@@ -17,25 +17,28 @@ namespace orbx {
 
 // Stage launch order: p pyramid, b blur, f FAST, q quadtree, o orient+BRIEF;
 // the pyramid first, FAST before the quadtree, both the blur and the
-// quadtree before orient+BRIEF, orient+BRIEF last. Default "pfqbo": the
-// quadtree right behind FAST, the blur (read only by orient+BRIEF) after it
-// (pipelined C3 172.5 -> 174.4 k frames/s, KITTI14 151.8 -> 159.0 k against
-// "pbfqo"). ORBX_EXTRACT_ORDER overrides it (A/B). Stage
-// event i + 1 closes the i-th stage launched (orbx_get_stage_order).
+// quadtree before orient+BRIEF, orient+BRIEF last. The stages' results do not
+// depend on it; how a launch interleaves with other streams' work does. Default
+// "pfqbo": the quadtree right behind FAST, the blur (read only by
+// orient+BRIEF) after it (pipelined C3 172.5 -> 174.4 k frames/s, KITTI14
+// 151.8 -> 159.0 k against "pbfqo"). ORBX_EXTRACT_ORDER
+// overrides the default, orbx_set_stage_order a handle's. Stage event i + 1
+// closes the i-th stage launched.
+bool valid_stage_order(const char* e) {
+  return e && strlen(e) == 5 && e[0] == 'p' && e[4] == 'o' && strchr(e, 'b') && strchr(e, 'f') && strchr(e, 'q') &&
+         strchr(e, 'q') > strchr(e, 'f');
+}
 const char* extract_stage_order() {
   static const char* order = [] {
     const char* e = getenv("ORBX_EXTRACT_ORDER");
-    if (!e || strlen(e) != 5 || e[0] != 'p' || e[4] != 'o' || !strchr(e, 'b') || !strchr(e, 'f') ||
-        !strchr(e, 'q') || strchr(e, 'q') < strchr(e, 'f'))
-      return "pfqbo";
-    return e;
+    return valid_stage_order(e) ? e : "pfqbo";
   }();
   return order;
 }
 
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames, int batch,
                    size_t frame_pitch, size_t row_stride, orbx_kp* d_kps, uint8_t* d_desc, int* d_counts,
-                   void* stream_, void** ev, void* pyr_event, int* status_dst) {
+                   void* stream_, void** ev, void* pyr_event, int* status_dst, const char* stage_order) {
   hipStream_t stream = (hipStream_t)stream_;
   ExtractParams Q = P;
   Q.B = batch;
@@ -55,7 +58,7 @@ int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_
   auto rec = [&](int i) {
     if (ev) (void)hipEventRecord((hipEvent_t)ev[i], stream);
   };
-  const char* order = extract_stage_order();
+  const char* order = stage_order ? stage_order : extract_stage_order();
   int rc;
   rec(0);
   for (int i = 0; i < 5; ++i) {

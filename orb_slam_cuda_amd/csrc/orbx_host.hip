@@ -154,6 +154,7 @@ struct orbx_extractor {
   // ORBX_EXTRACT_PROF=1 (diagnostics): orbx_extract's host phases per call
   // (s), their medians printed by orbx_destroy: staging copy, issue, wait, copy-out
   std::vector<float> prof_t[4];
+  char order[6] = {};  // the stages' launch order (orbx_set_stage_order; default extract_stage_order())
   std::mutex mu;
 };
 
@@ -929,6 +930,7 @@ int orbx_create(const orbx_config* cfg, orbx_handle* out) {
     return fail(ORBX_EDEVICE, "device %d is %s; liborbx is built for gfx950 only", c.device, prop.gcnArchName);
   orbx_extractor* h = new orbx_extractor();
   h->cfg = c;
+  memcpy(h->order, extract_stage_order(), 6);
   compute_scales(h);
   h->plan.B = c.max_batch;
   int rc = deferred ? ORBX_OK : build_plan(h, c.width, c.height, c.max_batch);
@@ -990,7 +992,7 @@ int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch, size_t
   h->has_user_ev = false;
   if (h->ws.before((hipStream_t)stream)) return fail(ORBX_EDEVICE, "stream wait on the handle's last use failed");
   const int rc = launch_extract(h->plan.P, buffers_of(h->plan), d_frames, batch, frame_pitch, row_stride, d_kps,
-                                d_desc, d_counts, stream, ev);
+                                d_desc, d_counts, stream, ev, nullptr, nullptr, h->order);
   if (!rc && h->ws.after((hipStream_t)stream)) return fail(ORBX_EDEVICE, "event record failed");
   h->last_batch = batch;
   h->last_frames = d_frames;
@@ -1043,7 +1045,7 @@ static int issue_one_frame(orbx_extractor* h, size_t pitch, int hh, int cap_fram
   const bool hp = h->host_pyr && P.L > 1;
   const int rc = launch_extract(P, buffers_of(h->plan), h->d_in.as<uint8_t>(), 1, pitch * hh, pitch,
                                 (orbx_kp*)(d + 16), d + doff, (int*)d, s, h->timing ? (void**)h->ev : nullptr,
-                                hp ? (void*)h->pev[0] : nullptr, (int*)d + 1);
+                                hp ? (void*)h->pev[0] : nullptr, (int*)d + 1, h->order);
   if (rc) return fail(rc, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
   if (hp) {
     // fork: the pyramid levels go to pinned host memory beside FAST .. BRIEF
@@ -1429,9 +1431,23 @@ int orbx_get_tie_stats(orbx_handle h, int frame0, int nframes, int* out) {
   return ORBX_OK;
 }
 
-int orbx_get_stage_order(char* out) {
+int orbx_get_stage_order(orbx_handle h, char* out) {
   if (!out) return fail(ORBX_EINVAL, "null argument");
-  memcpy(out, extract_stage_order(), 6);
+  memcpy(out, h ? h->order : extract_stage_order(), 6);
+  return ORBX_OK;
+}
+
+int orbx_set_stage_order(orbx_handle h, const char* order) {
+  if (!h) return fail(ORBX_EINVAL, "null handle");
+  if (!valid_stage_order(order))
+    return fail(ORBX_EINVAL, "stage order must be 5 letters of p b f q o: p first, o last, f before q");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (memcmp(h->order, order, 5) == 0) return ORBX_OK;
+  // the single-frame graph was captured with the old order (after the launches using it)
+  if (h->ws.ev) (void)hipEventSynchronize(h->ws.ev);
+  if (h->graph) (void)hipGraphExecDestroy(h->graph);
+  h->graph = nullptr;
+  memcpy(h->order, order, 6);
   return ORBX_OK;
 }
 
@@ -1445,7 +1461,7 @@ int orbx_get_stage_times(orbx_handle h, float* ms, const char** names, int cap, 
       default: return "Compute angle+ORB descriptor+scale";
     }
   };
-  const char* order = extract_stage_order();
+  const char* order = h->order;
   if (!h || !n) return fail(ORBX_EINVAL, "null argument");
   *n = 0;
   if (!h->timing) return ORBX_OK;

@@ -213,15 +213,16 @@ struct ExtractBuffers {
   int* err;            // device error word
 };
 
-// orbx_extract.hip: the stages' launch order, one letter each (p pyramid, b
-// blur, f FAST, q quadtree, o orient+BRIEF)
+// orbx_extract.hip: the stages' default launch order, one letter each (p
+// pyramid, b blur, f FAST, q quadtree, o orient+BRIEF), and the check of one
 const char* extract_stage_order();
+bool valid_stage_order(const char* order);
 // pyr_event (optional): recorded on `stream` right after the pyramid stage, so
 // a caller can fork work that only needs the pyramid (orbx_extract's host copy)
 int launch_extract(const ExtractParams& P, const ExtractBuffers& X, const uint8_t* d_frames,
                    int batch, size_t frame_pitch, size_t row_stride, orbx_kp* d_kps,
                    uint8_t* d_desc, int* d_counts, void* stream, void** stage_events,
-                   void* pyr_event = nullptr, int* status_dst = nullptr);
+                   void* pyr_event = nullptr, int* status_dst = nullptr, const char* stage_order = nullptr);
 
 // orbx_match.hip
 int launch_hamming_top2(const uint8_t* A, size_t a_pitch, const int* nA, int a_cap,

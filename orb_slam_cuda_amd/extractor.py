@@ -101,6 +101,13 @@ class ORBextractor:
                                      None, 2**31 - 1, None, C.byref(n)))
         return self.frame_capacity
 
+    def set_stage_order(self, order: str) -> None:
+        """The stages' launch order for later extractions (orbx_set_stage_order)."""
+        check(lib().orbx_set_stage_order(self._h, order.encode()))
+
+    def stage_order(self) -> list:
+        return _lib.stage_order(self._h)
+
     def extract_batch_device(self, d_frames: int, batch: int, frame_pitch: int, row_stride: int,
                              d_kps: int, d_desc: int, d_counts: int, stream=None) -> None:
         """Asynchronous batched extraction on device pointers (orbx_extract_batch)."""

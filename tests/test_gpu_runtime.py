@@ -145,3 +145,43 @@ def test_stereo_batches_on_two_streams_share_one_matcher(pkg, O):
                 O.pyramid(cfg, R["pairs"][i][0]), O.pyramid(cfg, R["pairs"][i][1]),
                 O.level_info(cfg)["scale"], O.level_info(cfg)["inv_scale"], MB, MBF)
             assert kept[i] == rk and np.array_equal(u[i, :nl], ru)
+
+
+def test_stage_order_per_handle(pkg, O):
+    """orbx_set_stage_order: every valid launch order gives the oracle's output
+    (single-frame calls re-capture their graph with the new order, batch calls
+    launch in it); an invalid order is refused and leaves the handle's order."""
+    import ctypes as C
+
+    from orb_slam_cuda_amd import _lib
+    from orb_slam_cuda_amd.synth import SynthSequence
+    W, H = 1241, 376
+    frames = SynthSequence(7, W, H).frames(2)
+    cfg = O.config(nfeatures=2000, width=W, height=H)
+    want = [O.extract(cfg, f) for f in frames]
+    ext = pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H, max_batch=2)
+    pitch = (W + 63) & ~63
+    d = _lib.DeviceArray(2 * H * pitch)
+    img = np.zeros((2, H, pitch), np.uint8)
+    img[:, :, :W] = frames
+    d.upload(img)
+    cap = ext.frame_capacity
+    dk, dd, dc = _lib.DeviceArray(2 * cap * 28), _lib.DeviceArray(2 * cap * 32), _lib.DeviceArray(16)
+    for order in ("pbfqo", "pfbqo", "pfqbo"):
+        ext.set_stage_order(order)
+        assert "".join("f" if s == "fast_grid" else s[0] for s in ext.stage_order()) == order
+        for _ in range(2):  # plain launches, then the captured graph
+            for f, (wk, wd) in zip(frames, want):
+                k, dsc = ext(f)
+                assert np.array_equal(k.view(np.uint8), wk.view(np.uint8)) and np.array_equal(dsc, wd), order
+        ext.extract_batch_device(d.ptr, 2, H * pitch, pitch, dk.ptr, dd.ptr, dc.ptr)
+        n = dc.download(2, np.int32)
+        kb = dk.download(2 * cap * 28, np.uint8).reshape(2, cap, 28)
+        for i, (wk, wd) in enumerate(want):
+            assert n[i] == len(wk) and np.array_equal(kb[i, :n[i]].reshape(-1), wk.view(np.uint8).reshape(-1)), order
+    for bad in ("pqfbo", "bpfqo", "pfqob", "pfq", "pfqbx", ""):
+        with pytest.raises(pkg.OrbxError):
+            ext.set_stage_order(bad)
+    assert ext.stage_order()[1] == "fast_grid"  # still "pfqbo"
+    st = C.c_int(0)
+    assert _lib.lib().orbx_get_status(ext.handle, 1, C.byref(st)) == 0 and st.value == 0
