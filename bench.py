@@ -822,6 +822,15 @@ def run_mono(args, cfg, rank, world, local, dist):
                               " not measured in this run",
             "algorithmic_bytes_per_launch": int(hbm_stages[rk] * BS),
             "avg_launch_ms": round(st[rk], 4)}
+    # the same kernel run alone (--serial): its committed rocprofv3 average, so
+    # the pipelined event time's share of waiting for CUs beside the other
+    # streams (which grows as the pipeline overlaps more) can be told apart
+    alone = serial_avg_ms(KERNELS[rk], BS)
+    if alone:
+        roof["alone"] = {"avg_launch_ms": round(alone[0], 4),
+                         "achieved": round(hbm_stages[rk] * BS / (alone[0] * 1e-3) / 1e9, 1),
+                         "frac": round(hbm_stages[rk] * BS / (alone[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "source": alone[1] + " (committed --serial rocprofv3 summary, not measured in this run)"}
     # the same kernel against VALU issue (it is latency / issue bound, not HBM bound):
     # its committed SQ_INSTS_VALU per launch over this run's launch time
     vi = sq_valu(KERNELS[rk])
@@ -972,6 +981,21 @@ def rocprof_ranking(top=6):
             "by_total_time": [{"kernel": r["Name"].split("(")[0].replace("void ", "").replace("orbx::", ""),
                                "avg_us": round(float(r["AverageNs"]) / 1e3, 1), "pct": float(r["Percentage"])}
                               for r in rows[:top]]}
+
+
+def serial_avg_ms(kernel, launch_frames):
+    """(average ms, file) of `kernel` in the newest committed --serial rocprofv3
+    summary of the default C3 command (profiles/rNN_serial_kernel_stats.csv),
+    for launches of SQ_LAUNCH_FRAMES frames only."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_serial_kernel_stats.csv")))
+    if not files or launch_frames != SQ_LAUNCH_FRAMES:
+        return None
+    for r in csv.DictReader(open(files[-1])):
+        if r["Name"].split("(")[0].replace("void ", "").replace("orbx::", "").split("<")[0] == kernel.split("<")[0]:
+            return float(r["AverageNs"]) / 1e6, os.path.relpath(files[-1], ROOT)
+    return None
 
 
 def sq_valu(kernel):
