@@ -1333,6 +1333,9 @@ def run_stereo(args, cfg, rank, world, local, dist):
     for _ in range(NSET):
         eL = pkg.ORBextractor(*ext_params(cfg), W, H, device=local, max_batch=B)
         eR = pkg.ORBextractor(*ext_params(cfg), W, H, device=local, max_batch=B)
+        if args.stage_order:
+            eL.set_stage_order(args.stage_order)
+            eR.set_stage_order(args.stage_order)
         cap = eL.frame_capacity
         sL = s_one or _lib.Stream()
         sets.append(dict(eL=eL, eR=eR, sL=sL, sR=s_one or _lib.Stream(),

@@ -172,3 +172,43 @@ def test_stereo_frame_one_round_trip_equals_oracle(pkg, O):
     got = pkg.ExtractStereo(eL, eR, imL, imR, m, MB, float(MBF))
     want = oracle(imL, imR)
     assert np.array_equal(got[4], want[4]) and got[6] == want[6]
+
+
+def test_stereo_frames_from_two_threads(pkg, O):
+    """Two host threads each running orbm_stereo_frame on their own extractor
+    pair and matcher (the library's one staging helper thread serves one call
+    at a time; the other copies inline): every frame equals the same call made
+    alone."""
+    import threading
+
+    from orb_slam_cuda_amd.synth import stereo_pair
+    W, H = 1241, 376
+    pairs = [stereo_pair(40 + i, W, H) for i in range(6)]
+    ref = {}
+    eL, eR, m = (pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H), pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H),
+                 pkg.ORBmatcher(max_kps=4096))
+    for i, (L, R) in enumerate(pairs):
+        ref[i] = pkg.ExtractStereo(eL, eR, L, R, m, MB, float(MBF))
+    errors = []
+
+    def worker(t):
+        try:
+            a, b, mm = (pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H), pkg.ORBextractor(2000, 1.2, 8, 20, 7, W, H),
+                        pkg.ORBmatcher(max_kps=4096))
+            for rep in range(4):
+                for i in range(t, len(pairs), 2):
+                    got = pkg.ExtractStereo(a, b, pairs[i][0], pairs[i][1], mm, MB, float(MBF))
+                    for g, w in zip(got[:6], ref[i][:6]):
+                        if not np.array_equal(np.asarray(g).view(np.uint8), np.asarray(w).view(np.uint8)):
+                            errors.append((t, rep, i))
+                    if got[6] != ref[i][6]:
+                        errors.append((t, rep, i, "kept"))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
