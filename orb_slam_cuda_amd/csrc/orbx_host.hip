@@ -742,7 +742,9 @@ static int build_plan(orbx_extractor* h, int W, int Hh, int B) {
     // the sorted path's rounds hold two nodes per thread
     if (maxnodes > 2 * (P.qt_big ? 1024 : kQtThreads)) P.qt_sorted = 0;
     if (getenv("ORBX_PLAN_INFO"))  // diagnostics: the quadtree block's LDS per path
-      fprintf(stderr, "plan %dx%d B %d: quadtree LDS legacy %zu sorted %zu (budget %zu) sorted %d big %d maxnodes %d nbmax %d tabmax %d ownmax %d\n",
+      fprintf(stderr,
+              "plan %dx%d B %d: quadtree LDS legacy %zu sorted %zu (budget %zu) sorted %d big %d maxnodes %d "
+              "nbmax %d tabmax %d ownmax %d\n",
               W, Hh, B, base, P.qt_nbmax ? quadtree_sorted_lds_bytes(P, P.qt_big) : (size_t)0, budget, P.qt_sorted,
               P.qt_big, maxnodes, P.qt_nbmax, P.qt_tabmax, P.qt_ownmax);
   }
