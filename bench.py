@@ -166,10 +166,12 @@ def parse_args(argv=None):
                     help="also SearchByBoW of every frame against its predecessor as reference keyframe (implies --bow)")
     ap.add_argument("--match-streams", type=int, choices=[1, 2], default=1,
                     help="2: SearchForInitialization on its own stream, beside the dense top-2")
-    ap.add_argument("--match-order", type=match_order, default="top2,bow,init",
+    ap.add_argument("--match-order", type=match_order, default=None,
                     help="order of the matching stages on the matching stream: a permutation of top2 (dense "
                          "Hamming top-2), bow (ComputeBoW [+ SearchByBoW], with --bow/--bow-match), init "
-                         "(SearchForInitialization)")
+                         "(SearchForInitialization); default init,top2,bow (top2,bow,init with --bow / "
+                         "--bow-match: SearchForInitialization first is 7 %% faster on KITTI14, 4-7 %% on EuRoC, "
+                         "but 14 %% slower with the BoW stages, DESIGN.md section 6)")
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
                     help="stream that copies a batch's last frame for the next batch's first pair")
     ap.add_argument("--stage-order", default="",
@@ -203,7 +205,10 @@ def parse_args(argv=None):
                     help="run even with diagnostic ORBX_* variables set (phase clocks, library variants); "
                          "the line then carries them and is not a valid measurement")
     ap.add_argument("--stub-worker", action="store_true", help=argparse.SUPPRESS)  # launcher tests (CPU)
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.match_order is None:
+        a.match_order = "top2,bow,init" if (a.bow or a.bow_match) else "init,top2,bow"
+    return a
 
 
 # ORBX_* variables the library reads (INTEGRATION.md "Environment variables").
