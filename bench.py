@@ -169,7 +169,7 @@ def parse_args(argv=None):
     ap.add_argument("--match-order", type=match_order, default=None,
                     help="order of the matching stages on the matching stream: a permutation of top2 (dense "
                          "Hamming top-2), bow (ComputeBoW [+ SearchByBoW], with --bow/--bow-match), init "
-                         "(SearchForInitialization); default init,top2,bow (top2,bow,init with --bow / "
+                         "(SearchForInitialization); default init,top2,bow (bow,init,top2 with --bow / "
                          "--bow-match: SearchForInitialization first is 7 %% faster on KITTI14, 4-7 %% on EuRoC, "
                          "but 14 %% slower with the BoW stages, DESIGN.md section 6)")
     ap.add_argument("--carry", choices=["match", "ext"], default="match",
@@ -207,7 +207,7 @@ def parse_args(argv=None):
     ap.add_argument("--stub-worker", action="store_true", help=argparse.SUPPRESS)  # launcher tests (CPU)
     a = ap.parse_args(argv)
     if a.match_order is None:
-        a.match_order = "top2,bow,init" if (a.bow or a.bow_match) else "init,top2,bow"
+        a.match_order = "bow,init,top2" if (a.bow or a.bow_match) else "init,top2,bow"
     return a
 
 

@@ -85,7 +85,7 @@ def test_parse_defaults():
     a = bench.parse_args([])
     assert a.gpus == 1 and a.batch == 64 and a.pool % a.batch == 0 and a.pool * 1280 * 376 > 256 * 2 ** 20
     assert a.match_order == "init,top2,bow" and not a.match_priority
-    assert bench.parse_args(["--bow-match"]).match_order == "top2,bow,init"
+    assert bench.parse_args(["--bow-match"]).match_order == "bow,init,top2"
 
 
 @pytest.mark.parametrize("order,ok", [("init,top2,bow", True), ("bow,top2,init", True), ("top2,bow", False),
