@@ -1141,7 +1141,10 @@ static void extract_stage(orbx_extractor* h, const uint8_t* img, int w, int hh, 
   }
 }
 
-static int extract_issue(orbx_extractor* h, int w, int hh) {
+// mark: record the handle's workspace event after the chain (for work another
+// stream orders after it: the stereo pair's left chain); the synchronous
+// callers wait for the chain themselves, so later users find it finished
+static int extract_issue(orbx_extractor* h, int w, int hh, bool mark) {
   const int cap_frame = h->plan.P.kp_per_frame;
   const size_t pitch = ((size_t)w + 63) & ~(size_t)63;
   int rc;
@@ -1150,7 +1153,7 @@ static int extract_issue(orbx_extractor* h, int w, int hh) {
     h->graph = nullptr;
   };
   // the plan buffers may still be in use by a batch call on another stream
-  if (h->ws.before(h->stream)) return fail(ORBX_EDEVICE, "stream wait on the handle's last use failed");
+  if (h->ws.before_pending(h->stream)) return fail(ORBX_EDEVICE, "stream wait on the handle's last use failed");
   static const bool use_graph = !(getenv("ORBX_EXTRACT_GRAPH") && getenv("ORBX_EXTRACT_GRAPH")[0] == '0');
   // the first call of a size runs plain (one-time uploads and attribute
   // queries of the launchers happen outside any capture); later ones replay
@@ -1183,7 +1186,7 @@ static int extract_issue(orbx_extractor* h, int w, int hh) {
     h->warm_w = w;
     h->warm_h = hh;
   }
-  if (h->ws.after(h->stream)) return fail(ORBX_EDEVICE, "event record failed");
+  if (mark && h->ws.after(h->stream)) return fail(ORBX_EDEVICE, "event record failed");
   h->last_batch = 1;
   h->last_single = true;
   h->last_frames = h->d_in.as<uint8_t>();
@@ -1197,7 +1200,7 @@ static int extract_submit(orbx_extractor* h, const uint8_t* img, int w, int hh, 
   if (rc) return rc;
   extract_stage(h, img, w, hh, stride);
   if (t_staged) *t_staged = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-  return extract_issue(h, w, hh);
+  return extract_issue(h, w, hh, false);
 }
 
 static int extract_finish(orbx_extractor* h, orbx_kp* kps, int cap, uint8_t* desc, int* n) {
@@ -1658,7 +1661,7 @@ int orbx::extract_pair(orbx_handle L, orbx_handle R, const uint8_t* imL, size_t 
   const bool posted = use_helper && StageHelper::get().try_post(R, imR, w, hh, strideR);
   extract_stage(L, imL, w, hh, strideL);
   stamp(0);
-  if ((rc = extract_issue(L, w, hh))) {
+  if ((rc = extract_issue(L, w, hh, true))) {
     if (posted) StageHelper::get().wait();
     return rc;
   }
@@ -1666,7 +1669,7 @@ int orbx::extract_pair(orbx_handle L, orbx_handle R, const uint8_t* imL, size_t 
   if (posted) StageHelper::get().wait();
   else extract_stage(R, imR, w, hh, strideR);
   stamp(2);
-  if ((rc = extract_issue(R, w, hh))) return rc;
+  if ((rc = extract_issue(R, w, hh, false))) return rc;
   stamp(3);
   const int rb = between(R->stream);
   stamp(4);

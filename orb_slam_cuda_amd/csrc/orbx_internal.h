@@ -324,6 +324,14 @@ struct WsOrder {
   int before(hipStream_t s) {
     return used && hipStreamWaitEvent(s, ev, 0) != hipSuccess ? ORBX_EDEVICE : ORBX_OK;
   }
+  // the same, but no wait when the last use has already finished (a
+  // cross-stream wait is a barrier packet the next launch pays for); for the
+  // synchronous entry points, which wait for their own work before returning
+  // and so record no event after it
+  int before_pending(hipStream_t s) {
+    if (!used || hipEventQuery(ev) == hipSuccess) return ORBX_OK;
+    return hipStreamWaitEvent(s, ev, 0) != hipSuccess ? ORBX_EDEVICE : ORBX_OK;
+  }
   int after(hipStream_t s) {
     if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return ORBX_EDEVICE;
     if (hipEventRecord(ev, s) != hipSuccess) return ORBX_EDEVICE;

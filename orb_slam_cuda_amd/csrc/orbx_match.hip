@@ -1861,11 +1861,13 @@ int orbm_search_by_bow_batch(orbm_handle m, int pairs, int kp_pitch, int node_pi
   return ORBX_OK;
 }
 
-int orbm_compute_stereo_matches_batch(orbm_handle m, orbx_handle left, int left_frame0, orbx_handle right,
-                                      int right_frame0, const orbx_kp* d_kpL, const uint8_t* d_descL,
-                                      const int* d_nL, const orbx_kp* d_kpR, const uint8_t* d_descR,
-                                      const int* d_nR, int kp_pitch, int pairs, float mb, float mbf,
-                                      float* d_uRight, float* d_depth, int* d_nkept, void* stream) {
+// sync: a synchronous caller that waits for the launch itself: its
+// workspaces' earlier users are waited for only if still running, and no
+// event is recorded after it (no barrier packets around its kernels)
+static int stereo_batch(orbm_handle m, orbx_handle left, int left_frame0, orbx_handle right, int right_frame0,
+                        const orbx_kp* d_kpL, const uint8_t* d_descL, const int* d_nL, const orbx_kp* d_kpR,
+                        const uint8_t* d_descR, const int* d_nR, int kp_pitch, int pairs, float mb, float mbf,
+                        float* d_uRight, float* d_depth, int* d_nkept, void* stream, bool sync) {
   if (!m || !left || !right || !d_kpL || !d_descL || !d_nL || !d_kpR || !d_descR || !d_nR || !d_uRight ||
       !d_depth || !d_nkept || pairs < 1 || kp_pitch < 1)
     return mfail(ORBX_EINVAL, "bad argument");
@@ -1906,13 +1908,23 @@ int orbm_compute_stereo_matches_batch(orbm_handle m, orbx_handle left, int left_
   hipStream_t s = (hipStream_t)stream;
   WsOrder* wl = extractor_ws(left);
   WsOrder* wr2 = extractor_ws(right);
-  if (m->ws.before(s) || wl->before(s) || wr2->before(s))
+  if (sync ? (m->ws.before_pending(s) || wl->before_pending(s) || wr2->before_pending(s))
+           : (m->ws.before(s) || wl->before(s) || wr2->before(s)))
     return mfail(ORBX_EDEVICE, "stream wait on the workspaces failed");
   if (launch_stereo(P, d_kpL, d_descL, d_nL, d_kpR, d_descR, d_nR, pairs, d_uRight, d_depth, m->stereo_sad, d_nkept,
                     stream) != ORBX_OK)
     return mfail(ORBX_EDEVICE, "stereo launch: %s", hipGetErrorString(hipGetLastError()));
-  if (m->ws.after(s) || wl->after(s) || wr2->after(s)) return mfail(ORBX_EDEVICE, "event record failed");
+  if (!sync && (m->ws.after(s) || wl->after(s) || wr2->after(s))) return mfail(ORBX_EDEVICE, "event record failed");
   return ORBX_OK;
+}
+
+int orbm_compute_stereo_matches_batch(orbm_handle m, orbx_handle left, int left_frame0, orbx_handle right,
+                                      int right_frame0, const orbx_kp* d_kpL, const uint8_t* d_descL,
+                                      const int* d_nL, const orbx_kp* d_kpR, const uint8_t* d_descR,
+                                      const int* d_nR, int kp_pitch, int pairs, float mb, float mbf,
+                                      float* d_uRight, float* d_depth, int* d_nkept, void* stream) {
+  return stereo_batch(m, left, left_frame0, right, right_frame0, d_kpL, d_descL, d_nL, d_kpR, d_descR, d_nR,
+                      kp_pitch, pairs, mb, mbf, d_uRight, d_depth, d_nkept, stream, false);
 }
 
 int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle right, const orbx_kp* kpL,
@@ -1948,8 +1960,8 @@ int orbm_compute_stereo_matches(orbm_handle m, orbx_handle left, orbx_handle rig
     MHIP(hipMemcpyAsync(ddr, descR, (size_t)nR * 32, hipMemcpyHostToDevice, st));
   }
   MHIP(hipMemcpyAsync(dn, hn, 8, hipMemcpyHostToDevice, st));
-  rc = orbm_compute_stereo_matches_batch(m, left, 0, right, 0, dkl, ddl, dn, dkr, ddr, dn + 1, pitch, 1, mb, mbf,
-                                         du, dd, dn + 2, st);
+  rc = stereo_batch(m, left, 0, right, 0, dkl, ddl, dn, dkr, ddr, dn + 1, pitch, 1, mb, mbf, du, dd, dn + 2, st,
+                    true);
   if (rc) return rc;
   int kept = 0;
   MHIP(hipMemcpyAsync(&kept, dn + 2, 4, hipMemcpyDeviceToHost, st));
@@ -2016,8 +2028,7 @@ int orbm_compute_stereo_matches_last(orbm_handle m, orbx_handle left, orbx_handl
   float* dd = du + capL;
   if (!m->stream) MHIP(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
   hipStream_t st = m->stream;
-  rc = orbm_compute_stereo_matches_batch(m, left, 0, right, 0, dkl, ddl, dnL, dkr, ddr, dnR, capL, 1, mb, mbf, du, dd,
-                                         dk, st);
+  rc = stereo_batch(m, left, 0, right, 0, dkl, ddl, dnL, dkr, ddr, dnR, capL, 1, mb, mbf, du, dd, dk, st, true);
   if (rc == ORBX_ECAPACITY) return host_fallback();  // checked before any launch
   if (rc) return rc;
   uint8_t* h = (uint8_t*)m->h_stage;
@@ -2108,8 +2119,7 @@ int orbm_stereo_frame(orbm_handle m, orbx_handle left, orbx_handle right, const 
     int* dk = (int*)m->stage;
     float* du = (float*)m->stage + 4;
     float* dd = du + cap;
-    rc = orbm_compute_stereo_matches_batch(m, left, 0, right, 0, dkl, ddl, dnL, dkr, ddr, dnR, cap, 1, mb, mbf, du,
-                                           dd, dk, st);
+    rc = stereo_batch(m, left, 0, right, 0, dkl, ddl, dnL, dkr, ddr, dnR, cap, 1, mb, mbf, du, dd, dk, st, true);
     if (rc == ORBX_ECAPACITY) return (brc = ORBX_ECAPACITY), ORBX_OK;  // checked before any launch
     if (rc) return brc = rc;
     if ((rc = copy_to_host_async(m->h_stage, dk, bytes, st))) return brc = mfail(rc, "%s", orbx_last_error());
