@@ -158,7 +158,9 @@ int orbx_extract(orbx_handle h, const uint8_t* img, int w, int h_, size_t stride
  * readable up to ceil16(width) bytes from its start (a 64-byte pitch, as
  * bench.py uses, always is). Outputs: frame i's keypoints at
  * d_kps + i*cap, descriptors at d_desc + i*cap*32, count in d_counts[i],
- * where cap = orbx_frame_capacity(h). Level-major order as the reference. */
+ * where cap = orbx_frame_capacity(h). Level-major order as the reference.
+ * Calls on one handle from several threads are serialised by the handle's
+ * lock (a synchronous orbx_extract holds it until its own work finished). */
 int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch,
                        size_t frame_pitch, size_t row_stride, orbx_kp* d_kps,
                        uint8_t* d_desc, int* d_counts, void* stream);

@@ -989,6 +989,10 @@ int orbx_extract_batch(orbx_handle h, const uint8_t* d_frames, int batch, size_t
   if (h->plan.W == 0)
     return fail(ORBX_EINVAL, "no frame size yet: the handle was created with width/height 0 and has seen no orbx_extract");
   if (row_stride < (size_t)h->plan.W) return fail(ORBX_EINVAL, "row_stride < width");
+  // one call of a handle at a time: a synchronous orbx_extract in flight on
+  // another thread holds the lock until its chain has finished (it records
+  // no workspace event for a batch call to wait on)
+  std::lock_guard<std::mutex> lk(h->mu);
   HIP_OK(hipSetDevice(h->cfg.device));
   void** ev = h->has_user_ev ? h->user_ev : (h->timing ? (void**)h->ev : nullptr);
   h->has_user_ev = false;
